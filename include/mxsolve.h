@@ -1,0 +1,178 @@
+/*
+ * mxsolve.h -- C ABI of libmxsolve.so, the MI355X-native (gfx950) hot path of
+ * the Dxslab/mpi-petsc4py-example workflow:
+ *
+ *     createAIJ(csr=...)  ->  MatMult (VecScatter halo + SpMV)  ->  KSPSolve CG/GMRES + Jacobi
+ *
+ * Every entry point replaces one petsc4py/PETSc call the reference makes; the
+ * "replaces" line cites the reference call site (file:line in the read-only
+ * reference tree) and the PETSc routine it reaches.  Plain C types only: opaque
+ * handles, raw pointers, sizes.  Device pointers ("_dev") are HIP device
+ * addresses on the handle's GPU (the Python shim passes torch tensor
+ * data_ptr()s); everything else is host memory.
+ *
+ * Return value of every function: 0 (MX_OK) or an MX_ERR_* class;
+ * mx_last_error() returns the calling thread's last message.  The Python shim
+ * maps MX_ERR_ARG to ValueError and the other classes to PETSc.Error.
+ *
+ * Collective calls (marked [collective]) must be made by every rank of the
+ * communicator in the same order, as PETSc requires.
+ */
+#ifndef MXSOLVE_H
+#define MXSOLVE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MX_ABI_VERSION 1
+
+enum {
+  MX_OK = 0,
+  MX_ERR_ARG = 1,         /* bad argument (petsc4py ValueError)               */
+  MX_ERR_OUTOFRANGE = 2,  /* index out of range (PETSC_ERR_ARG_OUTOFRANGE)    */
+  MX_ERR_HIP = 3,         /* HIP runtime failure                              */
+  MX_ERR_COMM = 4,        /* RCCL / communicator failure                      */
+  MX_ERR_MEM = 5,         /* device allocation failure                        */
+  MX_ERR_UNSUPPORTED = 6, /* valid request outside what this build implements */
+  MX_ERR_INTERNAL = 7
+};
+
+typedef struct mx_comm_s *mx_comm;
+typedef struct mx_mat_s *mx_mat;
+
+/* ---- KSP parameters / results (KSPSetType, KSPSetTolerances, PCSetType) ---- */
+enum { MX_KSP_CG = 0, MX_KSP_GMRES = 1, MX_KSP_PREONLY = 2 };
+enum { MX_PC_NONE = 0, MX_PC_JACOBI = 1 };
+enum { MX_NORM_DEFAULT = -1, MX_NORM_NONE = 0, MX_NORM_PRECONDITIONED = 1,
+       MX_NORM_UNPRECONDITIONED = 2, MX_NORM_NATURAL = 3 };
+enum { MX_INSERT_VALUES = 0, MX_ADD_VALUES = 1 };
+
+typedef struct {
+  int ksp_type;        /* MX_KSP_*                              (KSPSetType)          */
+  int pc_type;         /* MX_PC_*                               (PCSetType)           */
+  int norm_type;       /* MX_NORM_*                             (KSPSetNormType)      */
+  int max_it;          /* default 10000                         (KSPSetTolerances)    */
+  int restart;         /* GMRES restart, default 30             (KSPGMRESSetRestart)  */
+  int guess_nonzero;   /* 0: x <- 0 first   (KSPSetInitialGuessNonzero)               */
+  double rtol, atol, dtol; /* 1e-5, 1e-50, 1e5                                         */
+  double haptol;       /* GMRES happy breakdown, 1e-30                                */
+  double breakdowntol; /* GMRES restart consistency check, 0.1                        */
+  int poll_every;      /* host polls the device convergence flag every k its (0: 16) */
+  int profile;         /* 1: time every SpMV launch with HIP events                   */
+} mx_ksp_params;
+
+typedef struct {
+  int its;             /* KSPGetIterationNumber                                     */
+  int reason;          /* KSPConvergedReason value                                  */
+  double rnorm;        /* KSPGetResidualNorm                                        */
+  double solve_ms;     /* device time of the solve (HIP events, first to last kernel) */
+  double spmv_ms;      /* sum of profiled SpMV launch times (profile = 1)           */
+  int spmv_count;      /* SpMV launches profiled                                    */
+  int launched_its;    /* iterations enqueued (>= its; the tail are device no-ops)  */
+} mx_ksp_result;
+
+typedef struct {
+  int64_t M, N;          /* global sizes                       (MatGetSize)          */
+  int64_t m, n;          /* local rows / cols                  (MatGetLocalSize)     */
+  int64_t rstart, cstart;/* ownership starts                   (MatGetOwnershipRange) */
+  int64_t nnz_d, nnz_o;  /* diagonal / off-diagonal block nonzeros                    */
+  int64_t nghost;        /* |garray|                                                  */
+  int64_t sell_slots_d, sell_slots_o; /* padded SELL-64 slots (bytes model)           */
+  int nsend_peers, nrecv_peers;       /* halo neighbours                              */
+  int64_t nsend, nrecv;               /* halo values per MatMult                      */
+} mx_mat_info;
+
+/* ---- library ---------------------------------------------------------------- */
+int mx_version(void);
+int mx_last_error(char *buf, size_t len);
+
+/* ---- communicators (the comm= argument of createAIJ / KSP().create:
+ *      test.py:24,33 ; petsc_funcs.py:6) ----------------------------------------- */
+/* RCCL unique id for mx_comm_create_rccl (rank 0 creates, shim broadcasts it). */
+int mx_get_unique_id(void *out, size_t len);
+/* One process per GPU over RCCL/xGMI (replaces MPI_COMM_WORLD, test.py:55).   */
+int mx_comm_create_rccl(int rank, int size, int device, const void *uid, size_t uid_len,
+                        mx_comm *out);
+/* Single-rank communicator (PETSC_COMM_SELF / MPI.COMM_WORLD of size 1).       */
+int mx_comm_create_self(int device, mx_comm *out);
+/* In-process virtual ranks that share one GPU (testing N>1 on a 1-GPU box):
+ * one world, then one comm per rank, each used from its own host thread.       */
+int mx_world_create_local(int size, void **world);
+int mx_comm_create_local(void *world, int rank, int device, mx_comm *out);
+int mx_world_destroy(void *world);
+int mx_comm_destroy(mx_comm c);
+int mx_comm_info(mx_comm c, int *rank, int *size, int *device);
+/* The HIP stream every kernel of this communicator runs on (hipStream_t).      */
+int mx_comm_stream(mx_comm c, void **stream);
+int mx_comm_barrier(mx_comm c);  /* [collective] */
+
+/* ---- layout: PetscSplitOwnership (test.py:68-74, test2.py:33-37) ---------- */
+int mx_layout_split(int64_t N, int P, int64_t *ranges /* P+1 */);
+
+/* ---- Mat ------------------------------------------------------------------ */
+/* replaces PETSc.Mat().createAIJ(comm, size=(M,N), csr=(indptr, indices, data))
+ * + assemble()  (petsc_funcs.py:6-7, test.py:24-28) -> MatCreate/MatSetSizes/
+ * MatSetType(AIJ)/MatMPIAIJSetPreallocationCSR/MatSetValues/MatAssemblyEnd/
+ * MatSetUpMultiply_MPIAIJ.  [collective]
+ * m_local/n_local < 0 mean PETSC_DECIDE (PetscSplitOwnership).  indptr has
+ * m_local+1 entries of indptr_bytes (4|8), cols nnz entries of col_bytes (4|8)
+ * holding GLOBAL column ids.  Negative column ids are ignored, duplicates
+ * follow insert_mode (INSERT: last wins; ADD: summed in input order).
+ * Checks (petsc4py Mat_AllocAIJ_CSR): indptr[0] == 0, indptr[m] == nnz,
+ * nondecreasing -> MX_ERR_ARG; column >= N -> MX_ERR_OUTOFRANGE.
+ * src_is_device: the three arrays are device pointers.                          */
+int mx_mat_create_csr(mx_comm c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
+                      const void *indptr, int indptr_bytes, const void *cols, int col_bytes,
+                      const double *vals, int64_t nnz, int insert_mode, int src_is_device,
+                      mx_mat *A);
+/* MatSetPreallocationCOO/MatSetValuesCOO-style assembly of locally owned rows
+ * (global row/col ids, any order; negative ids ignored).  [collective]        */
+int mx_mat_create_coo(mx_comm c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
+                      const int64_t *rows, const int64_t *cols, const double *vals, int64_t n,
+                      int insert_mode, int src_is_device, mx_mat *A);
+/* Device-side generator of the synthetic operators feeding the
+ * same COO assembly; kind 0: 2D 5-pt nx*ny, 1: 3D 7-pt, 2: 3D 27-pt,
+ * 3: 3D convection-diffusion 7-pt.  Each rank generates its own rows.  [collective] */
+int mx_mat_create_stencil(mx_comm c, int kind, int64_t nx, int64_t ny, int64_t nz, mx_mat *A);
+int mx_mat_get_info(mx_mat A, mx_mat_info *info);
+/* replaces Mat.getValuesCSR (MatGetRow_MPIAIJ): local rows, GLOBAL sorted cols. */
+int mx_mat_get_csr(mx_mat A, int64_t *indptr, int64_t *cols, double *vals);
+/* The PETSc MPIAIJ split: A_d (local cols), A_o (ghost index), garray.      */
+int mx_mat_get_split(mx_mat A, int64_t *dptr, int32_t *dcol, double *dval, int64_t *optr,
+                     int32_t *ocol, double *oval, int64_t *garray);
+/* replaces MatMult (KSP_MatMult inside ksp.solve, test.py:50): halo + SpMV.  [collective] */
+int mx_mat_mult(mx_mat A, const double *x_dev, double *y_dev);
+/* replaces MatGetDiagonal (PCSetUp_Jacobi).                                  */
+int mx_mat_get_diagonal(mx_mat A, double *d_dev);
+/* Timing helper for bench.py: `iters` back-to-back MatMults; average device ms
+ * per SpMV kernel launch and per full MatMult (halo included).  [collective]     */
+int mx_mat_bench_mult(mx_mat A, const double *x_dev, double *y_dev, int iters,
+                      double *spmv_ms, double *mult_ms);
+int mx_mat_destroy(mx_mat A);
+
+/* ---- Vec (local length n, device pointers; reductions are collective) ----- */
+int mx_vec_dot(mx_comm c, int64_t n, const double *x_dev, const double *y_dev, double *out);
+int mx_vec_norm2(mx_comm c, int64_t n, const double *x_dev, double *out);
+int mx_vec_axpy(mx_comm c, int64_t n, double alpha, const double *x_dev, double *y_dev);
+int mx_vec_aypx(mx_comm c, int64_t n, double alpha, const double *x_dev, double *y_dev);
+int mx_vec_pointwise_mult(mx_comm c, int64_t n, const double *x_dev, const double *y_dev,
+                          double *w_dev);
+int mx_vec_scale(mx_comm c, int64_t n, double alpha, double *x_dev);
+int mx_vec_set(mx_comm c, int64_t n, double alpha, double *x_dev);
+/* b_i = (splitmix64(i + 42 phi) >> 11) 2^-53 for global i in [i0, i0+n) */
+int mx_vec_rhs_hash(mx_comm c, int64_t i0, int64_t n, double *b_dev);
+
+/* ---- KSP: replaces ksp.solve(b, x) (test.py:50) -> KSPSolve with the
+ *      configuration of test.py:33-47 + options.  [collective]              */
+int mx_ksp_solve(mx_mat A, const mx_ksp_params *p, const double *b_dev, double *x_dev,
+                 mx_ksp_result *res, double *history_host /* NULL or max_it+2 */);
+void mx_ksp_default_params(mx_ksp_params *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,388 @@
+// mx_abi.hip -- extern "C" entry points of libmxsolve.so (declared in include/mxsolve.h).
+// Every call: set the handle's device, run, translate exceptions to an error
+// code + thread-local message.  No torch types cross this boundary.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "mx_internal.hpp"
+
+struct mx_comm_s { mx::Comm *c; };
+struct mx_mat_s { mx::Mat *A; };
+
+namespace mx {
+
+static thread_local std::string g_err;
+
+[[noreturn]] void fail(int code, const std::string &msg) { throw Error(code, msg); }
+
+void hip_check(hipError_t e, const char *what, const char *file, int line) {
+  if (e != hipSuccess) {
+    char buf[512];
+    std::snprintf(buf, sizeof buf, "%s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+    fail(e == hipErrorOutOfMemory ? MX_ERR_MEM : MX_ERR_HIP, buf);
+  }
+}
+
+template <class F> static int guard(F &&f) {
+  try {
+    f();
+    return MX_OK;
+  } catch (const Error &e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    g_err = "host allocation failed";
+    return MX_ERR_MEM;
+  } catch (const std::exception &e) {
+    g_err = e.what();
+    return MX_ERR_INTERNAL;
+  }
+}
+
+static Comm *C(mx_comm c) {
+  if (!c || !c->c) fail(MX_ERR_ARG, "null communicator");
+  HIPCHECK(hipSetDevice(c->c->device));
+  return c->c;
+}
+static Mat *M(mx_mat a) {
+  if (!a || !a->A) fail(MX_ERR_ARG, "null matrix");
+  HIPCHECK(hipSetDevice(a->A->comm->device));
+  return a->A;
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+extern "C" {
+
+int mx_version(void) { return MX_ABI_VERSION; }
+
+int mx_last_error(char *buf, size_t len) {
+  if (buf && len) {
+    std::strncpy(buf, g_err.c_str(), len - 1);
+    buf[len - 1] = 0;
+  }
+  return (int)g_err.size();
+}
+
+int mx_get_unique_id(void *out, size_t len) { return guard([&] { get_unique_id(out, len); }); }
+
+int mx_comm_create_rccl(int rank, int size, int device, const void *uid, size_t uid_len, mx_comm *out) {
+  return guard([&] {
+    if (size < 1 || rank < 0 || rank >= size) fail(MX_ERR_ARG, "bad rank/size");
+    *out = new mx_comm_s{make_rccl_comm(rank, size, device, uid, uid_len)};
+  });
+}
+
+int mx_comm_create_self(int device, mx_comm *out) {
+  return guard([&] { *out = new mx_comm_s{make_self_comm(device)}; });
+}
+
+int mx_world_create_local(int size, void **world) { return guard([&] { *world = make_local_world(size); }); }
+
+int mx_comm_create_local(void *world, int rank, int device, mx_comm *out) {
+  return guard([&] { *out = new mx_comm_s{make_local_comm(world, rank, device)}; });
+}
+
+int mx_world_destroy(void *world) { return guard([&] { destroy_local_world(world); }); }
+
+int mx_comm_destroy(mx_comm c) {
+  return guard([&] {
+    if (!c) return;
+    if (c->c) { (void)hipSetDevice(c->c->device); delete c->c; }
+    delete c;
+  });
+}
+
+int mx_comm_info(mx_comm c, int *rank, int *size, int *device) {
+  return guard([&] {
+    Comm *k = C(c);
+    if (rank) *rank = k->rank;
+    if (size) *size = k->size;
+    if (device) *device = k->device;
+  });
+}
+
+int mx_comm_stream(mx_comm c, void **stream) { return guard([&] { *stream = (void *)C(c)->stream; }); }
+
+int mx_comm_barrier(mx_comm c) { return guard([&] { C(c)->barrier(); }); }
+
+int mx_layout_split(int64_t N, int P, int64_t *ranges) {
+  return guard([&] {
+    if (P < 1 || N < 0) fail(MX_ERR_ARG, "bad layout");
+    const int64_t q = N / P, r = N % P;
+    ranges[0] = 0;
+    for (int i = 0; i < P; ++i) ranges[i + 1] = ranges[i] + q + (i < r ? 1 : 0);
+  });
+}
+
+int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_t n_local,
+                      const void *indptr, int indptr_bytes, const void *cols, int col_bytes,
+                      const double *vals, int64_t nnz, int insert_mode, int src_is_device, mx_mat *A) {
+  return guard([&] {
+    Comm *k = C(c);
+    if (Mg < 0 || Ng < 0) fail(MX_ERR_ARG, "negative global size");
+    if ((indptr_bytes != 4 && indptr_bytes != 8) || (col_bytes != 4 && col_bytes != 8))
+      fail(MX_ERR_ARG, "index width must be 4 or 8 bytes");
+    // local row count for the argument checks (the same split assemble() uses)
+    int64_t m = m_local;
+    if (m < 0) { const int64_t q = Mg / k->size, r = Mg % k->size; m = q + (k->rank < r ? 1 : 0); }
+    hipStream_t st = k->stream;
+    DBuf<int64_t> ip((size_t)m + 1), cl((size_t)(nnz > 0 ? nnz : 1));
+    DBuf<double> vl((size_t)(nnz > 0 ? nnz : 1));
+    // host-side copies of the two scalars petsc4py checks
+    int64_t first = 0, last = 0;
+    if (src_is_device) {
+      convert_index(indptr, indptr_bytes, m + 1, ip.p, st);
+      HIPCHECK(hipMemcpyAsync(&first, ip.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(&last, ip.p + m, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+    } else {
+      auto rd = [&](int64_t i) -> int64_t {
+        return indptr_bytes == 8 ? static_cast<const int64_t *>(indptr)[i] : static_cast<const int32_t *>(indptr)[i];
+      };
+      first = rd(0);
+      last = rd(m);
+    }
+    if (first != 0) fail(MX_ERR_ARG, "I[0] is " + std::to_string(first) + ", expected 0");
+    if (last != nnz) fail(MX_ERR_ARG, "size(J) is " + std::to_string(nnz) + ", expected " + std::to_string(last));
+    if (!src_is_device) {
+      DBuf<char> stage((size_t)std::max<int64_t>((m + 1) * indptr_bytes, nnz * col_bytes) + 8);
+      HIPCHECK(hipMemcpyAsync(stage.p, indptr, (size_t)(m + 1) * indptr_bytes, hipMemcpyHostToDevice, st));
+      convert_index(stage.p, indptr_bytes, m + 1, ip.p, st);
+      HIPCHECK(hipStreamSynchronize(st));
+      if (nnz) {
+        HIPCHECK(hipMemcpyAsync(stage.p, cols, (size_t)nnz * col_bytes, hipMemcpyHostToDevice, st));
+        convert_index(stage.p, col_bytes, nnz, cl.p, st);
+        HIPCHECK(hipMemcpyAsync(vl.p, vals, sizeof(double) * nnz, hipMemcpyHostToDevice, st));
+      }
+      HIPCHECK(hipStreamSynchronize(st));
+    } else if (nnz) {
+      convert_index(cols, col_bytes, nnz, cl.p, st);
+      HIPCHECK(hipMemcpyAsync(vl.p, vals, sizeof(double) * nnz, hipMemcpyDeviceToDevice, st));
+    }
+    AssemblyInput in;
+    in.rowptr = ip.p; in.cols = cl.p; in.vals = vl.p; in.nnz = nnz;
+    in.insert_mode = insert_mode;
+    *A = new mx_mat_s{assemble(k, Mg, Ng, m_local, n_local, in)};
+  });
+}
+
+int mx_mat_create_coo(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_t n_local,
+                      const int64_t *rows, const int64_t *cols, const double *vals, int64_t n,
+                      int insert_mode, int src_is_device, mx_mat *A) {
+  return guard([&] {
+    Comm *k = C(c);
+    hipStream_t st = k->stream;
+    const size_t cnt = (size_t)(n > 0 ? n : 1);
+    DBuf<int64_t> r(cnt), cl(cnt);
+    DBuf<double> v(cnt);
+    if (n) {
+      const hipMemcpyKind kind = src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+      HIPCHECK(hipMemcpyAsync(r.p, rows, sizeof(int64_t) * n, kind, st));
+      HIPCHECK(hipMemcpyAsync(cl.p, cols, sizeof(int64_t) * n, kind, st));
+      HIPCHECK(hipMemcpyAsync(v.p, vals, sizeof(double) * n, kind, st));
+    }
+    AssemblyInput in;
+    in.coo_rows = r.p; in.cols = cl.p; in.vals = v.p; in.nnz = n; in.insert_mode = insert_mode;
+    *A = new mx_mat_s{assemble(k, Mg, Ng, m_local, n_local, in)};
+  });
+}
+
+int mx_mat_create_stencil(mx_comm c, int kind, int64_t nx, int64_t ny, int64_t nz, mx_mat *A) {
+  return guard([&] {
+    Comm *k = C(c);
+    if (kind < 0 || kind > 3 || nx < 1 || ny < 1 || nz < 1) fail(MX_ERR_ARG, "bad stencil");
+    const int64_t Mg = kind == 0 ? nx * ny : nx * ny * nz;
+    const int64_t q = Mg / k->size, r = Mg % k->size;
+    int64_t row0 = 0;
+    for (int i = 0; i < k->rank; ++i) row0 += q + (i < r ? 1 : 0);
+    const int64_t m = q + (k->rank < r ? 1 : 0);
+    DBuf<int64_t> rp, cl;
+    DBuf<double> vl;
+    stencil_coo(k, kind, nx, ny, nz, row0, m, rp, cl, vl);
+    AssemblyInput in;
+    in.rowptr = rp.p; in.cols = cl.p; in.vals = vl.p;
+    in.nnz = m * (kind == 0 ? 5 : (kind == 2 ? 27 : 7));
+    in.insert_mode = MX_INSERT_VALUES;
+    *A = new mx_mat_s{assemble(k, Mg, Mg, -1, -1, in)};
+  });
+}
+
+int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
+  return guard([&] {
+    Mat *A = M(a);
+    std::memset(info, 0, sizeof(*info));
+    info->M = A->M; info->N = A->N; info->m = A->m; info->n = A->n;
+    info->rstart = A->rstart; info->cstart = A->cstart;
+    info->nnz_d = A->nnz_d; info->nnz_o = A->nnz_o; info->nghost = A->nghost;
+    info->sell_slots_d = A->sd.slots; info->sell_slots_o = A->so.slots;
+    info->nsend_peers = (int)A->halo.send_peer.size();
+    info->nrecv_peers = (int)A->halo.recv_peer.size();
+    info->nsend = A->halo.nsend; info->nrecv = A->halo.nrecv;
+  });
+}
+
+int mx_mat_get_split(mx_mat a, int64_t *dptr, int32_t *dcol, double *dval, int64_t *optr,
+                     int32_t *ocol, double *oval, int64_t *garray) {
+  return guard([&] {
+    Mat *A = M(a);
+    hipStream_t st = A->comm->stream;
+    auto d2h = [&](void *dst, const void *src, size_t bytes) {
+      if (dst && bytes) HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    };
+    d2h(dptr, A->dptr.p, sizeof(int64_t) * (A->m + 1));
+    d2h(optr, A->optr.p, sizeof(int64_t) * (A->m + 1));
+    d2h(dcol, A->dcol.p, sizeof(int32_t) * A->nnz_d);
+    d2h(dval, A->dval.p, sizeof(double) * A->nnz_d);
+    d2h(ocol, A->ocol.p, sizeof(int32_t) * A->nnz_o);
+    d2h(oval, A->oval.p, sizeof(double) * A->nnz_o);
+    d2h(garray, A->garray.p, sizeof(int64_t) * A->nghost);
+    HIPCHECK(hipStreamSynchronize(st));
+  });
+}
+
+int mx_mat_get_csr(mx_mat a, int64_t *indptr, int64_t *cols, double *vals) {
+  return guard([&] {
+    Mat *A = M(a);
+    const int64_t m = A->m;
+    std::vector<int64_t> dp(m + 1), op(m + 1), g(A->garray_h);
+    std::vector<int32_t> dc(A->nnz_d), oc(A->nnz_o);
+    std::vector<double> dv(A->nnz_d), ov(A->nnz_o);
+    hipStream_t st = A->comm->stream;
+    HIPCHECK(hipMemcpyAsync(dp.data(), A->dptr.p, sizeof(int64_t) * (m + 1), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpyAsync(op.data(), A->optr.p, sizeof(int64_t) * (m + 1), hipMemcpyDeviceToHost, st));
+    if (A->nnz_d) {
+      HIPCHECK(hipMemcpyAsync(dc.data(), A->dcol.p, sizeof(int32_t) * A->nnz_d, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(dv.data(), A->dval.p, sizeof(double) * A->nnz_d, hipMemcpyDeviceToHost, st));
+    }
+    if (A->nnz_o) {
+      HIPCHECK(hipMemcpyAsync(oc.data(), A->ocol.p, sizeof(int32_t) * A->nnz_o, hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipMemcpyAsync(ov.data(), A->oval.p, sizeof(double) * A->nnz_o, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHECK(hipStreamSynchronize(st));
+    // MatGetRow_MPIAIJ merge: ghosts left of cstart, diagonal block, ghosts right
+    int64_t p = 0;
+    indptr[0] = 0;
+    for (int64_t i = 0; i < m; ++i) {
+      int64_t o = op[i];
+      const int64_t oe = op[i + 1];
+      for (; o < oe && g[oc[o]] < A->cstart; ++o) { cols[p] = g[oc[o]]; vals[p++] = ov[o]; }
+      for (int64_t d = dp[i]; d < dp[i + 1]; ++d) { cols[p] = dc[d] + A->cstart; vals[p++] = dv[d]; }
+      for (; o < oe; ++o) { cols[p] = g[oc[o]]; vals[p++] = ov[o]; }
+      indptr[i + 1] = p;
+    }
+  });
+}
+
+int mx_mat_mult(mx_mat a, const double *x, double *y) {
+  return guard([&] {
+    Mat *A = M(a);
+    mat_mult(A, x, y);
+    HIPCHECK(hipStreamSynchronize(A->comm->stream));
+  });
+}
+
+int mx_mat_get_diagonal(mx_mat a, double *d) {
+  return guard([&] {
+    Mat *A = M(a);
+    if (A->m) HIPCHECK(hipMemcpyAsync(d, A->diag.p, sizeof(double) * A->m, hipMemcpyDeviceToDevice, A->comm->stream));
+    HIPCHECK(hipStreamSynchronize(A->comm->stream));
+  });
+}
+
+int mx_mat_bench_mult(mx_mat a, const double *x, double *y, int iters, double *spmv_ms, double *mult_ms) {
+  return guard([&] {
+    Mat *A = M(a);
+    hipStream_t st = A->comm->stream;
+    if (iters < 1) fail(MX_ERR_ARG, "iters must be positive");
+    std::vector<hipEvent_t> ev(2 * (size_t)iters + 2);
+    for (auto &e : ev) HIPCHECK(hipEventCreate(&e));
+    mat_mult(A, x, y);  // warm
+    HIPCHECK(hipEventRecord(ev[0], st));
+    for (int k = 0; k < iters; ++k) {
+      halo_begin(A, x);
+      HIPCHECK(hipEventRecord(ev[2 + 2 * k], st));
+      spmv_launch(A, x, y, SPMV_PLAIN, nullptr, nullptr, nullptr);
+      HIPCHECK(hipEventRecord(ev[3 + 2 * k], st));
+    }
+    HIPCHECK(hipEventRecord(ev[1], st));
+    HIPCHECK(hipEventSynchronize(ev[1]));
+    double s = 0.0;
+    for (int k = 0; k < iters; ++k) {
+      float t = 0.f;
+      HIPCHECK(hipEventElapsedTime(&t, ev[2 + 2 * k], ev[3 + 2 * k]));
+      s += t;
+    }
+    float tot = 0.f;
+    HIPCHECK(hipEventElapsedTime(&tot, ev[0], ev[1]));
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    if (spmv_ms) *spmv_ms = s / iters;
+    if (mult_ms) *mult_ms = (double)tot / iters;
+  });
+}
+
+int mx_mat_destroy(mx_mat a) {
+  return guard([&] {
+    if (!a) return;
+    if (a->A) {
+      (void)hipSetDevice(a->A->comm->device);
+      (void)hipStreamSynchronize(a->A->comm->stream);
+      delete a->A;
+    }
+    delete a;
+  });
+}
+
+int mx_vec_dot(mx_comm c, int64_t n, const double *x, const double *y, double *out) {
+  return guard([&] { *out = host_dot(C(c), n, x, y); });
+}
+int mx_vec_norm2(mx_comm c, int64_t n, const double *x, double *out) {
+  return guard([&] { *out = std::sqrt(host_dot(C(c), n, x, x)); });
+}
+int mx_vec_axpy(mx_comm c, int64_t n, double a, const double *x, double *y) {
+  return guard([&] { Comm *k = C(c); vec_axpy(k->stream, n, a, x, y); HIPCHECK(hipStreamSynchronize(k->stream)); });
+}
+int mx_vec_aypx(mx_comm c, int64_t n, double a, const double *x, double *y) {
+  return guard([&] { Comm *k = C(c); vec_aypx(k->stream, n, a, x, y); HIPCHECK(hipStreamSynchronize(k->stream)); });
+}
+int mx_vec_pointwise_mult(mx_comm c, int64_t n, const double *x, const double *y, double *w) {
+  return guard([&] { Comm *k = C(c); vec_pmult(k->stream, n, x, y, w); HIPCHECK(hipStreamSynchronize(k->stream)); });
+}
+int mx_vec_scale(mx_comm c, int64_t n, double a, double *x) {
+  return guard([&] { Comm *k = C(c); vec_scale(k->stream, n, a, x); HIPCHECK(hipStreamSynchronize(k->stream)); });
+}
+int mx_vec_set(mx_comm c, int64_t n, double a, double *x) {
+  return guard([&] { Comm *k = C(c); vec_set(k->stream, n, a, x); HIPCHECK(hipStreamSynchronize(k->stream)); });
+}
+int mx_vec_rhs_hash(mx_comm c, int64_t i0, int64_t n, double *b) {
+  return guard([&] { Comm *k = C(c); vec_rhs_hash(k->stream, i0, n, b); HIPCHECK(hipStreamSynchronize(k->stream)); });
+}
+
+void mx_ksp_default_params(mx_ksp_params *p) {
+  std::memset(p, 0, sizeof(*p));
+  p->ksp_type = MX_KSP_GMRES;   // PETSc's default KSP
+  p->pc_type = MX_PC_JACOBI;
+  p->norm_type = MX_NORM_DEFAULT;
+  p->max_it = 10000;
+  p->restart = 30;
+  p->rtol = 1e-5;
+  p->atol = 1e-50;
+  p->dtol = 1e5;
+  p->haptol = 1e-30;
+  p->breakdowntol = 0.1;
+  p->poll_every = 16;
+}
+
+int mx_ksp_solve(mx_mat a, const mx_ksp_params *p, const double *b, double *x, mx_ksp_result *res,
+                 double *history) {
+  return guard([&] {
+    Mat *A = M(a);
+    ksp_solve(A, *p, b, x, *res, history);
+  });
+}
+
+}  // extern "C"

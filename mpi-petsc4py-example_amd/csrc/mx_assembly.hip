@@ -1,0 +1,647 @@
+// mx_assembly.hip -- device-side AIJ assembly (gfx950).
+//
+// Replaces what PETSc does behind PETSc.Mat().createAIJ(csr=...) + assemble()
+// (petsc_funcs.py:6-7, test.py:24-28): MatMPIAIJSetPreallocationCSR ->
+// MatSetValues(INSERT) row by row -> MatAssemblyEnd -> MatSetUpMultiply_MPIAIJ
+// (SURVEY.md §2 N1-N3).  Semantics restated in oracle/petsc_oracle.c
+// (canon_row, build_block):
+//   * per row, columns end up sorted; negative columns are ignored;
+//   * a repeated column keeps the LAST value (INSERT) or the values added in
+//     input order (ADD: first stored, later ones added);
+//   * explicit zeros are kept; column >= N is an out-of-range error;
+//   * the row block splits into A_d (columns owned by this rank, stored as
+//     local column ids) and A_o (other columns, renumbered into [0, nghost) in
+//     ascending global order = garray).
+//
+// Device pipeline (all on the communicator's stream):
+//   [COO: row histogram -> scan -> scatter with the input position kept]
+//   canonicalise rows: W-lane segments (W = 8..64) bitonic-sort (col, pos)
+//     pairs in registers with xor shuffles, then a segmented last-wins /
+//     ordered-fold dedupe with ballot compaction; rows longer than 64 go to a
+//     block-per-row LDS bitonic sort (<= 2048 entries);
+//   split + ghost bitmap (atomicOr) -> scans -> bitmap popcount-scan gives
+//     garray and the A_o renumbering without any sort;
+//   SELL-64 copies of A_d and A_o for the SpMV;
+//   halo plan: garray owners from the column layout, one count all-to-all,
+//     requested indices sent to their owners, contiguous send ranges detected.
+#include <algorithm>
+#include <climits>
+
+#include "mx_internal.hpp"
+
+namespace mx {
+
+constexpr int64_t KEY_DROP = LLONG_MAX;
+constexpr int LONG_ROW_MAX = 2048;
+
+// ---------------------------------------------------------------- helpers
+__global__ void cvt_i32_i64_kernel(const int32_t *__restrict__ s, int64_t n, int64_t *__restrict__ d) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) d[i] = s[i];
+}
+
+void convert_index(const void *src, int bytes, int64_t n, int64_t *dst, hipStream_t s) {
+  if (n <= 0) return;
+  if (bytes == 8) {
+    HIPCHECK(hipMemcpyAsync(dst, src, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, s));
+  } else if (bytes == 4) {
+    cvt_i32_i64_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(static_cast<const int32_t *>(src), n, dst);
+    HIPCHECK(hipGetLastError());
+  } else {
+    fail(MX_ERR_ARG, "index width must be 4 or 8 bytes");
+  }
+}
+
+__global__ void row_len_max_kernel(int64_t m, const int64_t *__restrict__ rowptr,
+                                   unsigned long long *__restrict__ out, int *__restrict__ err) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long mx = 0;
+  if (i < m) {
+    int64_t len = rowptr[i + 1] - rowptr[i];
+    if (len < 0) atomicOr(err, 4);
+    else mx = (unsigned long long)len;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long t = __shfl_xor(mx, o, 64);
+    mx = t > mx ? t : mx;
+  }
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(out, mx);
+}
+
+// ---------------------------------------------------------------- COO bucketing
+__global__ void coo_count_kernel(int64_t n, const int64_t *__restrict__ rows,
+                                 const int64_t *__restrict__ cols, int64_t rstart, int64_t m,
+                                 unsigned long long *__restrict__ cnt, int *__restrict__ err) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    int64_t r = rows[k];
+    if (r < 0 || cols[k] < 0) continue;                 // MatSetValues ignores negative indices
+    if (r < rstart || r >= rstart + m) { atomicOr(err, 8); continue; }
+    atomicAdd(&cnt[r - rstart], 1ULL);
+  }
+}
+
+__global__ void coo_scatter_kernel(int64_t n, const int64_t *__restrict__ rows,
+                                   const int64_t *__restrict__ cols, const double *__restrict__ vals,
+                                   int64_t rstart, int64_t m, const int64_t *__restrict__ rowptr,
+                                   unsigned long long *__restrict__ cursor, int64_t *__restrict__ gcol,
+                                   double *__restrict__ gval, int64_t *__restrict__ gpos) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    int64_t r = rows[k];
+    if (r < 0 || cols[k] < 0 || r < rstart || r >= rstart + m) continue;
+    int64_t i = r - rstart;
+    int64_t slot = rowptr[i] + (int64_t)atomicAdd(&cursor[i], 1ULL);
+    gcol[slot] = cols[k]; gval[slot] = vals[k]; gpos[slot] = k;   // k restores input order
+  }
+}
+
+// ---------------------------------------------------------------- row canonicalisation
+// One W-lane segment per row (W | 64).  Keys (col, pos) are unique per row
+// except the dropped/padding lanes, which all carry (KEY_DROP, KEY_DROP).
+template <int W>
+__global__ void __launch_bounds__(256) canon_rows_wave_kernel(
+    int64_t m, const int64_t *__restrict__ rowptr, const int64_t *__restrict__ col,
+    const double *__restrict__ val, const int64_t *__restrict__ pos, int64_t N, int add,
+    int64_t *__restrict__ ccol, double *__restrict__ cval, int64_t *__restrict__ cnt_out,
+    int64_t *__restrict__ long_rows, unsigned long long *__restrict__ nlong, int *__restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int l = lane % W;
+  const int64_t row = (int64_t)blockIdx.x * (256 / W) + threadIdx.x / W;
+  const bool rvalid = row < m;
+  const int64_t start = rvalid ? rowptr[row] : 0;
+  const int64_t len = rvalid ? rowptr[row + 1] - start : 0;
+  const bool too_long = len > W;
+  if (rvalid && too_long && l == 0) long_rows[atomicAdd(nlong, 1ULL)] = row;
+  const bool active = rvalid && !too_long;
+
+  int64_t c = KEY_DROP, p = KEY_DROP;
+  double v = 0.0;
+  if (active && l < len) {
+    int64_t cc = col[start + l];
+    if (cc >= 0) {
+      if (cc >= N) atomicOr(err, 1);
+      c = cc;
+      p = pos ? pos[start + l] : (int64_t)l;
+      v = val[start + l];
+    }
+  }
+  // bitonic sort of (c, p) ascending inside each W-lane segment
+#pragma unroll
+  for (int k = 2; k <= W; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      int64_t c2 = __shfl_xor(c, j, 64);
+      int64_t p2 = __shfl_xor(p, j, 64);
+      double v2 = __shfl_xor(v, j, 64);
+      const bool up = (l & k) == 0;
+      const bool lower = (l & j) == 0;
+      const bool mine_less = (c < c2) || (c == c2 && p < p2);
+      const bool keep = (lower == up) ? mine_less : !mine_less;
+      if (!keep) { c = c2; p = p2; v = v2; }
+    }
+  }
+  const bool valid = c != KEY_DROP;
+  const int64_t c_next = __shfl(c, (lane + 1) & 63, 64);
+  const int64_t c_prev = __shfl(c, (lane + 63) & 63, 64);
+  bool keep;
+  double out = v;
+  if (!add) {
+    keep = valid && (l == W - 1 || c_next != c);       // INSERT: last occurrence wins
+  } else {
+    keep = valid && (l == 0 || c_prev != c);           // ADD: run head folds its run in order
+    bool run = true;
+#pragma unroll
+    for (int t = 1; t < W; ++t) {
+      const double vt = __shfl(v, (lane + t) & 63, 64);
+      const int64_t ct = __shfl(c, (lane + t) & 63, 64);
+      run = run && (l + t < W) && (ct == c);
+      if (run) out = out + vt;
+    }
+  }
+  const unsigned long long ball = __ballot(keep);
+  const int gbase = lane - l;
+  const unsigned long long gmask =
+      (W == 64) ? ball : ((ball >> gbase) & ((1ULL << (W == 64 ? 0 : W)) - 1ULL));
+  const int idx = __popcll(gmask & ((l == 0) ? 0ULL : ((1ULL << l) - 1ULL)));
+  if (active) {
+    if (keep) { ccol[start + idx] = c; cval[start + idx] = out; }
+    if (l == 0) cnt_out[row] = __popcll(gmask);
+  }
+}
+
+// Rows longer than 64 entries: one block per row, LDS bitonic sort, then a
+// sequential (exactly ordered) dedupe by one thread.
+__global__ void __launch_bounds__(256) canon_rows_block_kernel(
+    const int64_t *__restrict__ rows_list, const int64_t *__restrict__ rowptr,
+    const int64_t *__restrict__ col, const double *__restrict__ val,
+    const int64_t *__restrict__ pos, int64_t N, int add, int64_t *__restrict__ ccol,
+    double *__restrict__ cval, int64_t *__restrict__ cnt_out, int *__restrict__ err) {
+  __shared__ int64_t kc[LONG_ROW_MAX];
+  __shared__ int64_t kp[LONG_ROW_MAX];
+  __shared__ double kv[LONG_ROW_MAX];
+  const int64_t row = rows_list[blockIdx.x];
+  const int64_t start = rowptr[row];
+  const int64_t len = rowptr[row + 1] - start;
+  if (len > LONG_ROW_MAX) {
+    if (threadIdx.x == 0) atomicOr(err, 2);
+    return;
+  }
+  int npad = 1;
+  while (npad < len) npad <<= 1;
+  for (int i = threadIdx.x; i < npad; i += 256) {
+    int64_t c = KEY_DROP, p = KEY_DROP;
+    double v = 0.0;
+    if (i < len) {
+      int64_t cc = col[start + i];
+      if (cc >= 0) {
+        if (cc >= N) atomicOr(err, 1);
+        c = cc; p = pos ? pos[start + i] : (int64_t)i; v = val[start + i];
+      }
+    }
+    kc[i] = c; kp[i] = p; kv[i] = v;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npad; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < npad; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const bool greater = (kc[i] > kc[ixj]) || (kc[i] == kc[ixj] && kp[i] > kp[ixj]);
+          if (greater == up) {
+            int64_t tc = kc[i]; kc[i] = kc[ixj]; kc[ixj] = tc;
+            int64_t tp = kp[i]; kp[i] = kp[ixj]; kp[ixj] = tp;
+            double tv = kv[i]; kv[i] = kv[ixj]; kv[ixj] = tv;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    int64_t k = 0;
+    for (int64_t i = 0; i < len && kc[i] != KEY_DROP; ++i) {
+      if (k > 0 && ccol[start + k - 1] == kc[i]) {
+        if (add) cval[start + k - 1] = cval[start + k - 1] + kv[i];
+        else cval[start + k - 1] = kv[i];
+      } else {
+        ccol[start + k] = kc[i]; cval[start + k] = kv[i]; ++k;
+      }
+    }
+    cnt_out[row] = k;
+  }
+}
+
+// ---------------------------------------------------------------- split
+__global__ void split_count_kernel(int64_t m, const int64_t *__restrict__ rowptr,
+                                   const int64_t *__restrict__ cnt, const int64_t *__restrict__ ccol,
+                                   int64_t cstart, int64_t cend, int64_t *__restrict__ cnt_d,
+                                   int64_t *__restrict__ cnt_o, unsigned *__restrict__ bitmap) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int64_t s = rowptr[i], n = cnt[i];
+  int64_t d = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t c = ccol[s + j];
+    if (c >= cstart && c < cend) d++;
+    else atomicOr(&bitmap[c >> 5], 1u << (c & 31));
+  }
+  cnt_d[i] = d;
+  cnt_o[i] = n - d;
+}
+
+__global__ void popc_kernel(int64_t nw, const unsigned *__restrict__ bitmap, int64_t *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) out[w] = __popc(bitmap[w]);
+}
+
+__global__ void garray_kernel(int64_t nw, const unsigned *__restrict__ bitmap,
+                              const int64_t *__restrict__ wbase, int64_t *__restrict__ garray) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+    unsigned b = bitmap[w];
+    int64_t k = wbase[w];
+    while (b) {
+      int bit = __ffs(b) - 1;
+      garray[k++] = (w << 5) + bit;
+      b &= b - 1;
+    }
+  }
+}
+
+__global__ void fill_split_kernel(int64_t m, const int64_t *__restrict__ rowptr,
+                                  const int64_t *__restrict__ cnt, const int64_t *__restrict__ ccol,
+                                  const double *__restrict__ cval, int64_t cstart, int64_t cend,
+                                  int64_t rstart, const int64_t *__restrict__ dptr,
+                                  const int64_t *__restrict__ optr, int32_t *__restrict__ dcol,
+                                  double *__restrict__ dval, int32_t *__restrict__ ocol,
+                                  double *__restrict__ oval, double *__restrict__ diag,
+                                  const unsigned *__restrict__ bitmap,
+                                  const int64_t *__restrict__ wbase) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int64_t s = rowptr[i], n = cnt[i];
+  int64_t pd = dptr[i], po = optr[i];
+  double dg = 0.0;
+  const int64_t grow = rstart + i;
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t c = ccol[s + j];
+    const double v = cval[s + j];
+    if (c >= cstart && c < cend) {
+      dcol[pd] = (int32_t)(c - cstart); dval[pd++] = v;
+      if (c == grow) dg = v;
+    } else {
+      const int64_t w = c >> 5;
+      const unsigned b = (unsigned)(c & 31);
+      ocol[po] = (int32_t)(wbase[w] + __popc(bitmap[w] & ((1u << b) - 1u)));
+      oval[po++] = v;
+    }
+  }
+  diag[i] = dg;
+}
+
+// ---------------------------------------------------------------- SELL-64
+__global__ void sell_width_kernel(int64_t m, const int64_t *__restrict__ ptr, int64_t nslices,
+                                  int32_t *__restrict__ width, int64_t *__restrict__ slots) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t row = s * SLICE + lane;
+  int len = 0;
+  if (s < nslices && row < m) len = (int)(ptr[row + 1] - ptr[row]);
+  for (int o = 32; o > 0; o >>= 1) len = max(len, __shfl_xor(len, o, 64));
+  if (s < nslices && lane == 0) { width[s] = len; slots[s] = (int64_t)len * SLICE; }
+}
+
+__global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
+                                 const int32_t *__restrict__ ccol, const double *__restrict__ cval,
+                                 int64_t nslices, const int64_t *__restrict__ sptr,
+                                 const int32_t *__restrict__ width, int32_t *__restrict__ scol,
+                                 double *__restrict__ sval) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = s * SLICE + lane;
+  const int w = width[s];
+  const int64_t base = sptr[s] + lane;
+  const int64_t rs = row < m ? ptr[row] : 0;
+  const int len = row < m ? (int)(ptr[row + 1] - rs) : 0;
+  for (int j = 0; j < w; ++j) {
+    const bool in = j < len;
+    scol[base + (int64_t)j * SLICE] = in ? ccol[rs + j] : -1;
+    sval[base + (int64_t)j * SLICE] = in ? cval[rs + j] : 0.0;
+  }
+}
+
+static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *col, const double *val,
+                       hipStream_t st) {
+  S.nslices = cdiv(m, SLICE);
+  const int64_t ns = S.nslices;
+  S.width.alloc((size_t)std::max<int64_t>(ns, 1));
+  S.sptr.alloc((size_t)std::max<int64_t>(ns, 1));
+  if (ns == 0) { S.slots = 0; return; }
+  sell_width_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, ns, S.width.p, S.sptr.p);
+  HIPCHECK(hipGetLastError());
+  exclusive_scan_i64(S.sptr.p, S.sptr.p, ns, st, &S.slots);
+  S.col.alloc((size_t)std::max<int64_t>(S.slots, 1));
+  S.val.alloc((size_t)std::max<int64_t>(S.slots, 1));
+  sell_fill_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
+                                                          S.col.p, S.val.p);
+  HIPCHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- halo plan
+static void build_halo(Mat *A) {
+  Comm *c = A->comm;
+  const int P = c->size;
+  Halo &H = A->halo;
+  std::vector<int64_t> want(P, 0), give(P, 0);
+  // ghosts grouped by owning rank of the COLUMN layout (garray is sorted)
+  std::vector<int64_t> off(P + 1, 0);
+  {
+    int q = 0;
+    for (int64_t k = 0; k < A->nghost; ++k) {
+      const int64_t g = A->garray_h[k];
+      while (g >= A->cranges[q + 1]) ++q;
+      want[q]++;
+    }
+    for (int q2 = 0; q2 < P; ++q2) off[q2 + 1] = off[q2] + want[q2];
+  }
+  if (want[c->rank] != 0) fail(MX_ERR_INTERNAL, "ghost owned by self");
+  c->alltoall_i64(want.data(), give.data());
+  std::vector<int32_t> req_h((size_t)std::max<int64_t>(A->nghost, 1));
+  for (int q = 0; q < P; ++q)
+    for (int64_t k = off[q]; k < off[q + 1]; ++k) req_h[k] = (int32_t)(A->garray_h[k] - A->cranges[q]);
+  H.nrecv = A->nghost;
+  H.nsend = 0;
+  for (int q = 0; q < P; ++q) {
+    if (want[q]) { H.recv_peer.push_back(q); H.recv_off.push_back(off[q]); H.recv_cnt.push_back(want[q]); }
+    if (give[q]) { H.send_peer.push_back(q); H.send_off.push_back(H.nsend); H.send_cnt.push_back(give[q]); H.nsend += give[q]; }
+  }
+  DBuf<int32_t> req((size_t)std::max<int64_t>(A->nghost, 1));
+  H.send_idx.alloc((size_t)std::max<int64_t>(H.nsend, 1));
+  H.send_buf.alloc((size_t)std::max<int64_t>(H.nsend, 1));
+  H.lvec.alloc((size_t)std::max<int64_t>(A->nghost, 1));
+  if (A->nghost) HIPCHECK(hipMemcpyAsync(req.p, req_h.data(), sizeof(int32_t) * A->nghost, hipMemcpyHostToDevice, c->stream));
+  std::vector<Msg> sends, recvs;
+  for (size_t i = 0; i < H.recv_peer.size(); ++i)
+    sends.push_back({H.recv_peer[i], req.p + H.recv_off[i], sizeof(int32_t) * (size_t)H.recv_cnt[i]});
+  for (size_t i = 0; i < H.send_peer.size(); ++i)
+    recvs.push_back({H.send_peer[i], H.send_idx.p + H.send_off[i], sizeof(int32_t) * (size_t)H.send_cnt[i]});
+  c->exchange(sends, recvs);
+  std::vector<int32_t> sidx((size_t)std::max<int64_t>(H.nsend, 1));
+  if (H.nsend) HIPCHECK(hipMemcpyAsync(sidx.data(), H.send_idx.p, sizeof(int32_t) * H.nsend, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  H.need_pack = false;
+  for (size_t i = 0; i < H.send_peer.size(); ++i) {
+    const int32_t *s = sidx.data() + H.send_off[i];
+    bool contig = true;
+    for (int64_t k = 1; k < H.send_cnt[i]; ++k) if (s[k] != s[0] + k) { contig = false; break; }
+    H.send_contig_start.push_back(contig ? s[0] : -1);
+    if (!contig) H.need_pack = true;
+  }
+}
+
+// ---------------------------------------------------------------- driver
+static void layout(Comm *c, int64_t G, int64_t local, std::vector<int64_t> &ranges) {
+  const int P = c->size;
+  ranges.assign(P + 1, 0);
+  if (local < 0) {
+    const int64_t q = G / P, r = G % P;
+    for (int i = 0; i < P; ++i) ranges[i + 1] = ranges[i] + q + (i < r ? 1 : 0);
+  } else {
+    std::vector<int64_t> all(P);
+    c->allgather_i64(local, all.data());
+    for (int i = 0; i < P; ++i) ranges[i + 1] = ranges[i] + all[i];
+    if (ranges[P] != G)
+      fail(MX_ERR_ARG, "Sum of local lengths " + std::to_string(ranges[P]) +
+                           " does not equal global length " + std::to_string(G));
+  }
+}
+
+Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
+              const AssemblyInput &in) {
+  hipStream_t st = c->stream;
+  std::unique_ptr<Mat> A(new Mat());
+  A->comm = c;
+  A->M = M; A->N = N;
+  layout(c, M, m_local, A->rranges);
+  layout(c, N, n_local, A->cranges);
+  A->rstart = A->rranges[c->rank];
+  A->m = A->rranges[c->rank + 1] - A->rstart;
+  A->cstart = A->cranges[c->rank];
+  A->cend = A->cranges[c->rank + 1];
+  A->n = A->cend - A->cstart;
+  const int64_t m = A->m, nnz = in.nnz;
+
+  DBuf<int> err(1);
+  HIPCHECK(hipMemsetAsync(err.p, 0, sizeof(int), st));
+
+  // ---- group entries by row
+  DBuf<int64_t> rowptr_own, gcol, gpos;
+  DBuf<double> gval;
+  const int64_t *rowptr = in.rowptr;
+  const int64_t *col = in.cols;
+  const double *val = in.vals;
+  const int64_t *pos = nullptr;
+  if (in.coo_rows) {
+    DBuf<unsigned long long> cnt((size_t)m + 1);
+    HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * (m + 1), st));
+    if (nnz) {
+      coo_count_kernel<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(nnz, in.coo_rows, in.cols, A->rstart, m, cnt.p, err.p);
+      HIPCHECK(hipGetLastError());
+    }
+    rowptr_own.alloc((size_t)m + 1);
+    int64_t total = 0;
+    exclusive_scan_i64(reinterpret_cast<int64_t *>(cnt.p), rowptr_own.p, m + 1, st, &total);
+    int herr = 0;
+    HIPCHECK(hipMemcpy(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr & 8) fail(MX_ERR_UNSUPPORTED, "COO entry for a row owned by another rank (off-process stash not implemented)");
+    HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * (m + 1), st));
+    gcol.alloc((size_t)std::max<int64_t>(total, 1));
+    gval.alloc((size_t)std::max<int64_t>(total, 1));
+    gpos.alloc((size_t)std::max<int64_t>(total, 1));
+    if (nnz) {
+      coo_scatter_kernel<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(nnz, in.coo_rows, in.cols, in.vals, A->rstart, m,
+                                                                   rowptr_own.p, cnt.p, gcol.p, gval.p, gpos.p);
+      HIPCHECK(hipGetLastError());
+    }
+    rowptr = rowptr_own.p; col = gcol.p; val = gval.p; pos = gpos.p;
+  }
+
+  // ---- longest row picks the segment width
+  DBuf<unsigned long long> lmax(2);
+  HIPCHECK(hipMemsetAsync(lmax.p, 0, sizeof(unsigned long long) * 2, st));
+  if (m) {
+    row_len_max_kernel<<<(unsigned)cdiv(m, 256), 256, 0, st>>>(m, rowptr, lmax.p, err.p);
+    HIPCHECK(hipGetLastError());
+  }
+  unsigned long long Lh = 0;
+  HIPCHECK(hipMemcpyAsync(&Lh, lmax.p, sizeof(Lh), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  int64_t tot_in = 0;
+  if (m) HIPCHECK(hipMemcpy(&tot_in, rowptr + m, sizeof(int64_t), hipMemcpyDeviceToHost));
+
+  // ---- canonicalise rows
+  DBuf<int64_t> ccol((size_t)std::max<int64_t>(tot_in, 1));
+  DBuf<double> cval((size_t)std::max<int64_t>(tot_in, 1));
+  DBuf<int64_t> cnt_out((size_t)m + 1);
+  DBuf<int64_t> long_rows((size_t)m + 1);
+  if (m) {
+    const int add = in.insert_mode == MX_ADD_VALUES;
+    int W = 64;
+    if (Lh <= 8) W = 8; else if (Lh <= 16) W = 16; else if (Lh <= 32) W = 32;
+    const unsigned grid = (unsigned)cdiv(m, 256 / W);
+#define CANON(WW) canon_rows_wave_kernel<WW><<<grid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, long_rows.p, &lmax.p[1], err.p)
+    switch (W) { case 8: CANON(8); break; case 16: CANON(16); break; case 32: CANON(32); break; default: CANON(64); }
+#undef CANON
+    HIPCHECK(hipGetLastError());
+    if (Lh > 64) {
+      unsigned long long nl = 0;
+      HIPCHECK(hipMemcpyAsync(&nl, &lmax.p[1], sizeof(nl), hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (nl) {
+        canon_rows_block_kernel<<<(unsigned)nl, 256, 0, st>>>(long_rows.p, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, err.p);
+        HIPCHECK(hipGetLastError());
+      }
+    }
+  }
+  int herr = 0;
+  HIPCHECK(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  if (herr & 4) fail(MX_ERR_ARG, "row pointer array is not nondecreasing");
+  if (herr & 1) fail(MX_ERR_OUTOFRANGE, "Column too large: max " + std::to_string(N - 1));
+  if (herr & 2) fail(MX_ERR_UNSUPPORTED, "row with more than 2048 entries (long-row sort not implemented)");
+
+  // ---- split into A_d / A_o with a ghost bitmap
+  const bool multi = c->size > 1;
+  const int64_t nw = multi ? cdiv(N, 32) : 0;
+  DBuf<unsigned> bitmap((size_t)std::max<int64_t>(nw, 1));
+  DBuf<int64_t> wbase((size_t)std::max<int64_t>(nw, 1));
+  if (nw) HIPCHECK(hipMemsetAsync(bitmap.p, 0, sizeof(unsigned) * nw, st));
+  A->dptr.alloc((size_t)m + 1);
+  A->optr.alloc((size_t)m + 1);
+  HIPCHECK(hipMemsetAsync(A->dptr.p, 0, sizeof(int64_t) * (m + 1), st));
+  HIPCHECK(hipMemsetAsync(A->optr.p, 0, sizeof(int64_t) * (m + 1), st));
+  if (m) {
+    split_count_kernel<<<(unsigned)cdiv(m, 256), 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, A->cstart, A->cend,
+                                                                A->dptr.p, A->optr.p, bitmap.p);
+    HIPCHECK(hipGetLastError());
+  }
+  exclusive_scan_i64(A->dptr.p, A->dptr.p, m + 1, st, &A->nnz_d);
+  exclusive_scan_i64(A->optr.p, A->optr.p, m + 1, st, &A->nnz_o);
+  if (!multi && A->nnz_o) fail(MX_ERR_INTERNAL, "off-diagonal entries on one rank");
+  A->nghost = 0;
+  if (nw) {
+    popc_kernel<<<grid_for(nw, 256, 8192), 256, 0, st>>>(nw, bitmap.p, wbase.p);
+    HIPCHECK(hipGetLastError());
+    exclusive_scan_i64(wbase.p, wbase.p, nw, st, &A->nghost);
+  }
+  A->garray.alloc((size_t)std::max<int64_t>(A->nghost, 1));
+  if (A->nghost) {
+    garray_kernel<<<grid_for(nw, 256, 8192), 256, 0, st>>>(nw, bitmap.p, wbase.p, A->garray.p);
+    HIPCHECK(hipGetLastError());
+  }
+  A->dcol.alloc((size_t)std::max<int64_t>(A->nnz_d, 1));
+  A->dval.alloc((size_t)std::max<int64_t>(A->nnz_d, 1));
+  A->ocol.alloc((size_t)std::max<int64_t>(A->nnz_o, 1));
+  A->oval.alloc((size_t)std::max<int64_t>(A->nnz_o, 1));
+  A->diag.alloc((size_t)std::max<int64_t>(m, 1));
+  if (m) {
+    fill_split_kernel<<<(unsigned)cdiv(m, 256), 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, cval.p, A->cstart, A->cend,
+                                                               A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p,
+                                                               A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p);
+    HIPCHECK(hipGetLastError());
+  }
+  A->garray_h.resize((size_t)A->nghost);
+  if (A->nghost) HIPCHECK(hipMemcpyAsync(A->garray_h.data(), A->garray.p, sizeof(int64_t) * A->nghost, hipMemcpyDeviceToHost, st));
+
+  // ---- SpMV layouts
+  build_sell(A->sd, m, A->dptr.p, A->dcol.p, A->dval.p, st);
+  build_sell(A->so, m, A->optr.p, A->ocol.p, A->oval.p, st);
+  A->partials.alloc((size_t)std::max(spmv_blocks(A.get()), RED_BLOCKS) * 4 + 64);
+  HIPCHECK(hipStreamSynchronize(st));
+
+  // ---- halo plan (collective)
+  if (multi) build_halo(A.get());
+  return A.release();
+}
+
+// ---------------------------------------------------------------- stencil generator
+// Rows [row0, row0+m) of the synthetic operators of SURVEY.md §8d, written as
+// a fixed-stride CSR (S slots per row, missing neighbours = column -1, which
+// assembly ignores).  Values are dyadic, identical to oracle/petsc_oracle.c.
+__device__ __forceinline__ double kappa_d(int64_t a, int64_t b, int64_t c) {
+  int64_t t = ((a + 2 * b + 3 * c) % 4 + 4) % 4;
+  return 1.0 + (double)t * 0.25;
+}
+
+__global__ void stencil_kernel(int kind, int64_t nx, int64_t ny, int64_t nz, int64_t row0, int64_t m,
+                               int S, int64_t *__restrict__ cols, double *__restrict__ vals) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < m; li += stride) {
+    const int64_t row = row0 + li;
+    const int64_t i = row % nx, j = (row / nx) % ny, k = (kind == 0) ? 0 : row / (nx * ny);
+    int64_t *cp = cols + li * S;
+    double *vp = vals + li * S;
+    int t = 0;
+    if (kind == 0) {
+      const int di[5] = {0, -1, 0, 1, 0}, dj[5] = {-1, 0, 0, 0, 1};
+      for (int q = 0; q < 5; ++q, ++t) {
+        const int64_t ii = i + di[q], jj = j + dj[q];
+        const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny;
+        cp[t] = in ? ii + nx * jj : -1;
+        vp[t] = (q == 2) ? 4.0 : -1.0;
+      }
+    } else if (kind == 1 || kind == 3) {
+      const int di[7] = {0, 0, -1, 0, 1, 0, 0}, dj[7] = {0, -1, 0, 0, 0, 1, 0}, dk[7] = {-1, 0, 0, 0, 0, 0, 1};
+      double diag = 6.0;
+      if (kind == 3)
+        diag = kappa_d(i - 1, j, k) + kappa_d(i, j, k) + kappa_d(i, j - 1, k) + kappa_d(i, j, k) +
+               kappa_d(i, j, k - 1) + kappa_d(i, j, k) + 0.5;
+      for (int q = 0; q < 7; ++q, ++t) {
+        const int64_t ii = i + di[q], jj = j + dj[q], kk = k + dk[q];
+        const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny && kk >= 0 && kk < nz;
+        cp[t] = in ? ii + nx * (jj + ny * kk) : -1;
+        double v;
+        if (q == 3) v = diag;
+        else if (kind == 1) v = -1.0;
+        else {
+          v = -kappa_d(i < ii ? i : ii, j < jj ? j : jj, k < kk ? k : kk);
+          if (q == 2) v = v - 0.5;
+        }
+        vp[t] = v;
+      }
+    } else {
+      for (int dk = -1; dk <= 1; ++dk)
+        for (int dj = -1; dj <= 1; ++dj)
+          for (int di = -1; di <= 1; ++di, ++t) {
+            const int64_t ii = i + di, jj = j + dj, kk = k + dk;
+            const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny && kk >= 0 && kk < nz;
+            cp[t] = in ? ii + nx * (jj + ny * kk) : -1;
+            vp[t] = (di == 0 && dj == 0 && dk == 0) ? 26.0 : -1.0;
+          }
+    }
+  }
+}
+
+__global__ void stride_rowptr_kernel(int64_t m, int S, int64_t *__restrict__ rowptr) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= m; i += stride) rowptr[i] = i * S;
+}
+
+void stencil_coo(Comm *c, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t row0, int64_t m,
+                 DBuf<int64_t> &rowptr, DBuf<int64_t> &cols, DBuf<double> &vals) {
+  const int S = kind == 0 ? 5 : (kind == 2 ? 27 : 7);
+  rowptr.alloc((size_t)m + 1);
+  cols.alloc((size_t)std::max<int64_t>(m * S, 1));
+  vals.alloc((size_t)std::max<int64_t>(m * S, 1));
+  stride_rowptr_kernel<<<grid_for(m + 1, 256, 8192), 256, 0, c->stream>>>(m, S, rowptr.p);
+  HIPCHECK(hipGetLastError());
+  if (m) {
+    stencil_kernel<<<grid_for(m, 256, 8192), 256, 0, c->stream>>>(kind, nx, ny, nz, row0, m, S, cols.p, vals.p);
+    HIPCHECK(hipGetLastError());
+  }
+}
+
+}  // namespace mx

@@ -1,0 +1,173 @@
+// mx_internal.hpp -- shared internals of libmxsolve.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mxsolve.h"
+
+namespace mx {
+
+// ---------------------------------------------------------------- errors
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] void fail(int code, const std::string &msg);
+void hip_check(hipError_t e, const char *what, const char *file, int line);
+#define HIPCHECK(x) ::mx::hip_check((x), #x, __FILE__, __LINE__)
+
+// ---------------------------------------------------------------- device buffers
+// Owning device allocation (hipMalloc).  The library allocates matrix storage
+// and solver work vectors itself; user vectors arrive as raw device pointers.
+template <class T> struct DBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  DBuf() = default;
+  explicit DBuf(size_t count) { alloc(count); }
+  DBuf(const DBuf &) = delete;
+  DBuf &operator=(const DBuf &) = delete;
+  DBuf(DBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DBuf &operator=(DBuf &&o) noexcept { reset(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; return *this; }
+  ~DBuf() { reset(); }
+  void alloc(size_t count) {
+    reset();
+    n = count;
+    if (count) {
+      hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T));
+      if (e != hipSuccess) { p = nullptr; n = 0; fail(MX_ERR_MEM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed"); }
+    }
+  }
+  void reset() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+  T *get() const { return p; }
+};
+
+// ---------------------------------------------------------------- communicator
+struct Msg { int peer; void *buf; size_t bytes; };
+
+// One rank's view of a communicator.  Device payloads move on `stream`.
+struct Comm {
+  int rank = 0, size = 1, device = 0;
+  hipStream_t stream = nullptr;
+  DBuf<double> red_scratch;  // scratch for reductions
+  virtual ~Comm();
+  // In-place SUM all-reduce of n doubles living in device memory, on stream.
+  virtual void allreduce_sum(double *dev, int n) = 0;
+  // Grouped point-to-point exchange of device buffers, on stream.
+  virtual void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs) = 0;
+  // Host all-to-all of one int64 per peer (setup only; synchronous).
+  virtual void alltoall_i64(const int64_t *send, int64_t *recv) = 0;
+  // Host all-gather of one int64 per rank (setup only; synchronous).
+  virtual void allgather_i64(int64_t v, int64_t *all) = 0;
+  virtual void barrier() = 0;
+};
+
+Comm *make_self_comm(int device);
+Comm *make_rccl_comm(int rank, int size, int device, const void *uid, size_t len);
+void *make_local_world(int size);
+Comm *make_local_comm(void *world, int rank, int device);
+void destroy_local_world(void *world);
+void get_unique_id(void *out, size_t len);
+
+// ---------------------------------------------------------------- matrix
+constexpr int SLICE = 64;  // SELL-C with C = one wavefront
+
+struct Sell {
+  int64_t nslices = 0, slots = 0;
+  DBuf<int64_t> sptr;    // [nslices] slot offset of each slice
+  DBuf<int32_t> width;   // [nslices]
+  DBuf<int32_t> col;     // [slots], -1 = padding
+  DBuf<double> val;      // [slots]
+};
+
+struct Halo {
+  // receive side: ghosts arrive grouped by owner, contiguous in lvec
+  std::vector<int> recv_peer;
+  std::vector<int64_t> recv_off, recv_cnt;
+  // send side
+  std::vector<int> send_peer;
+  std::vector<int64_t> send_off, send_cnt;
+  std::vector<int64_t> send_contig_start;  // >= 0: x + start is the payload (no pack)
+  DBuf<int32_t> send_idx;                   // [nsend] local rows to pack
+  DBuf<double> send_buf;                    // [nsend]
+  DBuf<double> lvec;                        // [nghost]
+  int64_t nsend = 0, nrecv = 0;
+  bool need_pack = false;
+};
+
+struct Mat {
+  Comm *comm = nullptr;
+  int64_t M = 0, N = 0, m = 0, n = 0, rstart = 0, cstart = 0, cend = 0;
+  std::vector<int64_t> rranges, cranges;  // P+1 each
+  // canonical PETSc MPIAIJ split (CSR)
+  DBuf<int64_t> dptr, optr;
+  DBuf<int32_t> dcol, ocol;
+  DBuf<double> dval, oval, diag;
+  DBuf<int64_t> garray;
+  int64_t nnz_d = 0, nnz_o = 0, nghost = 0;
+  std::vector<int64_t> garray_h;
+  Sell sd, so;  // SELL-64 copies used by SpMV
+  Halo halo;
+  DBuf<double> partials;   // per-block reduction partials
+  DBuf<double> scratch_x;  // helper vectors
+};
+
+// assembly entry (mx_assembly.hip)
+struct AssemblyInput {
+  // grouped input: rows [0, m), entries of row i at [rowptr[i], rowptr[i+1])
+  // for CSR; for COO, `coo_rows` is set and rowptr is built internally.
+  const int64_t *rowptr = nullptr;   // device, m+1 (CSR)
+  const int64_t *coo_rows = nullptr; // device, nnz (COO, global rows)
+  const int64_t *cols = nullptr;     // device, nnz (global cols)
+  const double *vals = nullptr;      // device, nnz
+  int64_t nnz = 0;
+  int insert_mode = MX_INSERT_VALUES;
+};
+Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
+              const AssemblyInput &in);
+void stencil_coo(Comm *c, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t row0,
+                 int64_t m, DBuf<int64_t> &rows, DBuf<int64_t> &cols, DBuf<double> &vals);
+void convert_index(const void *src, int bytes, int64_t n, int64_t *dst, hipStream_t s);
+
+// SpMV (mx_spmv.hip)
+enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2 };
+void halo_begin(Mat *A, const double *x);  // pack + exchange into A->halo.lvec
+void spmv_launch(Mat *A, const double *x, double *y, int mode, const double *dinv,
+                 double *partials, int *done_flag);
+int spmv_blocks(const Mat *A);
+void mat_mult(Mat *A, const double *x, double *y);
+
+// vector kernels (mx_vec.hip)
+constexpr int RED_BLOCKS = 1024;   // fixed grid of the reduction kernels
+void finish_reduce(const double *partials, int nblocks, int nvals, double *out, hipStream_t s,
+                   int *done_flag = nullptr);
+double host_dot(Comm *c, int64_t n, const double *x, const double *y);
+void vec_axpy(hipStream_t s, int64_t n, double a, const double *x, double *y);
+void vec_aypx(hipStream_t s, int64_t n, double a, const double *x, double *y);
+void vec_pmult(hipStream_t s, int64_t n, const double *x, const double *y, double *w);
+void vec_scale(hipStream_t s, int64_t n, double a, double *x);
+void vec_set(hipStream_t s, int64_t n, double a, double *x);
+void vec_rhs_hash(hipStream_t s, int64_t i0, int64_t n, double *b);
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t s,
+                        int64_t *total_host);
+
+// KSP (mx_ksp.hip)
+void ksp_solve(Mat *A, const mx_ksp_params &p, const double *b, double *x, mx_ksp_result &r,
+               double *hist);
+
+// grid helpers
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline unsigned grid_for(int64_t n, int block, int64_t cap = 1 << 16) {
+  int64_t g = cdiv(n, block);
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace mx

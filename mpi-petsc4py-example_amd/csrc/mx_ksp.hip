@@ -1,0 +1,752 @@
+// mx_ksp.hip -- KSPSolve on gfx950: CG, GMRES(restart) and PREONLY with Jacobi.
+//
+// Replaces ksp.solve(b, x) (test.py:50) under -ksp_type cg|gmres|preonly
+// -pc_type jacobi|none.  The algorithms,
+// scalar recurrences, stopping rule (KSPConvergedDefault) and breakdown checks
+// are PETSc's, restated in oracle/petsc_oracle.c (solve_cg, solve_gmres,
+// converged).
+//
+// MI355X design: the whole solve stays on the device.  Every scalar of the
+// recurrence (alpha, beta, Hessenberg, Givens rotations, the convergence test
+// and the KSPConvergedReason) lives in device memory and is updated by one
+// thread right after the reduction that feeds it, so the host never waits on
+// the GPU inside an iteration.  Kernels read a `done` flag and become no-ops
+// once the solve has stopped; the host polls that flag every `poll_every`
+// iterations one batch behind (the GPU never idles) and stops enqueueing.
+// The iteration count is therefore exactly PETSc's.  With P > 1 each
+// reduction is one ncclAllReduce of 1-3 (CG) or k+1 (GMRES MDot) doubles on
+// the same stream, and the halo is the grouped send/recv of halo_begin().
+//
+// Fused vector passes (bytes per row of the CG iteration: SpMV + 88 B):
+//   cg_p_kernel      z = d.*r recomputed, p = z + (beta/betaold) p   (r,d,p -> p)
+//   SpMV + dot       w = A p and p.w partials in one pass
+//   cg_update_kernel x += a p (fma), r -= a w (fma), z = d.*r, [z.z, z.r, r.r]
+//   GMRES: SpMV with the Jacobi scaling fused, MDot of k+1 vectors in one pass,
+//          MAXPY + norm in one pass.
+#include <cmath>
+#include <cstring>
+
+#include "mx_device.hpp"
+#include "mx_internal.hpp"
+
+namespace mx {
+
+enum {
+  R_ITERATING = 0, R_CONVERGED_RTOL = 2, R_CONVERGED_ATOL = 3, R_CONVERGED_ITS = 4,
+  R_DIVERGED_NULL = -2, R_DIVERGED_ITS = -3, R_DIVERGED_DTOL = -4, R_DIVERGED_BREAKDOWN = -5,
+  R_DIVERGED_INDEFINITE_PC = -8, R_DIVERGED_NANORINF = -9, R_DIVERGED_INDEFINITE_MAT = -10
+};
+
+constexpr int MAX_RESTART = 1000;
+
+// Device-resident solver state (one allocation, zeroed then parameterised).
+struct KspState {
+  double red[8];
+  double beta, betaold, dpi, dpiold, alpha, dp, rnorm0, ttol;
+  double rtol, atol, dtol, haptol, breakdowntol;
+  double res, ksp_rnorm, gm_rnorm0, scale;
+  int its, reason, done, max_it;
+  int normtype, guess_zero, inner_stop, it;
+  int itcount, max_k, nv, pad;
+};
+
+// ------------------------------------------------------------------ shared scalar logic
+__device__ __forceinline__ bool not_finite(double v) { return isnan(v) || isinf(v); }
+
+// KSPConvergedDefault (KSPConvergedSkip when the norm type is NONE).
+__device__ int dev_converged(KspState *s, int n, double rnorm, bool guess_zero, double snorm) {
+  if (s->normtype == MX_NORM_NONE) return n >= s->max_it ? R_CONVERGED_ITS : R_ITERATING;
+  if (n == 0) {
+    if (!guess_zero) {
+      if (snorm == 0.0) snorm = rnorm;
+      s->rnorm0 = snorm;
+    } else {
+      s->rnorm0 = rnorm;
+    }
+    s->ttol = fmax(s->rtol * s->rnorm0, s->atol);
+  }
+  if (not_finite(rnorm)) return R_DIVERGED_NANORINF;
+  if (rnorm <= s->ttol) return rnorm < s->atol ? R_CONVERGED_ATOL : R_CONVERGED_RTOL;
+  if (rnorm >= s->dtol * s->rnorm0) return R_DIVERGED_DTOL;
+  return R_ITERATING;
+}
+
+__device__ __forceinline__ void stop(KspState *s, int reason) {
+  s->reason = reason;
+  s->done = 1;
+  s->inner_stop = 1;
+}
+
+// Either one thread after an all-reduce (P > 1), or a fused single block that
+// first folds the per-block partials itself (P == 1, no collective between).
+template <int NV>
+__device__ __forceinline__ bool gather_red(KspState *s, const double *partials, int nblocks,
+                                           bool fused) {
+  if (fused) {
+    for (int v = 0; v < NV; ++v) {
+      const double t = block_sum_array(partials + (size_t)v * nblocks, nblocks);
+      if (threadIdx.x == 0) s->red[v] = t;
+    }
+  }
+  return threadIdx.x == 0;
+}
+
+// ------------------------------------------------------------------ PCSetUp_Jacobi
+__global__ void jacobi_setup_kernel(int64_t n, const double *__restrict__ diag, double *__restrict__ dinv) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double d = diag[i];
+    dinv[i] = d == 0.0 ? 1.0 : 1.0 / d;   // zero diagonal entries use 1
+  }
+}
+
+// ------------------------------------------------------------------ CG kernels
+// partials of [z.z, z.r, r.r] (z = d.*r) and, when b != null, the same of b
+// for the nonzero-guess rnorm0 (KSPConvergedDefault n == 0).
+template <int NV>
+__global__ void __launch_bounds__(256) cg_norms_kernel(int64_t n, const double *__restrict__ r,
+                                                      const double *__restrict__ b,
+                                                      const double *__restrict__ dinv,
+                                                      double *__restrict__ partials) {
+  double v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const double ri = r[i];
+    const double zi = dinv ? ri * dinv[i] : ri;
+    v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
+    if (NV == 6) {
+      const double bi = b[i];
+      const double zb = dinv ? bi * dinv[i] : bi;
+      v[3 % NV] += zb * zb; v[4 % NV] += bi * zb; v[5 % NV] += bi * bi;
+    }
+  }
+  block_sum_to_partials<NV>(v, partials, gridDim.x);
+}
+
+// after the initial norms: dp, rnorm0/ttol, beta, checks for iteration 0
+template <int NV>
+__global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double *partials, int nblocks,
+                                                      int fused, double *hist) {
+  if (!gather_red<NV>(s, partials, nblocks, fused)) return;
+  const double zz = s->red[0], zr = s->red[1], rr = s->red[2];
+  double dp;
+  switch (s->normtype) {
+    case MX_NORM_PRECONDITIONED: dp = sqrt(zz); break;
+    case MX_NORM_UNPRECONDITIONED: dp = sqrt(rr); break;
+    case MX_NORM_NATURAL: dp = sqrt(fabs(zr)); break;
+    default: dp = 0.0;
+  }
+  s->its = 0;
+  s->beta = zr;
+  s->dp = dp;
+  if (hist) hist[0] = dp;
+  if (not_finite(dp)) { stop(s, R_DIVERGED_NANORINF); return; }
+  double snorm = 0.0;
+  if (!s->guess_zero && NV == 6) {
+    const double bz = s->red[3 % NV], bzr = s->red[4 % NV], bb = s->red[5 % NV];
+    snorm = s->normtype == MX_NORM_UNPRECONDITIONED ? sqrt(bb)
+            : s->normtype == MX_NORM_NATURAL        ? sqrt(fabs(bzr))
+                                                    : sqrt(bz);
+  }
+  const int reason = dev_converged(s, 0, dp, s->guess_zero, snorm);
+  if (reason) { stop(s, reason); return; }
+  if (not_finite(s->beta)) { stop(s, R_DIVERGED_NANORINF); return; }
+  s->its = 1;                                   // top of iteration 0
+  if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
+}
+
+// p = z + (beta/betaold) p  (i == 0: p = z), z = d.*r recomputed
+__global__ void cg_p_kernel(int64_t n, int i, const KspState *__restrict__ s, const double *__restrict__ r,
+                            const double *__restrict__ dinv, double *__restrict__ p) {
+  if (s->done) return;
+  const double b = i == 0 ? 0.0 : s->beta / s->betaold;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const double z = dinv ? r[k] * dinv[k] : r[k];
+    p[k] = (b == 0.0) ? z : z + b * p[k];       // VecAYPX_Seq (b == 0 copies)
+  }
+}
+
+// dpi = p.w, indefiniteness checks, alpha = beta/dpi
+__global__ void __launch_bounds__(256) cg_alpha_kernel(KspState *s, int i, const double *partials,
+                                                       int nblocks, int fused) {
+  if (s->done) return;
+  if (!gather_red<1>(s, partials, nblocks, fused)) return;
+  s->dpiold = s->dpi;
+  s->dpi = s->red[0];
+  if (not_finite(s->dpi)) { stop(s, R_DIVERGED_NANORINF); return; }
+  s->betaold = s->beta;
+  const double dpi = s->dpi, dpo = s->dpiold;
+  const int sg = (dpi > 0) - (dpi < 0), sgo = (dpo > 0) - (dpo < 0);
+  if (dpi == 0.0 || (i > 0 && sg * sgo < 0)) { stop(s, R_DIVERGED_INDEFINITE_MAT); return; }
+  s->alpha = s->beta / s->dpi;
+}
+
+// x += a p, r -= a w (BLAS daxpy = fma), z = d.*r, partials [z.z, z.r, r.r]
+__global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, const KspState *__restrict__ s,
+                                                        const double *__restrict__ p,
+                                                        const double *__restrict__ w,
+                                                        double *__restrict__ x, double *__restrict__ r,
+                                                        const double *__restrict__ dinv,
+                                                        double *__restrict__ partials) {
+  if (s->done) return;
+  const double a = s->alpha;
+  double v[3] = {0.0, 0.0, 0.0};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    x[i] = fma(a, p[i], x[i]);
+    const double ri = fma(-a, w[i], r[i]);
+    r[i] = ri;
+    const double zi = dinv ? ri * dinv[i] : ri;
+    v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
+  }
+  block_sum_to_partials<3>(v, partials, gridDim.x);
+}
+
+// dp, history, convergence at its = i+1, beta for the next iteration
+__global__ void __launch_bounds__(256) cg_conv_kernel(KspState *s, int i, const double *partials,
+                                                      int nblocks, int fused, double *hist) {
+  if (s->done) return;
+  if (!gather_red<3>(s, partials, nblocks, fused)) return;
+  const double zz = s->red[0], zr = s->red[1], rr = s->red[2];
+  double dp;
+  switch (s->normtype) {
+    case MX_NORM_PRECONDITIONED: dp = sqrt(zz); break;
+    case MX_NORM_UNPRECONDITIONED: dp = sqrt(rr); break;
+    case MX_NORM_NATURAL: dp = sqrt(fabs(zr)); break;
+    default: dp = 0.0;
+  }
+  s->dp = dp;
+  if (not_finite(dp)) { stop(s, R_DIVERGED_NANORINF); return; }
+  if (hist) hist[i + 1] = dp;
+  const int reason = dev_converged(s, i + 1, dp, true, 0.0);
+  if (reason) { stop(s, reason); return; }
+  s->beta = zr;
+  if (not_finite(zr)) { stop(s, R_DIVERGED_NANORINF); return; }
+  if (i + 1 >= s->max_it) { stop(s, R_DIVERGED_ITS); return; }
+  s->its = i + 2;                               // top of iteration i+1
+  if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
+  if (s->beta * s->betaold < 0.0) { stop(s, R_DIVERGED_INDEFINITE_PC); return; }
+}
+
+// ------------------------------------------------------------------ GMRES kernels
+__global__ void gm_resid_kernel(int64_t n, const double *__restrict__ b, const double *__restrict__ ax,
+                                const double *__restrict__ dinv, double *__restrict__ v0) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double t = ax ? fma(-1.0, ax[i], b[i]) : b[i];   // VecCopy + VecAXPY(-1)
+    v0[i] = dinv ? t * dinv[i] : t;                          // PCApply
+  }
+}
+
+__global__ void __launch_bounds__(256) sumsq_kernel(int64_t n, const double *__restrict__ x,
+                                                    double *__restrict__ partials, const int *__restrict__ stop_flag) {
+  if (stop_flag && *stop_flag) return;
+  double v[1] = {0.0};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) v[0] += x[i] * x[i];
+  block_sum_to_partials<1>(v, partials, gridDim.x);
+}
+
+// cycle start: VecNormalize(vv0), restart consistency check, convergence test
+__global__ void __launch_bounds__(256) gm_start_kernel(KspState *s, const double *partials, int nblocks,
+                                                       int fused, double *grs, double *hist, double snorm) {
+  if (!gather_red<1>(s, partials, nblocks, fused)) return;
+  const double res = sqrt(s->red[0]);
+  s->it = 0;
+  s->res = res;
+  s->scale = res != 0.0 ? 1.0 / res : 1.0;
+  if (not_finite(res)) { stop(s, R_DIVERGED_NANORINF); return; }
+  if (s->ksp_rnorm > 0.0 && fabs(res - s->ksp_rnorm) > s->breakdowntol * s->gm_rnorm0) {
+    stop(s, R_DIVERGED_BREAKDOWN); return;
+  }
+  grs[0] = res;
+  s->gm_rnorm0 = res;
+  s->ksp_rnorm = res;
+  if (hist && s->its == 0) hist[0] = res;
+  if (res == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
+  const int reason = dev_converged(s, s->its, res, s->its == 0 ? s->guess_zero : true, snorm);
+  if (reason) { stop(s, reason); return; }
+  s->inner_stop = (s->its >= s->max_it) ? 1 : 0;
+}
+
+__global__ void scale_by_state_kernel(int64_t n, const KspState *__restrict__ s, double *__restrict__ x,
+                                      int expect_it) {
+  if (s->done && expect_it < 0) return;
+  if (expect_it >= 0 && s->it != expect_it) return;
+  if (s->res == 0.0 && expect_it < 0) return;
+  const double a = s->scale;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = a * x[i];
+}
+
+// VecMDot: h_j = w . v_j for j in [j0, j0+NV), one pass over w
+template <int NV>
+__global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__restrict__ w,
+                                                   const double *__restrict__ V, int64_t ldv, int j0,
+                                                   double *__restrict__ partials, const int *__restrict__ stop_flag) {
+  if (*stop_flag) return;
+  double acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const double wi = w[i];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] += wi * V[(int64_t)(j0 + k) * ldv + i];
+  }
+  block_sum_to_partials<NV>(acc, partials + (size_t)j0 * gridDim.x, gridDim.x);
+}
+
+__global__ void __launch_bounds__(256) gm_orth_kernel(KspState *s, int k, double *red_k, double *lhh,
+                                                      double *hh, int ld) {
+  if (s->inner_stop) return;
+  if (threadIdx.x != 0) return;
+  for (int j = 0; j <= k; ++j) {
+    if (not_finite(red_k[j])) { stop(s, R_DIVERGED_NANORINF); return; }
+    lhh[j] = -red_k[j];
+  }
+  for (int j = 0; j <= k; ++j) hh[(size_t)k * ld + j] = 0.0 - lhh[j];
+}
+
+// VecMAXPY_Seq grouping (first nv%4 vectors, then groups of four), then ||w||^2
+__global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__restrict__ w,
+                                                         const double *__restrict__ V, int64_t ldv, int nv,
+                                                         const double *__restrict__ alpha,
+                                                         double *__restrict__ partials,
+                                                         const int *__restrict__ stop_flag) {
+  if (*stop_flag) return;
+  __shared__ double a[MAX_RESTART + 1];
+  for (int j = threadIdx.x; j < nv; j += 256) a[j] = alpha[j];
+  __syncthreads();
+  const int rem = nv & 3;
+  double v[1] = {0.0};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    double u = w[i];
+    int j = 0;
+    if (rem == 1) { u = a[0] * V[i] + u; j = 1; }
+    else if (rem == 2) { u = u + (a[0] * V[i] + a[1] * V[ldv + i]); j = 2; }
+    else if (rem == 3) { u = u + ((a[0] * V[i] + a[1] * V[ldv + i]) + a[2] * V[2 * ldv + i]); j = 3; }
+    for (; j < nv; j += 4)
+      u = u + (((a[j] * V[(int64_t)j * ldv + i] + a[j + 1] * V[(int64_t)(j + 1) * ldv + i]) +
+                a[j + 2] * V[(int64_t)(j + 2) * ldv + i]) + a[j + 3] * V[(int64_t)(j + 3) * ldv + i]);
+    w[i] = u;
+    v[0] += u * u;
+  }
+  block_sum_to_partials<1>(v, partials, gridDim.x);
+}
+
+// normalise vv[k+1], happy breakdown, KSPGMRESUpdateHessenberg, convergence
+__global__ void __launch_bounds__(256) gm_step_kernel(KspState *s, int k, const double *partials, int nblocks,
+                                                      int fused, double *hh, int ld, double *grs, double *cc,
+                                                      double *ss, double *hist) {
+  if (s->inner_stop) return;
+  if (!gather_red<1>(s, partials, nblocks, fused)) return;
+  const double tt = sqrt(s->red[0]);
+  s->scale = tt != 0.0 ? 1.0 / tt : 1.0;
+  if (not_finite(tt)) { stop(s, R_DIVERGED_NANORINF); return; }
+  double *h = hh + (size_t)k * ld;   // column k
+  h[k + 1] = tt;
+  double hapbnd = fabs(tt / grs[k]);
+  if (hapbnd > s->haptol) hapbnd = s->haptol;
+  const bool hapend = tt < hapbnd;
+  // apply the previous rotations to column k
+  for (int j = 1; j <= k; ++j) {
+    const double t = h[j - 1];
+    h[j - 1] = cc[j - 1] * t + ss[j - 1] * h[j];
+    h[j] = cc[j - 1] * h[j] - (ss[j - 1] * t);
+  }
+  double res;
+  if (!hapend) {
+    const double t = sqrt(h[k] * h[k] + h[k + 1] * h[k + 1]);
+    if (t == 0.0) { stop(s, R_DIVERGED_NULL); return; }
+    cc[k] = h[k] / t;
+    ss[k] = h[k + 1] / t;
+    grs[k + 1] = -(ss[k] * grs[k]);
+    grs[k] = cc[k] * grs[k];
+    h[k] = cc[k] * h[k] + ss[k] * h[k + 1];
+    res = fabs(grs[k + 1]);
+  } else {
+    res = 0.0;
+  }
+  s->it = k + 1;
+  s->its += 1;
+  s->ksp_rnorm = res;
+  s->res = tt;          // the scale kernel reads s->scale; res kept nonzero for it
+  if (hist) hist[s->its] = res;
+  int reason = dev_converged(s, s->its, res, true, 0.0);
+  if (hapend && !reason) reason = R_DIVERGED_BREAKDOWN;
+  if (reason) { stop(s, reason); return; }
+  if (s->it >= s->max_k || s->its >= s->max_it) s->inner_stop = 1;
+}
+
+// KSPGMRESBuildSoln: back substitution into grs (in place)
+__global__ void gm_buildsoln_kernel(KspState *s, const double *hh, int ld, double *grs) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  s->nv = 0;
+  const int it = s->it - 1;
+  if (it < 0 || s->reason == R_DIVERGED_NULL || s->reason == R_DIVERGED_NANORINF) return;
+  if (s->reason == R_DIVERGED_BREAKDOWN && s->ksp_rnorm > 0.0 && s->it == 0) return;
+#define HHd(a, b) hh[(size_t)(b) * ld + (a)]
+  if (HHd(it, it) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->done = 1; return; }
+  grs[it] = grs[it] / HHd(it, it);
+  for (int ii = 1; ii <= it; ++ii) {
+    const int k = it - ii;
+    double t = grs[k];
+    for (int j = k + 1; j <= it; ++j) t = t - HHd(k, j) * grs[j];
+    if (HHd(k, k) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->done = 1; return; }
+    grs[k] = t / HHd(k, k);
+  }
+#undef HHd
+  s->nv = it + 1;
+}
+
+// x += sum_j nrs_j v_j  (VecMAXPY from zero, then VecAXPY(x, 1, TEMP))
+__global__ void __launch_bounds__(256) gm_update_x_kernel(int64_t n, const KspState *__restrict__ s,
+                                                          const double *__restrict__ V, int64_t ldv,
+                                                          const double *__restrict__ nrs, double *__restrict__ x) {
+  const int nv = s->nv;
+  if (nv == 0) return;
+  __shared__ double a[MAX_RESTART + 1];
+  for (int j = threadIdx.x; j < nv; j += 256) a[j] = nrs[j];
+  __syncthreads();
+  const int rem = nv & 3;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double u = 0.0;
+    int j = 0;
+    if (rem == 1) { u = a[0] * V[i] + u; j = 1; }
+    else if (rem == 2) { u = u + (a[0] * V[i] + a[1] * V[ldv + i]); j = 2; }
+    else if (rem == 3) { u = u + ((a[0] * V[i] + a[1] * V[ldv + i]) + a[2] * V[2 * ldv + i]); j = 3; }
+    for (; j < nv; j += 4)
+      u = u + (((a[j] * V[(int64_t)j * ldv + i] + a[j + 1] * V[(int64_t)(j + 1) * ldv + i]) +
+                a[j + 2] * V[(int64_t)(j + 2) * ldv + i]) + a[j + 3] * V[(int64_t)(j + 3) * ldv + i]);
+    x[i] = fma(1.0, u, x[i]);
+  }
+}
+
+__global__ void gm_cycle_end_kernel(KspState *s) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  s->itcount += s->it;
+  if (s->itcount >= s->max_it && !s->reason) s->reason = R_DIVERGED_ITS;
+  if (s->reason) s->done = 1;
+  s->guess_zero = 0;
+}
+
+// ------------------------------------------------------------------ host drivers
+namespace {
+
+struct Poller {
+  hipStream_t st;
+  int *pinned = nullptr;
+  hipEvent_t ev[2];
+  int pending = 0;  // batches enqueued
+  explicit Poller(hipStream_t s) : st(s) {
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&pinned), 2 * sizeof(int), hipHostMallocDefault));
+    pinned[0] = pinned[1] = 0;
+    HIPCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  }
+  ~Poller() {
+    (void)hipStreamSynchronize(st);
+    (void)hipHostFree(pinned);
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
+  }
+  // enqueue the flag copy for this batch; return true if the PREVIOUS batch saw done
+  bool batch(const int *dev_done) {
+    const int slot = pending & 1;
+    HIPCHECK(hipMemcpyAsync(&pinned[slot], dev_done, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipEventRecord(ev[slot], st));
+    ++pending;
+    if (pending >= 2) {
+      const int prev = (pending - 2) & 1;
+      HIPCHECK(hipEventSynchronize(ev[prev]));
+      if (pinned[prev]) return true;
+    }
+    return false;
+  }
+};
+
+struct SpmvTimer {
+  bool on = false;
+  std::vector<hipEvent_t> ev;
+  size_t used = 0;
+  hipStream_t st;
+  SpmvTimer(bool enable, hipStream_t s, int maxpairs) : on(enable), st(s) {
+    if (!on) return;
+    ev.resize(2 * (size_t)maxpairs);
+    for (auto &e : ev) HIPCHECK(hipEventCreate(&e));
+  }
+  ~SpmvTimer() { for (auto &e : ev) (void)hipEventDestroy(e); }
+  void begin() { if (on && used + 2 <= ev.size()) HIPCHECK(hipEventRecord(ev[used], st)); }
+  void end() { if (on && used + 2 <= ev.size()) { HIPCHECK(hipEventRecord(ev[used + 1], st)); used += 2; } }
+  void collect(double &ms, int &count) {
+    ms = 0.0; count = 0;
+    if (!on) return;
+    HIPCHECK(hipStreamSynchronize(st));
+    for (size_t k = 0; k + 1 < used; k += 2) {
+      float t = 0.f;
+      HIPCHECK(hipEventElapsedTime(&t, ev[k], ev[k + 1]));
+      ms += t; count++;
+    }
+  }
+};
+
+struct Events {
+  hipEvent_t a, b;
+  Events() { HIPCHECK(hipEventCreate(&a)); HIPCHECK(hipEventCreate(&b)); }
+  ~Events() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
+};
+
+void init_state(KspState &h, const mx_ksp_params &p, int normtype) {
+  std::memset(&h, 0, sizeof(h));
+  h.rtol = p.rtol; h.atol = p.atol; h.dtol = p.dtol; h.haptol = p.haptol;
+  h.breakdowntol = p.breakdowntol; h.max_it = p.max_it; h.normtype = normtype;
+  h.guess_zero = !p.guess_nonzero; h.max_k = p.restart; h.ksp_rnorm = -1.0;
+}
+
+void read_state(hipStream_t st, const KspState *d, KspState &h) {
+  HIPCHECK(hipMemcpyAsync(&h, d, sizeof(KspState), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+}
+
+}  // namespace
+
+static void cg_solve(Mat *A, const mx_ksp_params &p, const double *dinv, const double *b, double *x,
+                     mx_ksp_result &res, double *hist_host) {
+  Comm *c = A->comm;
+  hipStream_t st = c->stream;
+  const int64_t n = A->m;
+  const bool fused = c->size == 1;
+  int normtype = p.norm_type == MX_NORM_DEFAULT ? MX_NORM_PRECONDITIONED : p.norm_type;
+  DBuf<double> r((size_t)std::max<int64_t>(n, 1)), pv((size_t)std::max<int64_t>(n, 1)),
+      w((size_t)std::max<int64_t>(n, 1));
+  DBuf<KspState> sd(1);
+  const int nb_spmv = spmv_blocks(A);
+  DBuf<double> part((size_t)std::max(nb_spmv, RED_BLOCKS) * 6 + 64);
+  DBuf<double> hist(hist_host ? (size_t)p.max_it + 2 : 0);
+  KspState hs;
+  init_state(hs, p, normtype);
+  HIPCHECK(hipMemcpyAsync(sd.p, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  Events ev;
+  SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
+  HIPCHECK(hipEventRecord(ev.a, st));
+
+  // r = b - A x  (or b)
+  if (p.guess_nonzero) {
+    mat_mult(A, x, r.p);
+    vec_aypx(st, n, -1.0, b, r.p);
+  } else {
+    vec_set(st, n, 0.0, x);
+    HIPCHECK(hipMemcpyAsync(r.p, b, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+  }
+  KspState *s = sd.p;
+  double *red = reinterpret_cast<double *>(s);   // red[] is the first member
+  const int nv0 = p.guess_nonzero ? 6 : 3;
+  if (nv0 == 6) cg_norms_kernel<6><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
+  else cg_norms_kernel<3><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
+  HIPCHECK(hipGetLastError());
+  if (!fused) { finish_reduce(part.p, RED_BLOCKS, nv0, red, st); c->allreduce_sum(red, nv0); }
+  if (nv0 == 6) cg_init_kernel<6><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
+  else cg_init_kernel<3><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
+  HIPCHECK(hipGetLastError());
+
+  const int poll = p.poll_every > 0 ? p.poll_every : 16;
+  Poller poller(st);
+  int i = 0;
+  const unsigned egrid = grid_for(n, 256, 8192);
+  int *done = &s->done;
+  for (; i < p.max_it; ++i) {
+    cg_p_kernel<<<egrid, 256, 0, st>>>(n, i, s, r.p, dinv, pv.p);
+    halo_begin(A, pv.p);
+    timer.begin();
+    spmv_launch(A, pv.p, w.p, SPMV_DOT, nullptr, part.p, done);
+    timer.end();
+    if (!fused) { finish_reduce(part.p, nb_spmv, 1, red, st, done); c->allreduce_sum(red, 1); }
+    cg_alpha_kernel<<<1, 256, 0, st>>>(s, i, part.p, nb_spmv, fused);
+    cg_update_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, s, pv.p, w.p, x, r.p, dinv, part.p);
+    if (!fused) { finish_reduce(part.p, RED_BLOCKS, 3, red, st, done); c->allreduce_sum(red, 3); }
+    cg_conv_kernel<<<1, 256, 0, st>>>(s, i, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
+    HIPCHECK(hipGetLastError());
+    if ((i + 1) % poll == 0 && poller.batch(done)) { ++i; break; }
+  }
+  HIPCHECK(hipEventRecord(ev.b, st));
+  read_state(st, s, hs);
+  float ms = 0.f;
+  HIPCHECK(hipEventElapsedTime(&ms, ev.a, ev.b));
+  res.its = hs.its;
+  res.reason = hs.reason;
+  res.rnorm = hs.dp;
+  res.solve_ms = ms;
+  res.launched_its = i;
+  timer.collect(res.spmv_ms, res.spmv_count);
+  if (hist_host) HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)hs.its + 1), hipMemcpyDeviceToHost));
+}
+
+template <int NV>
+static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int j0,
+                        double *partials, const int *stop_flag) {
+  mdot_kernel<NV><<<RED_BLOCKS, 256, 0, st>>>(n, w, V, ldv, j0, partials, stop_flag);
+}
+
+static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
+                 double *partials, const int *stop_flag) {
+  for (int j0 = 0; j0 < nv; j0 += 8) {
+    const int k = std::min(8, nv - j0);
+    switch (k) {
+      case 1: launch_mdot<1>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+      case 2: launch_mdot<2>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+      case 3: launch_mdot<3>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+      case 4: launch_mdot<4>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+      case 5: launch_mdot<5>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+      case 6: launch_mdot<6>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+      case 7: launch_mdot<7>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+      default: launch_mdot<8>(st, n, w, V, ldv, j0, partials, stop_flag); break;
+    }
+    HIPCHECK(hipGetLastError());
+  }
+}
+
+// per-value finish into out[] (one block per value), used for MDot (k+1 values)
+__global__ void __launch_bounds__(256) finish_many_kernel(const double *__restrict__ partials, int nblocks,
+                                                          double *__restrict__ out, const int *__restrict__ stop_flag) {
+  if (*stop_flag) return;
+  const double t = block_sum_array(partials + (size_t)blockIdx.x * nblocks, nblocks);
+  if (threadIdx.x == 0) out[blockIdx.x] = t;
+}
+
+static void gmres_solve(Mat *A, const mx_ksp_params &p, const double *dinv, const double *b, double *x,
+                        mx_ksp_result &res, double *hist_host) {
+  Comm *c = A->comm;
+  hipStream_t st = c->stream;
+  const int64_t n = A->m;
+  const int max_k = p.restart > 0 ? p.restart : 30;
+  if (max_k > MAX_RESTART) fail(MX_ERR_UNSUPPORTED, "GMRES restart above 1000");
+  const int ld = max_k + 2;
+  const int64_t ldv = (std::max<int64_t>(n, 1) + 31) / 32 * 32;
+  DBuf<double> V((size_t)ldv * (max_k + 1)), tmat((size_t)ldv);
+  DBuf<double> hh((size_t)ld * (max_k + 1)), grs((size_t)max_k + 2), cc((size_t)max_k + 1),
+      ss((size_t)max_k + 1), lhh((size_t)max_k + 1), red((size_t)max_k + 2);
+  HIPCHECK(hipMemsetAsync(hh.p, 0, sizeof(double) * hh.n, st));
+  DBuf<double> part((size_t)RED_BLOCKS * (max_k + 2) + (size_t)spmv_blocks(A) + 64);
+  DBuf<KspState> sd(1);
+  DBuf<double> hist(hist_host ? (size_t)p.max_it + 2 : 0);
+  KspState hs;
+  init_state(hs, p, MX_NORM_PRECONDITIONED);
+  if (p.norm_type != MX_NORM_DEFAULT && p.norm_type != MX_NORM_PRECONDITIONED)
+    fail(MX_ERR_UNSUPPORTED, "GMRES with left preconditioning supports the preconditioned norm only");
+  hs.max_k = max_k;
+  HIPCHECK(hipMemcpyAsync(sd.p, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  KspState *s = sd.p;
+  double *sred = reinterpret_cast<double *>(s);
+  const bool fused = c->size == 1;
+  double *hist_d = hist_host ? hist.p : nullptr;
+  Events ev;
+  SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
+  HIPCHECK(hipEventRecord(ev.a, st));
+  const unsigned egrid = grid_for(n, 256, 8192);
+  if (!p.guess_nonzero) vec_set(st, n, 0.0, x);
+  // snorm for a nonzero first guess: || B b ||
+  double snorm = 0.0;
+  if (p.guess_nonzero) {
+    gm_resid_kernel<<<egrid, 256, 0, st>>>(n, b, nullptr, dinv, tmat.p);
+    sumsq_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, tmat.p, part.p, nullptr);
+    finish_reduce(part.p, RED_BLOCKS, 1, red.p, st);
+    c->allreduce_sum(red.p, 1);
+    HIPCHECK(hipMemcpyAsync(&snorm, red.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    snorm = std::sqrt(snorm);
+  }
+  int first = 1, launched = 0;
+  int *istop = &s->inner_stop;
+  while (true) {
+    // KSPInitialResidual: vv0 = B (b - A x)
+    if (first && !p.guess_nonzero) {
+      gm_resid_kernel<<<egrid, 256, 0, st>>>(n, b, nullptr, dinv, V.p);
+    } else {
+      mat_mult(A, x, tmat.p);
+      gm_resid_kernel<<<egrid, 256, 0, st>>>(n, b, tmat.p, dinv, V.p);
+    }
+    sumsq_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, V.p, part.p, nullptr);
+    if (!fused) { finish_reduce(part.p, RED_BLOCKS, 1, sred, st); c->allreduce_sum(sred, 1); }
+    gm_start_kernel<<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, grs.p, hist_d, first ? snorm : 0.0);
+    scale_by_state_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, -1);
+    HIPCHECK(hipGetLastError());
+    first = 0;
+    const int nbs = spmv_blocks(A);
+    for (int k = 0; k < max_k; ++k) {
+      double *vk = V.p + (int64_t)k * ldv, *vk1 = V.p + (int64_t)(k + 1) * ldv;
+      halo_begin(A, vk);
+      timer.begin();
+      spmv_launch(A, vk, vk1, dinv ? SPMV_JACOBI : SPMV_PLAIN, dinv, nullptr, istop);
+      timer.end();
+      mdot(st, n, vk1, V.p, ldv, k + 1, part.p, istop);
+      finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, RED_BLOCKS, red.p, istop);
+      c->allreduce_sum(red.p, k + 1);
+      gm_orth_kernel<<<1, 64, 0, st>>>(s, k, red.p, lhh.p, hh.p, ld);
+      maxpy_norm_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, lhh.p, part.p, istop);
+      if (!fused) { finish_reduce(part.p, RED_BLOCKS, 1, sred, st, istop); c->allreduce_sum(sred, 1); }
+      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, fused, hh.p, ld, grs.p, cc.p, ss.p, hist_d);
+      scale_by_state_kernel<<<egrid, 256, 0, st>>>(n, s, vk1, k + 1);
+      HIPCHECK(hipGetLastError());
+      ++launched;
+      (void)nbs;
+    }
+    gm_buildsoln_kernel<<<1, 64, 0, st>>>(s, hh.p, ld, grs.p);
+    gm_update_x_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, ldv, grs.p, x);
+    gm_cycle_end_kernel<<<1, 64, 0, st>>>(s);
+    HIPCHECK(hipGetLastError());
+    read_state(st, s, hs);
+    if (hs.done) break;
+  }
+  HIPCHECK(hipEventRecord(ev.b, st));
+  HIPCHECK(hipEventSynchronize(ev.b));
+  float ms = 0.f;
+  HIPCHECK(hipEventElapsedTime(&ms, ev.a, ev.b));
+  res.its = hs.its;
+  res.reason = hs.reason;
+  res.rnorm = hs.ksp_rnorm;
+  res.solve_ms = ms;
+  res.launched_its = launched;
+  timer.collect(res.spmv_ms, res.spmv_count);
+  if (hist_host) HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)hs.its + 1), hipMemcpyDeviceToHost));
+}
+
+void ksp_solve(Mat *A, const mx_ksp_params &p, const double *b, double *x, mx_ksp_result &r,
+               double *hist) {
+  std::memset(&r, 0, sizeof(r));
+  if (A->M != A->N || A->m != A->n) fail(MX_ERR_UNSUPPORTED, "KSPSolve needs a square matrix with matching row/column layouts");
+  if (p.max_it < 1) fail(MX_ERR_ARG, "max_it must be positive");
+  hipStream_t st = A->comm->stream;
+  const int64_t n = A->m;
+  DBuf<double> dinv;
+  const double *dv = nullptr;
+  if (p.pc_type == MX_PC_JACOBI) {
+    dinv.alloc((size_t)std::max<int64_t>(n, 1));
+    if (n) {
+      jacobi_setup_kernel<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, A->diag.p, dinv.p);
+      HIPCHECK(hipGetLastError());
+    }
+    dv = dinv.p;
+  } else if (p.pc_type != MX_PC_NONE) {
+    fail(MX_ERR_UNSUPPORTED, "unsupported PC type");
+  }
+  switch (p.ksp_type) {
+    case MX_KSP_CG: cg_solve(A, p, dv, b, x, r, hist); break;
+    case MX_KSP_GMRES: gmres_solve(A, p, dv, b, x, r, hist); break;
+    case MX_KSP_PREONLY:   // KSPSolve_PREONLY: x = B b, its = 1, CONVERGED_ITS
+      if (dv) vec_pmult(st, n, b, dv, x);
+      else if (n) HIPCHECK(hipMemcpyAsync(x, b, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      r.its = 1; r.reason = R_CONVERGED_ITS;
+      break;
+    default: fail(MX_ERR_UNSUPPORTED, "unsupported KSP type");
+  }
+  HIPCHECK(hipStreamSynchronize(st));
+}
+
+}  // namespace mx

@@ -1,0 +1,226 @@
+// mx_vec.hip -- Vec kernels, deterministic reductions and scans (gfx950).
+//
+// Element-wise arithmetic follows PETSc's rounding exactly (SURVEY.md §2 N6;
+// oracle/petsc_oracle.c): VecAXPY is a fused multiply-add (BLAS daxpy's
+// OpenBLAS Haswell/Zen kernel), VecAYPX / VecPointwiseMult / VecScale round
+// each operation (PETSc's own C loops, conda-forge -march=nocona).  The library
+// is compiled with -ffp-contract=off so nothing else fuses.
+//
+// Reductions are two-level and deterministic: every block folds its lanes with
+// a fixed xor-butterfly (wave64) plus a fixed 4-wave sum, writes one partial,
+// and finish_reduce sums the partials in a fixed order.  Results are therefore
+// bitwise reproducible run to run (the order differs from PETSc's BLAS ddot,
+// which is itself unspecified).
+#include "mx_device.hpp"
+#include "mx_internal.hpp"
+
+namespace mx {
+
+// one block per value: out[v] = sum_b partials[v][b], fixed order.
+__global__ void __launch_bounds__(256) finish_kernel(const double *__restrict__ partials,
+                                                     int nblocks, double *__restrict__ out,
+                                                     const int *done) {
+  if (done && *done) return;
+  const double *p = partials + (size_t)blockIdx.x * nblocks;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nblocks; i += 256) s += p[i];
+  __shared__ double sh[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+void finish_reduce(const double *partials, int nblocks, int nvals, double *out, hipStream_t s,
+                   int *done_flag) {
+  finish_kernel<<<nvals, 256, 0, s>>>(partials, nblocks, out, done_flag);
+  HIPCHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------- dot / norm
+__global__ void __launch_bounds__(256) dot_partials_kernel(int64_t n, const double *__restrict__ x,
+                                                           const double *__restrict__ y,
+                                                           double *__restrict__ partials) {
+  double v[1] = {0.0};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) v[0] += x[i] * y[i];
+  block_sum_to_partials<1>(v, partials, gridDim.x);
+}
+
+double host_dot(Comm *c, int64_t n, const double *x, const double *y) {
+  if ((int)c->red_scratch.n < RED_BLOCKS + 64) c->red_scratch.alloc(RED_BLOCKS + 64);
+  double *part = c->red_scratch.p, *out = c->red_scratch.p + RED_BLOCKS;
+  dot_partials_kernel<<<RED_BLOCKS, 256, 0, c->stream>>>(n, x, y, part);
+  HIPCHECK(hipGetLastError());
+  finish_reduce(part, RED_BLOCKS, 1, out, c->stream);
+  c->allreduce_sum(out, 1);
+  double h = 0.0;
+  HIPCHECK(hipMemcpyAsync(&h, out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  return h;
+}
+
+// ------------------------------------------------------------- element-wise
+__global__ void axpy_kernel(int64_t n, double a, const double *__restrict__ x, double *__restrict__ y) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = fma(a, x[i], y[i]);
+}
+__global__ void aypx_kernel(int64_t n, double a, const double *__restrict__ x, double *__restrict__ y) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = x[i] + a * y[i];
+}
+__global__ void xmy_kernel(int64_t n, const double *__restrict__ x, double *__restrict__ y) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = x[i] - y[i];
+}
+__global__ void pmult_kernel(int64_t n, const double *__restrict__ x, const double *__restrict__ y, double *__restrict__ w) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) w[i] = x[i] * y[i];
+}
+__global__ void scale_kernel(int64_t n, double a, double *__restrict__ x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = a * x[i];
+}
+__global__ void set_kernel(int64_t n, double a, double *__restrict__ x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = a;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+__global__ void rhs_hash_kernel(int64_t i0, int64_t n, double *__restrict__ b) {
+  const uint64_t seed = 42ULL * 0x9E3779B97F4A7C15ULL;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    b[i] = (double)(splitmix64((uint64_t)(i0 + i) + seed) >> 11) * 0x1.0p-53;
+}
+
+constexpr int EW_BLOCK = 256;
+static unsigned ew_grid(int64_t n) { return grid_for(n, EW_BLOCK, 8192); }
+
+void vec_axpy(hipStream_t s, int64_t n, double a, const double *x, double *y) {
+  if (a == 0.0 || n == 0) return;   // VecAXPY_Seq returns early for alpha == 0
+  axpy_kernel<<<ew_grid(n), EW_BLOCK, 0, s>>>(n, a, x, y);
+  HIPCHECK(hipGetLastError());
+}
+// VecAYPX_Seq: alpha == 0 -> copy, 1 -> VecAXPY, -1 -> x - y, else x + alpha*y
+void vec_aypx(hipStream_t s, int64_t n, double a, const double *x, double *y) {
+  if (n == 0) return;
+  if (a == 0.0) { HIPCHECK(hipMemcpyAsync(y, x, sizeof(double) * n, hipMemcpyDeviceToDevice, s)); return; }
+  if (a == 1.0) { vec_axpy(s, n, 1.0, x, y); return; }
+  if (a == -1.0) xmy_kernel<<<ew_grid(n), EW_BLOCK, 0, s>>>(n, x, y);
+  else aypx_kernel<<<ew_grid(n), EW_BLOCK, 0, s>>>(n, a, x, y);
+  HIPCHECK(hipGetLastError());
+}
+void vec_pmult(hipStream_t s, int64_t n, const double *x, const double *y, double *w) {
+  if (n == 0) return;
+  pmult_kernel<<<ew_grid(n), EW_BLOCK, 0, s>>>(n, x, y, w);
+  HIPCHECK(hipGetLastError());
+}
+void vec_scale(hipStream_t s, int64_t n, double a, double *x) {
+  if (n == 0) return;
+  scale_kernel<<<ew_grid(n), EW_BLOCK, 0, s>>>(n, a, x);
+  HIPCHECK(hipGetLastError());
+}
+void vec_set(hipStream_t s, int64_t n, double a, double *x) {
+  if (n == 0) return;
+  set_kernel<<<ew_grid(n), EW_BLOCK, 0, s>>>(n, a, x);
+  HIPCHECK(hipGetLastError());
+}
+void vec_rhs_hash(hipStream_t s, int64_t i0, int64_t n, double *b) {
+  if (n == 0) return;
+  rhs_hash_kernel<<<ew_grid(n), EW_BLOCK, 0, s>>>(i0, n, b);
+  HIPCHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------- exclusive scan (int64)
+constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 8, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+__device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t *total) {
+  __shared__ int64_t wsum[SCAN_BLOCK / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  int64_t woff = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_BLOCK / 64; ++k) {
+    if (k < wid) woff += wsum[k];
+    tot += wsum[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return woff + incl - v;
+}
+
+__global__ void __launch_bounds__(SCAN_BLOCK) scan_reduce_kernel(const int64_t *__restrict__ in, int64_t n,
+                                                                 int64_t *__restrict__ bsum) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) if (base + k < n) s += in[base + k];
+  int64_t tot;
+  (void)block_exclusive_scan(s, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(SCAN_BLOCK) scan_apply_kernel(const int64_t *__restrict__ in, int64_t n,
+                                                                const int64_t *__restrict__ boff,
+                                                                int64_t *__restrict__ out,
+                                                                int64_t *__restrict__ total_out) {
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+  int64_t loc[SCAN_ITEMS];
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) { loc[k] = (base + k < n) ? in[base + k] : 0; s += loc[k]; }
+  int64_t tot;
+  int64_t off = block_exclusive_scan(s, &tot) + (boff ? boff[blockIdx.x] : 0);
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; ++k) {
+    if (base + k < n) out[base + k] = off;
+    off += loc[k];
+  }
+  if (total_out && blockIdx.x == gridDim.x - 1 && threadIdx.x == SCAN_BLOCK - 1) *total_out = off;
+}
+
+// out may alias in.  total_host (optional) gets sum(in) (synchronises the stream).
+void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t s,
+                        int64_t *total_host) {
+  DBuf<int64_t> tot(1);
+  if (n <= 0) {
+    if (total_host) *total_host = 0;
+    return;
+  }
+  int64_t nb = cdiv(n, SCAN_TILE);
+  if (nb == 1) {
+    scan_apply_kernel<<<1, SCAN_BLOCK, 0, s>>>(in, n, nullptr, out, tot.p);
+    HIPCHECK(hipGetLastError());
+  } else {
+    DBuf<int64_t> bsum((size_t)nb);
+    scan_reduce_kernel<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, bsum.p);
+    HIPCHECK(hipGetLastError());
+    exclusive_scan_i64(bsum.p, bsum.p, nb, s, nullptr);
+    scan_apply_kernel<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, bsum.p, out, tot.p);
+    HIPCHECK(hipGetLastError());
+    if (total_host) {
+      HIPCHECK(hipMemcpyAsync(total_host, tot.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      return;
+    }
+    HIPCHECK(hipStreamSynchronize(s));  // bsum is freed on return
+    return;
+  }
+  if (total_host) HIPCHECK(hipMemcpyAsync(total_host, tot.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+}
+
+}  // namespace mx

@@ -1,0 +1,206 @@
+"""GPU parity of the hot path against the oracle (C restatement of PETSc).
+
+Bar: assembly and SpMV bit-exact; KSP iteration counts equal and the fp64
+solution within relative L2 1e-10 (north_star).  All calls go through the C ABI.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-10
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+
+
+def assert_csr_equal(got, exp):
+    for g, e, name in zip(got, exp, ("indptr", "cols", "vals")):
+        assert g.shape == e.shape, name
+        if name == "vals":
+            assert np.array_equal(g.view(np.uint64), e.view(np.uint64)), name
+        else:
+            assert np.array_equal(g, e), name
+
+
+def test_assembly_reference_system(selfcomm, golden):
+    """test.py's seed-42 CSR (canonical) comes back byte-identical (MatGetRow)."""
+    from mxsolve.core import DMat
+    A = DMat.from_csr(selfcomm, 100, 100, golden["sys_indptr"], golden["sys_indices"], golden["sys_data"])
+    ip, c, v = A.csr()
+    assert_csr_equal((ip, c, v), (golden["sys_indptr"].astype(np.int64),
+                                  golden["sys_indices"].astype(np.int64), golden["sys_data"]))
+    d = torch.zeros(100, dtype=torch.float64, device="cuda")
+    A.diagonal(d)
+    S = np.zeros(100)
+    for i in range(100):
+        for k in range(golden["sys_indptr"][i], golden["sys_indptr"][i + 1]):
+            if golden["sys_indices"][k] == i:
+                S[i] = golden["sys_data"][k]
+    assert np.array_equal(d.cpu().numpy(), S)
+
+
+@pytest.mark.parametrize("add", [False, True])
+@pytest.mark.parametrize("maxlen", [5, 12, 40, 64, 300, 2048])
+def test_assembly_unsorted_duplicates(selfcomm, oracle_mod, add, maxlen):
+    """MatSetValues semantics: unsorted rows, duplicate columns, negative ids, zeros."""
+    from mxsolve.core import DMat
+    rng = np.random.default_rng(maxlen + 7 * add)
+    M, N = 257, 300
+    lens = rng.integers(0, maxlen + 1, M)
+    lens[rng.integers(0, M)] = maxlen
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nnz = int(ip[-1])
+    cols = rng.integers(-3, min(N, max(8, maxlen // 2)), nnz).astype(np.int64)
+    vals = rng.standard_normal(nnz)
+    vals[rng.random(nnz) < 0.05] = 0.0
+    A = DMat.from_csr(selfcomm, M, N, ip, cols, vals, add=add)
+    O = oracle_mod.OracleMat.from_csr(M, N, ip, cols, vals, P=1, add=add)
+    assert_csr_equal(A.csr(), O.csr())
+
+
+def test_assembly_coo(selfcomm, oracle_mod):
+    from mxsolve.core import DMat
+    rng = np.random.default_rng(3)
+    M = N = 500
+    n = 6000
+    rows = rng.integers(-1, M, n)
+    cols = rng.integers(-1, N, n)
+    vals = rng.standard_normal(n)
+    for add in (False, True):
+        A = DMat.from_coo(selfcomm, M, N, rows, cols, vals, add=add)
+        O = oracle_mod.OracleMat.from_coo(M, N, np.array([0, n]), rows, cols, vals, P=1, add=add)
+        assert_csr_equal(A.csr(), O.csr())
+
+
+def test_assembly_errors(selfcomm):
+    from mxsolve._lib import MxError
+    from mxsolve.core import DMat
+    with pytest.raises(MxError) as e:
+        DMat.from_csr(selfcomm, 3, 3, np.array([1, 2, 3, 4]), np.array([0, 1, 2]), np.ones(3))
+    assert e.value.code == 1
+    with pytest.raises(MxError) as e:
+        DMat.from_csr(selfcomm, 3, 3, np.array([0, 1, 2, 3]), np.array([0, 1, 7]), np.ones(3))
+    assert e.value.code == 2
+
+
+@pytest.mark.parametrize("kind,n", [("poisson2d", 37), ("poisson3d", 19), ("poisson3d27", 11), ("convdiff3d", 13)])
+def test_stencil_generator(selfcomm, oracle_mod, kind, n):
+    from mxsolve.core import DMat
+    A = DMat.stencil(selfcomm, kind, n)
+    assert_csr_equal(A.csr(), oracle_mod.stencil(kind, n))
+
+
+@pytest.mark.parametrize("kind,n", [("poisson3d", 24), ("poisson3d27", 9), ("convdiff3d", 10)])
+def test_spmv_bitexact(selfcomm, oracle_mod, kind, n):
+    from mxsolve.core import DMat
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    x = np.random.default_rng(1).standard_normal(M)
+    y = torch.zeros(M, dtype=torch.float64, device="cuda")
+    A.mult(to_dev(x), y)
+    assert np.array_equal(y.cpu().numpy().view(np.uint64), O.mult(x).view(np.uint64))
+
+
+def test_spmv_bitexact_random(selfcomm, oracle_mod, golden):
+    from mxsolve.core import DMat
+    A = DMat.from_csr(selfcomm, 100, 100, golden["sys_indptr"], golden["sys_indices"], golden["sys_data"])
+    O = oracle_mod.OracleMat.from_csr(100, 100, golden["sys_indptr"], golden["sys_indices"], golden["sys_data"])
+    x = golden["sys_X"]
+    y = torch.zeros(100, dtype=torch.float64, device="cuda")
+    A.mult(to_dev(x), y)
+    assert np.array_equal(y.cpu().numpy(), O.mult(x))
+
+
+def rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("kind,n,ksp", [("poisson3d", 24, "cg"), ("poisson2d", 64, "cg"),
+                                       ("poisson3d27", 12, "cg"), ("convdiff3d", 12, "gmres"),
+                                       ("poisson3d", 12, "gmres")])
+def test_ksp_parity(selfcomm, oracle_mod, kind, n, ksp):
+    from mxsolve.core import DMat, rhs_hash
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    A = DMat.stencil(selfcomm, kind, n)
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    b = torch.zeros(M, dtype=torch.float64, device="cuda")
+    rhs_hash(selfcomm, 0, b)
+    bh = b.cpu().numpy()
+    assert np.array_equal(bh, oracle_mod.rhs_hash(0, M))
+    x = torch.zeros(M, dtype=torch.float64, device="cuda")
+    r = A.solve(b, x, ksp=ksp, history=True)
+    o = O.solve(bh, ksp=ksp, history=True)
+    assert r["reason"] == o["reason"] and r["reason"] > 0
+    assert r["its"] == o["its"]
+    assert rel(x.cpu().numpy(), o["x"]) <= REL_TOL
+    assert np.allclose(r["history"], o["history"], rtol=1e-8)
+
+
+@pytest.mark.parametrize("norm", ["unpreconditioned", "natural", "none"])
+def test_cg_norm_types(selfcomm, oracle_mod, norm):
+    from mxsolve.core import DMat, rhs_hash
+    n = 16
+    ip, c, v = oracle_mod.stencil("poisson3d", n)
+    M = ip.size - 1
+    A = DMat.stencil(selfcomm, "poisson3d", n)
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    b = torch.zeros(M, dtype=torch.float64, device="cuda")
+    rhs_hash(selfcomm, 0, b)
+    x = torch.zeros(M, dtype=torch.float64, device="cuda")
+    kw = dict(max_it=40) if norm == "none" else {}
+    r = A.solve(b, x, ksp="cg", norm=norm, **kw)
+    o = O.solve(b.cpu().numpy(), ksp="cg", norm=norm, **kw)
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"])
+    assert rel(x.cpu().numpy(), o["x"]) <= REL_TOL
+
+
+def test_cg_nonzero_guess_and_maxit(selfcomm, oracle_mod):
+    from mxsolve.core import DMat, rhs_hash
+    n = 16
+    ip, c, v = oracle_mod.stencil("poisson3d", n)
+    M = ip.size - 1
+    A = DMat.stencil(selfcomm, "poisson3d", n)
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    b = torch.zeros(M, dtype=torch.float64, device="cuda")
+    rhs_hash(selfcomm, 0, b)
+    x0 = np.sin(np.arange(M))
+    x = to_dev(x0)
+    r = A.solve(b, x, ksp="cg", guess_nonzero=True)
+    o = O.solve(b.cpu().numpy(), x0=x0, ksp="cg")
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"])
+    assert rel(x.cpu().numpy(), o["x"]) <= REL_TOL
+    x = torch.zeros(M, dtype=torch.float64, device="cuda")
+    r = A.solve(b, x, ksp="cg", max_it=7)
+    o = O.solve(b.cpu().numpy(), ksp="cg", max_it=7)
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) == (7, -3)
+    assert rel(x.cpu().numpy(), o["x"]) <= REL_TOL
+
+
+def test_cg_zero_rhs(selfcomm):
+    from mxsolve.core import DMat
+    A = DMat.stencil(selfcomm, "poisson3d", 8)
+    b = torch.zeros(512, dtype=torch.float64, device="cuda")
+    x = torch.ones(512, dtype=torch.float64, device="cuda")
+    r = A.solve(b, x, ksp="cg")
+    assert (r["its"], r["reason"]) == (0, 3)
+    assert float(x.abs().max()) == 0.0
+
+
+def test_gmres_reference_system(selfcomm, oracle_mod, golden):
+    """test.py's system with -ksp_type gmres -ksp_gmres_restart 100 -pc_type jacobi."""
+    from mxsolve.core import DMat
+    A = DMat.from_csr(selfcomm, 100, 100, golden["sys_indptr"], golden["sys_indices"], golden["sys_data"])
+    O = oracle_mod.OracleMat.from_csr(100, 100, golden["sys_indptr"], golden["sys_indices"], golden["sys_data"])
+    b = to_dev(golden["sys_B"])
+    x = torch.zeros(100, dtype=torch.float64, device="cuda")
+    r = A.solve(b, x, ksp="gmres", restart=100, max_it=1000)
+    o = O.solve(golden["sys_B"], ksp="gmres", restart=100, max_it=1000)
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"])
+    assert rel(x.cpu().numpy(), o["x"]) <= 1e-8
+    assert np.allclose(x.cpu().numpy(), golden["sys_X"])       # test.py:149's check
