@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline benchmark: CG iterations/s + SpMV HBM GB/s on 3D 7-point Poisson 256^3.
+
+BASELINE.json metric: "CG iters/s + SpMV HBM GB/s (% peak), 3D Poisson 256^3 at
+1/2/4/8 GPUs" (config C3).  A step is one global KSPSolve_CG iteration (halo +
+SpMV + fused vector passes + 2 reductions) of the Jacobi-preconditioned CG on
+the 256^3 system; the matrix and right-hand side are generated and assembled
+on the GPUs before timing (synthetic data).  Work per step is
+fixed across N (strong scaling): value = K / max-over-ranks(time of K steps).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 256]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+The timed solve runs with rtol = 0 so exactly K iterations execute; the
+converged solve (default rtol 1e-5) is reported separately as time-to-solution.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpi-petsc4py-example_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak, MI355X_MICROARCH.md chip table
+METRIC = "CG iters/s + SpMV HBM GB/s (% peak), 3D Poisson 256³ at 1/2/4/8 GPUs"
+
+
+def spmv_bytes(m: int, nnz: int, nghost: int) -> int:
+    """Algorithmic bytes of one SpMV on one rank:
+    fp64 values + int32 columns, row pointer, x (local + ghosts) read once, y written once."""
+    return 12 * nnz + 4 * (m + 1) + 8 * (m + nghost) + 8 * m
+
+
+def cg_iter_bytes(m: int, nnz: int, nghost: int) -> int:
+    """Fused CG iteration minimum: SpMV + 88 B/row of vector traffic."""
+    return spmv_bytes(m, nnz, nghost) + 88 * m
+
+
+def cpu_baseline(grid: int, budget_s: float, threads: int) -> dict:
+    """The oracle's C restatement of PETSc's CG (oracle/petsc_oracle.c) timed on the
+    host cores over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle
+    t0 = time.perf_counter()
+    ip, c, v = oracle.stencil("poisson3d", grid)
+    M = ip.size - 1
+    A = oracle.OracleMat.from_csr(M, M, ip, c, v)
+    del ip, c, v
+    b = oracle.rhs_hash(0, M)
+    setup = time.perf_counter() - t0
+    A.solve(b, ksp="cg", rtol=0.0, max_it=2, nthreads=threads)      # warm threads/pages
+    t0 = time.perf_counter()
+    A.solve(b, ksp="cg", rtol=0.0, max_it=10, nthreads=threads)
+    probe = (time.perf_counter() - t0) / 10
+    its = int(max(20, min(5000, budget_s / max(probe, 1e-6))))
+    t0 = time.perf_counter()
+    r = A.solve(b, ksp="cg", rtol=0.0, max_it=its, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(r["its"] / dt, 3), "unit": "CG iterations/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{r['its']} CG+Jacobi iterations on the full {grid}^3 7-point system "
+                      f"(oracle/petsc_oracle.c, PETSc-restatement not PETSc, OpenMP {threads} threads, "
+                      f"{dt:.1f} s; matrix build {setup:.1f} s untimed)"}
+
+
+def load_traffic(grid: int, n_gpus: int):
+    path = os.path.join(ROOT, "profiles", "spmv_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        key = f"{grid}^3/N{n_gpus}"
+        return d.get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--grid", type=int, default=256)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-solve", action="store_true", help="skip the converged solve")
+    args = ap.parse_args()
+
+    import torch
+    from mxsolve.core import DeviceComm, DMat, rhs_hash, unique_id
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        uid = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = DeviceComm.rccl(rank, world, uid[0], device=local)
+    else:
+        comm = DeviceComm.self_comm(local)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(v: float) -> float:
+        if dist is None:
+            return v
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    n = args.grid
+    barrier()
+    t0 = time.perf_counter()
+    A = DMat.stencil(comm, "poisson3d", n)
+    barrier()
+    t_asm = max_over_ranks(time.perf_counter() - t0)
+    info = A.info()
+    m, nnz_loc, ng = info["m"], info["nnz_d"] + info["nnz_o"], info["nghost"]
+    b = comm.empty(m)
+    rhs_hash(comm, info["rstart"], b)
+    x = comm.zeros(m)
+
+    # warmup: W iterations
+    if args.warmup > 0:
+        A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=args.warmup)
+    # timed: exactly K iterations (rtol = 0 never stops early)
+    barrier()
+    t0 = time.perf_counter()
+    r = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=args.steps, profile=True)
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    assert r["its"] == args.steps, r
+    value = args.steps / dt
+
+    spmv_avg_ms = r["spmv_ms"] / max(r["spmv_count"], 1)
+    bytes_spmv = spmv_bytes(m, nnz_loc, ng)
+    achieved = bytes_spmv / (spmv_avg_ms * 1e-3) / 1e9
+    # standalone SpMV timing (same kernel, back-to-back)
+    y = comm.empty(m)
+    spmv_alone_ms, mult_ms = A.bench_mult(b, y, 50)
+
+    solve = None
+    if not args.no_solve:
+        x.zero_()
+        barrier()
+        t0 = time.perf_counter()
+        rs = A.solve(b, x, ksp="cg", pc="jacobi")
+        barrier()
+        ts = max_over_ranks(time.perf_counter() - t0)
+        solve = {"its": rs["its"], "reason": rs["reason"], "time_s": round(ts, 4),
+                 "its_per_s": round(rs["its"] / ts, 2), "assembly_s": round(t_asm, 3),
+                 "time_to_solution_s": round(ts + t_asm, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+        threads = max(1, min(threads, 16))
+        cpu = cpu_baseline(n, args.cpu_seconds, threads)
+
+    if rank == 0:
+        traffic = load_traffic(n, world)
+        out = {
+            "metric": METRIC, "value": round(value, 3), "unit": "CG iterations/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"3D 7-point Poisson {n}^3, CG + Jacobi, fp64, row-block partitioned",
+                       "rows": info["M"], "nnz": int(7 * n**3 - 6 * n**2),
+                       "parallelism": f"row-block x{world} (RCCL halo + allreduce)" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "spmv_sell_kernel<SPMV_DOT> (in-solve launches, rank 0)",
+                         "bytes_per_launch": bytes_spmv, "avg_launch_ms": round(spmv_avg_ms, 5)},
+            "cpu_baseline": cpu,
+            "spmv_standalone": {"avg_ms": round(spmv_alone_ms, 5),
+                                "GBps": round(bytes_spmv / (spmv_alone_ms * 1e-3) / 1e9, 1),
+                                "matmult_ms": round(mult_ms, 5)},
+            "cg_iter_bytes_alg": cg_iter_bytes(m, nnz_loc, ng),
+            "cg_iter_GBps_alg": round(cg_iter_bytes(m, nnz_loc, ng) * value / 1e9, 1),
+            "solve": solve,
+        }
+        print(json.dumps(out), flush=True)
+    A.destroy()
+    comm.destroy()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

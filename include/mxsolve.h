@@ -172,6 +172,19 @@ int mx_ksp_solve(mx_mat A, const mx_ksp_params *p, const double *b_dev, double *
                  mx_ksp_result *res, double *history_host /* NULL or max_it+2 */);
 void mx_ksp_default_params(mx_ksp_params *p);
 
+/* ---- direct solve: replaces KSPPREONLY + PCLU (+ MUMPS) of test.py:38-43,138
+ *      (SURVEY.md §8f F1).  The caller gathers the whole square system (global
+ *      CSR, host) to one rank; it is densified and LU-factored with partial
+ *      pivoting on that rank's GPU.  n <= 16384.                              */
+int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *cols,
+                    const double *vals, const double *b, double *x);
+
+/* ---- measurement knobs (A/B runs only; defaults are the product path) -------
+ * key 1: SpMV non-temporal matrix loads (0/1); key 2: plain, unpaired SELL
+ * layout (0/1, needs MX_SPMV_AB=1 in the environment at assembly);
+ * key 3: SpMV grid size in workgroups.  Returns the previous value.          */
+int mx_debug_set(int key, int value);
+
 #ifdef __cplusplus
 }
 #endif

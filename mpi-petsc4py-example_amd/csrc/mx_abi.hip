@@ -377,6 +377,22 @@ void mx_ksp_default_params(mx_ksp_params *p) {
   p->poll_every = 16;
 }
 
+int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *cols,
+                    const double *vals, const double *b, double *x) {
+  return guard([&] { dense_lu_solve(C(c), n, indptr, cols, vals, b, x); });
+}
+
+int mx_debug_set(int key, int value) {
+  int old = -1;
+  switch (key) {
+    case 1: old = g_knobs.spmv_nt; g_knobs.spmv_nt = value; break;
+    case 2: old = g_knobs.spmv_plain; g_knobs.spmv_plain = value; break;
+    case 3: old = g_knobs.spmv_grid; if (value > 0) g_knobs.spmv_grid = value; break;
+    default: break;
+  }
+  return old;
+}
+
 int mx_ksp_solve(mx_mat a, const mx_ksp_params *p, const double *b, double *x, mx_ksp_result *res,
                  double *history) {
   return guard([&] {

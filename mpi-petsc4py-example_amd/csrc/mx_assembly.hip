@@ -26,6 +26,7 @@
 //     requested indices sent to their owners, contiguous send ranges detected.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "mx_internal.hpp"
 
@@ -65,7 +66,14 @@ __global__ void row_len_max_kernel(int64_t m, const int64_t *__restrict__ rowptr
     unsigned long long t = __shfl_xor(mx, o, 64);
     mx = t > mx ? t : mx;
   }
-  if ((threadIdx.x & 63) == 0 && mx) atomicMax(out, mx);
+  __shared__ unsigned long long sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mx = sh[0];
+    for (int k = 1; k < 4; ++k) mx = sh[k] > mx ? sh[k] : mx;
+    if (mx) atomicMax(out, mx);   // one atomic per block
+  }
 }
 
 // ---------------------------------------------------------------- COO bucketing
@@ -313,6 +321,7 @@ __global__ void sell_width_kernel(int64_t m, const int64_t *__restrict__ ptr, in
   if (s < nslices && lane == 0) { width[s] = len; slots[s] = (int64_t)len * SLICE; }
 }
 
+template <bool PAIRED>
 __global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
                                  const int32_t *__restrict__ ccol, const double *__restrict__ cval,
                                  int64_t nslices, const int64_t *__restrict__ sptr,
@@ -323,13 +332,17 @@ __global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
   const int lane = threadIdx.x & 63;
   const int64_t row = s * SLICE + lane;
   const int w = width[s];
-  const int64_t base = sptr[s] + lane;
+  const int64_t base = sptr[s];
   const int64_t rs = row < m ? ptr[row] : 0;
   const int len = row < m ? (int)(ptr[row + 1] - rs) : 0;
   for (int j = 0; j < w; ++j) {
     const bool in = j < len;
-    scol[base + (int64_t)j * SLICE] = in ? ccol[rs + j] : -1;
-    sval[base + (int64_t)j * SLICE] = in ? cval[rs + j] : 0.0;
+    int64_t t;
+    if (PAIRED) t = base + ((j >> 1) < (w >> 1) ? (int64_t)(j >> 1) * 2 * SLICE + 2 * lane + (j & 1)
+                                                 : (int64_t)(w >> 1) * 2 * SLICE + lane);
+    else t = base + (int64_t)j * SLICE + lane;
+    scol[t] = in ? ccol[rs + j] : -1;
+    sval[t] = in ? cval[rs + j] : 0.0;
   }
 }
 
@@ -345,9 +358,17 @@ static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *co
   exclusive_scan_i64(S.sptr.p, S.sptr.p, ns, st, &S.slots);
   S.col.alloc((size_t)std::max<int64_t>(S.slots, 1));
   S.val.alloc((size_t)std::max<int64_t>(S.slots, 1));
-  sell_fill_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
-                                                          S.col.p, S.val.p);
+  sell_fill_kernel<true><<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
+                                                                S.col.p, S.val.p);
   HIPCHECK(hipGetLastError());
+  const char *ab = std::getenv("MX_SPMV_AB");
+  if (ab && ab[0] == '1') {   // plain-layout copy for A/B measurements only
+    S.col_plain.alloc((size_t)std::max<int64_t>(S.slots, 1));
+    S.val_plain.alloc((size_t)std::max<int64_t>(S.slots, 1));
+    sell_fill_kernel<false><<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
+                                                                   S.col_plain.p, S.val_plain.p);
+    HIPCHECK(hipGetLastError());
+  }
 }
 
 // ---------------------------------------------------------------- halo plan

@@ -78,13 +78,26 @@ void get_unique_id(void *out, size_t len);
 // ---------------------------------------------------------------- matrix
 constexpr int SLICE = 64;  // SELL-C with C = one wavefront
 
+// SELL-64: slice s = rows [64 s, 64 s + 64), `width[s]` slots per row.
+// Paired layout (default): entries (2p, 2p+1) of a row are adjacent, so a lane
+// loads 16 B of values and 8 B of column ids per pair; an odd last entry sits
+// in a trailing single region:  pair p at sptr + 128 p + 2 lane (+0/+1),
+// tail at sptr + 128 (w/2) + lane.  Same slot count as the plain layout
+// (entry j at sptr + 64 j + lane), which is kept only for A/B runs.
 struct Sell {
   int64_t nslices = 0, slots = 0;
+  bool paired = true;
   DBuf<int64_t> sptr;    // [nslices] slot offset of each slice
   DBuf<int32_t> width;   // [nslices]
   DBuf<int32_t> col;     // [slots], -1 = padding
   DBuf<double> val;      // [slots]
+  DBuf<int32_t> col_plain;  // A/B only (MX_SPMV_AB=1)
+  DBuf<double> val_plain;
 };
+
+// runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
+struct Knobs { int spmv_nt = 1; int spmv_plain = 0; int spmv_grid = 2048; };
+extern Knobs g_knobs;
 
 struct Halo {
   // receive side: ghosts arrive grouped by owner, contiguous in lvec
@@ -156,6 +169,10 @@ void vec_set(hipStream_t s, int64_t n, double a, double *x);
 void vec_rhs_hash(hipStream_t s, int64_t i0, int64_t n, double *b);
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t s,
                         int64_t *total_host);
+
+// direct solve (mx_direct.hip)
+void dense_lu_solve(Comm *c, int64_t n, const int64_t *ip, const int64_t *cj, const double *vv,
+                    const double *b, double *x);
 
 // KSP (mx_ksp.hip)
 void ksp_solve(Mat *A, const mx_ksp_params &p, const double *b, double *x, mx_ksp_result &r,

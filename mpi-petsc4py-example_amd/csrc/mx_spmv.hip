@@ -17,14 +17,30 @@
 // own row sequentially -- which is exactly the order PETSc sums in.  Padding
 // slots carry column -1 and are skipped.  A_o gets its own SELL structure;
 // slices with no ghost entries have width 0 and cost one scalar load.
+#include <algorithm>
+
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 
 namespace mx {
 
-constexpr int SPMV_WAVES = 4;  // 256-thread workgroups, one slice per wave
+constexpr int SPMV_WAVES = 4;  // 256-thread workgroups, one slice per wave at a time
+Knobs g_knobs;
 
-template <int MODE>
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef int int2v __attribute__((ext_vector_type(2)));
+
+template <bool NT, class T> __device__ __forceinline__ T ld(const T *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+// One wave sweeps slices; lane = row.  Grid-stride over a fixed grid whose
+// blocks are grouped by XCD (block b runs on XCD b % 8 under the observed
+// round-robin dispatch): each XCD walks one contiguous eighth of the slices in
+// order, so the +-1 / +-n / +-n^2 re-reads of x stay in that XCD's 4 MB L2.
+// Placement only affects speed, never results.
+template <int MODE, bool NT, bool PAIRED>
 __global__ void __launch_bounds__(256) spmv_sell_kernel(
     int64_t m, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
@@ -34,45 +50,86 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     const double *__restrict__ lvec, double *__restrict__ y, const double *__restrict__ dinv,
     double *__restrict__ partials, const int *__restrict__ done) {
   if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
-  const int lane = threadIdx.x & 63;
-  const int64_t s = (int64_t)blockIdx.x * SPMV_WAVES + (threadIdx.x >> 6);
-  const int64_t row = s * SLICE + lane;
-  double sum = 0.0;
-  if (s < nslices) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t s0, sstep, send;
+  if ((gridDim.x & 7) == 0) {
+    const int64_t per = gridDim.x >> 3;                 // blocks per XCD group
+    const int64_t xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int64_t chunk = (nslices + 7) >> 3;
+    s0 = xcd * chunk + j * SPMV_WAVES + wid;
+    sstep = per * SPMV_WAVES;
+    send = min(nslices, (xcd + 1) * chunk);
+  } else {
+    s0 = (int64_t)blockIdx.x * SPMV_WAVES + wid;
+    sstep = (int64_t)gridDim.x * SPMV_WAVES;
+    send = nslices;
+  }
+  double dot = 0.0;
+  for (int64_t s = s0; s < send; s += sstep) {
+    const int64_t row = s * SLICE + lane;
+    double sum = 0.0;
     const int w = wid_d[s];
-    const int32_t *__restrict__ cp = col_d + sptr_d[s] + lane;
-    const double *__restrict__ vp = val_d + sptr_d[s] + lane;
+    const int64_t base = sptr_d[s];
+    if (PAIRED) {
+      const int np = w >> 1;
+      const int2v *__restrict__ cp = reinterpret_cast<const int2v *>(col_d + base) + lane;
+      const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(val_d + base) + lane;
+#pragma unroll 2
+      for (int p = 0; p < np; ++p) {
+        const int2v c = ld<NT>(cp + (int64_t)p * SLICE);
+        const dbl2 v = ld<NT>(vp + (int64_t)p * SLICE);
+        if (c.x >= 0) sum = sum + v.x * x[c.x];
+        if (c.y >= 0) sum = sum + v.y * x[c.y];
+      }
+      if (w & 1) {
+        const int64_t t = base + (int64_t)np * 2 * SLICE + lane;
+        const int c = ld<NT>(col_d + t);
+        const double v = ld<NT>(val_d + t);
+        if (c >= 0) sum = sum + v * x[c];
+      }
+    } else {
+      const int32_t *__restrict__ cp = col_d + base + lane;
+      const double *__restrict__ vp = val_d + base + lane;
 #pragma unroll 4
-    for (int j = 0; j < w; ++j) {
-      const int c = cp[(int64_t)j * SLICE];
-      const double v = vp[(int64_t)j * SLICE];
-      if (c >= 0) sum = sum + v * x[c];
+      for (int j = 0; j < w; ++j) {
+        const int c = ld<NT>(cp + (int64_t)j * SLICE);
+        const double v = ld<NT>(vp + (int64_t)j * SLICE);
+        if (c >= 0) sum = sum + v * x[c];
+      }
     }
     if (lvec) {
       const int wo = wid_o[s];
-      if (wo) {
-        const int32_t *__restrict__ co = col_o + sptr_o[s] + lane;
-        const double *__restrict__ vo = val_o + sptr_o[s] + lane;
+      if (wo) {   // ghost block: rare, plain sequential continuation of the row sum
+        const int64_t bo = sptr_o[s];
         for (int j = 0; j < wo; ++j) {
-          const int c = co[(int64_t)j * SLICE];
-          const double v = vo[(int64_t)j * SLICE];
+          int64_t t;
+          if (PAIRED) t = bo + ((j >> 1) < (wo >> 1) ? (int64_t)(j >> 1) * 2 * SLICE + 2 * lane + (j & 1)
+                                                     : (int64_t)(wo >> 1) * 2 * SLICE + lane);
+          else t = bo + (int64_t)j * SLICE + lane;
+          const int c = col_o[t];
+          const double v = val_o[t];
           if (c >= 0) sum = sum + v * lvec[c];
         }
       }
     }
+    if (row < m) {
+      if (MODE == SPMV_JACOBI) y[row] = sum * dinv[row];   // PCApply_Jacobi fused: w_i * d_i
+      else y[row] = sum;
+      if (MODE == SPMV_DOT) dot += x[row] * sum;           // VecDot(p, w) partial, p = x
+    }
   }
-  if (MODE == SPMV_JACOBI) {
-    if (row < m) y[row] = sum * dinv[row];      // PCApply_Jacobi fused: w_i * d_i
-  } else {
-    if (row < m) y[row] = sum;
-  }
-  if (MODE == SPMV_DOT) {                       // VecDot(p, w) partial, p = x
-    double v[1] = {row < m ? x[row] * sum : 0.0};
+  if (MODE == SPMV_DOT) {
+    double v[1] = {dot};
     block_sum_to_partials<1>(v, partials, gridDim.x);
   }
 }
 
-int spmv_blocks(const Mat *A) { return (int)std::max<int64_t>(1, cdiv(A->sd.nslices, SPMV_WAVES)); }
+int spmv_blocks(const Mat *A) {
+  const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
+  int64_t g = std::min<int64_t>(need, g_knobs.spmv_grid);
+  if (g >= 64) g &= ~int64_t(7);   // multiple of 8: XCD grouping
+  return (int)std::max<int64_t>(1, g);
+}
 
 __global__ void pack_kernel(int64_t n, const int32_t *__restrict__ idx, const double *__restrict__ x,
                             double *__restrict__ buf) {
@@ -106,15 +163,32 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, const double *din
   hipStream_t st = A->comm->stream;
   const unsigned grid = (unsigned)spmv_blocks(A);
   const double *lvec = A->nghost ? A->halo.lvec.p : nullptr;
-#define SPMV_ARGS                                                                              \
-  A->m, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->so.sptr.p,   \
-      A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, dinv, partials, done_flag
+  const bool plain = g_knobs.spmv_plain && A->sd.col_plain.p;
+  const int32_t *cd = plain ? A->sd.col_plain.p : A->sd.col.p;
+  const double *vd = plain ? A->sd.val_plain.p : A->sd.val.p;
+  const int32_t *co = plain ? A->so.col_plain.p : A->so.col.p;
+  const double *vo = plain ? A->so.val_plain.p : A->so.val.p;
+  if (plain && A->nghost && !co) fail(MX_ERR_INTERNAL, "plain SELL copy missing");
+#define SPMV_ARGS                                                                        \
+  A->m, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, cd, vd, A->so.sptr.p, A->so.width.p, \
+      co, vo, x, lvec, y, dinv, partials, done_flag
+#define SPMV_GO(MODE)                                                                           \
+  do {                                                                                          \
+    if (plain) {                                                                                \
+      if (g_knobs.spmv_nt) spmv_sell_kernel<MODE, true, false><<<grid, 256, 0, st>>>(SPMV_ARGS);  \
+      else spmv_sell_kernel<MODE, false, false><<<grid, 256, 0, st>>>(SPMV_ARGS);                 \
+    } else {                                                                                    \
+      if (g_knobs.spmv_nt) spmv_sell_kernel<MODE, true, true><<<grid, 256, 0, st>>>(SPMV_ARGS);   \
+      else spmv_sell_kernel<MODE, false, true><<<grid, 256, 0, st>>>(SPMV_ARGS);                  \
+    }                                                                                           \
+  } while (0)
   switch (mode) {
-    case SPMV_PLAIN: spmv_sell_kernel<SPMV_PLAIN><<<grid, 256, 0, st>>>(SPMV_ARGS); break;
-    case SPMV_JACOBI: spmv_sell_kernel<SPMV_JACOBI><<<grid, 256, 0, st>>>(SPMV_ARGS); break;
-    case SPMV_DOT: spmv_sell_kernel<SPMV_DOT><<<grid, 256, 0, st>>>(SPMV_ARGS); break;
+    case SPMV_PLAIN: SPMV_GO(SPMV_PLAIN); break;
+    case SPMV_JACOBI: SPMV_GO(SPMV_JACOBI); break;
+    case SPMV_DOT: SPMV_GO(SPMV_DOT); break;
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
+#undef SPMV_GO
 #undef SPMV_ARGS
   HIPCHECK(hipGetLastError());
 }

@@ -89,6 +89,8 @@ SIGNATURES = {
     "mx_vec_rhs_hash": (C.c_int, [P, I64, I64, P]),
     "mx_ksp_solve": (C.c_int, [P, C.POINTER(KSPParams), P, P, C.POINTER(KSPResult), P]),
     "mx_ksp_default_params": (None, [C.POINTER(KSPParams)]),
+    "mx_lu_solve_csr": (C.c_int, [P, I64, P, P, P, P, P]),
+    "mx_debug_set": (C.c_int, [C.c_int, C.c_int]),
 }
 
 _lib = None

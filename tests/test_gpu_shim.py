@@ -1,0 +1,144 @@
+"""The petsc4py/mpi4py/slepc4py-compatible API on the GPU: the reference's call
+sequences (test.py, test2.py, petsc_funcs.py) through our from-scratch drivers."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMPAT = os.path.join(ROOT, "mpi-petsc4py-example_amd", "compat")
+
+
+def run_driver(script, *args, timeout=300):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "examples", script), *args],
+                         capture_output=True, text=True, timeout=timeout, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return out.stdout
+
+
+def test_linear_solve_driver_lu():
+    """test.py as shipped: preonly + lu (mumps) -> prints True (test.py:149)."""
+    assert run_driver("linear_solve_driver.py").strip().splitlines()[-1] == "True"
+
+
+def test_linear_solve_driver_gmres_options():
+    """test.py with -ksp_type gmres -ksp_gmres_restart 100 -pc_type jacobi (options override, test.py:46)."""
+    out = run_driver("linear_solve_driver.py", "-ksp_type", "gmres", "-ksp_gmres_restart", "100",
+                     "-pc_type", "jacobi", "-ksp_converged_reason", "-ksp_rtol", "1e-12")
+    lines = out.strip().splitlines()
+    assert lines[-1] == "True"
+    assert any("Linear solve converged due to CONVERGED_RTOL" in ln for ln in lines)
+
+
+def test_eigen_driver(golden):
+    out = run_driver("eigen_driver.py")
+    vals = [float(ln.split()[-1]) for ln in out.splitlines() if ln.startswith("Eigenvalue")]
+    assert len(vals) >= 1
+    assert abs(vals[0] - 558.4042205474284) <= 1e-8 * 558.4
+    ev = golden["tri_eigs"]
+    top = ev[np.argsort(-np.abs(ev))][: len(vals)]
+    assert np.allclose(vals, top, rtol=1e-8)
+
+
+@pytest.fixture(scope="module")
+def PETSc():
+    sys.path.insert(0, COMPAT)
+    from mxsolve import PETSc as P
+    return P
+
+
+def test_create_petsc_mat_roundtrip(PETSc, golden):
+    from mxsolve import petsc_funcs
+    from mxsolve import MPI
+    A = petsc_funcs.createPETScMat(MPI.COMM_WORLD, (100, 100),
+                                   (golden["sys_indptr"], golden["sys_indices"], golden["sys_data"]))
+    ip, cj, vv = A.getValuesCSR()
+    assert np.array_equal(ip, golden["sys_indptr"]) and np.array_equal(cj, golden["sys_indices"])
+    assert np.array_equal(vv, golden["sys_data"])
+    assert A.getSize() == (100, 100) and A.getOwnershipRange() == (0, 100) and A.getType() == "seqaij"
+    with pytest.raises(ValueError):
+        PETSc.Mat().createAIJ(size=(100, 100), csr=(golden["sys_indptr"][:-1], golden["sys_indices"], golden["sys_data"]))
+    with pytest.raises(ValueError):
+        PETSc.Mat().createAIJ(size=(100, 100), csr=(golden["sys_indptr"], golden["sys_indices"][:-1], golden["sys_data"]))
+    bad = golden["sys_indices"].copy()
+    bad[5] = 100
+    with pytest.raises(PETSc.Error):
+        PETSc.Mat().createAIJ(size=(100, 100), csr=(golden["sys_indptr"], bad, golden["sys_data"]))
+
+
+def test_setvalues_assembly(PETSc, oracle_mod):
+    rng = np.random.default_rng(11)
+    n = 60
+    A = PETSc.Mat().createAIJ(size=(n, n), nnz=8)
+    rows, cols, vals = [], [], []
+    for _ in range(300):
+        i, j = rng.integers(0, n, 2)
+        v = float(rng.integers(-4, 5))
+        A.setValue(int(i), int(j), v, addv=PETSc.InsertMode.ADD_VALUES)
+        rows.append(i); cols.append(j); vals.append(v)
+    A.assemble()
+    O = oracle_mod.OracleMat.from_coo(n, n, np.array([0, len(rows)]), np.array(rows), np.array(cols), np.array(vals), add=True)
+    ip, cj, vv = A.getValuesCSR()
+    oip, ocj, ovv = O.csr()
+    assert np.array_equal(ip, oip) and np.array_equal(cj, ocj) and np.array_equal(vv, ovv)
+
+
+def test_vec_ops(PETSc):
+    v = PETSc.Vec().createMPI(1000)
+    a = np.sin(np.arange(1000.0))
+    v.setArray(a)
+    w = v.duplicate()
+    w.setArray(np.cos(np.arange(1000.0)))
+    assert abs(v.dot(w) - a @ np.cos(np.arange(1000.0))) < 1e-12
+    assert abs(v.norm() - np.linalg.norm(a)) < 1e-12
+    w.axpy(2.0, v)
+    assert np.allclose(w.array, 2.0 * a + np.cos(np.arange(1000.0)), rtol=1e-15, atol=1e-15)
+    z = v.duplicate()
+    z.pointwiseMult(v, v)
+    assert np.array_equal(z.array, a * a)
+
+
+def test_ksp_cg_options(PETSc, oracle_mod):
+    PETSc.Options().setValue("ksp_type", "cg")
+    PETSc.Options().setValue("pc_type", "jacobi")
+    try:
+        ip, c, v = oracle_mod.stencil("poisson3d", 16)
+        M = ip.size - 1
+        A = PETSc.Mat().createAIJ(size=(M, M), csr=(ip, c, v))
+        x, b = A.getVecs()
+        b.setArray(oracle_mod.rhs_hash(0, M))
+        ksp = PETSc.KSP().create()
+        ksp.setType("gmres")           # overridden by the options database
+        ksp.setOperators(A)
+        ksp.setFromOptions()
+        ksp.solve(b, x)
+        o = oracle_mod.OracleMat.from_csr(M, M, ip, c, v).solve(oracle_mod.rhs_hash(0, M), ksp="cg")
+        assert ksp.getType() == "cg"
+        assert ksp.getIterationNumber() == o["its"] and ksp.getConvergedReason() == o["reason"]
+        assert np.linalg.norm(x.array - o["x"]) / np.linalg.norm(o["x"]) <= 1e-10
+        assert abs(ksp.getResidualNorm() - o["rnorm"]) <= 1e-8 * o["rnorm"]
+    finally:
+        PETSc.Options().delValue("ksp_type")
+        PETSc.Options().delValue("pc_type")
+
+
+def test_ksp_not_converged_does_not_raise(PETSc, oracle_mod):
+    ip, c, v = oracle_mod.stencil("poisson3d", 12)
+    M = ip.size - 1
+    A = PETSc.Mat().createAIJ(size=(M, M), csr=(ip, c, v))
+    x, b = A.getVecs()
+    b.set(1.0)
+    ksp = PETSc.KSP().create()
+    ksp.setType("cg")
+    ksp.getPC().setType("jacobi")
+    ksp.setTolerances(rtol=1e-12, max_it=5)
+    ksp.setOperators(A)
+    ksp.solve(b, x)
+    assert ksp.getConvergedReason() == PETSc.KSP.ConvergedReason.DIVERGED_ITS
+    assert ksp.getIterationNumber() == 5
