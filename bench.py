@@ -182,7 +182,8 @@ def main():
                        "parallelism": f"row-block x{world} (RCCL halo + allreduce)" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_detail": traffic,
                          "kernel": "spmv_sell_kernel<SPMV_DOT> (in-solve launches, rank 0)",
                          "bytes_per_launch": bytes_spmv, "avg_launch_ms": round(spmv_avg_ms, 5)},
             "cpu_baseline": cpu,

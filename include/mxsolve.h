@@ -184,6 +184,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * layout (0/1, needs MX_SPMV_AB=1 in the environment at assembly);
  * key 3: SpMV grid size in workgroups.  Returns the previous value.          */
 int mx_debug_set(int key, int value);
+/* Calibration stream for PMC byte counters: reads n doubles once with
+ * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,
+ * and writes one partial sum per workgroup to out_dev.                      */
+int mx_debug_stream_read(mx_comm c, const double *x_dev, int64_t n, int width_bytes, double *out_dev);
 
 #ifdef __cplusplus
 }

@@ -393,6 +393,14 @@ int mx_debug_set(int key, int value) {
   return old;
 }
 
+int mx_debug_stream_read(mx_comm c, const double *x, int64_t n, int width, double *out) {
+  return guard([&] {
+    Comm *k = C(c);
+    debug_stream_read(k->stream, x, n, width, out);
+    HIPCHECK(hipStreamSynchronize(k->stream));
+  });
+}
+
 int mx_ksp_solve(mx_mat a, const mx_ksp_params *p, const double *b, double *x, mx_ksp_result *res,
                  double *history) {
   return guard([&] {

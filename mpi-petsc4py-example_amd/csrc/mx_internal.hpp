@@ -167,6 +167,7 @@ void vec_pmult(hipStream_t s, int64_t n, const double *x, const double *y, doubl
 void vec_scale(hipStream_t s, int64_t n, double a, double *x);
 void vec_set(hipStream_t s, int64_t n, double a, double *x);
 void vec_rhs_hash(hipStream_t s, int64_t i0, int64_t n, double *b);
+void debug_stream_read(hipStream_t s, const double *x, int64_t n, int width, double *out);
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t s,
                         int64_t *total_host);
 

@@ -137,6 +137,32 @@ void vec_rhs_hash(hipStream_t s, int64_t i0, int64_t n, double *b) {
   HIPCHECK(hipGetLastError());
 }
 
+// ------------------------------------------------------------- PMC calibration stream
+typedef double dbl2v __attribute__((ext_vector_type(2)));
+template <int W>
+__global__ void __launch_bounds__(256) stream_read_kernel(const double *__restrict__ x, int64_t n,
+                                                          double *__restrict__ out) {
+  double v[1] = {0.0};
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  if (W == 16) {
+    const dbl2v *x2 = reinterpret_cast<const dbl2v *>(x);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n / 2; i += stride) {
+      const dbl2v t = __builtin_nontemporal_load(x2 + i);
+      v[0] += t.x + t.y;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+      v[0] += __builtin_nontemporal_load(x + i);
+  }
+  block_sum_to_partials<1>(v, out, gridDim.x);
+}
+
+void debug_stream_read(hipStream_t s, const double *x, int64_t n, int width, double *out) {
+  if (width == 16) stream_read_kernel<16><<<2048, 256, 0, s>>>(x, n, out);
+  else stream_read_kernel<8><<<2048, 256, 0, s>>>(x, n, out);
+  HIPCHECK(hipGetLastError());
+}
+
 // ------------------------------------------------------------- exclusive scan (int64)
 constexpr int SCAN_BLOCK = 256, SCAN_ITEMS = 8, SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 

@@ -91,6 +91,7 @@ SIGNATURES = {
     "mx_ksp_default_params": (None, [C.POINTER(KSPParams)]),
     "mx_lu_solve_csr": (C.c_int, [P, I64, P, P, P, P, P]),
     "mx_debug_set": (C.c_int, [C.c_int, C.c_int]),
+    "mx_debug_stream_read": (C.c_int, [P, P, I64, C.c_int, P]),
 }
 
 _lib = None

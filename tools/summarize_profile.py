@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Turn a gpurun_out/prof directory (tools/profile.sh) into committed
+profiles/: the rocprofv3 kernel stats, per-kernel PMC byte counts and the
+calibrated per-launch HBM traffic of the SpMV (profiles/spmv_traffic.json,
+read by bench.py for roofline.traffic).
+
+    python tools/summarize_profile.py gpurun_out/prof r01 [grid] [n_gpus]
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc(path):
+    per = {}
+    for r in csv.DictReader(open(path)):
+        per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    grid = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    ngpu = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    fetch = pmc(os.path.join(src, "fetch", "run_counter_collection.csv"))
+    write = pmc(os.path.join(src, "write", "run_counter_collection.csv"))
+    calib = pmc(os.path.join(src, "calib", "run_counter_collection.csv"))
+    known = (1 << 27) * 8
+    # the calibration runs 3 launches at 8 B/lane then 3 at 16 B/lane
+    cal = calib.get("stream_read_kernel", [])
+    f8 = known / (statistics.median(cal[:3]) * 1024) if len(cal) >= 6 else None
+    f16 = known / (statistics.median(cal[3:6]) * 1024) if len(cal) >= 6 else None
+    m = grid ** 3 // ngpu
+    nnz = 7 * grid ** 3 - 6 * grid ** 2
+    alg = 12 * nnz + 4 * (m + 1) + 8 * m + 8 * m
+    out = {}
+    lines = [f"# {tag}: rocprofv3 summary (3D 7-pt Poisson {grid}^3, N={ngpu}, bench.py --steps 50)", "",
+             "| kernel | calls | avg us | % time | FETCH_SIZE KB (raw, median) | WRITE_SIZE KB (median) |",
+             "|---|---|---|---|---|---|"]
+    for r in stats[:14]:
+        k = r["Name"]
+        fk = statistics.median(fetch[k]) if k in fetch else None
+        wk = statistics.median(write[k]) if k in write else None
+        lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.1f} | "
+                     f"{'' if fk is None else f'{fk:.0f}'} | {'' if wk is None else f'{wk:.0f}'} |")
+    sp = "spmv_sell_kernel"
+    if sp in fetch and sp in write:
+        fr = statistics.median(fetch[sp]) * 1024
+        wr = statistics.median(write[sp]) * 1024
+        corr = f16 if f16 else 2.0
+        traffic = fr * corr + wr
+        out[f"{grid}^3/N{ngpu}"] = {
+            "bytes_per_launch": round(traffic), "fetch_bytes_raw": round(fr), "write_bytes": round(wr),
+            "fetch_correction": round(corr, 4), "calib_8B_per_lane": f8 and round(f8, 4),
+            "calib_16B_per_lane": f16 and round(f16, 4), "algorithmic_bytes": alg,
+            "traffic_over_algorithmic": round(traffic / alg, 4), "source": f"profiles/{tag}_summary.md"}
+        lines += ["", f"SpMV per launch: FETCH_SIZE {fr/1e6:.1f} MB raw x {corr:.3f} (calibrated, 16 B/lane NT stream; "
+                  f"8 B/lane factor {f8 and round(f8, 3)}) + WRITE_SIZE {wr/1e6:.1f} MB = {traffic/1e6:.1f} MB "
+                  f"vs {alg/1e6:.1f} MB algorithmic ({traffic/alg:.3f}x)."]
+    with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    tj = os.path.join(dst, "spmv_traffic.json")
+    cur = json.load(open(tj)) if os.path.exists(tj) else {}
+    cur.update(out)
+    json.dump(cur, open(tj, "w"), indent=1, sort_keys=True)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
