@@ -84,6 +84,7 @@ typedef struct {
   int64_t sell_slots_d, sell_slots_o; /* padded SELL-64 slots (bytes model)           */
   int nsend_peers, nrecv_peers;       /* halo neighbours                              */
   int64_t nsend, nrecv;               /* halo values per MatMult                      */
+  int64_t dia_slices;                 /* A_d slices stored with aligned offsets       */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */
@@ -180,9 +181,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
                     const double *vals, const double *b, double *x);
 
 /* ---- measurement knobs (A/B runs only; defaults are the product path) -------
- * key 1: SpMV non-temporal matrix loads (0/1); key 2: plain, unpaired SELL
- * layout (0/1, needs MX_SPMV_AB=1 in the environment at assembly);
- * key 3: SpMV grid size in workgroups.  Returns the previous value.          */
+ * key 1: SpMV non-temporal matrix loads (0/1); key 3: SpMV grid size in
+ * workgroups; key 4: aligned-offset (DIA-in-SELL)
+ * slices at assembly (0/1, default 1).  Returns the previous value.          */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,

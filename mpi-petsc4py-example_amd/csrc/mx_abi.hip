@@ -223,6 +223,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->nsend_peers = (int)A->halo.send_peer.size();
     info->nrecv_peers = (int)A->halo.recv_peer.size();
     info->nsend = A->halo.nsend; info->nrecv = A->halo.nrecv;
+    info->dia_slices = A->sd.dia_slices;
   });
 }
 
@@ -386,8 +387,8 @@ int mx_debug_set(int key, int value) {
   int old = -1;
   switch (key) {
     case 1: old = g_knobs.spmv_nt; g_knobs.spmv_nt = value; break;
-    case 2: old = g_knobs.spmv_plain; g_knobs.spmv_plain = value; break;
     case 3: old = g_knobs.spmv_grid; if (value > 0) g_knobs.spmv_grid = value; break;
+    case 4: old = g_knobs.dia; g_knobs.dia = value; break;
     default: break;
   }
   return old;

@@ -310,65 +310,117 @@ __global__ void fill_split_kernel(int64_t m, const int64_t *__restrict__ rowptr,
 }
 
 // ---------------------------------------------------------------- SELL-64
-__global__ void sell_width_kernel(int64_t m, const int64_t *__restrict__ ptr, int64_t nslices,
-                                  int32_t *__restrict__ width, int64_t *__restrict__ slots) {
+// One wave per slice: longest row (SELL width) and, for the diagonal block,
+// the distinct column offsets d = col - row in ascending order (enumerated by
+// repeated wave-min over each lane's sorted row).  Picks the aligned-offset
+// format when 8 k + 4 < 12 w bytes per row.
+__global__ void slice_format_kernel(int64_t m, const int64_t *__restrict__ ptr,
+                                    const int32_t *__restrict__ col, int64_t nslices, int allow_dia,
+                                    int32_t *__restrict__ width, int64_t *__restrict__ slots,
+                                    int32_t *__restrict__ doff) {
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= nslices) return;   // wave-uniform
   const int lane = threadIdx.x & 63;
   const int64_t row = s * SLICE + lane;
-  int len = 0;
-  if (s < nslices && row < m) len = (int)(ptr[row + 1] - ptr[row]);
-  for (int o = 32; o > 0; o >>= 1) len = max(len, __shfl_xor(len, o, 64));
-  if (s < nslices && lane == 0) { width[s] = len; slots[s] = (int64_t)len * SLICE; }
+  int64_t a = 0, b = 0;
+  if (row < m) { a = ptr[row]; b = ptr[row + 1]; }
+  int len = (int)(b - a);
+  int w = len;
+  for (int o = 32; o > 0; o >>= 1) w = max(w, __shfl_xor(w, o, 64));
+  int k = 0;
+  if (allow_dia && w > 0) {
+    int64_t cur = a;
+    while (true) {
+      int my = cur < b ? (int)(col[cur] - row) : INT_MAX;
+      int mn = my;
+      for (int o = 32; o > 0; o >>= 1) mn = min(mn, __shfl_xor(mn, o, 64));
+      if (mn == INT_MAX) break;
+      if (k == DIA_MAX) { k = DIA_MAX + 1; break; }
+      if (lane == 0) doff[s * DIA_MAX + k] = mn;
+      ++k;
+      if (my == mn) ++cur;
+    }
+  }
+  const bool dia = allow_dia && w > 0 && k <= DIA_MAX && (8 * k + 4 < 12 * w);
+  if (lane == 0) {
+    width[s] = dia ? -k : w;
+    slots[s] = (int64_t)(dia ? k : w) * SLICE;
+  }
+}
+
+__device__ __forceinline__ int64_t sell_slot(int64_t base, int j, int w, int lane, bool paired) {
+  if (!paired) return base + (int64_t)j * SLICE + lane;
+  return base + ((j >> 1) < (w >> 1) ? (int64_t)(j >> 1) * 2 * SLICE + 2 * lane + (j & 1)
+                                     : (int64_t)(w >> 1) * 2 * SLICE + lane);
 }
 
 template <bool PAIRED>
 __global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
                                  const int32_t *__restrict__ ccol, const double *__restrict__ cval,
                                  int64_t nslices, const int64_t *__restrict__ sptr,
-                                 const int32_t *__restrict__ width, int32_t *__restrict__ scol,
-                                 double *__restrict__ sval) {
+                                 const int32_t *__restrict__ width, const int32_t *__restrict__ doff,
+                                 int32_t *__restrict__ scol, double *__restrict__ sval,
+                                 uint32_t *__restrict__ mask) {
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nslices) return;
   const int lane = threadIdx.x & 63;
   const int64_t row = s * SLICE + lane;
-  const int w = width[s];
+  const int wr = width[s];
   const int64_t base = sptr[s];
   const int64_t rs = row < m ? ptr[row] : 0;
   const int len = row < m ? (int)(ptr[row + 1] - rs) : 0;
+  if (wr < 0) {                       // aligned-offset slice
+    const int k = -wr;
+    uint32_t mk = 0;
+    int cur = 0;
+    for (int j = 0; j < k; ++j) {
+      const int off = doff[s * DIA_MAX + j];
+      const bool hit = cur < len && (int64_t)ccol[rs + cur] - row == off;
+      sval[sell_slot(base, j, k, lane, PAIRED)] = hit ? cval[rs + cur] : 0.0;
+      if (hit) { mk |= 1u << j; ++cur; }
+    }
+    mask[row] = mk;
+    return;
+  }
+  const int w = wr;
   for (int j = 0; j < w; ++j) {
     const bool in = j < len;
-    int64_t t;
-    if (PAIRED) t = base + ((j >> 1) < (w >> 1) ? (int64_t)(j >> 1) * 2 * SLICE + 2 * lane + (j & 1)
-                                                 : (int64_t)(w >> 1) * 2 * SLICE + lane);
-    else t = base + (int64_t)j * SLICE + lane;
+    const int64_t t = sell_slot(base, j, w, lane, PAIRED);
     scol[t] = in ? ccol[rs + j] : -1;
     sval[t] = in ? cval[rs + j] : 0.0;
   }
 }
 
 static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *col, const double *val,
-                       hipStream_t st) {
+                       hipStream_t st, bool allow_dia) {
   S.nslices = cdiv(m, SLICE);
   const int64_t ns = S.nslices;
   S.width.alloc((size_t)std::max<int64_t>(ns, 1));
   S.sptr.alloc((size_t)std::max<int64_t>(ns, 1));
+  S.doff.alloc((size_t)std::max<int64_t>(allow_dia ? ns * DIA_MAX : 1, 1));
+  S.mask.alloc((size_t)std::max<int64_t>(allow_dia ? ns * SLICE : 1, 1));
   if (ns == 0) { S.slots = 0; return; }
-  sell_width_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, ns, S.width.p, S.sptr.p);
+  slice_format_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, ns, allow_dia ? 1 : 0, S.width.p,
+                                                              S.sptr.p, S.doff.p);
   HIPCHECK(hipGetLastError());
+  if (allow_dia) {
+    std::vector<int32_t> wh((size_t)ns);
+    HIPCHECK(hipMemcpyAsync(wh.data(), S.width.p, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    S.dia_slices = 0;
+    int64_t hist[DIA_MAX + 1] = {0};
+    for (int32_t w : wh)
+      if (w < 0) { S.dia_slices++; hist[-w]++; }
+    S.dia_k = 0;
+    for (int k = 1; k <= DIA_MAX; ++k)
+      if (hist[k] > hist[S.dia_k]) S.dia_k = k;
+  }
   exclusive_scan_i64(S.sptr.p, S.sptr.p, ns, st, &S.slots);
   S.col.alloc((size_t)std::max<int64_t>(S.slots, 1));
   S.val.alloc((size_t)std::max<int64_t>(S.slots, 1));
   sell_fill_kernel<true><<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
-                                                                S.col.p, S.val.p);
+                                                                S.doff.p, S.col.p, S.val.p, S.mask.p);
   HIPCHECK(hipGetLastError());
-  const char *ab = std::getenv("MX_SPMV_AB");
-  if (ab && ab[0] == '1') {   // plain-layout copy for A/B measurements only
-    S.col_plain.alloc((size_t)std::max<int64_t>(S.slots, 1));
-    S.val_plain.alloc((size_t)std::max<int64_t>(S.slots, 1));
-    sell_fill_kernel<false><<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
-                                                                   S.col_plain.p, S.val_plain.p);
-    HIPCHECK(hipGetLastError());
-  }
 }
 
 // ---------------------------------------------------------------- halo plan
@@ -578,8 +630,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   if (A->nghost) HIPCHECK(hipMemcpyAsync(A->garray_h.data(), A->garray.p, sizeof(int64_t) * A->nghost, hipMemcpyDeviceToHost, st));
 
   // ---- SpMV layouts
-  build_sell(A->sd, m, A->dptr.p, A->dcol.p, A->dval.p, st);
-  build_sell(A->so, m, A->optr.p, A->ocol.p, A->oval.p, st);
+  build_sell(A->sd, m, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
+  build_sell(A->so, m, A->optr.p, A->ocol.p, A->oval.p, st, false);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()), RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
 

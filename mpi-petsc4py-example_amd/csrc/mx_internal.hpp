@@ -79,24 +79,32 @@ void get_unique_id(void *out, size_t len);
 constexpr int SLICE = 64;  // SELL-C with C = one wavefront
 
 // SELL-64: slice s = rows [64 s, 64 s + 64), `width[s]` slots per row.
-// Paired layout (default): entries (2p, 2p+1) of a row are adjacent, so a lane
-// loads 16 B of values and 8 B of column ids per pair; an odd last entry sits
-// in a trailing single region:  pair p at sptr + 128 p + 2 lane (+0/+1),
-// tail at sptr + 128 (w/2) + lane.  Same slot count as the plain layout
-// (entry j at sptr + 64 j + lane), which is kept only for A/B runs.
+// Paired layout: entries (2p, 2p+1) of a row are adjacent, so a lane loads
+// 16 B of values and 8 B of column ids per pair; an odd last entry sits in a
+// trailing single region:  pair p at sptr + 128 p + 2 lane (+0/+1), tail at
+// sptr + 128 (w/2) + lane.  Same slot count as plain SELL (entry j at
+// sptr + 64 j + lane), which measured 9.5% slower.
+//
+// Aligned-offset slices ("DIA-in-SELL"): when the 64 rows of a slice use few
+// distinct column offsets d = col - row (stencils: the stencil's offsets), the
+// slice stores k slots per row at those offsets (sorted ascending = PETSc's
+// column order), no column ids, and a per-row bitmask of the slots present.
+// width[s] < 0 marks such a slice (k = -width[s]); the offsets live in
+// doff[s * DIA_MAX + j].  Per row: 8 k + 4 bytes instead of 12 w.
+constexpr int DIA_MAX = 32;
 struct Sell {
-  int64_t nslices = 0, slots = 0;
-  bool paired = true;
+  int64_t nslices = 0, slots = 0, dia_slices = 0;
+  int dia_k = 0;         // most common aligned-offset width (kernel specialisation)
   DBuf<int64_t> sptr;    // [nslices] slot offset of each slice
-  DBuf<int32_t> width;   // [nslices]
-  DBuf<int32_t> col;     // [slots], -1 = padding
+  DBuf<int32_t> width;   // [nslices]  (< 0: aligned-offset slice with k = -width)
+  DBuf<int32_t> col;     // [slots], -1 = padding (unused for aligned-offset slices)
   DBuf<double> val;      // [slots]
-  DBuf<int32_t> col_plain;  // A/B only (MX_SPMV_AB=1)
-  DBuf<double> val_plain;
+  DBuf<int32_t> doff;    // [nslices * DIA_MAX] offsets of aligned-offset slices
+  DBuf<uint32_t> mask;   // [nslices * 64] slot-present bits of aligned-offset rows
 };
 
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
-struct Knobs { int spmv_nt = 1; int spmv_plain = 0; int spmv_grid = 2048; };
+struct Knobs { int spmv_nt = 1; int spmv_grid = 4096; int dia = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

@@ -35,82 +35,162 @@ template <bool NT, class T> __device__ __forceinline__ T ld(const T *p) {
   else return *p;
 }
 
+// Every slice body below issues all of its loads before the first use, with
+// predicated (never branching) lanes: absent entries gather the always-valid
+// x[0] and are then skipped by a select, so the running sum sees exactly the
+// present entries in ascending column order -- PETSc's order, bit for bit.
+
+// aligned-offset slice with a compile-time width K (the stencil's point count)
+template <int K, bool NT>
+__device__ __forceinline__ double dia_slice_fixed(const double *__restrict__ vbase, const int32_t *__restrict__ off,
+                                                  uint32_t mk, int64_t row, const double *__restrict__ x, int lane) {
+  constexpr int NP = K / 2;
+  double v[K], xv[K];
+  const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const dbl2 t = ld<NT>(vp + p * SLICE);
+    v[2 * p] = t.x;
+    v[2 * p + 1] = t.y;
+  }
+  if constexpr (K & 1) v[K - 1] = ld<NT>(vbase + NP * 2 * SLICE + lane);
+#pragma unroll
+  for (int j = 0; j < K; ++j) xv[j] = x[((mk >> j) & 1u) ? row + off[j] : 0];
+  double sum = 0.0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double t = sum + v[j] * xv[j];
+    sum = ((mk >> j) & 1u) ? t : sum;
+  }
+  return sum;
+}
+
+// aligned-offset slice, runtime width: batches of 8 slots
+template <bool NT>
+__device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase, const int32_t *__restrict__ off,
+                                                int k, uint32_t mk, int64_t row, const double *__restrict__ x, int lane) {
+  const int np = k >> 1;
+  const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
+  double sum = 0.0;
+  for (int p0 = 0; p0 < np; p0 += 4) {
+    double v[8], xv[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = p0 + q;
+      const dbl2 t = p < np ? ld<NT>(vp + (int64_t)p * SLICE) : dbl2{0.0, 0.0};
+      v[2 * q] = t.x;
+      v[2 * q + 1] = t.y;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = 2 * p0 + q;
+      const bool ok = j < 2 * np && ((mk >> j) & 1u);
+      xv[q] = x[ok ? row + off[j < 2 * np ? j : 0] : 0];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = 2 * p0 + q;
+      const double t = sum + v[q] * xv[q];
+      sum = (j < 2 * np && ((mk >> j) & 1u)) ? t : sum;
+    }
+  }
+  if (k & 1) {
+    const double v = ld<NT>(vbase + (int64_t)np * 2 * SLICE + lane);
+    const bool ok = (mk >> (k - 1)) & 1u;
+    const double xv = x[ok ? row + off[k - 1] : 0];
+    const double t = sum + v * xv;
+    sum = ok ? t : sum;
+  }
+  return sum;
+}
+
+// general SELL slice (paired layout), continuing `sum`: batches of 8 entries
+template <bool NT>
+__device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, const double *__restrict__ vbase,
+                                             int w, double sum, const double *__restrict__ x, int lane) {
+  const int np = w >> 1;
+  const int2v *__restrict__ cp = reinterpret_cast<const int2v *>(cbase) + lane;
+  const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
+  for (int p0 = 0; p0 < np; p0 += 4) {
+    int c[8];
+    double v[8], xv[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = p0 + q;
+      const int2v cc = p < np ? ld<NT>(cp + (int64_t)p * SLICE) : int2v{-1, -1};
+      const dbl2 t = p < np ? ld<NT>(vp + (int64_t)p * SLICE) : dbl2{0.0, 0.0};
+      c[2 * q] = cc.x; c[2 * q + 1] = cc.y;
+      v[2 * q] = t.x; v[2 * q + 1] = t.y;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xv[q] = x[c[q] >= 0 ? c[q] : 0];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double t = sum + v[q] * xv[q];
+      sum = c[q] >= 0 ? t : sum;
+    }
+  }
+  if (w & 1) {
+    const int64_t t = (int64_t)np * 2 * SLICE + lane;
+    const int c = ld<NT>(cbase + t);
+    const double v = ld<NT>(vbase + t);
+    const double xv = x[c >= 0 ? c : 0];
+    const double tt = sum + v * xv;
+    sum = c >= 0 ? tt : sum;
+  }
+  return sum;
+}
+
 // One wave sweeps slices; lane = row.  Grid-stride over a fixed grid whose
 // blocks are grouped by XCD (block b runs on XCD b % 8 under the observed
 // round-robin dispatch): each XCD walks one contiguous eighth of the slices in
 // order, so the +-1 / +-n / +-n^2 re-reads of x stay in that XCD's 4 MB L2.
-// Placement only affects speed, never results.
-template <int MODE, bool NT, bool PAIRED>
+// Placement only affects speed, never results.  KD > 0 specialises the
+// aligned-offset body for the matrix's dominant slice width.
+template <int MODE, bool NT, int KD>
 __global__ void __launch_bounds__(256) spmv_sell_kernel(
     int64_t m, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
-    const double *__restrict__ val_d, const int64_t *__restrict__ sptr_o,
+    const double *__restrict__ val_d, const int32_t *__restrict__ doff,
+    const uint32_t *__restrict__ dmask, const int64_t *__restrict__ sptr_o,
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o,
     const double *__restrict__ val_o, const double *__restrict__ x,
     const double *__restrict__ lvec, double *__restrict__ y, const double *__restrict__ dinv,
     double *__restrict__ partials, const int *__restrict__ done) {
   if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int64_t s0, sstep, send;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int s0, sstep, send;
   if ((gridDim.x & 7) == 0) {
-    const int64_t per = gridDim.x >> 3;                 // blocks per XCD group
-    const int64_t xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int64_t chunk = (nslices + 7) >> 3;
+    const int per = gridDim.x >> 3;                 // blocks per XCD group
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int chunk = (int)((nslices + 7) >> 3);
     s0 = xcd * chunk + j * SPMV_WAVES + wid;
     sstep = per * SPMV_WAVES;
-    send = min(nslices, (xcd + 1) * chunk);
+    send = (int)min(nslices, (int64_t)(xcd + 1) * chunk);
   } else {
-    s0 = (int64_t)blockIdx.x * SPMV_WAVES + wid;
-    sstep = (int64_t)gridDim.x * SPMV_WAVES;
-    send = nslices;
+    s0 = blockIdx.x * SPMV_WAVES + wid;
+    sstep = gridDim.x * SPMV_WAVES;
+    send = (int)nslices;
   }
   double dot = 0.0;
-  for (int64_t s = s0; s < send; s += sstep) {
-    const int64_t row = s * SLICE + lane;
-    double sum = 0.0;
+  for (int s = s0; s < send; s += sstep) {
+    const int64_t row = (int64_t)s * SLICE + lane;
     const int w = wid_d[s];
     const int64_t base = sptr_d[s];
-    if (PAIRED) {
-      const int np = w >> 1;
-      const int2v *__restrict__ cp = reinterpret_cast<const int2v *>(col_d + base) + lane;
-      const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(val_d + base) + lane;
-#pragma unroll 2
-      for (int p = 0; p < np; ++p) {
-        const int2v c = ld<NT>(cp + (int64_t)p * SLICE);
-        const dbl2 v = ld<NT>(vp + (int64_t)p * SLICE);
-        if (c.x >= 0) sum = sum + v.x * x[c.x];
-        if (c.y >= 0) sum = sum + v.y * x[c.y];
-      }
-      if (w & 1) {
-        const int64_t t = base + (int64_t)np * 2 * SLICE + lane;
-        const int c = ld<NT>(col_d + t);
-        const double v = ld<NT>(val_d + t);
-        if (c >= 0) sum = sum + v * x[c];
-      }
+    double sum;
+    if (w < 0) {
+      const int k = -w;
+      const uint32_t mk = dmask[row];
+      const int32_t *__restrict__ off = doff + (int64_t)s * DIA_MAX;
+      if (KD > 0 && k == KD) sum = dia_slice_fixed<(KD > 0 ? KD : 1), NT>(val_d + base, off, mk, row, x, lane);
+      else sum = dia_slice_any<NT>(val_d + base, off, k, mk, row, x, lane);
     } else {
-      const int32_t *__restrict__ cp = col_d + base + lane;
-      const double *__restrict__ vp = val_d + base + lane;
-#pragma unroll 4
-      for (int j = 0; j < w; ++j) {
-        const int c = ld<NT>(cp + (int64_t)j * SLICE);
-        const double v = ld<NT>(vp + (int64_t)j * SLICE);
-        if (c >= 0) sum = sum + v * x[c];
-      }
+      sum = sell_slice<NT>(col_d + base, val_d + base, w, 0.0, x, lane);
     }
     if (lvec) {
       const int wo = wid_o[s];
-      if (wo) {   // ghost block: rare, plain sequential continuation of the row sum
-        const int64_t bo = sptr_o[s];
-        for (int j = 0; j < wo; ++j) {
-          int64_t t;
-          if (PAIRED) t = bo + ((j >> 1) < (wo >> 1) ? (int64_t)(j >> 1) * 2 * SLICE + 2 * lane + (j & 1)
-                                                     : (int64_t)(wo >> 1) * 2 * SLICE + lane);
-          else t = bo + (int64_t)j * SLICE + lane;
-          const int c = col_o[t];
-          const double v = val_o[t];
-          if (c >= 0) sum = sum + v * lvec[c];
-        }
-      }
+      if (wo) sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wo, sum, lvec, lane);
     }
     if (row < m) {
       if (MODE == SPMV_JACOBI) y[row] = sum * dinv[row];   // PCApply_Jacobi fused: w_i * d_i
@@ -163,24 +243,25 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, const double *din
   hipStream_t st = A->comm->stream;
   const unsigned grid = (unsigned)spmv_blocks(A);
   const double *lvec = A->nghost ? A->halo.lvec.p : nullptr;
-  const bool plain = g_knobs.spmv_plain && A->sd.col_plain.p;
-  const int32_t *cd = plain ? A->sd.col_plain.p : A->sd.col.p;
-  const double *vd = plain ? A->sd.val_plain.p : A->sd.val.p;
-  const int32_t *co = plain ? A->so.col_plain.p : A->so.col.p;
-  const double *vo = plain ? A->so.val_plain.p : A->so.val.p;
-  if (plain && A->nghost && !co) fail(MX_ERR_INTERNAL, "plain SELL copy missing");
-#define SPMV_ARGS                                                                        \
-  A->m, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, cd, vd, A->so.sptr.p, A->so.width.p, \
-      co, vo, x, lvec, y, dinv, partials, done_flag
-#define SPMV_GO(MODE)                                                                           \
-  do {                                                                                          \
-    if (plain) {                                                                                \
-      if (g_knobs.spmv_nt) spmv_sell_kernel<MODE, true, false><<<grid, 256, 0, st>>>(SPMV_ARGS);  \
-      else spmv_sell_kernel<MODE, false, false><<<grid, 256, 0, st>>>(SPMV_ARGS);                 \
-    } else {                                                                                    \
-      if (g_knobs.spmv_nt) spmv_sell_kernel<MODE, true, true><<<grid, 256, 0, st>>>(SPMV_ARGS);   \
-      else spmv_sell_kernel<MODE, false, true><<<grid, 256, 0, st>>>(SPMV_ARGS);                  \
-    }                                                                                           \
+  const int kd = A->sd.dia_k;
+#define SPMV_ARGS                                                                           \
+  A->m, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
+      A->sd.mask.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, dinv,  \
+      partials, done_flag
+#define SPMV_KD(MODE, NT)                                                                     \
+  do {                                                                                        \
+    switch (kd) {                                                                             \
+      case 5: spmv_sell_kernel<MODE, NT, 5><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
+      case 7: spmv_sell_kernel<MODE, NT, 7><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
+      case 9: spmv_sell_kernel<MODE, NT, 9><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
+      case 27: spmv_sell_kernel<MODE, NT, 27><<<grid, 256, 0, st>>>(SPMV_ARGS); break;        \
+      default: spmv_sell_kernel<MODE, NT, 0><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
+    }                                                                                         \
+  } while (0)
+#define SPMV_GO(MODE)                                 \
+  do {                                                \
+    if (g_knobs.spmv_nt) SPMV_KD(MODE, true);         \
+    else SPMV_KD(MODE, false);                        \
   } while (0)
   switch (mode) {
     case SPMV_PLAIN: SPMV_GO(SPMV_PLAIN); break;
@@ -189,6 +270,7 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, const double *din
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
 #undef SPMV_GO
+#undef SPMV_KD
 #undef SPMV_ARGS
   HIPCHECK(hipGetLastError());
 }

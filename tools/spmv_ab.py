@@ -7,7 +7,6 @@ import os
 import sys
 import time
 
-os.environ.setdefault("MX_SPMV_AB", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "mpi-petsc4py-example_amd"))
 
@@ -24,22 +23,24 @@ def main():
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
     L = _lib.load()
     comm = DeviceComm.self_comm(0)
-    A = DMat.stencil(comm, kind, n)
-    info = A.info()
+    L.mx_debug_set(4, 0)
+    A0 = DMat.stencil(comm, kind, n)          # plain SELL (+ plain copy for A/B)
+    L.mx_debug_set(4, 1)
+    A1 = DMat.stencil(comm, kind, n)          # aligned-offset slices where they pay
+    info = A1.info()
     m, nnz = info["m"], info["nnz_d"]
     alg = 12 * nnz + 4 * (m + 1) + 8 * m + 8 * m
     x = comm.empty(m)
     rhs_hash(comm, 0, x)
     ref = comm.empty(m)
-    A.mult(x, ref)
+    A0.mult(x, ref)
     variants = {
-        "paired": (0, 0, 2048), "paired_nt": (1, 0, 2048), "plain": (0, 1, 2048), "plain_nt": (1, 1, 2048),
-        "paired_g1024": (0, 0, 1024), "paired_g4096": (0, 0, 4096), "paired_g16384": (0, 0, 16384),
-        "paired_nogrid": (0, 0, 1 << 30), "plain_nogrid": (0, 1, 1 << 30),
+        "sell_nt_g4096": (A0, 1, 4096), "sell_nt_g8192": (A0, 1, 8192),
+        "dia_nt_g2048": (A1, 1, 2048), "dia_nt_g4096": (A1, 1, 4096), "dia_g4096": (A1, 0, 4096),
+        "dia_nt_g8192": (A1, 1, 8192), "dia_nt_g16384": (A1, 1, 16384),
     }
     res = {k: [] for k in variants}
     y = comm.empty(m)
-    # copy-rate reference (torch copy kernel, 1 GiB each way)
     a = torch.empty(1 << 27, dtype=torch.float64, device="cuda")
     b = torch.empty_like(a)
     for _ in range(3):
@@ -52,15 +53,16 @@ def main():
     copy_gbs = 2 * a.numel() * 8 * 20 / (time.perf_counter() - t0) / 1e9
     del a, b
     for r in range(rounds):
-        for k, (nt, plain, grid) in variants.items():
-            L.mx_debug_set(1, nt); L.mx_debug_set(2, plain); L.mx_debug_set(3, grid)
+        for k, (A, nt, grid) in variants.items():
+            L.mx_debug_set(1, nt); L.mx_debug_set(3, grid)
             y.zero_()
             ms, _ = A.bench_mult(x, y, 20)
             res[k].append(ms)
             if r == 0:
                 assert torch.equal(y, ref), k
-    L.mx_debug_set(1, 1); L.mx_debug_set(2, 0); L.mx_debug_set(3, 2048)
+    L.mx_debug_set(1, 1); L.mx_debug_set(3, 4096)
     print(json.dumps({"kind": kind, "n": n, "rows": m, "nnz": nnz, "alg_bytes": alg,
+                      "dia_slices": info["dia_slices"], "slices": (m + 63) // 64,
                       "torch_copy_GBps": round(copy_gbs, 1)}))
     for k, v in res.items():
         med = float(np.median(v))
