@@ -305,9 +305,8 @@ int mx_mat_bench_mult(mx_mat a, const double *x, double *y, int iters, double *s
     mat_mult(A, x, y);  // warm
     HIPCHECK(hipEventRecord(ev[0], st));
     for (int k = 0; k < iters; ++k) {
-      halo_begin(A, x);
       HIPCHECK(hipEventRecord(ev[2 + 2 * k], st));
-      spmv_launch(A, x, y, SPMV_PLAIN, nullptr, nullptr, nullptr);
+      matmult_overlap(A, x, y, SPMV_PLAIN, Jac{}, nullptr, nullptr);
       HIPCHECK(hipEventRecord(ev[3 + 2 * k], st));
     }
     HIPCHECK(hipEventRecord(ev[1], st));
@@ -389,6 +388,8 @@ int mx_debug_set(int key, int value) {
     case 1: old = g_knobs.spmv_nt; g_knobs.spmv_nt = value; break;
     case 3: old = g_knobs.spmv_grid; if (value > 0) g_knobs.spmv_grid = value; break;
     case 4: old = g_knobs.dia; g_knobs.dia = value; break;
+    case 5: old = g_knobs.jac_const; g_knobs.jac_const = value; break;
+    case 6: old = g_knobs.overlap; g_knobs.overlap = value; break;
     default: break;
   }
   return old;

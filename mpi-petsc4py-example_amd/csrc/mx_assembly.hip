@@ -632,11 +632,22 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   // ---- SpMV layouts
   build_sell(A->sd, m, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
   build_sell(A->so, m, A->optr.p, A->ocol.p, A->oval.p, st, false);
-  A->partials.alloc((size_t)std::max(spmv_blocks(A.get()), RED_BLOCKS) * 4 + 64);
+  A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
 
-  // ---- halo plan (collective)
-  if (multi) build_halo(A.get());
+  // ---- halo plan (collective) + the slices that need ghosts
+  if (multi) {
+    build_halo(A.get());
+    std::vector<int32_t> wo((size_t)A->so.nslices), lst;
+    if (A->so.nslices)
+      HIPCHECK(hipMemcpy(wo.data(), A->so.width.p, sizeof(int32_t) * A->so.nslices, hipMemcpyDeviceToHost));
+    for (int64_t k = 0; k < A->so.nslices; ++k)
+      if (wo[k] > 0) lst.push_back((int32_t)k);
+    A->halo.nbnd = (int)lst.size();
+    A->halo.bnd_slices.alloc(std::max<size_t>(lst.size(), 1));
+    if (!lst.empty())
+      HIPCHECK(hipMemcpy(A->halo.bnd_slices.p, lst.data(), sizeof(int32_t) * lst.size(), hipMemcpyHostToDevice));
+  }
   return A.release();
 }
 

@@ -36,7 +36,7 @@ struct SelfComm : Comm {
   explicit SelfComm(int dev) { device = dev; rank = 0; size = 1; stream = new_stream(dev); }
   ~SelfComm() override { if (stream) (void)hipStreamDestroy(stream); }
   void allreduce_sum(double *, int) override {}
-  void exchange(const std::vector<Msg> &s, const std::vector<Msg> &r) override {
+  void exchange(const std::vector<Msg> &s, const std::vector<Msg> &r, hipStream_t) override {
     if (!s.empty() || !r.empty()) fail(MX_ERR_INTERNAL, "self communicator has no peers");
   }
   void alltoall_i64(const int64_t *s, int64_t *r) override { r[0] = s[0]; }
@@ -68,6 +68,7 @@ struct RcclComm : Comm {
     rank = r; size = s; device = dev;
     if (len < sizeof(ncclUniqueId)) fail(MX_ERR_ARG, "bad RCCL unique id length");
     stream = new_stream(dev);
+    comm_stream = new_stream(dev);
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
     NCCLCHECK(ncclCommInitRank(&nc, s, id, r));
@@ -76,16 +77,18 @@ struct RcclComm : Comm {
   ~RcclComm() override {
     if (nc) ncclCommDestroy(nc);
     if (stream) (void)hipStreamDestroy(stream);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
   }
   void allreduce_sum(double *dev, int n) override {
     if (size == 1 || n <= 0) return;
     NCCLCHECK(ncclAllReduce(dev, dev, (size_t)n, ncclDouble, ncclSum, nc, stream));
   }
-  void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs) override {
+  void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs, hipStream_t s) override {
     if (sends.empty() && recvs.empty()) return;
+    if (!s) s = stream;
     NCCLCHECK(ncclGroupStart());
-    for (const Msg &m : sends) NCCLCHECK(ncclSend(m.buf, m.bytes, ncclUint8, m.peer, nc, stream));
-    for (const Msg &m : recvs) NCCLCHECK(ncclRecv(m.buf, m.bytes, ncclUint8, m.peer, nc, stream));
+    for (const Msg &m : sends) NCCLCHECK(ncclSend(m.buf, m.bytes, ncclUint8, m.peer, nc, s));
+    for (const Msg &m : recvs) NCCLCHECK(ncclRecv(m.buf, m.bytes, ncclUint8, m.peer, nc, s));
     NCCLCHECK(ncclGroupEnd());
   }
   void alltoall_i64(const int64_t *send, int64_t *recv) override {
@@ -163,8 +166,12 @@ struct LocalComm : Comm {
   DBuf<double> tmp;
   LocalComm(LocalWorld *world, int r, int dev) : w(world) {
     rank = r; size = world->size; device = dev; stream = new_stream(dev);
+    comm_stream = new_stream(dev);
   }
-  ~LocalComm() override { if (stream) (void)hipStreamDestroy(stream); }
+  ~LocalComm() override {
+    if (stream) (void)hipStreamDestroy(stream);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
+  }
 
   void allreduce_sum(double *dev, int n) override {
     if (size == 1 || n <= 0) return;
@@ -186,21 +193,22 @@ struct LocalComm : Comm {
     w->barrier();
   }
 
-  void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs) override {
-    HIPCHECK(hipEventRecord(w->ev_ready[rank], stream));
+  void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs, hipStream_t st) override {
+    if (!st) st = stream;
+    HIPCHECK(hipEventRecord(w->ev_ready[rank], st));
     w->posted[rank] = sends;
     w->barrier();
     for (const Msg &r : recvs) {
       const Msg *src = nullptr;
       for (const Msg &s : w->posted[r.peer]) if (s.peer == rank) { src = &s; break; }
       if (!src || src->bytes != r.bytes) fail(MX_ERR_COMM, "local exchange: unmatched message");
-      HIPCHECK(hipStreamWaitEvent(stream, w->ev_ready[r.peer], 0));
-      if (r.bytes) HIPCHECK(hipMemcpyAsync(r.buf, src->buf, r.bytes, hipMemcpyDeviceToDevice, stream));
+      HIPCHECK(hipStreamWaitEvent(st, w->ev_ready[r.peer], 0));
+      if (r.bytes) HIPCHECK(hipMemcpyAsync(r.buf, src->buf, r.bytes, hipMemcpyDeviceToDevice, st));
     }
-    HIPCHECK(hipEventRecord(w->ev_done[rank], stream));
+    HIPCHECK(hipEventRecord(w->ev_done[rank], st));
     w->barrier();
     // the senders' buffers may be overwritten only after every receiver copied them
-    for (const Msg &s : sends) HIPCHECK(hipStreamWaitEvent(stream, w->ev_done[s.peer], 0));
+    for (const Msg &s : sends) HIPCHECK(hipStreamWaitEvent(st, w->ev_done[s.peer], 0));
     w->barrier();
   }
 

@@ -59,8 +59,10 @@ struct Comm {
   virtual ~Comm();
   // In-place SUM all-reduce of n doubles living in device memory, on stream.
   virtual void allreduce_sum(double *dev, int n) = 0;
-  // Grouped point-to-point exchange of device buffers, on stream.
-  virtual void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs) = 0;
+  hipStream_t comm_stream = nullptr;  // halo exchange stream (overlaps the interior SpMV)
+  // Grouped point-to-point exchange of device buffers, on stream `s` (default: stream).
+  virtual void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs,
+                        hipStream_t s = nullptr) = 0;
   // Host all-to-all of one int64 per peer (setup only; synchronous).
   virtual void alltoall_i64(const int64_t *send, int64_t *recv) = 0;
   // Host all-gather of one int64 per rank (setup only; synchronous).
@@ -104,7 +106,7 @@ struct Sell {
 };
 
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
-struct Knobs { int spmv_nt = 1; int spmv_grid = 4096; int dia = 1; };
+struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -120,6 +122,14 @@ struct Halo {
   DBuf<double> lvec;                        // [nghost]
   int64_t nsend = 0, nrecv = 0;
   bool need_pack = false;
+  // slices with ghost entries: finished after the exchange (overlap)
+  DBuf<int32_t> bnd_slices;
+  int nbnd = 0;
+  hipEvent_t ev_x = nullptr, ev_done = nullptr;
+  ~Halo() {
+    if (ev_x) (void)hipEventDestroy(ev_x);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+  }
 };
 
 struct Mat {
@@ -137,6 +147,10 @@ struct Mat {
   Halo halo;
   DBuf<double> partials;   // per-block reduction partials
   DBuf<double> scratch_x;  // helper vectors
+  // PCSetUp_Jacobi result, computed once per assembled operator (KSPSetUp)
+  DBuf<double> jac_dinv;
+  int jac_mode = -1;       // -1: not set up; 1: vector; 2: uniform scalar
+  double jac_c = 1.0;
 };
 
 // assembly entry (mx_assembly.hip)
@@ -156,11 +170,27 @@ void stencil_coo(Comm *c, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t 
                  int64_t m, DBuf<int64_t> &rows, DBuf<int64_t> &cols, DBuf<double> &vals);
 void convert_index(const void *src, int bytes, int64_t n, int64_t *dst, hipStream_t s);
 
+// PCJacobi application z_i = r_i * d_i.  mode 0: no PC; 1: per-row d (HBM
+// vector); 2: every diagonal entry equal, d is one scalar (bitwise the same
+// products, 8 B/row less traffic per application).
+struct Jac {
+  const double *d = nullptr;
+  double c = 1.0;
+  int mode = 0;
+};
+__device__ __forceinline__ double papply(const Jac &J, double r, int64_t i) {
+  return J.mode == 1 ? r * J.d[i] : (J.mode == 2 ? r * J.c : r);
+}
+
 // SpMV (mx_spmv.hip)
 enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2 };
-void halo_begin(Mat *A, const double *x);  // pack + exchange into A->halo.lvec
-void spmv_launch(Mat *A, const double *x, double *y, int mode, const double *dinv,
-                 double *partials, int *done_flag);
+void halo_begin(Mat *A, const double *x);  // pack + exchange into A->halo.lvec (compute stream)
+void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
+                 int *done_flag);
+// MatMult with the halo on the comm stream overlapping the interior slices;
+// returns the number of partials written (DOT mode) for the fold.
+int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
+                    int *done_flag);
 int spmv_blocks(const Mat *A);
 void mat_mult(Mat *A, const double *x, double *y);
 

@@ -147,7 +147,7 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
 // order, so the +-1 / +-n / +-n^2 re-reads of x stay in that XCD's 4 MB L2.
 // Placement only affects speed, never results.  KD > 0 specialises the
 // aligned-offset body for the matrix's dominant slice width.
-template <int MODE, bool NT, int KD>
+template <int MODE, bool NT, int KD, bool SPLIT>
 __global__ void __launch_bounds__(256) spmv_sell_kernel(
     int64_t m, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     const uint32_t *__restrict__ dmask, const int64_t *__restrict__ sptr_o,
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o,
     const double *__restrict__ val_o, const double *__restrict__ x,
-    const double *__restrict__ lvec, double *__restrict__ y, const double *__restrict__ dinv,
+    const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
     double *__restrict__ partials, const int *__restrict__ done) {
   if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
   const int lane = threadIdx.x & 63;
@@ -188,12 +188,19 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     } else {
       sum = sell_slice<NT>(col_d + base, val_d + base, w, 0.0, x, lane);
     }
-    if (lvec) {
+    if (SPLIT) {
+      // slice with ghost entries: store the diagonal-block sum; the boundary
+      // kernel continues it with A_o once the halo has arrived
+      if (wid_o[s]) {
+        if (row < m) y[row] = sum;
+        continue;
+      }
+    } else if (lvec) {
       const int wo = wid_o[s];
       if (wo) sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wo, sum, lvec, lane);
     }
     if (row < m) {
-      if (MODE == SPMV_JACOBI) y[row] = sum * dinv[row];   // PCApply_Jacobi fused: w_i * d_i
+      if (MODE == SPMV_JACOBI) y[row] = papply(jac, sum, row);   // PCApply_Jacobi fused: w_i * d_i
       else y[row] = sum;
       if (MODE == SPMV_DOT) dot += x[row] * sum;           // VecDot(p, w) partial, p = x
     }
@@ -209,6 +216,36 @@ int spmv_blocks(const Mat *A) {
   int64_t g = std::min<int64_t>(need, g_knobs.spmv_grid);
   if (g >= 64) g &= ~int64_t(7);   // multiple of 8: XCD grouping
   return (int)std::max<int64_t>(1, g);
+}
+
+// Second half of an overlapped MatMult: y_i continues from the diagonal-block
+// sum with the A_o entries in ghost order (MatMultAdd_SeqAIJ), then the fused
+// epilogue.  One wave per listed slice.
+template <int MODE>
+__global__ void __launch_bounds__(256) spmv_boundary_kernel(
+    int64_t m, const int32_t *__restrict__ list, int nlist, const int64_t *__restrict__ sptr_o,
+    const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o, const double *__restrict__ val_o,
+    const double *__restrict__ x, const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
+    double *__restrict__ partials, const int *__restrict__ done) {
+  if (done && *done) return;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double dot = 0.0;
+  for (int k = blockIdx.x * SPMV_WAVES + wid; k < nlist; k += gridDim.x * SPMV_WAVES) {
+    const int s = list[k];
+    const int64_t row = (int64_t)s * SLICE + lane;
+    double sum = row < m ? y[row] : 0.0;
+    sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wid_o[s], sum, lvec, lane);
+    if (row < m) {
+      if (MODE == SPMV_JACOBI) y[row] = papply(jac, sum, row);
+      else y[row] = sum;
+      if (MODE == SPMV_DOT) dot += x[row] * sum;
+    }
+  }
+  if (MODE == SPMV_DOT) {
+    double v[1] = {dot};
+    block_sum_to_partials<1>(v, partials, gridDim.x);
+  }
 }
 
 __global__ void pack_kernel(int64_t n, const int32_t *__restrict__ idx, const double *__restrict__ x,
@@ -238,30 +275,28 @@ void halo_begin(Mat *A, const double *x) {
   A->comm->exchange(sends, recvs);
 }
 
-void spmv_launch(Mat *A, const double *x, double *y, int mode, const double *dinv,
-                 double *partials, int *done_flag) {
-  hipStream_t st = A->comm->stream;
+static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
+                        int *done_flag, bool split, hipStream_t st) {
   const unsigned grid = (unsigned)spmv_blocks(A);
-  const double *lvec = A->nghost ? A->halo.lvec.p : nullptr;
+  const double *lvec = (A->nghost && !split) ? A->halo.lvec.p : nullptr;
   const int kd = A->sd.dia_k;
 #define SPMV_ARGS                                                                           \
   A->m, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
-      A->sd.mask.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, dinv,  \
+      A->sd.mask.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac,   \
       partials, done_flag
-#define SPMV_KD(MODE, NT)                                                                     \
-  do {                                                                                        \
-    switch (kd) {                                                                             \
-      case 5: spmv_sell_kernel<MODE, NT, 5><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
-      case 7: spmv_sell_kernel<MODE, NT, 7><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
-      case 9: spmv_sell_kernel<MODE, NT, 9><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
-      case 27: spmv_sell_kernel<MODE, NT, 27><<<grid, 256, 0, st>>>(SPMV_ARGS); break;        \
-      default: spmv_sell_kernel<MODE, NT, 0><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
-    }                                                                                         \
+#define SPMV_KD(MODE, NT, SP)                                                                    \
+  do {                                                                                           \
+    switch (kd) {                                                                                \
+      case 5: spmv_sell_kernel<MODE, NT, 5, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
+      case 7: spmv_sell_kernel<MODE, NT, 7, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
+      case 27: spmv_sell_kernel<MODE, NT, 27, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;       \
+      default: spmv_sell_kernel<MODE, NT, 0, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;        \
+    }                                                                                            \
   } while (0)
-#define SPMV_GO(MODE)                                 \
-  do {                                                \
-    if (g_knobs.spmv_nt) SPMV_KD(MODE, true);         \
-    else SPMV_KD(MODE, false);                        \
+#define SPMV_GO(MODE)                                                         \
+  do {                                                                        \
+    if (split) { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, true); else SPMV_KD(MODE, false, true); } \
+    else { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, false); else SPMV_KD(MODE, false, false); }     \
   } while (0)
   switch (mode) {
     case SPMV_PLAIN: SPMV_GO(SPMV_PLAIN); break;
@@ -275,9 +310,64 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, const double *din
   HIPCHECK(hipGetLastError());
 }
 
+void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
+                 int *done_flag) {
+  launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream);
+}
+
+constexpr int BND_BLOCKS = 64;
+
+int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
+                    int *done_flag) {
+  Comm *c = A->comm;
+  Halo &H = A->halo;
+  if (c->size == 1 || H.nbnd == 0 || !g_knobs.overlap) {
+    halo_begin(A, x);
+    launch_main(A, x, y, mode, jac, partials, done_flag, false, c->stream);
+    return spmv_blocks(A);
+  }
+  hipStream_t st = c->stream, cs = c->comm_stream;
+  if (!H.ev_x) {
+    HIPCHECK(hipEventCreateWithFlags(&H.ev_x, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&H.ev_done, hipEventDisableTiming));
+  }
+  // halo on the comm stream, after x is final on the compute stream
+  HIPCHECK(hipEventRecord(H.ev_x, st));
+  HIPCHECK(hipStreamWaitEvent(cs, H.ev_x, 0));
+  if (H.need_pack && H.nsend) {
+    pack_kernel<<<grid_for(H.nsend, 256, 4096), 256, 0, cs>>>(H.nsend, H.send_idx.p, x, H.send_buf.p);
+    HIPCHECK(hipGetLastError());
+  }
+  std::vector<Msg> sends, recvs;
+  for (size_t i = 0; i < H.send_peer.size(); ++i) {
+    void *buf = H.send_contig_start[i] >= 0 ? (void *)(x + H.send_contig_start[i])
+                                            : (void *)(H.send_buf.p + H.send_off[i]);
+    sends.push_back({H.send_peer[i], buf, sizeof(double) * (size_t)H.send_cnt[i]});
+  }
+  for (size_t i = 0; i < H.recv_peer.size(); ++i)
+    recvs.push_back({H.recv_peer[i], H.lvec.p + H.recv_off[i], sizeof(double) * (size_t)H.recv_cnt[i]});
+  c->exchange(sends, recvs, cs);
+  HIPCHECK(hipEventRecord(H.ev_done, cs));
+  // interior slices meanwhile; boundary slices after the exchange
+  const int nmain = spmv_blocks(A);
+  launch_main(A, x, y, mode, jac, partials, done_flag, true, st);
+  HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
+  const int nb = std::min(BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
+  double *pb = partials ? partials + nmain : nullptr;
+#define BND(MODE) spmv_boundary_kernel<MODE><<<nb, 256, 0, st>>>(A->m, H.bnd_slices.p, H.nbnd, A->so.sptr.p, \
+      A->so.width.p, A->so.col.p, A->so.val.p, x, H.lvec.p, y, jac, pb, done_flag)
+  switch (mode) {
+    case SPMV_PLAIN: BND(SPMV_PLAIN); break;
+    case SPMV_JACOBI: BND(SPMV_JACOBI); break;
+    default: BND(SPMV_DOT); break;
+  }
+#undef BND
+  HIPCHECK(hipGetLastError());
+  return nmain + nb;
+}
+
 void mat_mult(Mat *A, const double *x, double *y) {
-  halo_begin(A, x);
-  spmv_launch(A, x, y, SPMV_PLAIN, nullptr, nullptr, nullptr);
+  matmult_overlap(A, x, y, SPMV_PLAIN, Jac{}, nullptr, nullptr);
 }
 
 }  // namespace mx
