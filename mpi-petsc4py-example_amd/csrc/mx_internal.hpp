@@ -147,6 +147,9 @@ struct Mat {
   Halo halo;
   DBuf<double> partials;   // per-block reduction partials
   DBuf<double> scratch_x;  // helper vectors
+  // KSPSetUp work vectors / device state, kept across solves with this operator
+  DBuf<double> ksp_ws;
+  DBuf<char> ksp_state;
   // PCSetUp_Jacobi result, computed once per assembled operator (KSPSetUp)
   DBuf<double> jac_dinv;
   int jac_mode = -1;       // -1: not set up; 1: vector; 2: uniform scalar

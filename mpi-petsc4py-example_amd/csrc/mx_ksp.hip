@@ -28,6 +28,7 @@
 //          MAXPY + norm in one pass.
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
@@ -547,6 +548,28 @@ void read_state(hipStream_t st, const KspState *d, KspState &h) {
 
 }  // namespace
 
+// KSPSetUp work space: one device allocation per operator, grown on demand
+// and reused by later solves (no hipMalloc/hipFree inside a solve).
+struct Carve {
+  double *base;
+  size_t off = 0;
+  explicit Carve(double *b) : base(b) {}
+  double *take(size_t n) { double *p = base + off; off += (n + 31) / 32 * 32; return p; }
+};
+static size_t carve_size(std::initializer_list<size_t> parts) {
+  size_t t = 0;
+  for (size_t n : parts) t += (n + 31) / 32 * 32;
+  return t;
+}
+static double *workspace(Mat *A, size_t nd) {
+  if (A->ksp_ws.n < nd) A->ksp_ws.alloc(nd);
+  return A->ksp_ws.p;
+}
+static KspState *state_buf(Mat *A) {
+  if (!A->ksp_state.p) A->ksp_state.alloc(sizeof(KspState));
+  return reinterpret_cast<KspState *>(A->ksp_state.p);
+}
+
 static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const double *b, double *x,
                      mx_ksp_result &res, double *hist_host) {
   Comm *c = A->comm;
@@ -554,11 +577,12 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   const int64_t n = A->m;
   const bool fused = c->size == 1;
   int normtype = p.norm_type == MX_NORM_DEFAULT ? MX_NORM_PRECONDITIONED : p.norm_type;
-  DBuf<double> r((size_t)std::max<int64_t>(n, 1)), pv((size_t)std::max<int64_t>(n, 1)),
-      w((size_t)std::max<int64_t>(n, 1));
-  DBuf<KspState> sd(1);
-  DBuf<double> part((size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 64);
-  DBuf<double> hist(hist_host ? (size_t)p.max_it + 2 : 0);
+  const size_t nv = (size_t)std::max<int64_t>(n, 1);
+  const size_t npart = (size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 64;
+  const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
+  Carve cv(workspace(A, carve_size({nv, nv, nv, npart, nhist})));
+  struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
+  struct { KspState *p; } sd{state_buf(A)};
   KspState hs;
   init_state(hs, p, normtype);
   HIPCHECK(hipMemcpyAsync(sd.p, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
@@ -657,13 +681,17 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   if (max_k > MAX_RESTART) fail(MX_ERR_UNSUPPORTED, "GMRES restart above 1000");
   const int ld = max_k + 2;
   const int64_t ldv = (std::max<int64_t>(n, 1) + 31) / 32 * 32;
-  DBuf<double> V((size_t)ldv * (max_k + 1)), tmat((size_t)ldv);
-  DBuf<double> hh((size_t)ld * (max_k + 1)), grs((size_t)max_k + 2), cc((size_t)max_k + 1),
-      ss((size_t)max_k + 1), lhh((size_t)max_k + 1), red((size_t)max_k + 2);
+  const size_t nV = (size_t)ldv * (max_k + 1), nh = (size_t)ld * (max_k + 1);
+  const size_t npart = (size_t)RED_BLOCKS * (max_k + 2) + (size_t)spmv_blocks(A) + 128;
+  const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
+  const size_t k1 = (size_t)max_k + 1, k2 = (size_t)max_k + 2;
+  Carve cv(workspace(A, carve_size({nV, (size_t)ldv, nh, k2, k1, k1, k1, k2, npart, nhist})));
+  struct B { double *p; size_t n; };
+  B V{cv.take(nV), nV}, tmat{cv.take(ldv), (size_t)ldv}, hh{cv.take(nh), nh}, grs{cv.take(k2), k2},
+      cc{cv.take(k1), k1}, ss{cv.take(k1), k1}, lhh{cv.take(k1), k1}, red{cv.take(k2), k2},
+      part{cv.take(npart), npart}, hist{cv.take(nhist), nhist};
   HIPCHECK(hipMemsetAsync(hh.p, 0, sizeof(double) * hh.n, st));
-  DBuf<double> part((size_t)RED_BLOCKS * (max_k + 2) + (size_t)spmv_blocks(A) + 128);
-  DBuf<KspState> sd(1);
-  DBuf<double> hist(hist_host ? (size_t)p.max_it + 2 : 0);
+  struct { KspState *p; } sd{state_buf(A)};
   KspState hs;
   init_state(hs, p, MX_NORM_PRECONDITIONED);
   if (p.norm_type != MX_NORM_DEFAULT && p.norm_type != MX_NORM_PRECONDITIONED)

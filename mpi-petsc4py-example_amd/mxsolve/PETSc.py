@@ -237,6 +237,46 @@ def _split(N, P, r):
     return start, q + (1 if r < rem else 0)
 
 
+# ------------------------------------------------------------------ Viewer (binary)
+class Viewer:
+    """PETSc binary viewer (PetscViewerBinaryOpen): Mat/Vec in PETSc's file format.
+    Rank 0 writes the gathered object; every rank reads the file and keeps its rows."""
+
+    class Mode:
+        READ, WRITE, APPEND = "r", "w", "a"
+        R, W, A = "r", "w", "a"
+
+    class Format:
+        DEFAULT, ASCII_INFO = 0, 1
+
+    def __init__(self):
+        self._fh = None
+        self._mode = None
+        self._comm = None
+        self._name = None
+
+    def createBinary(self, name, mode="r", comm=None):
+        self._comm = Comm(_mpi(comm))
+        self._name = str(name)
+        self._mode = {"r": "rb", "w": "wb", "a": "ab"}[str(mode)[0].lower()]
+        mc = _mpi(comm)
+        if self._mode == "rb" or mc.Get_rank() == 0:
+            self._fh = open(self._name, self._mode)
+        return self
+
+    def destroy(self):
+        if self._fh:
+            self._fh.close()
+            self._fh = None
+        return self
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.destroy()
+
+
 # ------------------------------------------------------------------ Vec
 class Vec:
     """Distributed vector; the local rows live in a float64 tensor in HBM."""
@@ -275,9 +315,21 @@ class Vec:
         self._comm = comm if isinstance(comm, Comm) else Comm(_mpi(comm))
         return self
 
+    @staticmethod
+    def _vsize(size, mc):
+        """Vec sizes: N | (n, N) with None / DECIDE / DETERMINE entries."""
+        if isinstance(size, (tuple, list)):
+            n, N = size
+            n = DECIDE if n is None else int(n)
+            N = DETERMINE if N is None else int(N)
+            if N < 0:
+                N = mc.allreduce(n) if mc.Get_size() > 1 else n
+            return n, N
+        return DECIDE, int(size)
+
     def setSizes(self, size, bsize=None):
         mc = _mpi(self._comm)
-        (n, N), _ = _sizes(size, mc.Get_size(), mc.Get_rank())
+        n, N = self._vsize(size, mc)
         return self._setup(mc, n, N)
 
     def setType(self, t):
@@ -291,7 +343,7 @@ class Vec:
 
     def createMPI(self, size, bsize=None, comm=None):
         mc = _mpi(comm)
-        (n, N), _ = _sizes(size, mc.Get_size(), mc.Get_rank())
+        n, N = self._vsize(size, mc)
         return self._setup(mc, n, N)
 
     def createSeq(self, size, bsize=None, comm=None):
@@ -418,10 +470,28 @@ class Vec:
         return nrm
 
     def view(self, viewer=None):
+        from . import petsc_io
         arr = self.getArray()
+        mc = _mpi(self._comm)
+        if isinstance(viewer, Viewer):
+            parts = mc.allgather(arr) if mc.Get_size() > 1 else [arr]
+            if mc.Get_rank() == 0:
+                petsc_io.write_vec(viewer._fh, np.concatenate(parts))
+                viewer._fh.flush()
+            return
         print(f"Vec Object: {self._comm.size} MPI process(es)\n  type: {'mpi' if self._comm.size > 1 else 'seq'}")
         for v in arr:
             print(f"{v:g}")
+
+    def load(self, viewer):
+        """VecLoad: the next Vec in a binary viewer, split by PetscSplitOwnership."""
+        from . import petsc_io
+        vals = petsc_io.read_vec(viewer._fh)
+        mc = _mpi(viewer._comm)
+        self._setup(mc, -1, vals.size)
+        a, b = self.getOwnershipRange()
+        self.setArray(vals[a:b])
+        return self
 
     def __len__(self):
         return self.getLocalSize()
@@ -687,7 +757,30 @@ class Mat:
         _guard(self._h.diagonal, result._t)
         return result
 
+    def load(self, viewer):
+        """MatLoad: the next AIJ matrix of a binary viewer, rows split by
+        PetscSplitOwnership, assembled on the GPU."""
+        from . import petsc_io
+        M, N, ip, cj, vv = petsc_io.read_mat(viewer._fh)
+        mc = _mpi(viewer._comm)
+        r0, m = _split(M, mc.Get_size(), mc.Get_rank())
+        lip = ip[r0:r0 + m + 1] - ip[r0]
+        return self.createAIJ(size=(M, N), csr=(lip, cj[ip[r0]:ip[r0 + m]], vv[ip[r0]:ip[r0 + m]]), comm=mc)
+
     def view(self, viewer=None):
+        if isinstance(viewer, Viewer):
+            from . import petsc_io
+            mc = _mpi(self._comm)
+            part = self.getValuesCSR()
+            parts = mc.allgather(part) if mc.Get_size() > 1 else [part]
+            if mc.Get_rank() == 0:
+                M, N = self.getSize()
+                lens = np.concatenate([np.diff(p[0]) for p in parts])
+                ip = np.concatenate([[0], np.cumsum(lens)])
+                petsc_io.write_mat(viewer._fh, M, N, ip, np.concatenate([p[1] for p in parts]),
+                                   np.concatenate([p[2] for p in parts]))
+                viewer._fh.flush()
+            return
         i = self._info()
         print(f"Mat Object: {self._comm.size} MPI process(es)\n  type: {self.getType()}\n"
               f"  rows={i['M']}, cols={i['N']}, local nonzeros={i['nnz_d'] + i['nnz_o']} "

@@ -116,3 +116,24 @@ def test_mpi_shim_gloo(tmp_path, P):
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-2000:]
     assert outs[0][0].strip().splitlines()[-1] == f"OK {P}"
+
+
+def test_petsc_binary_format_roundtrip(tmp_path, golden):
+    """PETSc binary Mat/Vec layout (big-endian int32 header, row lengths, cols, values)."""
+    from mxsolve import petsc_io
+    f = tmp_path / "sys.bin"
+    with open(f, "wb") as fh:
+        petsc_io.write_mat(fh, 100, 100, golden["sys_indptr"], golden["sys_indices"], golden["sys_data"])
+        petsc_io.write_vec(fh, golden["sys_B"])
+    raw = np.fromfile(f, dtype=">i4", count=4)
+    assert list(raw) == [1211216, 100, 100, 1000]
+    with open(f, "rb") as fh:
+        M, N, ip, cj, vv = petsc_io.read_mat(fh)
+        b = petsc_io.read_vec(fh)
+    assert (M, N) == (100, 100)
+    assert np.array_equal(ip, golden["sys_indptr"]) and np.array_equal(cj, golden["sys_indices"])
+    assert np.array_equal(vv, golden["sys_data"]) and np.array_equal(b, golden["sys_B"])
+    with open(f, "rb") as fh:
+        fh.seek(4 * 4 + 4 * 100 + 4 * 1000 + 8 * 1000)
+        with pytest.raises(ValueError):
+            petsc_io.read_mat(fh)

@@ -142,3 +142,20 @@ def test_ksp_not_converged_does_not_raise(PETSc, oracle_mod):
     ksp.solve(b, x)
     assert ksp.getConvergedReason() == PETSc.KSP.ConvergedReason.DIVERGED_ITS
     assert ksp.getIterationNumber() == 5
+
+
+def test_binary_viewer_roundtrip(PETSc, golden, tmp_path):
+    """Mat/Vec view -> load through a binary viewer (F4), values bit-identical."""
+    A = PETSc.Mat().createAIJ(size=(100, 100), csr=(golden["sys_indptr"], golden["sys_indices"], golden["sys_data"]))
+    x, b = A.getVecs()
+    b.setArray(golden["sys_B"])
+    fn = str(tmp_path / "a.bin")
+    with PETSc.Viewer().createBinary(fn, "w") as vw:
+        A.view(vw)
+        b.view(vw)
+    with PETSc.Viewer().createBinary(fn, "r") as vr:
+        A2 = PETSc.Mat().load(vr)
+        b2 = PETSc.Vec().load(vr)
+    for u, v in zip(A2.getValuesCSR(), A.getValuesCSR()):
+        assert np.array_equal(u, v)
+    assert np.array_equal(b2.array, golden["sys_B"])
