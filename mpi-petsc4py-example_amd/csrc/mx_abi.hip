@@ -390,6 +390,8 @@ int mx_debug_set(int key, int value) {
     case 4: old = g_knobs.dia; g_knobs.dia = value; break;
     case 5: old = g_knobs.jac_const; g_knobs.jac_const = value; break;
     case 6: old = g_knobs.overlap; g_knobs.overlap = value; break;
+    case 7: old = g_knobs.graph; g_knobs.graph = value; break;
+    case 8: old = g_knobs.force_coll; g_knobs.force_coll = value; break;
     default: break;
   }
   return old;

@@ -80,7 +80,7 @@ struct RcclComm : Comm {
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
   }
   void allreduce_sum(double *dev, int n) override {
-    if (size == 1 || n <= 0) return;
+    if ((size == 1 && !g_knobs.force_coll) || n <= 0) return;
     NCCLCHECK(ncclAllReduce(dev, dev, (size_t)n, ncclDouble, ncclSum, nc, stream));
   }
   void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs, hipStream_t s) override {
@@ -166,6 +166,7 @@ struct LocalComm : Comm {
   DBuf<double> tmp;
   LocalComm(LocalWorld *world, int r, int dev) : w(world) {
     rank = r; size = world->size; device = dev; stream = new_stream(dev);
+    capturable = false;
     comm_stream = new_stream(dev);
   }
   ~LocalComm() override {

@@ -54,6 +54,7 @@ struct Msg { int peer; void *buf; size_t bytes; };
 // One rank's view of a communicator.  Device payloads move on `stream`.
 struct Comm {
   int rank = 0, size = 1, device = 0;
+  bool capturable = true;    // host-synchronous transports (LocalComm) cannot be graph-captured
   hipStream_t stream = nullptr;
   DBuf<double> red_scratch;  // scratch for reductions
   virtual ~Comm();
@@ -106,7 +107,7 @@ struct Sell {
 };
 
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
-struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; };
+struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 0; int force_coll = 0; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -154,6 +155,12 @@ struct Mat {
   DBuf<double> jac_dinv;
   int jac_mode = -1;       // -1: not set up; 1: vector; 2: uniform scalar
   double jac_c = 1.0;
+  // captured CG iteration batch (hipGraph), reused while its key matches
+  hipGraphExec_t cg_graph = nullptr;
+  std::vector<uintptr_t> cg_key;
+  ~Mat() {
+    if (cg_graph) (void)hipGraphExecDestroy(cg_graph);
+  }
 };
 
 // assembly entry (mx_assembly.hip)

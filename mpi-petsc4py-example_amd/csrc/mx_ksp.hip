@@ -190,10 +190,13 @@ __global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double 
   if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
 }
 
-// p = z + (beta/betaold) p  (i == 0: p = z), z = d.*r recomputed
-__global__ void cg_p_kernel(int64_t n, int i, const KspState *__restrict__ s, const double *__restrict__ r,
+// p = z + (beta/betaold) p  (i == 0: p = z), z = d.*r recomputed.  The
+// iteration index comes from the device state (its = i + 1 at the top of
+// iteration i), so every iteration is the same launch sequence (graph replay).
+__global__ void cg_p_kernel(int64_t n, const KspState *__restrict__ s, const double *__restrict__ r,
                             const Jac jac, double *__restrict__ p) {
   if (s->done) return;
+  const int i = s->its - 1;
   const double b = i == 0 ? 0.0 : s->beta / s->betaold;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
@@ -203,9 +206,10 @@ __global__ void cg_p_kernel(int64_t n, int i, const KspState *__restrict__ s, co
 }
 
 // dpi = p.w, indefiniteness checks, alpha = beta/dpi
-__global__ void __launch_bounds__(256) cg_alpha_kernel(KspState *s, int i, const double *partials,
+__global__ void __launch_bounds__(256) cg_alpha_kernel(KspState *s, const double *partials,
                                                        int nblocks, int fused) {
   if (s->done) return;
+  const int i = s->its - 1;
   if (!gather_red<1>(s, partials, nblocks, fused)) return;
   s->dpiold = s->dpi;
   s->dpi = s->red[0];
@@ -238,9 +242,10 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, const KspStat
 }
 
 // dp, history, convergence at its = i+1, beta for the next iteration
-__global__ void __launch_bounds__(256) cg_conv_kernel(KspState *s, int i, const double *partials,
+__global__ void __launch_bounds__(256) cg_conv_kernel(KspState *s, const double *partials,
                                                       int nblocks, int fused, double *hist) {
   if (s->done) return;
+  const int i = s->its - 1;
   if (!gather_red<3>(s, partials, nblocks, fused)) return;
   const double zz = s->red[0], zr = s->red[1], rr = s->red[2];
   double dp;
@@ -575,7 +580,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   Comm *c = A->comm;
   hipStream_t st = c->stream;
   const int64_t n = A->m;
-  const bool fused = c->size == 1;
+  const bool fused = c->size == 1 && !g_knobs.force_coll;
   int normtype = p.norm_type == MX_NORM_DEFAULT ? MX_NORM_PRECONDITIONED : p.norm_type;
   const size_t nv = (size_t)std::max<int64_t>(n, 1);
   const size_t npart = (size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 64;
@@ -614,18 +619,46 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   int i = 0;
   const unsigned egrid = grid_for(n, 256, 8192);
   int *done = &s->done;
-  for (; i < p.max_it; ++i) {
-    cg_p_kernel<<<egrid, 256, 0, st>>>(n, i, s, r.p, dinv, pv.p);
+  double *hist_d = hist_host ? hist.p : nullptr;
+  auto iteration = [&]() {
+    cg_p_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p);
     timer.begin();
     const int nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done);
     timer.end();
     if (!fused) { finish_reduce(part.p, nb_spmv, 1, red, st, done); c->allreduce_sum(red, 1); }
-    cg_alpha_kernel<<<1, 256, 0, st>>>(s, i, part.p, nb_spmv, fused);
+    cg_alpha_kernel<<<1, 256, 0, st>>>(s, part.p, nb_spmv, fused);
     cg_update_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, s, pv.p, w.p, x, r.p, dinv, part.p);
     if (!fused) { finish_reduce(part.p, RED_BLOCKS, 3, red, st, done); c->allreduce_sum(red, 3); }
-    cg_conv_kernel<<<1, 256, 0, st>>>(s, i, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
+    cg_conv_kernel<<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_d);
     HIPCHECK(hipGetLastError());
-    if ((i + 1) % poll == 0 && poller.batch(done)) { ++i; break; }
+  };
+  const bool graph = g_knobs.graph && c->capturable && !p.profile;
+  if (graph) {
+    // capture `poll` iterations once per (operator, vectors, PC) and replay
+    std::vector<uintptr_t> key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode,
+                                  (uintptr_t)dinv.d, (uintptr_t)(dinv.c * 1e9), (uintptr_t)poll,
+                                  (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt,
+                                  (uintptr_t)g_knobs.spmv_grid};
+    std::memcpy(&key[5], &dinv.c, sizeof(double));
+    if (!A->cg_graph || A->cg_key != key) {
+      if (A->cg_graph) { HIPCHECK(hipGraphExecDestroy(A->cg_graph)); A->cg_graph = nullptr; }
+      hipGraph_t g;
+      HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      for (int k = 0; k < poll; ++k) iteration();
+      HIPCHECK(hipStreamEndCapture(st, &g));
+      HIPCHECK(hipGraphInstantiate(&A->cg_graph, g, nullptr, nullptr, 0));
+      HIPCHECK(hipGraphDestroy(g));
+      A->cg_key = key;
+    }
+    for (; i < p.max_it; i += poll) {
+      HIPCHECK(hipGraphLaunch(A->cg_graph, st));
+      if (poller.batch(done)) { i += poll; break; }
+    }
+  } else {
+    for (; i < p.max_it; ++i) {
+      iteration();
+      if ((i + 1) % poll == 0 && poller.batch(done)) { ++i; break; }
+    }
   }
   HIPCHECK(hipEventRecord(ev.b, st));
   read_state(st, s, hs);
