@@ -181,9 +181,16 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
                     const double *vals, const double *b, double *x);
 
 /* ---- measurement knobs (A/B runs only; defaults are the product path) -------
- * key 1: SpMV non-temporal matrix loads (0/1); key 3: SpMV grid size in
- * workgroups; key 4: aligned-offset (DIA-in-SELL)
- * slices at assembly (0/1, default 1).  Returns the previous value.          */
+ * key 1: SpMV non-temporal matrix loads (0/1, default 1)
+ * key 3: SpMV grid size in workgroups (default 8192)
+ * key 4: aligned-offset (DIA-in-SELL) slices at assembly (0/1, default 1)
+ * key 5: uniform-diagonal Jacobi applied as one scalar (0/1, default 1)
+ * key 6: halo exchange overlapping the interior slices when P > 1 (0/1, default 1)
+ * key 7: CG iterations replayed from a captured hipGraph batch (0/1, default 0:
+ *        on ROCm 7 the graph path measured ~10% slower per iteration at N = 1)
+ * key 8: run the collective path (unfused folds + RCCL all-reduce) on a one-rank
+ *        RCCL communicator (testing, default 0)
+ * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,
