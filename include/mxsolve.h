@@ -186,8 +186,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 4: aligned-offset (DIA-in-SELL) slices at assembly (0/1, default 1)
  * key 5: uniform-diagonal Jacobi applied as one scalar (0/1, default 1)
  * key 6: halo exchange overlapping the interior slices when P > 1 (0/1, default 1)
- * key 7: CG iterations replayed from a captured hipGraph batch (0/1, default 0:
- *        on ROCm 7 the graph path measured ~10% slower per iteration at N = 1)
+ * key 7: CG iterations replayed from a captured hipGraph batch after one eager
+ *        batch (0/1, default 1; equal at 256^3, 2% faster at 64^3 per rank)
  * key 8: run the collective path (unfused folds + RCCL all-reduce) on a one-rank
  *        RCCL communicator (testing, default 0)
  * Returns the previous value.                                                   */

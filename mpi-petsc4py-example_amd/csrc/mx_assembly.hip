@@ -104,6 +104,129 @@ __global__ void coo_scatter_kernel(int64_t n, const int64_t *__restrict__ rows,
   }
 }
 
+// ---------------------------------------------------------------- off-process stash
+// MatSetValues on rows owned elsewhere go to PETSc's stash and are applied by
+// their owner at MatAssemblyEnd.  Here every COO entry is tagged with the
+// owner of its row, entries are stably partitioned by owner, one count
+// all-to-all and one grouped send/recv move them, and the owner appends the
+// received entries after its own (local first, then by source rank: a
+// deterministic version of PETSc's arrival order).
+struct CooEntry { int64_t row, col; double val; };
+
+__global__ void coo_owner_kernel(int64_t n, const int64_t *__restrict__ rows, const int64_t *__restrict__ cols,
+                                 const int64_t *__restrict__ ranges, int P, int64_t M, int *__restrict__ owner,
+                                 unsigned long long *__restrict__ cnt, int *__restrict__ err) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const int64_t r = rows[k];
+    int o = -1;
+    if (r >= 0 && cols[k] >= 0) {
+      if (r >= M) { atomicOr(err, 16); }
+      else {
+        int lo = 0, hi = P - 1;
+        while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (ranges[mid] <= r) lo = mid; else hi = mid - 1; }
+        o = lo;
+        atomicAdd(&cnt[o], 1ULL);
+      }
+    }
+    owner[k] = o;
+  }
+}
+
+__global__ void coo_flag_kernel(int64_t n, const int *__restrict__ owner, int q, int64_t *__restrict__ flag) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) flag[k] = owner[k] == q;
+}
+
+__global__ void coo_pack_kernel(int64_t n, const int *__restrict__ owner, int q, const int64_t *__restrict__ pos,
+                                const int64_t *__restrict__ rows, const int64_t *__restrict__ cols,
+                                const double *__restrict__ vals, CooEntry *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
+    if (owner[k] == q) out[pos[k]] = CooEntry{rows[k], cols[k], vals[k]};
+}
+
+__global__ void coo_unpack_kernel(int64_t n, const CooEntry *__restrict__ in, int64_t *__restrict__ rows,
+                                  int64_t *__restrict__ cols, double *__restrict__ vals) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const CooEntry e = in[k];
+    rows[k] = e.row; cols[k] = e.col; vals[k] = e.val;
+  }
+}
+
+// Returns the number of entries now held by this rank (all rows local).
+static int64_t coo_redistribute(Comm *c, const std::vector<int64_t> &rr, int64_t M, const int64_t *rows,
+                                const int64_t *cols, const double *vals, int64_t n, DBuf<int64_t> &orows,
+                                DBuf<int64_t> &ocols, DBuf<double> &ovals) {
+  const int P = c->size;
+  hipStream_t st = c->stream;
+  DBuf<int64_t> ranges((size_t)P + 1);
+  HIPCHECK(hipMemcpyAsync(ranges.p, rr.data(), sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, st));
+  DBuf<int> owner((size_t)std::max<int64_t>(n, 1)), err(1);
+  DBuf<unsigned long long> cnt((size_t)P);
+  HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * P, st));
+  HIPCHECK(hipMemsetAsync(err.p, 0, sizeof(int), st));
+  if (n) {
+    coo_owner_kernel<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, rows, cols, ranges.p, P, M, owner.p, cnt.p, err.p);
+    HIPCHECK(hipGetLastError());
+  }
+  std::vector<unsigned long long> cs(P);
+  int herr = 0;
+  HIPCHECK(hipMemcpyAsync(cs.data(), cnt.p, sizeof(unsigned long long) * P, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  int gerr = 0;
+  {
+    std::vector<int64_t> all(P);
+    c->allgather_i64(herr, all.data());
+    for (int64_t e : all) gerr |= (int)e;
+  }
+  if (gerr & 16) fail(MX_ERR_OUTOFRANGE, "Row too large: max " + std::to_string(M - 1));
+  std::vector<int64_t> send(P), recv(P);
+  for (int q = 0; q < P; ++q) send[q] = (int64_t)cs[q];
+  c->alltoall_i64(send.data(), recv.data());
+  // stable partition by owner into one buffer, owner segments in rank order
+  std::vector<int64_t> soff(P + 1, 0);
+  for (int q = 0; q < P; ++q) soff[q + 1] = soff[q] + send[q];
+  DBuf<CooEntry> sbuf((size_t)std::max<int64_t>(soff[P], 1));
+  DBuf<int64_t> pos((size_t)std::max<int64_t>(n, 1));
+  for (int q = 0; q < P; ++q) {
+    if (!send[q]) continue;
+    coo_flag_kernel<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, owner.p, q, pos.p);
+    exclusive_scan_i64(pos.p, pos.p, n, st, nullptr);
+    coo_pack_kernel<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, owner.p, q, pos.p, rows, cols, vals, sbuf.p + soff[q]);
+    HIPCHECK(hipGetLastError());
+  }
+  // received entries: own segment first, then the other ranks in order
+  int64_t total = send[c->rank];
+  std::vector<int64_t> roff(P, 0);
+  for (int q = 0; q < P; ++q) {
+    if (q == c->rank) continue;
+    roff[q] = total;
+    total += recv[q];
+  }
+  DBuf<CooEntry> rbuf((size_t)std::max<int64_t>(total, 1));
+  if (send[c->rank])
+    HIPCHECK(hipMemcpyAsync(rbuf.p, sbuf.p + soff[c->rank], sizeof(CooEntry) * send[c->rank], hipMemcpyDeviceToDevice, st));
+  std::vector<Msg> sends, recvs;
+  for (int q = 0; q < P; ++q) {
+    if (q == c->rank) continue;
+    if (send[q]) sends.push_back({q, sbuf.p + soff[q], sizeof(CooEntry) * (size_t)send[q]});
+    if (recv[q]) recvs.push_back({q, rbuf.p + roff[q], sizeof(CooEntry) * (size_t)recv[q]});
+  }
+  c->exchange(sends, recvs);
+  orows.alloc((size_t)std::max<int64_t>(total, 1));
+  ocols.alloc((size_t)std::max<int64_t>(total, 1));
+  ovals.alloc((size_t)std::max<int64_t>(total, 1));
+  if (total) {
+    coo_unpack_kernel<<<grid_for(total, 256, 8192), 256, 0, st>>>(total, rbuf.p, orows.p, ocols.p, ovals.p);
+    HIPCHECK(hipGetLastError());
+  }
+  HIPCHECK(hipStreamSynchronize(st));
+  return total;
+}
+
 // ---------------------------------------------------------------- row canonicalisation
 // One W-lane segment per row (W | 64).  Keys (col, pos) are unique per row
 // except the dropped/padding lanes, which all carry (KEY_DROP, KEY_DROP).
@@ -505,7 +628,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   A->cstart = A->cranges[c->rank];
   A->cend = A->cranges[c->rank + 1];
   A->n = A->cend - A->cstart;
-  const int64_t m = A->m, nnz = in.nnz;
+  const int64_t m = A->m;
+  int64_t nnz = in.nnz;
 
   DBuf<int> err(1);
   HIPCHECK(hipMemsetAsync(err.p, 0, sizeof(int), st));
@@ -517,7 +641,16 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   const int64_t *col = in.cols;
   const double *val = in.vals;
   const int64_t *pos = nullptr;
-  if (in.coo_rows) {
+  DBuf<int64_t> rd_rows, rd_cols;
+  DBuf<double> rd_vals;
+  AssemblyInput cin = in;
+  if (in.coo_rows && c->size > 1) {   // off-process rows: stash exchange first
+    cin.nnz = coo_redistribute(c, A->rranges, M, in.coo_rows, in.cols, in.vals, in.nnz, rd_rows, rd_cols, rd_vals);
+    cin.coo_rows = rd_rows.p; cin.cols = rd_cols.p; cin.vals = rd_vals.p;
+    nnz = cin.nnz;
+  }
+  if (cin.coo_rows) {
+    const AssemblyInput &in = cin;
     DBuf<unsigned long long> cnt((size_t)m + 1);
     HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * (m + 1), st));
     if (nnz) {
@@ -529,7 +662,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
     exclusive_scan_i64(reinterpret_cast<int64_t *>(cnt.p), rowptr_own.p, m + 1, st, &total);
     int herr = 0;
     HIPCHECK(hipMemcpy(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (herr & 8) fail(MX_ERR_UNSUPPORTED, "COO entry for a row owned by another rank (off-process stash not implemented)");
+    if (herr & 8) fail(MX_ERR_OUTOFRANGE, "Row out of range for this rank");
     HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * (m + 1), st));
     gcol.alloc((size_t)std::max<int64_t>(total, 1));
     gval.alloc((size_t)std::max<int64_t>(total, 1));

@@ -633,14 +633,26 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     HIPCHECK(hipGetLastError());
   };
   const bool graph = g_knobs.graph && c->capturable && !p.profile;
+  std::vector<uintptr_t> key;
   if (graph) {
-    // capture `poll` iterations once per (operator, vectors, PC) and replay
-    std::vector<uintptr_t> key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode,
-                                  (uintptr_t)dinv.d, (uintptr_t)(dinv.c * 1e9), (uintptr_t)poll,
-                                  (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt,
-                                  (uintptr_t)g_knobs.spmv_grid};
+    key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
+           (uintptr_t)poll, (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt, (uintptr_t)g_knobs.spmv_grid,
+           (uintptr_t)g_knobs.force_coll};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
-    if (!A->cg_graph || A->cg_key != key) {
+  }
+  bool use_graph = graph && A->cg_graph && A->cg_key == key;
+  // Eager until a graph for exactly this configuration exists: the first
+  // batch of the first solve also warms every RCCL connection it uses, so the
+  // capture that follows records only steady-state collective calls.
+  for (; i < p.max_it;) {
+    if (use_graph) {
+      HIPCHECK(hipGraphLaunch(A->cg_graph, st));
+      i += poll;
+    } else {
+      for (int k = 0; k < poll && i < p.max_it; ++k, ++i) iteration();
+    }
+    if (poller.batch(done)) break;
+    if (graph && !use_graph && i < p.max_it) {
       if (A->cg_graph) { HIPCHECK(hipGraphExecDestroy(A->cg_graph)); A->cg_graph = nullptr; }
       hipGraph_t g;
       HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
@@ -649,15 +661,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       HIPCHECK(hipGraphInstantiate(&A->cg_graph, g, nullptr, nullptr, 0));
       HIPCHECK(hipGraphDestroy(g));
       A->cg_key = key;
-    }
-    for (; i < p.max_it; i += poll) {
-      HIPCHECK(hipGraphLaunch(A->cg_graph, st));
-      if (poller.batch(done)) { i += poll; break; }
-    }
-  } else {
-    for (; i < p.max_it; ++i) {
-      iteration();
-      if ((i + 1) % poll == 0 && poller.batch(done)) { ++i; break; }
+      use_graph = true;
     }
   }
   HIPCHECK(hipEventRecord(ev.b, st));

@@ -412,26 +412,66 @@ class Vec:
     array_r = property(getArray)
 
     def setValues(self, indices, values, addv=None):
-        idx = np.atleast_1d(np.asarray(indices, dtype=np.int64)) - self._rstart
-        val = np.broadcast_to(np.asarray(values, dtype=np.float64), idx.shape)
-        keep = idx + self._rstart >= 0
-        if np.any((idx[keep] < 0) | (idx[keep] >= self.getLocalSize())):
-            raise Error(PETSC_ERR_SUP, "off-process Vec entries are not supported")
-        host = self.getArray()
-        if addv in (InsertMode.ADD_VALUES, InsertMode.ADD, True):
-            np.add.at(host, idx[keep], val[keep])
-        else:
-            host[idx[keep]] = val[keep]
-        self.setArray(host)
+        """VecSetValues: owned entries are applied now, the others go to the
+        stash and reach their owner at assemblyEnd (negative indices skipped)."""
+        gidx = np.atleast_1d(np.asarray(indices, dtype=np.int64))
+        val = np.broadcast_to(np.asarray(values, dtype=np.float64), gidx.shape)
+        add = addv in (InsertMode.ADD_VALUES, InsertMode.ADD, True)
+        mode = getattr(self, "_vmode", None)
+        if mode is not None and mode != add:
+            raise Error(PETSC_ERR_ARG_WRONG, "You have already added values; you cannot now insert")
+        self._vmode = add
+        keep = gidx >= 0
+        if np.any(gidx[keep] >= self._N):
+            raise Error(PETSC_ERR_ARG_OUTOFRANGE, f"Out of range index value {int(gidx[keep].max())} maximum {self._N}")
+        lo, hi = self.getOwnershipRange()
+        own = keep & (gidx >= lo) & (gidx < hi)
+        off = keep & ~own
+        if np.any(off):
+            self._vstash = getattr(self, "_vstash", []) + [(gidx[off].copy(), val[off].copy())]
+        if np.any(own):
+            host = self.getArray()
+            if add:
+                np.add.at(host, gidx[own] - lo, val[own])
+            else:
+                host[gidx[own] - lo] = val[own]
+            self.setArray(host)
+
+    def setValue(self, index, value, addv=None):
+        self.setValues([index], [value], addv)
 
     def assemblyBegin(self):
         return self
 
     def assemblyEnd(self):
+        """VecAssemblyEnd: deliver the stash (collective).  Entries arrive in
+        ascending source-rank order, each rank's in call order."""
+        mc = _mpi(self._comm)
+        stash = getattr(self, "_vstash", [])
+        add = getattr(self, "_vmode", None)
+        if mc.Get_size() > 1:
+            mine = (np.concatenate([s[0] for s in stash]) if stash else np.zeros(0, np.int64),
+                    np.concatenate([s[1] for s in stash]) if stash else np.zeros(0))
+            every = mc.allgather((mine, add))
+            modes = {m for (_, m) in every if m is not None}
+            if len(modes) > 1:
+                raise Error(PETSC_ERR_ARG_WRONG, "Some processors inserted values while others added")
+            lo, hi = self.getOwnershipRange()
+            got = [(i[(i >= lo) & (i < hi)], v[(i >= lo) & (i < hi)]) for (i, v), _ in every]
+            if any(g[0].size for g in got):
+                host = self.getArray()
+                for i, v in got:
+                    if modes == {True}:
+                        np.add.at(host, i - lo, v)
+                    else:
+                        host[i - lo] = v
+                self.setArray(host)
+        self._vstash, self._vmode = [], None
         return self
 
     def assemble(self):
-        return self
+        self.assemblyBegin()
+        return self.assemblyEnd()
 
     # -- algebra (all through libmxsolve) -------------------------------------------
     def set(self, alpha):

@@ -79,6 +79,35 @@ def split_ownership(N: int, P: int) -> np.ndarray:
     return r
 
 
+def stash_order(M: int, P: int, per_rank):
+    """MatAssemblyEnd's stash delivery, restated: every rank's MatSetValues
+    entries (in call order) end up on the owner of their row; the owner applies
+    its own entries first and then the stashed ones (PETSc's
+    MatAssemblyEnd_MPIAIJ -> MatStashScatterGetMesg loop).  PETSc applies the
+    messages in arrival order; the deterministic rule used here (and by the
+    device path) is ascending source rank.  Negative rows/columns are dropped
+    like MatSetValues does.  Returns (coo_ptr, rows, cols, vals) for
+    OracleMat.from_coo.  per_rank: list of P (rows, cols, vals) triples."""
+    ranges = split_ownership(M, P)
+    seg = [[] for _ in range(P)]
+    for q, (r, c, v) in enumerate(per_rank):
+        r, c, v = np.asarray(r, np.int64), np.asarray(c, np.int64), np.asarray(v, np.float64)
+        keep = (r >= 0) & (c >= 0)
+        r, c, v = r[keep], c[keep], v[keep]
+        own = np.searchsorted(ranges, r, side="right") - 1
+        for o in range(P):
+            sel = own == o
+            seg[o].append((q, r[sel], c[sel], v[sel]))
+    rows, cols, vals, ptr = [], [], [], [0]
+    for o in range(P):
+        parts = sorted(seg[o], key=lambda t: (t[0] != o, t[0]))   # own entries first, then by rank
+        for _, r, c, v in parts:
+            rows.append(r); cols.append(c); vals.append(v)
+        ptr.append(ptr[-1] + sum(p[1].size for p in parts))
+    cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)
+    return np.array(ptr, np.int64), cat(rows, np.int64), cat(cols, np.int64), cat(vals, np.float64)
+
+
 class OracleMat:
     """P-rank AIJ matrix assembled by the restated PETSc rules."""
 

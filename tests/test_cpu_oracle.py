@@ -78,6 +78,22 @@ def test_insert_and_add_semantics(oracle_mod):
         oracle_mod.OracleMat.from_csr(2, 4, ip, np.array([3, 1, 4, 3, 0, 2, 2]), vals)
 
 
+def test_stash_order(oracle_mod):
+    """Off-process MatSetValues: the owner applies its own entries first, then
+    the stashed ones by source rank; the assembled sum matches scipy's."""
+    per_rank = [(np.array([3, 0, 4]), np.array([0, 0, 1]), np.array([1.0, 2.0, 3.0])),
+                (np.array([0, 3, -1]), np.array([0, 0, 2]), np.array([10.0, 20.0, 99.0])),
+                (np.array([0]), np.array([1]), np.array([5.0]))]
+    ptr, r, c, v = oracle_mod.stash_order(5, 3, per_rank)   # ranges 0,2,4,5
+    assert list(ptr) == [0, 3, 5, 6]
+    assert list(zip(r, c, v)) == [(0, 0, 2.0), (0, 0, 10.0), (0, 1, 5.0), (3, 0, 20.0), (3, 0, 1.0), (4, 1, 3.0)]
+    A = oracle_mod.OracleMat.from_coo(5, 5, ptr, r, c, v, P=3, add=True)
+    I = oracle_mod.OracleMat.from_coo(5, 5, ptr, r, c, v, P=3, add=False)
+    ip, cj, vv = A.csr()
+    assert list(cj) == [0, 1, 0, 1] and list(vv) == [12.0, 5.0, 21.0, 3.0]
+    assert list(I.csr()[2]) == [10.0, 5.0, 1.0, 3.0]   # row 3: owner rank 1's 20, then rank 0's 1
+
+
 def test_spmv_matches_scipy(oracle_mod, golden):
     S = sp.csr_matrix((golden["sys_data"], golden["sys_indices"], golden["sys_indptr"]), shape=(100, 100))
     A = oracle_mod.OracleMat.from_csr(100, 100, golden["sys_indptr"], golden["sys_indices"], golden["sys_data"], P=3)

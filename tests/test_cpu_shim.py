@@ -137,3 +137,64 @@ def test_petsc_binary_format_roundtrip(tmp_path, golden):
         fh.seek(4 * 4 + 4 * 100 + 4 * 1000 + 8 * 1000)
         with pytest.raises(ValueError):
             petsc_io.read_mat(fh)
+
+
+VEC_STASH_SCRIPT = textwrap.dedent('''
+    import sys
+    import numpy as np, torch
+    sys.path.insert(0, {pkg!r})
+    from mxsolve import MPI, PETSc
+    comm = MPI.COMM_WORLD
+    rank, size = comm.Get_rank(), comm.Get_size()
+
+    class HostComm:            # host tensors: exercises the stash protocol only
+        def activate(self): pass
+
+    def vec(N):
+        v = PETSc.Vec()
+        v._comm, v._dc, v._N = PETSc.Comm(comm), HostComm(), N
+        v._rstart, n = PETSc._split(N, size, rank)
+        v._t = torch.zeros(n, dtype=torch.float64)
+        return v
+
+    N = 10
+    v = vec(N)
+    # every rank adds 1 + rank to every entry, plus rank 0 hits entry 9 twice; -1 is skipped
+    idx = np.concatenate([np.arange(N), [-1]] + ([[9]] if rank == 0 else []))
+    v.setValues(idx, np.full(idx.size, 1.0 + rank), addv=PETSc.InsertMode.ADD_VALUES)
+    v.assemble()
+    want = np.full(N, sum(1.0 + r for r in range(size))); want[9] += 1.0
+    lo, hi = v.getOwnershipRange()
+    assert np.array_equal(v.getArray(), want[lo:hi]), (rank, v.getArray())
+    w = vec(N)
+    w.setValues([N - 1 - rank], [float(rank)])      # INSERT, mostly off-process
+    w.assemble()
+    got = np.concatenate(comm.allgather(w.getArray()))
+    exp = np.zeros(N); exp[[N - 1 - r for r in range(size)]] = np.arange(size)
+    assert np.array_equal(got, exp), got
+    try:
+        w.setValues([N], [1.0])
+        raise SystemExit("no out-of-range error")
+    except PETSc.Error:
+        pass
+    if rank == 0:
+        print("OK", size)
+''')
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_vec_stash_gloo(tmp_path, P):
+    """VecSetValues on off-process entries reach their owner at assemblyEnd."""
+    script = tmp_path / "vec.py"
+    script.write_text(VEC_STASH_SCRIPT.format(pkg=PKG))
+    port = str(29700 + P + (os.getpid() % 1000))
+    procs = []
+    for r in range(P):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    assert outs[0][0].strip().splitlines()[-1] == f"OK {P}"

@@ -160,3 +160,69 @@ def test_overlap_matches_serial_halo(oracle_mod, P):
         assert np.array_equal(a[0].view(np.uint64), b[0].view(np.uint64))
         assert a[2] == b[2]
         assert np.linalg.norm(a[1] - b[1]) <= 1e-13 * np.linalg.norm(b[1])
+
+
+@pytest.mark.parametrize("P,add", [(2, True), (3, True), (4, False), (8, True)])
+def test_offprocess_coo_stash(oracle_mod, P, add):
+    """MatSetValues on rows owned by other ranks (the stash): every rank sets
+    a random slice of a 3-D Poisson matrix's entries with duplicates, some
+    negative (ignored) indices and rows anywhere in the matrix; after assembly
+    the split and the SpMV are bit-exact against the oracle's stash restatement
+    (own entries first, then by source rank)."""
+    from mxsolve.core import DMat
+    ip, c, v = oracle_mod.stencil("poisson3d", 10)
+    M = ip.size - 1
+    rows_all = np.repeat(np.arange(M, dtype=np.int64), np.diff(ip))
+    rng = np.random.default_rng(100 + P)
+    # duplicate every entry 1-3 times, shuffle, deal to ranks
+    rep = rng.integers(1, 4, rows_all.size)
+    R = np.repeat(rows_all, rep)
+    Cc = np.repeat(c, rep)
+    V = np.repeat(v, rep) * rng.uniform(0.5, 1.5, R.size)
+    perm = rng.permutation(R.size)
+    R, Cc, V = R[perm], Cc[perm], V[perm]
+    drop = rng.random(R.size) < 0.02
+    R[drop & (rng.random(R.size) < 0.5)] = -1
+    Cc[drop] = -1
+    owner_of = rng.integers(0, P, R.size)
+    per_rank = [(R[owner_of == q], Cc[owner_of == q], V[owner_of == q]) for q in range(P)]
+    ptr, sr, sc, sv = oracle_mod.stash_order(M, P, per_rank)
+    O = oracle_mod.OracleMat.from_coo(M, M, ptr, sr, sc, sv, P=P, add=add)
+    x = rng.standard_normal(M)
+    y_ref = O.mult(x)
+    ranges = oracle_mod.split_ownership(M, P)
+
+    def body(comm):
+        r = comm.rank
+        A = DMat.from_coo(comm, M, M, *per_rank[r], add=add)
+        sp = A.split()
+        xl = torch.from_numpy(x[ranges[r]:ranges[r + 1]].copy()).cuda()
+        yl = torch.zeros(ranges[r + 1] - ranges[r], dtype=torch.float64, device="cuda")
+        A.mult(xl, yl)
+        out = (sp, yl.cpu().numpy())
+        A.destroy()
+        return out
+
+    res = run_ranks(P, body)
+    for r, (sp, yl) in enumerate(res):
+        ob = O.block(r)
+        for k in ("dptr", "dcol", "optr", "ocol", "garray"):
+            assert np.array_equal(sp[k], ob[k]), (P, r, k)
+        for k in ("dval", "oval"):
+            assert np.array_equal(sp[k].view(np.uint64), ob[k].view(np.uint64)), (P, r, k)
+        assert np.array_equal(yl.view(np.uint64), y_ref[ranges[r]:ranges[r + 1]].view(np.uint64)), (P, r)
+
+
+def test_offprocess_row_out_of_range():
+    from mxsolve.core import DMat
+    from mxsolve._lib import MxError
+
+    def body(comm):
+        rows = np.array([comm.rank, 1000], np.int64)
+        try:
+            DMat.from_coo(comm, 10, 10, rows, np.array([0, 0], np.int64), np.ones(2))
+        except MxError as e:
+            return e.code
+        return 0
+
+    assert run_ranks(2, body) == [2, 2]
