@@ -105,6 +105,9 @@ int mx_comm_create_self(int device, mx_comm *out);
 int mx_world_create_local(int size, void **world);
 int mx_comm_create_local(void *world, int rank, int device, mx_comm *out);
 int mx_world_destroy(void *world);
+/* Mark the local world failed: every rank blocked in (or entering) one of its
+ * collectives returns MX_ERR_COMM instead of waiting for the failed rank.    */
+int mx_world_abort(void *world);
 int mx_comm_destroy(mx_comm c);
 int mx_comm_info(mx_comm c, int *rank, int *size, int *device);
 /* The HIP stream every kernel of this communicator runs on (hipStream_t).      */
@@ -190,6 +193,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        batch (0/1, default 1; equal at 256^3, 2% faster at 64^3 per rank)
  * key 8: run the collective path (unfused folds + RCCL all-reduce) on a one-rank
  *        RCCL communicator (testing, default 0)
+ * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the
+ *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
+ *        1 for <= 8M local rows, else 2)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

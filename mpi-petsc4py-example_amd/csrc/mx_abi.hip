@@ -88,6 +88,7 @@ int mx_comm_create_local(void *world, int rank, int device, mx_comm *out) {
 }
 
 int mx_world_destroy(void *world) { return guard([&] { destroy_local_world(world); }); }
+int mx_world_abort(void *world) { return guard([&] { abort_local_world(world); }); }
 
 int mx_comm_destroy(mx_comm c) {
   return guard([&] {
@@ -392,6 +393,7 @@ int mx_debug_set(int key, int value) {
     case 6: old = g_knobs.overlap; g_knobs.overlap = value; break;
     case 7: old = g_knobs.graph; g_knobs.graph = value; break;
     case 8: old = g_knobs.force_coll; g_knobs.force_coll = value; break;
+    case 9: old = g_knobs.cg_fuse; g_knobs.cg_fuse = value; break;
     default: break;
   }
   return old;

@@ -128,25 +128,33 @@ struct LocalWorld {
   std::condition_variable cv;
   int arrived = 0;
   long gen = 0;
-  std::vector<hipEvent_t> ev_ready, ev_done;
   std::vector<double *> red_ptr;
   std::vector<std::vector<Msg>> posted;
   std::vector<int64_t> slots;
-  explicit LocalWorld(int s)
-      : size(s), ev_ready(s), ev_done(s), red_ptr(s), posted(s), slots((size_t)s * s) {
-    for (int i = 0; i < s; ++i) {
-      HIPCHECK(hipEventCreateWithFlags(&ev_ready[i], hipEventDisableTiming));
-      HIPCHECK(hipEventCreateWithFlags(&ev_done[i], hipEventDisableTiming));
-    }
-  }
-  ~LocalWorld() {
-    for (int i = 0; i < size; ++i) { (void)hipEventDestroy(ev_ready[i]); (void)hipEventDestroy(ev_done[i]); }
-  }
-  void barrier() {
+  std::vector<int> tags;        // collective each rank entered (mismatch = error, not a race)
+  bool broken = false;          // a rank failed: every barrier throws instead of waiting
+  explicit LocalWorld(int s) : size(s), red_ptr(s), posted(s), slots((size_t)s * s), tags(s) {}
+  // tag: which collective the caller is in; all ranks must agree
+  void barrier(int rank = -1, int tag = 0) {
     std::unique_lock<std::mutex> lk(mu);
+    if (broken) fail(MX_ERR_COMM, "local world: another rank failed");
+    if (rank >= 0) tags[rank] = tag;
     long g = gen;
     if (++arrived == size) { arrived = 0; gen++; cv.notify_all(); }
-    else cv.wait(lk, [&] { return gen != g; });
+    else cv.wait(lk, [&] { return gen != g || broken; });
+    if (broken) fail(MX_ERR_COMM, "local world: another rank failed");
+    if (rank >= 0)
+      for (int q = 0; q < size; ++q)
+        if (tags[q] != tag) {
+          broken = true;
+          cv.notify_all();
+          fail(MX_ERR_COMM, "local world: ranks entered different collectives");
+        }
+  }
+  void abort_all() {
+    std::lock_guard<std::mutex> lk(mu);
+    broken = true;
+    cv.notify_all();
   }
 };
 
@@ -174,60 +182,54 @@ struct LocalComm : Comm {
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
   }
 
+  // Host-ordered: a rank's stream is drained before its buffers are
+  // published and again before peers may reuse them, so no HIP object is
+  // shared between the rank threads (test-only communicator).
   void allreduce_sum(double *dev, int n) override {
     if (size == 1 || n <= 0) return;
     if ((int)tmp.n < n) tmp.alloc((size_t)n < 64 ? 64 : (size_t)n);
-    HIPCHECK(hipEventRecord(w->ev_ready[rank], stream));
+    HIPCHECK(hipStreamSynchronize(stream));
     w->red_ptr[rank] = dev;
-    w->barrier();
+    w->barrier(rank, 1000 + n);
     PtrPack pk;
-    for (int q = 0; q < size; ++q) {
-      HIPCHECK(hipStreamWaitEvent(stream, w->ev_ready[q], 0));
-      pk.p[q] = w->red_ptr[q];
-    }
+    for (int q = 0; q < size; ++q) pk.p[q] = w->red_ptr[q];
     local_sum_kernel<<<grid_for(n, 256), 256, 0, stream>>>(pk, size, n, tmp.p);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipEventRecord(w->ev_done[rank], stream));
-    w->barrier();
-    for (int q = 0; q < size; ++q) HIPCHECK(hipStreamWaitEvent(stream, w->ev_done[q], 0));
+    HIPCHECK(hipStreamSynchronize(stream));
+    w->barrier();                  // every rank has read every dev
     HIPCHECK(hipMemcpyAsync(dev, tmp.p, sizeof(double) * n, hipMemcpyDeviceToDevice, stream));
-    w->barrier();
   }
 
   void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs, hipStream_t st) override {
     if (!st) st = stream;
-    HIPCHECK(hipEventRecord(w->ev_ready[rank], st));
+    HIPCHECK(hipStreamSynchronize(st));
     w->posted[rank] = sends;
-    w->barrier();
+    w->barrier(rank, 2);
     for (const Msg &r : recvs) {
       const Msg *src = nullptr;
       for (const Msg &s : w->posted[r.peer]) if (s.peer == rank) { src = &s; break; }
       if (!src || src->bytes != r.bytes) fail(MX_ERR_COMM, "local exchange: unmatched message");
-      HIPCHECK(hipStreamWaitEvent(st, w->ev_ready[r.peer], 0));
       if (r.bytes) HIPCHECK(hipMemcpyAsync(r.buf, src->buf, r.bytes, hipMemcpyDeviceToDevice, st));
     }
-    HIPCHECK(hipEventRecord(w->ev_done[rank], st));
-    w->barrier();
-    // the senders' buffers may be overwritten only after every receiver copied them
-    for (const Msg &s : sends) HIPCHECK(hipStreamWaitEvent(st, w->ev_done[s.peer], 0));
-    w->barrier();
+    HIPCHECK(hipStreamSynchronize(st));
+    w->barrier();                  // the senders' buffers may be overwritten now
   }
 
   void alltoall_i64(const int64_t *send, int64_t *recv) override {
     for (int q = 0; q < size; ++q) w->slots[(size_t)rank * size + q] = send[q];
-    w->barrier();
+    w->barrier(rank, 3);
     for (int q = 0; q < size; ++q) recv[q] = w->slots[(size_t)q * size + rank];
     w->barrier();
   }
   void allgather_i64(int64_t v, int64_t *all) override {
     w->slots[rank] = v;
-    w->barrier();
+    w->barrier(rank, 4);
     for (int q = 0; q < size; ++q) all[q] = w->slots[q];
     w->barrier();
   }
   void barrier() override {
     HIPCHECK(hipStreamSynchronize(stream));
-    w->barrier();
+    w->barrier(rank, 5);
   }
 };
 
@@ -241,5 +243,6 @@ Comm *make_local_comm(void *world, int rank, int device) {
   return new LocalComm(w, rank, device);
 }
 void destroy_local_world(void *world) { delete static_cast<LocalWorld *>(world); }
+void abort_local_world(void *world) { static_cast<LocalWorld *>(world)->abort_all(); }
 
 }  // namespace mx

@@ -35,7 +35,17 @@ __device__ __forceinline__ void block_sum_to_partials(double (&v)[NV], double *p
 __device__ __forceinline__ double block_sum_array(const double *__restrict__ p, int n) {
   __shared__ double sh[4];
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) s += p[i];
+  int i = threadIdx.x;
+  // eight loads in flight, summed in the same sequential order as the
+  // plain strided loop (the fold order, hence the bits, are unchanged)
+  for (; i + 7 * 256 < n; i += 8 * 256) {
+    double t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = p[i + q * 256];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += t[q];
+  }
+  for (; i < n; i += 256) s += p[i];
   s = wave_sum(s);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;

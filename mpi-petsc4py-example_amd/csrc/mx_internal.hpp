@@ -76,6 +76,7 @@ Comm *make_rccl_comm(int rank, int size, int device, const void *uid, size_t len
 void *make_local_world(int size);
 Comm *make_local_comm(void *world, int rank, int device);
 void destroy_local_world(void *world);
+void abort_local_world(void *world);
 void get_unique_id(void *out, size_t len);
 
 // ---------------------------------------------------------------- matrix
@@ -107,7 +108,7 @@ struct Sell {
 };
 
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
-struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; };
+struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -193,14 +194,27 @@ __device__ __forceinline__ double papply(const Jac &J, double r, int64_t i) {
 }
 
 // SpMV (mx_spmv.hip)
-enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2 };
+enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2, SPMV_CG = 3 };
+// SPMV_CG: the CG direction update and the deferred solution update ride in
+// the MatMult.  The operand is p_i = z + b p_{i-1} (z = jac(r), i == 0: p = z),
+// formed on the fly wherever the product reads it and stored once for the
+// owned rows; x += xa p_{i-1} is applied to the owned rows when xpend != 0.
+// coef -> device doubles {b, xa, xpend} written by the scalar kernels.
+struct CgFuse {
+  const double *r = nullptr;
+  const double *pold = nullptr;
+  double *pnew = nullptr;
+  double *x = nullptr;
+  const double *coef = nullptr;
+  Jac jac;
+};
 void halo_begin(Mat *A, const double *x);  // pack + exchange into A->halo.lvec (compute stream)
 void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                  int *done_flag);
 // MatMult with the halo on the comm stream overlapping the interior slices;
-// returns the number of partials written (DOT mode) for the fold.
+// returns the number of partials written (DOT / CG mode) for the fold.
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                    int *done_flag);
+                    int *done_flag, const CgFuse *cg = nullptr);
 int spmv_blocks(const Mat *A);
 void mat_mult(Mat *A, const double *x, double *y);
 

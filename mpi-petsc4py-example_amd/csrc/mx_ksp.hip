@@ -51,7 +51,10 @@ struct KspState {
   double res, ksp_rnorm, gm_rnorm0, scale;
   int its, reason, done, max_it;
   int normtype, guess_zero, inner_stop, it;
-  int itcount, max_k, nv, pad;
+  int itcount, max_k, nv, xi;
+  // fused CG (SPMV_CG): {b, xa, xpend} read by the MatMult -- p_i = z + b p_{i-1},
+  // x += xa p_{xi} pending while xpend != 0 (CgFuse::coef points at pb)
+  double pb, xa, xpend;
 };
 
 // ------------------------------------------------------------------ shared scalar logic
@@ -187,6 +190,7 @@ __global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double 
   if (reason) { stop(s, reason); return; }
   if (not_finite(s->beta)) { stop(s, R_DIVERGED_NANORINF); return; }
   s->its = 1;                                   // top of iteration 0
+  s->pb = 0.0;                                  // i == 0: p = z
   if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
 }
 
@@ -205,12 +209,34 @@ __global__ void cg_p_kernel(int64_t n, const KspState *__restrict__ s, const dou
   }
 }
 
+// cg_p_kernel plus the previous iteration's deferred x step, read from the
+// same p_{i-1} before it is overwritten: x += xa p_{i-1}; p = z + b p_{i-1}
+__global__ void cg_px_kernel(int64_t n, const KspState *__restrict__ s, const double *__restrict__ r,
+                             const Jac jac, double *__restrict__ p, double *__restrict__ x) {
+  if (s->done) return;
+  const int i = s->its - 1;
+  const double b = i == 0 ? 0.0 : s->beta / s->betaold;
+  const bool xp = s->xpend != 0.0;
+  const double a = s->xa;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    const double po = p[k];
+    const double z = papply(jac, r[k], k);
+    if (xp) x[k] = fma(a, po, x[k]);            // VecAXPY(X, a, P) of iteration i-1
+    p[k] = (b == 0.0) ? z : z + b * po;         // VecAYPX_Seq (b == 0 copies)
+  }
+}
+
 // dpi = p.w, indefiniteness checks, alpha = beta/dpi
+// fused_cg: this iteration's MatMult has applied the pending x step; the
+// step of this iteration becomes pending (applied by the next MatMult or by
+// cg_finish_x_kernel) -- the same x += a p, one iteration later.
 __global__ void __launch_bounds__(256) cg_alpha_kernel(KspState *s, const double *partials,
-                                                       int nblocks, int fused) {
+                                                       int nblocks, int fused, int fused_cg) {
   if (s->done) return;
   const int i = s->its - 1;
   if (!gather_red<1>(s, partials, nblocks, fused)) return;
+  if (fused_cg) s->xpend = 0.0;
   s->dpiold = s->dpi;
   s->dpi = s->red[0];
   if (not_finite(s->dpi)) { stop(s, R_DIVERGED_NANORINF); return; }
@@ -219,6 +245,7 @@ __global__ void __launch_bounds__(256) cg_alpha_kernel(KspState *s, const double
   const int sg = (dpi > 0) - (dpi < 0), sgo = (dpo > 0) - (dpo < 0);
   if (dpi == 0.0 || (i > 0 && sg * sgo < 0)) { stop(s, R_DIVERGED_INDEFINITE_MAT); return; }
   s->alpha = s->beta / s->dpi;
+  if (fused_cg) { s->xa = s->alpha; s->xpend = 1.0; s->xi = i; }
 }
 
 // x += a p, r -= a w (BLAS daxpy = fma), z = d.*r, partials [z.z, z.r, r.r]
@@ -232,7 +259,7 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, const KspStat
   double v[3] = {0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    x[i] = fma(a, p[i], x[i]);
+    if (x) x[i] = fma(a, p[i], x[i]);            // x == null: deferred into the next MatMult
     const double ri = fma(-a, w[i], r[i]);
     r[i] = ri;
     const double zi = papply(jac, ri, i);
@@ -264,8 +291,19 @@ __global__ void __launch_bounds__(256) cg_conv_kernel(KspState *s, const double 
   if (not_finite(zr)) { stop(s, R_DIVERGED_NANORINF); return; }
   if (i + 1 >= s->max_it) { stop(s, R_DIVERGED_ITS); return; }
   s->its = i + 2;                               // top of iteration i+1
+  s->pb = s->beta / s->betaold;                 // VecAYPX coefficient of iteration i+1
   if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
   if (s->beta * s->betaold < 0.0) { stop(s, R_DIVERGED_INDEFINITE_PC); return; }
+}
+
+// the x step still pending when the solve stopped (fused CG)
+__global__ void cg_finish_x_kernel(int64_t n, const KspState *__restrict__ s, const double *__restrict__ p0,
+                                   const double *__restrict__ p1, double *__restrict__ x) {
+  if (s->xpend == 0.0) return;
+  const double a = s->xa;
+  const double *__restrict__ p = (s->xi & 1) ? p1 : p0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = fma(a, p[i], x[i]);
 }
 
 // ------------------------------------------------------------------ GMRES kernels
@@ -585,8 +623,9 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   const size_t nv = (size_t)std::max<int64_t>(n, 1);
   const size_t npart = (size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 64;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
-  Carve cv(workspace(A, carve_size({nv, nv, nv, npart, nhist})));
+  Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist})));
   struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
+  double *pv2 = cv.take(nv);   // fused CG: p_i alternates between pv (i even) and pv2
   struct { KspState *p; } sd{state_buf(A)};
   KspState hs;
   init_state(hs, p, normtype);
@@ -620,24 +659,49 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   const unsigned egrid = grid_for(n, 256, 8192);
   int *done = &s->done;
   double *hist_d = hist_host ? hist.p : nullptr;
-  auto iteration = [&]() {
-    cg_p_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p);
-    timer.begin();
-    const int nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done);
-    timer.end();
+  // fused: the direction update and the previous x step ride in the MatMult
+  // (SPMV_CG); p ping-pongs between two buffers since neighbours read p_{i-1}
+  // 1: direction update + x step inside the MatMult (SPMV_CG)
+  // 2: x step deferred into the next direction update (cg_px_kernel)
+  // 3 (auto): 1 while r and p of the rank fit the 256 MB MALL (measured:
+  // -14% per iteration at 128^3, -8% at 64^3), else 2 (-4% at 256^3, where
+  // the two-vector gathers of mode 1 overflow the per-XCD L2)
+  const int fmode = g_knobs.cg_fuse == 3 ? (n <= (int64_t(8) << 20) ? 1 : 2) : g_knobs.cg_fuse;
+  const bool fuse_cg = fmode == 1;
+  const bool defer_x = fmode != 0;
+  // p_{-1} = -0.0: iteration 0's z + (+0)(-0) is exactly z (VecCopy)
+  if (fuse_cg) vec_set(st, n, -0.0, pv2);
+  auto iteration = [&](int it) {
+    int nb_spmv;
+    if (fuse_cg) {
+      CgFuse cg;
+      cg.r = r.p; cg.pold = (it & 1) ? pv.p : pv2; cg.pnew = (it & 1) ? pv2 : pv.p;
+      cg.x = x; cg.coef = &s->pb; cg.jac = dinv;
+      timer.begin();
+      nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg);
+      timer.end();
+    } else {
+      if (defer_x) cg_px_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p, x);
+      else cg_p_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p);
+      timer.begin();
+      nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done);
+      timer.end();
+    }
     if (!fused) { finish_reduce(part.p, nb_spmv, 1, red, st, done); c->allreduce_sum(red, 1); }
-    cg_alpha_kernel<<<1, 256, 0, st>>>(s, part.p, nb_spmv, fused);
-    cg_update_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, s, pv.p, w.p, x, r.p, dinv, part.p);
+    cg_alpha_kernel<<<1, 256, 0, st>>>(s, part.p, nb_spmv, fused, defer_x);
+    const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : pv.p;
+    cg_update_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, part.p);
     if (!fused) { finish_reduce(part.p, RED_BLOCKS, 3, red, st, done); c->allreduce_sum(red, 3); }
     cg_conv_kernel<<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_d);
     HIPCHECK(hipGetLastError());
   };
-  const bool graph = g_knobs.graph && c->capturable && !p.profile;
+  // a captured batch must start on an even iteration when p ping-pongs
+  const bool graph = g_knobs.graph && c->capturable && !p.profile && (!fuse_cg || (poll & 1) == 0);
   std::vector<uintptr_t> key;
   if (graph) {
     key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
            (uintptr_t)poll, (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt, (uintptr_t)g_knobs.spmv_grid,
-           (uintptr_t)g_knobs.force_coll};
+           (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;
@@ -649,20 +713,24 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       HIPCHECK(hipGraphLaunch(A->cg_graph, st));
       i += poll;
     } else {
-      for (int k = 0; k < poll && i < p.max_it; ++k, ++i) iteration();
+      for (int k = 0; k < poll && i < p.max_it; ++k, ++i) iteration(i);
     }
     if (poller.batch(done)) break;
     if (graph && !use_graph && i < p.max_it) {
       if (A->cg_graph) { HIPCHECK(hipGraphExecDestroy(A->cg_graph)); A->cg_graph = nullptr; }
       hipGraph_t g;
       HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-      for (int k = 0; k < poll; ++k) iteration();
+      for (int k = 0; k < poll; ++k) iteration(i + k);
       HIPCHECK(hipStreamEndCapture(st, &g));
       HIPCHECK(hipGraphInstantiate(&A->cg_graph, g, nullptr, nullptr, 0));
       HIPCHECK(hipGraphDestroy(g));
       A->cg_key = key;
       use_graph = true;
     }
+  }
+  if (defer_x) {   // p is in place for mode 2: both buffer slots are pv
+    cg_finish_x_kernel<<<egrid, 256, 0, st>>>(n, s, pv.p, fuse_cg ? pv2 : pv.p, x);
+    HIPCHECK(hipGetLastError());
   }
   HIPCHECK(hipEventRecord(ev.b, st));
   read_state(st, s, hs);

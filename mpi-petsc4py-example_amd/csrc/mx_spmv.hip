@@ -35,15 +35,56 @@ template <bool NT, class T> __device__ __forceinline__ T ld(const T *p) {
   else return *p;
 }
 
+// The operand of the product is read through a source functor: a plain
+// vector, or (SPMV_CG) the CG direction p_i = z + b p_{i-1}, z = jac(r),
+// evaluated from r and p_{i-1} at every index the product touches.  The
+// expression is the one VecAYPX applies (one multiply, one add, each rounded),
+// so every evaluation of p_i[j] -- here, in the halo pack and in the owner's
+// store -- yields the same bits as a separate update pass would.
+// at(base, lane) = value at base + lane for a wave-uniform base: the address
+// is one SGPR pair plus the lane's fixed byte offset, shared by every gather
+struct XPlain {
+  const double *__restrict__ x;
+  __device__ __forceinline__ double operator()(int64_t j) const { return x[j]; }
+  __device__ __forceinline__ double at(int64_t base, int lane) const { return (x + base)[lane]; }
+};
+// JM = the Jacobi form, compile-time so every load is unconditional (a
+// runtime form turns each gather into a branch around the dinv load)
+template <int JM>
+struct XCg {
+  const double *__restrict__ r;
+  const double *__restrict__ p;
+  const double *__restrict__ d;
+  double c, b;
+  __device__ __forceinline__ double form(double rj, double pj, double dj) const {
+    double z = rj;
+    if constexpr (JM == 1) z = rj * dj;             // PCApply_Jacobi, vector
+    else if constexpr (JM == 2) z = rj * c;         // uniform diagonal, scalar
+    // VecAYPX_Seq.  Its b == 0 copy needs no select: iteration 0 runs with
+    // b = +0 against p_{-1} = -0.0, and z + (+0)(-0) = z + (-0) = z for every z
+    return z + b * pj;
+  }
+  __device__ __forceinline__ double operator()(int64_t j) const {
+    return form(r[j], p[j], JM == 1 ? d[j] : 0.0);
+  }
+  __device__ __forceinline__ double at(int64_t base, int lane) const {
+    return form((r + base)[lane], (p + base)[lane], JM == 1 ? (d + base)[lane] : 0.0);
+  }
+};
+
 // Every slice body below issues all of its loads before the first use, with
 // predicated (never branching) lanes: absent entries gather the always-valid
 // x[0] and are then skipped by a select, so the running sum sees exactly the
 // present entries in ascending column order -- PETSc's order, bit for bit.
 
 // aligned-offset slice with a compile-time width K (the stencil's point count)
-template <int K, bool NT>
+// inb: every gather of the slice lies inside x (wave-uniform), so the
+// absent entries can read their in-range neighbour and every gather uses the
+// uniform-base form; otherwise absent entries read x[0]
+template <int K, bool NT, class XS>
 __device__ __forceinline__ double dia_slice_fixed(const double *__restrict__ vbase, const int32_t *__restrict__ off,
-                                                  uint32_t mk, int64_t row, const double *__restrict__ x, int lane) {
+                                                  uint32_t mk, int64_t row, const XS &x, int lane, bool inb,
+                                                  int64_t srow) {
   constexpr int NP = K / 2;
   double v[K], xv[K];
   const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
@@ -54,8 +95,13 @@ __device__ __forceinline__ double dia_slice_fixed(const double *__restrict__ vba
     v[2 * p + 1] = t.y;
   }
   if constexpr (K & 1) v[K - 1] = ld<NT>(vbase + NP * 2 * SLICE + lane);
+  if (inb) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) xv[j] = x[((mk >> j) & 1u) ? row + off[j] : 0];
+    for (int j = 0; j < K; ++j) xv[j] = x.at(srow + off[j], lane);
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) xv[j] = x(((mk >> j) & 1u) ? row + off[j] : 0);
+  }
   double sum = 0.0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -66,9 +112,10 @@ __device__ __forceinline__ double dia_slice_fixed(const double *__restrict__ vba
 }
 
 // aligned-offset slice, runtime width: batches of 8 slots
-template <bool NT>
+template <bool NT, class XS>
 __device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase, const int32_t *__restrict__ off,
-                                                int k, uint32_t mk, int64_t row, const double *__restrict__ x, int lane) {
+                                                int k, uint32_t mk, int64_t row, const XS &x, int lane, bool inb,
+                                                int64_t srow) {
   const int np = k >> 1;
   const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
   double sum = 0.0;
@@ -85,7 +132,8 @@ __device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase
     for (int q = 0; q < 8; ++q) {
       const int j = 2 * p0 + q;
       const bool ok = j < 2 * np && ((mk >> j) & 1u);
-      xv[q] = x[ok ? row + off[j < 2 * np ? j : 0] : 0];
+      const int jj = j < 2 * np ? j : 0;
+      xv[q] = inb ? x.at(srow + off[jj], lane) : x(ok ? row + off[jj] : 0);
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -97,7 +145,7 @@ __device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase
   if (k & 1) {
     const double v = ld<NT>(vbase + (int64_t)np * 2 * SLICE + lane);
     const bool ok = (mk >> (k - 1)) & 1u;
-    const double xv = x[ok ? row + off[k - 1] : 0];
+    const double xv = inb ? x.at(srow + off[k - 1], lane) : x(ok ? row + off[k - 1] : 0);
     const double t = sum + v * xv;
     sum = ok ? t : sum;
   }
@@ -105,9 +153,9 @@ __device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase
 }
 
 // general SELL slice (paired layout), continuing `sum`: batches of 8 entries
-template <bool NT>
+template <bool NT, class XS>
 __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, const double *__restrict__ vbase,
-                                             int w, double sum, const double *__restrict__ x, int lane) {
+                                             int w, double sum, const XS &x, int lane) {
   const int np = w >> 1;
   const int2v *__restrict__ cp = reinterpret_cast<const int2v *>(cbase) + lane;
   const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
@@ -123,7 +171,7 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
       v[2 * q] = t.x; v[2 * q + 1] = t.y;
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) xv[q] = x[c[q] >= 0 ? c[q] : 0];
+    for (int q = 0; q < 8; ++q) xv[q] = x(c[q] >= 0 ? c[q] : 0);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const double t = sum + v[q] * xv[q];
@@ -134,7 +182,7 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
     const int64_t t = (int64_t)np * 2 * SLICE + lane;
     const int c = ld<NT>(cbase + t);
     const double v = ld<NT>(vbase + t);
-    const double xv = x[c >= 0 ? c : 0];
+    const double xv = x(c >= 0 ? c : 0);
     const double tt = sum + v * xv;
     sum = c >= 0 ? tt : sum;
   }
@@ -147,16 +195,16 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
 // order, so the +-1 / +-n / +-n^2 re-reads of x stay in that XCD's 4 MB L2.
 // Placement only affects speed, never results.  KD > 0 specialises the
 // aligned-offset body for the matrix's dominant slice width.
-template <int MODE, bool NT, int KD, bool SPLIT>
+template <int MODE, bool NT, int KD, bool SPLIT, int JM = 0>
 __global__ void __launch_bounds__(256) spmv_sell_kernel(
-    int64_t m, int64_t nslices, const int64_t *__restrict__ sptr_d,
+    int64_t m, int64_t ncols, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
     const double *__restrict__ val_d, const int32_t *__restrict__ doff,
     const uint32_t *__restrict__ dmask, const int64_t *__restrict__ sptr_o,
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o,
     const double *__restrict__ val_o, const double *__restrict__ x,
     const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
-    double *__restrict__ partials, const int *__restrict__ done) {
+    double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg) {
   if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -173,20 +221,57 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     sstep = gridDim.x * SPMV_WAVES;
     send = (int)nslices;
   }
+  // operand source
+  using XS = typename std::conditional<MODE == SPMV_CG, XCg<JM>, XPlain>::type;
+  XS X;
+  double xa = 0.0;
+  bool xpend = false;
+  if constexpr (MODE == SPMV_CG) {
+    X = XCg<JM>{cg.r, cg.pold, cg.jac.d, cg.jac.c, cg.coef[0]};
+    xa = cg.coef[1];
+    xpend = cg.coef[2] != 0.0;
+  } else {
+    X = XPlain{x};
+  }
   double dot = 0.0;
   for (int s = s0; s < send; s += sstep) {
     const int64_t row = (int64_t)s * SLICE + lane;
     const int w = wid_d[s];
     const int64_t base = sptr_d[s];
+    // CG: the owned row's r, p_{i-1}, x (and dinv) are loaded with the
+    // slice's first loads so their latency overlaps the gathers
+    double own_r = 0.0, own_p = 0.0, own_x = 0.0, own_d = 0.0;
+    if constexpr (MODE == SPMV_CG) {
+      const int64_t rc = row < m ? row : 0;
+      own_r = cg.r[rc];
+      own_p = cg.pold[rc];
+      own_x = cg.x[rc];
+      if constexpr (JM == 1) own_d = cg.jac.d[rc];
+    }
     double sum;
     if (w < 0) {
       const int k = -w;
       const uint32_t mk = dmask[row];
       const int32_t *__restrict__ off = doff + (int64_t)s * DIA_MAX;
-      if (KD > 0 && k == KD) sum = dia_slice_fixed<(KD > 0 ? KD : 1), NT>(val_d + base, off, mk, row, x, lane);
-      else sum = dia_slice_any<NT>(val_d + base, off, k, mk, row, x, lane);
+      const int64_t srow = (int64_t)s * SLICE;
+      int omin = off[0], omax = off[0];
+      for (int j = 1; j < k; ++j) { omin = min(omin, off[j]); omax = max(omax, off[j]); }
+      const bool inb = srow + omin >= 0 && srow + (SLICE - 1) + omax < ncols;
+      if (KD > 0 && k == KD) sum = dia_slice_fixed<(KD > 0 ? KD : 1), NT>(val_d + base, off, mk, row, X, lane, inb, srow);
+      else sum = dia_slice_any<NT>(val_d + base, off, k, mk, row, X, lane, inb, srow);
     } else {
-      sum = sell_slice<NT>(col_d + base, val_d + base, w, 0.0, x, lane);
+      sum = sell_slice<NT>(col_d + base, val_d + base, w, 0.0, X, lane);
+    }
+    double xr = 0.0;   // operand at the owned row (DOT / CG)
+    if constexpr (MODE == SPMV_CG) {
+      double z = own_r;                         // same expression as XCg
+      if constexpr (JM == 1) z = own_r * own_d;
+      else if constexpr (JM == 2) z = own_r * cg.jac.c;
+      xr = z + X.b * own_p;
+      if (row < m) {
+        cg.pnew[row] = xr;
+        if (xpend) cg.x[row] = fma(xa, own_p, own_x);   // VecAXPY(X, a, P) of the previous step
+      }
     }
     if (SPLIT) {
       // slice with ghost entries: store the diagonal-block sum; the boundary
@@ -197,15 +282,16 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       }
     } else if (lvec) {
       const int wo = wid_o[s];
-      if (wo) sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wo, sum, lvec, lane);
+      if (wo) sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wo, sum, XPlain{lvec}, lane);
     }
     if (row < m) {
       if (MODE == SPMV_JACOBI) y[row] = papply(jac, sum, row);   // PCApply_Jacobi fused: w_i * d_i
       else y[row] = sum;
       if (MODE == SPMV_DOT) dot += x[row] * sum;           // VecDot(p, w) partial, p = x
+      if (MODE == SPMV_CG) dot += xr * sum;
     }
   }
-  if (MODE == SPMV_DOT) {
+  if (MODE == SPMV_DOT || MODE == SPMV_CG) {
     double v[1] = {dot};
     block_sum_to_partials<1>(v, partials, gridDim.x);
   }
@@ -235,7 +321,7 @@ __global__ void __launch_bounds__(256) spmv_boundary_kernel(
     const int s = list[k];
     const int64_t row = (int64_t)s * SLICE + lane;
     double sum = row < m ? y[row] : 0.0;
-    sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wid_o[s], sum, lvec, lane);
+    sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wid_o[s], sum, XPlain{lvec}, lane);
     if (row < m) {
       if (MODE == SPMV_JACOBI) y[row] = papply(jac, sum, row);
       else y[row] = sum;
@@ -254,36 +340,56 @@ __global__ void pack_kernel(int64_t n, const int32_t *__restrict__ idx, const do
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) buf[k] = x[idx[k]];
 }
 
+// halo payload of the CG direction p_i, formed from r and p_{i-1}
+template <int JM>
+__global__ void pack_cg_kernel(int64_t n, const int32_t *__restrict__ idx, const CgFuse cg,
+                               const int *__restrict__ done, double *__restrict__ buf) {
+  if (done && *done) return;
+  const XCg<JM> X{cg.r, cg.pold, cg.jac.d, cg.jac.c, cg.coef[0]};
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) buf[k] = X(idx[k]);
+}
+
 // VecScatterBegin/End(x -> lvec): pack (only if some peer's rows are not a
-// contiguous range), then one grouped send/recv with every neighbour.
-void halo_begin(Mat *A, const double *x) {
+// contiguous range; always for the CG operand, which is formed on the fly),
+// then one grouped send/recv with every neighbour, on stream `st`.
+static void halo_exchange(Mat *A, const double *x, const CgFuse *cg, const int *done, hipStream_t st) {
   Halo &H = A->halo;
-  if (A->comm->size == 1) return;
-  hipStream_t st = A->comm->stream;
-  if (H.need_pack && H.nsend) {
-    pack_kernel<<<grid_for(H.nsend, 256, 4096), 256, 0, st>>>(H.nsend, H.send_idx.p, x, H.send_buf.p);
+  const bool pack = cg || H.need_pack;
+  if (pack && H.nsend) {
+    const unsigned g = grid_for(H.nsend, 256, 4096);
+    if (cg && cg->jac.mode == 1) pack_cg_kernel<1><<<g, 256, 0, st>>>(H.nsend, H.send_idx.p, *cg, done, H.send_buf.p);
+    else if (cg && cg->jac.mode == 2) pack_cg_kernel<2><<<g, 256, 0, st>>>(H.nsend, H.send_idx.p, *cg, done, H.send_buf.p);
+    else if (cg) pack_cg_kernel<0><<<g, 256, 0, st>>>(H.nsend, H.send_idx.p, *cg, done, H.send_buf.p);
+    else pack_kernel<<<grid_for(H.nsend, 256, 4096), 256, 0, st>>>(H.nsend, H.send_idx.p, x, H.send_buf.p);
     HIPCHECK(hipGetLastError());
   }
   std::vector<Msg> sends, recvs;
   for (size_t i = 0; i < H.send_peer.size(); ++i) {
-    void *buf = H.send_contig_start[i] >= 0 ? (void *)(x + H.send_contig_start[i])
-                                            : (void *)(H.send_buf.p + H.send_off[i]);
+    void *buf = (!cg && H.send_contig_start[i] >= 0) ? (void *)(x + H.send_contig_start[i])
+                                                     : (void *)(H.send_buf.p + H.send_off[i]);
     sends.push_back({H.send_peer[i], buf, sizeof(double) * (size_t)H.send_cnt[i]});
   }
   for (size_t i = 0; i < H.recv_peer.size(); ++i)
     recvs.push_back({H.recv_peer[i], H.lvec.p + H.recv_off[i], sizeof(double) * (size_t)H.recv_cnt[i]});
-  A->comm->exchange(sends, recvs);
+  A->comm->exchange(sends, recvs, st);
+}
+
+void halo_begin(Mat *A, const double *x) {
+  if (A->comm->size == 1) return;
+  halo_exchange(A, x, nullptr, nullptr, A->comm->stream);
 }
 
 static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                        int *done_flag, bool split, hipStream_t st) {
+                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp) {
   const unsigned grid = (unsigned)spmv_blocks(A);
   const double *lvec = (A->nghost && !split) ? A->halo.lvec.p : nullptr;
   const int kd = A->sd.dia_k;
+  const CgFuse cg = cgp ? *cgp : CgFuse{};
 #define SPMV_ARGS                                                                           \
-  A->m, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
+  A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
       A->sd.mask.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac,   \
-      partials, done_flag
+      partials, done_flag, cg
 #define SPMV_KD(MODE, NT, SP)                                                                    \
   do {                                                                                           \
     switch (kd) {                                                                                \
@@ -292,6 +398,15 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
       case 27: spmv_sell_kernel<MODE, NT, 27, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;       \
       default: spmv_sell_kernel<MODE, NT, 0, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;        \
     }                                                                                            \
+  } while (0)
+#define SPMV_CGKD(JM, SP)                                                                                   \
+  do {                                                                                                      \
+    switch (kd) {                                                                                           \
+      case 5: spmv_sell_kernel<SPMV_CG, true, 5, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;           \
+      case 7: spmv_sell_kernel<SPMV_CG, true, 7, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;           \
+      case 27: spmv_sell_kernel<SPMV_CG, true, 27, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
+      default: spmv_sell_kernel<SPMV_CG, true, 0, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
+    }                                                                                                       \
   } while (0)
 #define SPMV_GO(MODE)                                                         \
   do {                                                                        \
@@ -302,9 +417,18 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
     case SPMV_PLAIN: SPMV_GO(SPMV_PLAIN); break;
     case SPMV_JACOBI: SPMV_GO(SPMV_JACOBI); break;
     case SPMV_DOT: SPMV_GO(SPMV_DOT); break;
+    case SPMV_CG:   // always non-temporal; Jacobi form as a template argument
+      if (!cgp) fail(MX_ERR_INTERNAL, "CG-fused SpMV without operands");
+      switch (cg.jac.mode) {
+        case 1: if (split) SPMV_CGKD(1, true); else SPMV_CGKD(1, false); break;
+        case 2: if (split) SPMV_CGKD(2, true); else SPMV_CGKD(2, false); break;
+        default: if (split) SPMV_CGKD(0, true); else SPMV_CGKD(0, false); break;
+      }
+      break;
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
 #undef SPMV_GO
+#undef SPMV_CGKD
 #undef SPMV_KD
 #undef SPMV_ARGS
   HIPCHECK(hipGetLastError());
@@ -312,50 +436,42 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
 
 void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                  int *done_flag) {
-  launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream);
+  launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream, nullptr);
 }
 
 constexpr int BND_BLOCKS = 64;
 
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                    int *done_flag) {
+                    int *done_flag, const CgFuse *cg) {
   Comm *c = A->comm;
   Halo &H = A->halo;
+  hipStream_t st = c->stream;
   if (c->size == 1 || H.nbnd == 0 || !g_knobs.overlap) {
-    halo_begin(A, x);
-    launch_main(A, x, y, mode, jac, partials, done_flag, false, c->stream);
+    if (c->size > 1) halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, st);
+    launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg);
     return spmv_blocks(A);
   }
-  hipStream_t st = c->stream, cs = c->comm_stream;
+  hipStream_t cs = c->comm_stream;
   if (!H.ev_x) {
     HIPCHECK(hipEventCreateWithFlags(&H.ev_x, hipEventDisableTiming));
     HIPCHECK(hipEventCreateWithFlags(&H.ev_done, hipEventDisableTiming));
   }
-  // halo on the comm stream, after x is final on the compute stream
+  // halo on the comm stream, after the operand's inputs are final on the
+  // compute stream; the CG operand's inputs (r, p_{i-1}) are only read by both
   HIPCHECK(hipEventRecord(H.ev_x, st));
   HIPCHECK(hipStreamWaitEvent(cs, H.ev_x, 0));
-  if (H.need_pack && H.nsend) {
-    pack_kernel<<<grid_for(H.nsend, 256, 4096), 256, 0, cs>>>(H.nsend, H.send_idx.p, x, H.send_buf.p);
-    HIPCHECK(hipGetLastError());
-  }
-  std::vector<Msg> sends, recvs;
-  for (size_t i = 0; i < H.send_peer.size(); ++i) {
-    void *buf = H.send_contig_start[i] >= 0 ? (void *)(x + H.send_contig_start[i])
-                                            : (void *)(H.send_buf.p + H.send_off[i]);
-    sends.push_back({H.send_peer[i], buf, sizeof(double) * (size_t)H.send_cnt[i]});
-  }
-  for (size_t i = 0; i < H.recv_peer.size(); ++i)
-    recvs.push_back({H.recv_peer[i], H.lvec.p + H.recv_off[i], sizeof(double) * (size_t)H.recv_cnt[i]});
-  c->exchange(sends, recvs, cs);
+  halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, cs);
   HIPCHECK(hipEventRecord(H.ev_done, cs));
   // interior slices meanwhile; boundary slices after the exchange
   const int nmain = spmv_blocks(A);
-  launch_main(A, x, y, mode, jac, partials, done_flag, true, st);
+  launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg);
   HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
   const int nb = std::min(BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
   double *pb = partials ? partials + nmain : nullptr;
+  // the boundary rows' operand values were stored by the main kernel (CG)
+  const double *xb = mode == SPMV_CG ? cg->pnew : x;
 #define BND(MODE) spmv_boundary_kernel<MODE><<<nb, 256, 0, st>>>(A->m, H.bnd_slices.p, H.nbnd, A->so.sptr.p, \
-      A->so.width.p, A->so.col.p, A->so.val.p, x, H.lvec.p, y, jac, pb, done_flag)
+      A->so.width.p, A->so.col.p, A->so.val.p, xb, H.lvec.p, y, jac, pb, done_flag)
   switch (mode) {
     case SPMV_PLAIN: BND(SPMV_PLAIN); break;
     case SPMV_JACOBI: BND(SPMV_JACOBI); break;

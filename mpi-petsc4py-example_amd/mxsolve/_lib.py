@@ -64,6 +64,7 @@ SIGNATURES = {
     "mx_world_create_local": (C.c_int, [C.c_int, C.POINTER(P)]),
     "mx_comm_create_local": (C.c_int, [P, C.c_int, C.c_int, C.POINTER(P)]),
     "mx_world_destroy": (C.c_int, [P]),
+    "mx_world_abort": (C.c_int, [P]),
     "mx_comm_destroy": (C.c_int, [P]),
     "mx_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "mx_comm_stream": (C.c_int, [P, C.POINTER(P)]),

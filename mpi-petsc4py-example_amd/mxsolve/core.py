@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import KSPParams, KSPResult, MatInfo, call
+from ._lib import KSPParams, KSPResult, MatInfo, MxError, call
 
 KSP_TYPES = {"cg": 0, "gmres": 1, "preonly": 2}
 PC_TYPES = {"none": 0, "jacobi": 1}
@@ -95,6 +95,10 @@ class DeviceComm:
             self.h = None
 
 
+def _peer_abort(e) -> bool:
+    return isinstance(e, MxError) and "another rank failed" in str(e)
+
+
 class LocalWorld:
     """P virtual ranks sharing one GPU in one process (one host thread per rank)."""
 
@@ -123,6 +127,7 @@ class LocalWorld:
                 out[r] = fn(c)
             except BaseException as e:  # noqa: BLE001
                 errs[r] = e
+                call("mx_world_abort", self.h)     # release ranks waiting on this one
             finally:
                 torch.cuda.synchronize(device)
                 c.destroy()
@@ -132,9 +137,9 @@ class LocalWorld:
             t.start()
         for t in ts:
             t.join()
-        for e in errs:
-            if e is not None:
-                raise e
+        first = [e for e in errs if e is not None and not _peer_abort(e)]
+        for e in first or [e for e in errs if e is not None]:
+            raise e
         return out
 
 

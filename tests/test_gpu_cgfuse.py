@@ -1,0 +1,102 @@
+"""CG with the direction update and the x step fused into the MatMult
+(SPMV_CG, knob 9) against the separate-pass iteration: identical bits in x,
+the residual history, the iteration count and the reason -- on one rank, on
+2 and 4 in-process ranks with the overlapped halo, for uniform and variable
+Jacobi, no preconditioner, every norm type, a nonzero guess, max_it limits
+and an indefinite stop.  Both are checked against the oracle elsewhere."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _knob(v):
+    from mxsolve import _lib
+    return _lib.load().mx_debug_set(9, v)
+
+
+def _mat(comm, oracle, kind):
+    from mxsolve.core import DMat
+    if kind == "varidiag":         # SPD, non-uniform diagonal: the vector Jacobi path
+        ip, c, v = oracle.stencil("poisson3d", 12)
+        M = ip.size - 1
+        rows = np.repeat(np.arange(M), np.diff(ip))
+        d = 1.0 + np.random.default_rng(3).random(M)
+        R = np.concatenate([rows, np.arange(M)])
+        Cc = np.concatenate([c, np.arange(M)])
+        V = np.concatenate([v, d])
+        r0, r1 = oracle.split_ownership(M, comm.size)[comm.rank:comm.rank + 2]
+        sel = (R >= r0) & (R < r1)
+        return DMat.from_coo(comm, M, M, R[sel], Cc[sel], V[sel], add=True)
+    if kind == "indef":
+        M = 40
+        d = np.linspace(4.0, -1.0, M)
+        r0, r1 = oracle.split_ownership(M, comm.size)[comm.rank:comm.rank + 2]
+        idx = np.arange(r0, r1)
+        return DMat.from_coo(comm, M, M, idx, idx, d[r0:r1])
+    return DMat.stencil(comm, kind, 14)
+
+
+def _run(comm, oracle, kind, fuse, **kw):
+    old = _knob(fuse)
+    try:
+        return _solve(comm, oracle, kind, **kw)
+    finally:
+        _knob(old)
+
+
+def _solve(comm, oracle, kind, **kw):
+    from mxsolve.core import rhs_hash
+    if True:
+        A = _mat(comm, oracle, kind)
+        info = A.info()
+        b = comm.empty(info["m"])
+        rhs_hash(comm, info["rstart"], b)
+        x = comm.zeros(info["m"])
+        if kw.pop("negzero", False):     # -0.0 entries: p_0 = z keeps the sign of zero
+            b[::5] = -0.0
+        if kw.pop("guess", False):
+            rhs_hash(comm, info["rstart"] + 7, x)
+            x.mul_(0.25)
+            kw["guess_nonzero"] = True
+        r = A.solve(b, x, ksp="cg", history=True, **kw)
+        A.destroy()
+        return r["its"], r["reason"], r["history"], x.cpu().numpy()
+
+
+CASES = [("poisson3d", {}), ("poisson3d", {"max_it": 7}), ("poisson3d", {"max_it": 16}),
+         ("poisson3d", {"pc": "none"}), ("poisson3d", {"norm": "unpreconditioned"}),
+         ("poisson3d", {"norm": "natural"}), ("poisson3d", {"norm": "none", "max_it": 20}),
+         ("poisson3d", {"guess": True}), ("poisson3d27", {}), ("varidiag", {}),
+         ("varidiag", {"max_it": 5}), ("indef", {"pc": "none"}), ("poisson3d", {"negzero": True, "max_it": 3})]
+
+
+def _same(a, b):
+    assert (a[0], a[1]) == (b[0], b[1])
+    assert np.array_equal(a[2].view(np.uint64), b[2].view(np.uint64))
+    assert np.array_equal(a[3].view(np.uint64), b[3].view(np.uint64))
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("kind,kw", CASES)
+def test_fused_equals_separate_one_rank(selfcomm, oracle_mod, kind, kw, mode):
+    _same(_run(selfcomm, oracle_mod, kind, mode, **dict(kw)), _run(selfcomm, oracle_mod, kind, 0, **dict(kw)))
+
+
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("kind,kw", [("poisson3d", {}), ("varidiag", {}), ("poisson3d", {"max_it": 9})])
+def test_fused_equals_separate_ranks(oracle_mod, P, kind, kw):
+    from mxsolve.core import LocalWorld
+    outs = {}
+    for fuse in (1, 2, 0):
+        w = LocalWorld(P)
+        old = _knob(fuse)          # set once, outside the rank threads
+        try:
+            outs[fuse] = w.run(lambda comm: _solve(comm, oracle_mod, kind, **dict(kw)))
+        finally:
+            _knob(old)
+            w.destroy()
+    for mode in (1, 2):
+        for a, b in zip(outs[mode], outs[0]):
+            _same(a, b)

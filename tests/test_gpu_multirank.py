@@ -226,3 +226,18 @@ def test_offprocess_row_out_of_range():
         return 0
 
     assert run_ranks(2, body) == [2, 2]
+
+
+def test_failed_rank_releases_peers():
+    """A rank that raises before a collective must not leave its peers waiting:
+    they get MX_ERR_COMM and LocalWorld.run re-raises the original error."""
+    from mxsolve.core import DMat
+
+    def body(comm):
+        if comm.rank == 1:
+            raise KeyError("rank 1 fails first")
+        A = DMat.stencil(comm, "poisson3d", 12)   # collective: needs rank 1
+        A.destroy()
+
+    with pytest.raises(KeyError):
+        run_ranks(3, body)

@@ -9,6 +9,7 @@ read by bench.py for roofline.traffic).
 import csv
 import json
 import os
+import re
 import shutil
 import statistics
 import sys
@@ -16,10 +17,17 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def short(name):
+    """'void mx::spmv_sell_kernel<3, true, 7, false>(long, ...)' -> 'spmv_sell_kernel<3,true,7,false>'."""
+    n = re.sub(r"^void\s+", "", name)
+    n = n.split("(")[0].replace("mx::", "").replace(" ", "")
+    return n
+
+
 def pmc(path):
     per = {}
     for r in csv.DictReader(open(path)):
-        per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+        per.setdefault(short(r["Kernel_Name"]), []).append(float(r["Counter_Value"]))
     return per
 
 
@@ -36,23 +44,30 @@ def main():
     calib = pmc(os.path.join(src, "calib", "run_counter_collection.csv"))
     known = (1 << 27) * 8
     # the calibration runs 3 launches at 8 B/lane then 3 at 16 B/lane
-    cal = calib.get("stream_read_kernel", [])
-    f8 = known / (statistics.median(cal[:3]) * 1024) if len(cal) >= 6 else None
-    f16 = known / (statistics.median(cal[3:6]) * 1024) if len(cal) >= 6 else None
+    c8 = next((v for k, v in calib.items() if k.startswith("stream_read_kernel<8")), [])
+    c16 = next((v for k, v in calib.items() if k.startswith("stream_read_kernel<16")), [])
+    f8 = known / (statistics.median(c8) * 1024) if c8 else None
+    f16 = known / (statistics.median(c16) * 1024) if c16 else None
     m = grid ** 3 // ngpu
     nnz = 7 * grid ** 3 - 6 * grid ** 2
-    alg = 12 * nnz + 4 * (m + 1) + 8 * m + 8 * m
+    ghosts = 0 if ngpu == 1 else (grid * grid * (1 if ngpu == 2 else 2))
+    spmv_alg = 12 * nnz // ngpu + 4 * (m + 1) + 8 * (m + ghosts) + 8 * m
+    alg = spmv_alg + 32 * m          # SPMV_CG: + r read, x read/write, p_i write
     out = {}
     lines = [f"# {tag}: rocprofv3 summary (3D 7-pt Poisson {grid}^3, N={ngpu}, bench.py --steps 50)", "",
              "| kernel | calls | avg us | % time | FETCH_SIZE KB (raw, median) | WRITE_SIZE KB (median) |",
              "|---|---|---|---|---|---|"]
     for r in stats[:14]:
-        k = r["Name"]
+        k = short(r["Name"])
         fk = statistics.median(fetch[k]) if k in fetch else None
         wk = statistics.median(write[k]) if k in write else None
         lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.1f} | "
                      f"{'' if fk is None else f'{fk:.0f}'} | {'' if wk is None else f'{wk:.0f}'} |")
-    sp = "spmv_sell_kernel"
+    # the CG-fused MatMult (mode 3) of the solve; mode 2 when fusion is off
+    sp = next((k for k in fetch if k.startswith("spmv_sell_kernel<3,")), None) or \
+        next((k for k in fetch if k.startswith("spmv_sell_kernel<2,")), None)
+    if sp and not sp.startswith("spmv_sell_kernel<3,"):
+        alg = spmv_alg
     if sp in fetch and sp in write:
         fr = statistics.median(fetch[sp]) * 1024
         wr = statistics.median(write[sp]) * 1024
@@ -62,8 +77,9 @@ def main():
             "bytes_per_launch": round(traffic), "fetch_bytes_raw": round(fr), "write_bytes": round(wr),
             "fetch_correction": round(corr, 4), "calib_8B_per_lane": f8 and round(f8, 4),
             "calib_16B_per_lane": f16 and round(f16, 4), "algorithmic_bytes": alg,
-            "traffic_over_algorithmic": round(traffic / alg, 4), "source": f"profiles/{tag}_summary.md"}
-        lines += ["", f"SpMV per launch: FETCH_SIZE {fr/1e6:.1f} MB raw x {corr:.3f} (calibrated, 16 B/lane NT stream; "
+            "traffic_over_algorithmic": round(traffic / alg, 4), "kernel": sp,
+            "source": f"profiles/{tag}_summary.md"}
+        lines += ["", f"{sp} per launch: FETCH_SIZE {fr/1e6:.1f} MB raw x {corr:.3f} (calibrated, 16 B/lane NT stream; "
                   f"8 B/lane factor {f8 and round(f8, 3)}) + WRITE_SIZE {wr/1e6:.1f} MB = {traffic/1e6:.1f} MB "
                   f"vs {alg/1e6:.1f} MB algorithmic ({traffic/alg:.3f}x)."]
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
