@@ -159,6 +159,7 @@ struct Mat {
   // captured CG iteration batch (hipGraph), reused while its key matches
   hipGraphExec_t cg_graph = nullptr;
   std::vector<uintptr_t> cg_key;
+  bool cg_graph_failed = false;     // capture failed once: this operator stays eager
   ~Mat() {
     if (cg_graph) (void)hipGraphExecDestroy(cg_graph);
   }

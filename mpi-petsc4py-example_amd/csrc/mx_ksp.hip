@@ -696,7 +696,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     HIPCHECK(hipGetLastError());
   };
   // a captured batch must start on an even iteration when p ping-pongs
-  const bool graph = g_knobs.graph && c->capturable && !p.profile && (!fuse_cg || (poll & 1) == 0);
+  bool graph = g_knobs.graph && c->capturable && !p.profile && (!fuse_cg || (poll & 1) == 0) &&
+               !A->cg_graph_failed;
   std::vector<uintptr_t> key;
   if (graph) {
     key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
@@ -718,14 +719,31 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     if (poller.batch(done)) break;
     if (graph && !use_graph && i < p.max_it) {
       if (A->cg_graph) { HIPCHECK(hipGraphExecDestroy(A->cg_graph)); A->cg_graph = nullptr; }
-      hipGraph_t g;
-      HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-      for (int k = 0; k < poll; ++k) iteration(i + k);
-      HIPCHECK(hipStreamEndCapture(st, &g));
-      HIPCHECK(hipGraphInstantiate(&A->cg_graph, g, nullptr, nullptr, 0));
-      HIPCHECK(hipGraphDestroy(g));
-      A->cg_key = key;
-      use_graph = true;
+      // A capture that fails (a runtime or collective library that cannot
+      // record some call) leaves the iterations un-run: drop the graph for
+      // this operator and carry on eagerly from the same state.
+      hipGraph_t g = nullptr;
+      try {
+        HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+        for (int k = 0; k < poll; ++k) iteration(i + k);
+        HIPCHECK(hipStreamEndCapture(st, &g));
+        HIPCHECK(hipGraphInstantiate(&A->cg_graph, g, nullptr, nullptr, 0));
+        HIPCHECK(hipGraphDestroy(g));
+        A->cg_key = key;
+        use_graph = true;
+      } catch (const Error &) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+          hipGraph_t junk = nullptr;
+          (void)hipStreamEndCapture(st, &junk);
+          if (junk) (void)hipGraphDestroy(junk);
+        }
+        if (g) (void)hipGraphDestroy(g);
+        if (A->cg_graph) { (void)hipGraphExecDestroy(A->cg_graph); A->cg_graph = nullptr; }
+        (void)hipGetLastError();
+        A->cg_graph_failed = true;
+        graph = false;
+      }
     }
   }
   if (defer_x) {   // p is in place for mode 2: both buffer slots are pv

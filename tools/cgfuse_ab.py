@@ -14,7 +14,7 @@ kind = sys.argv[2] if len(sys.argv) > 2 else "poisson3d"
 A = DMat.stencil(comm, kind, n)
 m = A.info()["m"]
 b = comm.empty(m); rhs_hash(comm, 0, b); x = comm.zeros(m)
-variants = [(0, 8192), (1, 8192), (1, 2048), (2, 8192), (3, 8192)]
+variants = [(int(a), int(b)) for a, b in (v.split(":") for v in (sys.argv[3] if len(sys.argv) > 3 else "0:8192,1:8192,2:8192,3:8192").split(","))]
 res = {v: [] for v in variants}
 spmv = {v: [] for v in variants}
 for rnd in range(3):

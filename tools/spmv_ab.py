@@ -34,11 +34,9 @@ def main():
     rhs_hash(comm, 0, x)
     ref = comm.empty(m)
     A0.mult(x, ref)
-    variants = {
-        "sell_nt_g4096": (A0, 1, 4096), "sell_nt_g8192": (A0, 1, 8192),
-        "dia_nt_g2048": (A1, 1, 2048), "dia_nt_g4096": (A1, 1, 4096), "dia_g4096": (A1, 0, 4096),
-        "dia_nt_g8192": (A1, 1, 8192), "dia_nt_g16384": (A1, 1, 16384),
-    }
+    variants = {"sell_nt_g8192": (A0, 1, 8192)}
+    for g in (1024, 1536, 1792, 2048, 2560, 3584, 4096, 8192):
+        variants[f"dia_nt_g{g}"] = (A1, 1, g)
     res = {k: [] for k in variants}
     y = comm.empty(m)
     a = torch.empty(1 << 27, dtype=torch.float64, device="cuda")
@@ -60,7 +58,7 @@ def main():
             res[k].append(ms)
             if r == 0:
                 assert torch.equal(y, ref), k
-    L.mx_debug_set(1, 1); L.mx_debug_set(3, 4096)
+    L.mx_debug_set(1, 1); L.mx_debug_set(3, 8192)
     print(json.dumps({"kind": kind, "n": n, "rows": m, "nnz": nnz, "alg_bytes": alg,
                       "dia_slices": info["dia_slices"], "slices": (m + 63) // 64,
                       "torch_copy_GBps": round(copy_gbs, 1)}))
