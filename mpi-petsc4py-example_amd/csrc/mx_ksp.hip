@@ -664,9 +664,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // 1: direction update + x step inside the MatMult (SPMV_CG)
   // 2: x step deferred into the next direction update (cg_px_kernel)
   // 3 (auto): 1 while r and p of the rank fit the 256 MB MALL (measured:
-  // -14% per iteration at 128^3, -8% at 64^3), else 2 (-4% at 256^3, where
-  // the two-vector gathers of mode 1 overflow the per-XCD L2)
-  const int fmode = g_knobs.cg_fuse == 3 ? (n <= (int64_t(8) << 20) ? 1 : 2) : g_knobs.cg_fuse;
+  // -14% per iteration at 128^3, -8% at 64^3), else 0 (at 256^3 the
+  // two-vector gathers of mode 1 overflow the per-XCD L2, +10%, and mode 2's
+  // saved pass is repaid by a slower MatMult behind its two-vector writes)
+  const int fmode = g_knobs.cg_fuse == 3 ? (n <= (int64_t(8) << 20) ? 1 : 0) : g_knobs.cg_fuse;
   const bool fuse_cg = fmode == 1;
   const bool defer_x = fmode != 0;
   // p_{-1} = -0.0: iteration 0's z + (+0)(-0) is exactly z (VecCopy)

@@ -14,10 +14,12 @@ kind = sys.argv[2] if len(sys.argv) > 2 else "poisson3d"
 A = DMat.stencil(comm, kind, n)
 m = A.info()["m"]
 b = comm.empty(m); rhs_hash(comm, 0, b); x = comm.zeros(m)
-variants = [(int(a), int(b)) for a, b in (v.split(":") for v in (sys.argv[3] if len(sys.argv) > 3 else "0:8192,1:8192,2:8192,3:8192").split(","))]
+# variant = fusion(knob 9):grid(knob 3)
+variants = [tuple(int(t) for t in v.split(":")[:2])
+            for v in (sys.argv[3] if len(sys.argv) > 3 else "0:8192,1:8192,2:8192,3:8192").split(",")]
 res = {v: [] for v in variants}
 spmv = {v: [] for v in variants}
-for rnd in range(3):
+for rnd in range(4):
     for v in variants:
         L.mx_debug_set(9, v[0]); L.mx_debug_set(3, v[1])
         A.solve(b, x, ksp="cg", rtol=0.0, max_it=32)

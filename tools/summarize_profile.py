@@ -39,6 +39,12 @@ def main():
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    # per-launch durations from the trace: the median is the working launch
+    # (launches after a solve has stopped are ~5 us no-ops and skew the mean)
+    durs = {}
+    for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
+        durs.setdefault(short(r["Kernel_Name"]), []).append(
+            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     fetch = pmc(os.path.join(src, "fetch", "run_counter_collection.csv"))
     write = pmc(os.path.join(src, "write", "run_counter_collection.csv"))
     calib = pmc(os.path.join(src, "calib", "run_counter_collection.csv"))
@@ -55,13 +61,14 @@ def main():
     alg = spmv_alg + 32 * m          # SPMV_CG: + r read, x read/write, p_i write
     out = {}
     lines = [f"# {tag}: rocprofv3 summary (3D 7-pt Poisson {grid}^3, N={ngpu}, bench.py --steps 50)", "",
-             "| kernel | calls | avg us | % time | FETCH_SIZE KB (raw, median) | WRITE_SIZE KB (median) |",
-             "|---|---|---|---|---|---|"]
+             "| kernel | calls | avg us | median us (trace) | % time | FETCH_SIZE KB (raw, median) | WRITE_SIZE KB (median) |",
+             "|---|---|---|---|---|---|---|"]
     for r in stats[:14]:
         k = short(r["Name"])
         fk = statistics.median(fetch[k]) if k in fetch else None
         wk = statistics.median(write[k]) if k in write else None
-        lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.1f} | "
+        med = statistics.median(durs[k]) if k in durs else float("nan")
+        lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {med:.1f} | {float(r['Percentage']):.1f} | "
                      f"{'' if fk is None else f'{fk:.0f}'} | {'' if wk is None else f'{wk:.0f}'} |")
     # the CG-fused MatMult (mode 3) of the solve; mode 2 when fusion is off
     sp = next((k for k in fetch if k.startswith("spmv_sell_kernel<3,")), None) or \
@@ -78,6 +85,7 @@ def main():
             "fetch_correction": round(corr, 4), "calib_8B_per_lane": f8 and round(f8, 4),
             "calib_16B_per_lane": f16 and round(f16, 4), "algorithmic_bytes": alg,
             "traffic_over_algorithmic": round(traffic / alg, 4), "kernel": sp,
+            "median_launch_us": round(statistics.median(durs[sp]), 1) if sp in durs else None,
             "source": f"profiles/{tag}_summary.md"}
         lines += ["", f"{sp} per launch: FETCH_SIZE {fr/1e6:.1f} MB raw x {corr:.3f} (calibrated, 16 B/lane NT stream; "
                   f"8 B/lane factor {f8 and round(f8, 3)}) + WRITE_SIZE {wr/1e6:.1f} MB = {traffic/1e6:.1f} MB "
