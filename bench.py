@@ -57,7 +57,7 @@ def cg_iter_bytes_design(m: int, nnz: int, nghost: int, mode: int) -> int:
 
 def fusion_mode(knob: int, m: int) -> int:
     """The mode cg_solve runs for knob 9 (3 = auto, mx_ksp.hip)."""
-    return (1 if m <= (8 << 20) else 0) if knob == 3 else knob
+    return (1 if m <= (6 << 20) else 0) if knob == 3 else knob
 
 
 def cpu_baseline(grid: int, budget_s: float, threads: int) -> dict:
@@ -108,8 +108,8 @@ def load_traffic(grid: int, n_gpus: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--grid", type=int, default=256)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=25.0)

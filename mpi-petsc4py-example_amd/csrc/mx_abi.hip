@@ -394,6 +394,8 @@ int mx_debug_set(int key, int value) {
     case 7: old = g_knobs.graph; g_knobs.graph = value; break;
     case 8: old = g_knobs.force_coll; g_knobs.force_coll = value; break;
     case 9: old = g_knobs.cg_fuse; g_knobs.cg_fuse = value; break;
+    case 10: old = g_knobs.cg_fold; g_knobs.cg_fold = value; break;
+    case 11: old = g_knobs.ws_skew; g_knobs.ws_skew = value; break;
     default: break;
   }
   return old;

@@ -108,7 +108,7 @@ struct Sell {
 };
 
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
-struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; };
+struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -200,23 +200,28 @@ enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2, SPMV_CG = 3 };
 // the MatMult.  The operand is p_i = z + b p_{i-1} (z = jac(r), i == 0: p = z),
 // formed on the fly wherever the product reads it and stored once for the
 // owned rows; x += xa p_{i-1} is applied to the owned rows when xpend != 0.
-// coef -> device doubles {b, xa, xpend} written by the scalar kernels.
+// The kernel evaluates the iteration's scalar top (cg_top, mx_cg.hpp) from
+// the solver state `st` itself; the main MatMult launch commits it.
+struct KspState;
+struct Fold;
 struct CgFuse {
   const double *r = nullptr;
   const double *pold = nullptr;
   double *pnew = nullptr;
   double *x = nullptr;
-  const double *coef = nullptr;
+  KspState *st = nullptr;
+  double *hist = nullptr;   // residual history (device) or null
   Jac jac;
 };
 void halo_begin(Mat *A, const double *x);  // pack + exchange into A->halo.lvec (compute stream)
 void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                  int *done_flag);
 // MatMult with the halo on the comm stream overlapping the interior slices;
-// returns the number of partials written (DOT / CG mode) for the fold.
+// returns the number of partials written (DOT / CG mode).  fold != null: the
+// p.w partials are folded into fold->out inside the launch(es).
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                    int *done_flag, const CgFuse *cg = nullptr);
-int spmv_blocks(const Mat *A);
+                    int *done_flag, const CgFuse *cg = nullptr, const Fold *fold = nullptr);
+int spmv_blocks(const Mat *A, int mode = SPMV_PLAIN);
 void mat_mult(Mat *A, const double *x, double *y);
 
 // vector kernels (mx_vec.hip)

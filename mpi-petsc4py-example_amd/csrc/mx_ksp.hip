@@ -30,57 +30,37 @@
 #include <cstring>
 #include <initializer_list>
 
+#include "mx_cg.hpp"
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 
 namespace mx {
 
-enum {
-  R_ITERATING = 0, R_CONVERGED_RTOL = 2, R_CONVERGED_ATOL = 3, R_CONVERGED_ITS = 4,
-  R_DIVERGED_NULL = -2, R_DIVERGED_ITS = -3, R_DIVERGED_DTOL = -4, R_DIVERGED_BREAKDOWN = -5,
-  R_DIVERGED_INDEFINITE_PC = -8, R_DIVERGED_NANORINF = -9, R_DIVERGED_INDEFINITE_MAT = -10
-};
-
 constexpr int MAX_RESTART = 1000;
-
-// Device-resident solver state (one allocation, zeroed then parameterised).
-struct KspState {
-  double red[8];
-  double beta, betaold, dpi, dpiold, alpha, dp, rnorm0, ttol;
-  double rtol, atol, dtol, haptol, breakdowntol;
-  double res, ksp_rnorm, gm_rnorm0, scale;
-  int its, reason, done, max_it;
-  int normtype, guess_zero, inner_stop, it;
-  int itcount, max_k, nv, xi;
-  // fused CG (SPMV_CG): {b, xa, xpend} read by the MatMult -- p_i = z + b p_{i-1},
-  // x += xa p_{xi} pending while xpend != 0 (CgFuse::coef points at pb)
-  double pb, xa, xpend;
-};
+constexpr int64_t CG_FUSE_MAX_ROWS = int64_t(6) << 20;   // auto CG fusion: mode 1 up to here
 
 // ------------------------------------------------------------------ shared scalar logic
-__device__ __forceinline__ bool not_finite(double v) { return isnan(v) || isinf(v); }
-
 // KSPConvergedDefault (KSPConvergedSkip when the norm type is NONE).
 __device__ int dev_converged(KspState *s, int n, double rnorm, bool guess_zero, double snorm) {
-  if (s->normtype == MX_NORM_NONE) return n >= s->max_it ? R_CONVERGED_ITS : R_ITERATING;
+  if (s->top.normtype == MX_NORM_NONE) return n >= s->top.max_it ? R_CONVERGED_ITS : R_ITERATING;
   if (n == 0) {
     if (!guess_zero) {
       if (snorm == 0.0) snorm = rnorm;
-      s->rnorm0 = snorm;
+      s->top.rnorm0 = snorm;
     } else {
-      s->rnorm0 = rnorm;
+      s->top.rnorm0 = rnorm;
     }
-    s->ttol = fmax(s->rtol * s->rnorm0, s->atol);
+    s->top.ttol = fmax(s->rtol * s->top.rnorm0, s->top.atol);
   }
   if (not_finite(rnorm)) return R_DIVERGED_NANORINF;
-  if (rnorm <= s->ttol) return rnorm < s->atol ? R_CONVERGED_ATOL : R_CONVERGED_RTOL;
-  if (rnorm >= s->dtol * s->rnorm0) return R_DIVERGED_DTOL;
+  if (rnorm <= s->top.ttol) return rnorm < s->top.atol ? R_CONVERGED_ATOL : R_CONVERGED_RTOL;
+  if (rnorm >= s->top.dtol * s->top.rnorm0) return R_DIVERGED_DTOL;
   return R_ITERATING;
 }
 
 __device__ __forceinline__ void stop(KspState *s, int reason) {
   s->reason = reason;
-  s->done = 1;
+  s->top.done = 1;
   s->inner_stop = 1;
 }
 
@@ -168,7 +148,7 @@ __global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double 
   if (!gather_red<NV>(s, partials, nblocks, fused)) return;
   const double zz = s->red[0], zr = s->red[1], rr = s->red[2];
   double dp;
-  switch (s->normtype) {
+  switch (s->top.normtype) {
     case MX_NORM_PRECONDITIONED: dp = sqrt(zz); break;
     case MX_NORM_UNPRECONDITIONED: dp = sqrt(rr); break;
     case MX_NORM_NATURAL: dp = sqrt(fabs(zr)); break;
@@ -182,8 +162,8 @@ __global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double 
   double snorm = 0.0;
   if (!s->guess_zero && NV == 6) {
     const double bz = s->red[3 % NV], bzr = s->red[4 % NV], bb = s->red[5 % NV];
-    snorm = s->normtype == MX_NORM_UNPRECONDITIONED ? sqrt(bb)
-            : s->normtype == MX_NORM_NATURAL        ? sqrt(fabs(bzr))
+    snorm = s->top.normtype == MX_NORM_UNPRECONDITIONED ? sqrt(bb)
+            : s->top.normtype == MX_NORM_NATURAL        ? sqrt(fabs(bzr))
                                                     : sqrt(bz);
   }
   const int reason = dev_converged(s, 0, dp, s->guess_zero, snorm);
@@ -191,116 +171,134 @@ __global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double 
   if (not_finite(s->beta)) { stop(s, R_DIVERGED_NANORINF); return; }
   s->its = 1;                                   // top of iteration 0
   s->pb = 0.0;                                  // i == 0: p = z
+  s->top.betas[0] = s->beta;
+  s->top.it_u = 0;
   if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
 }
 
-// p = z + (beta/betaold) p  (i == 0: p = z), z = d.*r recomputed.  The
-// iteration index comes from the device state (its = i + 1 at the top of
-// iteration i), so every iteration is the same launch sequence (graph replay).
-__global__ void cg_p_kernel(int64_t n, const KspState *__restrict__ s, const double *__restrict__ r,
-                            const Jac jac, double *__restrict__ p) {
-  if (s->done) return;
-  const int i = s->its - 1;
-  const double b = i == 0 ? 0.0 : s->beta / s->betaold;
+// p = z + b p  (i == 0: p = z), z = d.*r recomputed, b = beta_i / beta_{i-1}
+// from the iteration's scalar top (cg_top), which this launch commits.  Every
+// iteration is the same launch sequence (graph replay): the index comes from
+// the device state.
+__global__ void cg_p_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
+                            const Jac jac, double *__restrict__ p, double *__restrict__ hist) {
+  const CgTopIn top = s->top;
+  if (top.done) return;
+  const CgTop t = cg_top(top);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(s, t, hist);
+  if (t.reason) return;
+  const double b = t.b;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
     const double z = papply(jac, r[k], k);
-    p[k] = (b == 0.0) ? z : z + b * p[k];       // VecAYPX_Seq (b == 0 copies)
+    p[k] = (b == 0.0) ? z : z + b * p[k];       // VecAYPX_Seq (b == 0 copies; i == 0: b = 0)
   }
 }
 
 // cg_p_kernel plus the previous iteration's deferred x step, read from the
 // same p_{i-1} before it is overwritten: x += xa p_{i-1}; p = z + b p_{i-1}
-__global__ void cg_px_kernel(int64_t n, const KspState *__restrict__ s, const double *__restrict__ r,
-                             const Jac jac, double *__restrict__ p, double *__restrict__ x) {
-  if (s->done) return;
-  const int i = s->its - 1;
-  const double b = i == 0 ? 0.0 : s->beta / s->betaold;
-  const bool xp = s->xpend != 0.0;
-  const double a = s->xa;
+__global__ void cg_px_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
+                             const Jac jac, double *__restrict__ p, double *__restrict__ x,
+                             double *__restrict__ hist) {
+  const CgTopIn top = s->top;
+  if (top.done) return;
+  const CgTop t = cg_top(top);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(s, t, hist);
+  if (t.reason) return;
+  const double b = t.b;
+  const bool xp = top.xpend != 0.0;
+  const double a = top.xa;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
     const double po = p[k];
     const double z = papply(jac, r[k], k);
     if (xp) x[k] = fma(a, po, x[k]);            // VecAXPY(X, a, P) of iteration i-1
-    p[k] = (b == 0.0) ? z : z + b * po;         // VecAYPX_Seq (b == 0 copies)
+    p[k] = (b == 0.0) ? z : z + b * po;         // VecAYPX_Seq (b == 0 copies; i == 0: b = 0)
   }
 }
 
-// dpi = p.w, indefiniteness checks, alpha = beta/dpi
-// fused_cg: this iteration's MatMult has applied the pending x step; the
-// step of this iteration becomes pending (applied by the next MatMult or by
-// cg_finish_x_kernel) -- the same x += a p, one iteration later.
-__global__ void __launch_bounds__(256) cg_alpha_kernel(KspState *s, const double *partials,
-                                                       int nblocks, int fused, int fused_cg) {
-  if (s->done) return;
-  const int i = s->its - 1;
-  if (!gather_red<1>(s, partials, nblocks, fused)) return;
-  if (fused_cg) s->xpend = 0.0;
-  s->dpiold = s->dpi;
-  s->dpi = s->red[0];
-  if (not_finite(s->dpi)) { stop(s, R_DIVERGED_NANORINF); return; }
-  s->betaold = s->beta;
-  const double dpi = s->dpi, dpo = s->dpiold;
+// dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
+// Read-only; cg_update_kernel's workgroup 0 commits it.
+struct CgAlpha { int i, reason; double dpi, alpha; };
+__device__ __forceinline__ CgAlpha cg_alpha(const KspState *s) {
+  // every input loaded before the first branch
+  const int i = s->it_k;
+  const double dpi = s->red1, d0 = s->dpis[0], d1 = s->dpis[1];
+  const double b0 = s->top.betas[0], b1 = s->top.betas[1];
+  CgAlpha a;
+  a.i = i;
+  a.reason = R_ITERATING;
+  a.dpi = dpi;
+  a.alpha = 0.0;
+  if (not_finite(dpi)) { a.reason = R_DIVERGED_NANORINF; return a; }
+  const double dpo = i > 0 ? ((i & 1) ? d0 : d1) : 0.0;     // dpi_{i-1}
   const int sg = (dpi > 0) - (dpi < 0), sgo = (dpo > 0) - (dpo < 0);
-  if (dpi == 0.0 || (i > 0 && sg * sgo < 0)) { stop(s, R_DIVERGED_INDEFINITE_MAT); return; }
-  s->alpha = s->beta / s->dpi;
-  if (fused_cg) { s->xa = s->alpha; s->xpend = 1.0; s->xi = i; }
+  if (dpi == 0.0 || (i > 0 && sg * sgo < 0)) { a.reason = R_DIVERGED_INDEFINITE_MAT; return a; }
+  a.alpha = ((i & 1) ? b1 : b0) / dpi;                        // beta_i / dpi
+  return a;
 }
 
-// x += a p, r -= a w (BLAS daxpy = fma), z = d.*r, partials [z.z, z.r, r.r]
-__global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, const KspState *__restrict__ s,
+// x += a p, r -= a w (BLAS daxpy = fma), z = d.*r, [z.z, z.r, r.r] folded
+// into red3 inside the launch.  x == null: the x step is deferred (modes 1/2:
+// applied by the next iteration's first kernel, or by cg_finish_x_kernel).
+__global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__restrict__ s,
                                                         const double *__restrict__ p,
                                                         const double *__restrict__ w,
                                                         double *__restrict__ x, double *__restrict__ r,
-                                                        const Jac jac, double *__restrict__ partials) {
-  if (s->done) return;
-  const double a = s->alpha;
+                                                        const Jac jac, double *__restrict__ partials,
+                                                        const Fold fold) {
+  if (s->top.done) return;
+  const CgAlpha al = cg_alpha(s);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    s->dpi = al.dpi;
+    s->top.xpend = 0.0;            // a deferred step of i-1 was applied by this iteration's first kernel
+    if (al.reason) {
+      stop(s, al.reason);
+    } else {
+      s->dpis[al.i & 1] = al.dpi;
+      s->alpha = al.alpha;
+      if (!x) { s->top.xa = al.alpha; s->top.xpend = 1.0; s->xi = al.i; }
+      s->top.it_u = al.i + 1;
+    }
+  }
+  if (al.reason) return;
+  const double a = al.alpha;
   double v[3] = {0.0, 0.0, 0.0};
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    if (x) x[i] = fma(a, p[i], x[i]);            // x == null: deferred into the next MatMult
+    if (x) x[i] = fma(a, p[i], x[i]);
     const double ri = fma(-a, w[i], r[i]);
     r[i] = ri;
     const double zi = papply(jac, ri, i);
     v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
   }
-  block_sum_to_partials<3>(v, partials, gridDim.x);
+  block_partials<3>(v, partials, gridDim.x, fold);
 }
 
-// dp, history, convergence at its = i+1, beta for the next iteration
-__global__ void __launch_bounds__(256) cg_conv_kernel(KspState *s, const double *partials,
-                                                      int nblocks, int fused, double *hist) {
-  if (s->done) return;
-  const int i = s->its - 1;
-  if (!gather_red<3>(s, partials, nblocks, fused)) return;
-  const double zz = s->red[0], zr = s->red[1], rr = s->red[2];
-  double dp;
-  switch (s->normtype) {
-    case MX_NORM_PRECONDITIONED: dp = sqrt(zz); break;
-    case MX_NORM_UNPRECONDITIONED: dp = sqrt(rr); break;
-    case MX_NORM_NATURAL: dp = sqrt(fabs(zr)); break;
-    default: dp = 0.0;
+// one-block fold of per-workgroup partials (block_sum_array's order, the same
+// bits as an in-launch fold)
+template <int NV>
+__global__ void __launch_bounds__(256) fold_kernel(const double *__restrict__ partials, int nblocks,
+                                                   double *__restrict__ out, const int *__restrict__ done) {
+  if (*done) return;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double t = block_sum_array<16>(partials + (size_t)k * nblocks, nblocks);
+    if (threadIdx.x == 0) out[k] = t;
   }
-  s->dp = dp;
-  if (not_finite(dp)) { stop(s, R_DIVERGED_NANORINF); return; }
-  if (hist) hist[i + 1] = dp;
-  const int reason = dev_converged(s, i + 1, dp, true, 0.0);
-  if (reason) { stop(s, reason); return; }
-  s->beta = zr;
-  if (not_finite(zr)) { stop(s, R_DIVERGED_NANORINF); return; }
-  if (i + 1 >= s->max_it) { stop(s, R_DIVERGED_ITS); return; }
-  s->its = i + 2;                               // top of iteration i+1
-  s->pb = s->beta / s->betaold;                 // VecAYPX coefficient of iteration i+1
-  if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
-  if (s->beta * s->betaold < 0.0) { stop(s, R_DIVERGED_INDEFINITE_PC); return; }
+}
+
+// the scalar top after the last launched iteration (max_it reached without a stop)
+__global__ void cg_tail_kernel(KspState *s, double *hist) {
+  if (threadIdx.x != 0 || s->top.done) return;
+  cg_commit_top(s, cg_top(s->top), hist);
 }
 
 // the x step still pending when the solve stopped (fused CG)
 __global__ void cg_finish_x_kernel(int64_t n, const KspState *__restrict__ s, const double *__restrict__ p0,
                                    const double *__restrict__ p1, double *__restrict__ x) {
-  if (s->xpend == 0.0) return;
-  const double a = s->xa;
+  if (s->top.xpend == 0.0) return;
+  const double a = s->top.xa;
   const double *__restrict__ p = (s->xi & 1) ? p1 : p0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = fma(a, p[i], x[i]);
@@ -344,12 +342,12 @@ __global__ void __launch_bounds__(256) gm_start_kernel(KspState *s, const double
   if (res == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
   const int reason = dev_converged(s, s->its, res, s->its == 0 ? s->guess_zero : true, snorm);
   if (reason) { stop(s, reason); return; }
-  s->inner_stop = (s->its >= s->max_it) ? 1 : 0;
+  s->inner_stop = (s->its >= s->top.max_it) ? 1 : 0;
 }
 
 __global__ void scale_by_state_kernel(int64_t n, const KspState *__restrict__ s, double *__restrict__ x,
                                       int expect_it) {
-  if (s->done && expect_it < 0) return;
+  if (s->top.done && expect_it < 0) return;
   if (expect_it >= 0 && s->it != expect_it) return;
   if (s->res == 0.0 && expect_it < 0) return;
   const double a = s->scale;
@@ -455,7 +453,7 @@ __global__ void __launch_bounds__(256) gm_step_kernel(KspState *s, int k, const 
   int reason = dev_converged(s, s->its, res, true, 0.0);
   if (hapend && !reason) reason = R_DIVERGED_BREAKDOWN;
   if (reason) { stop(s, reason); return; }
-  if (s->it >= s->max_k || s->its >= s->max_it) s->inner_stop = 1;
+  if (s->it >= s->max_k || s->its >= s->top.max_it) s->inner_stop = 1;
 }
 
 // KSPGMRESBuildSoln: back substitution into grs (in place)
@@ -466,13 +464,13 @@ __global__ void gm_buildsoln_kernel(KspState *s, const double *hh, int ld, doubl
   if (it < 0 || s->reason == R_DIVERGED_NULL || s->reason == R_DIVERGED_NANORINF) return;
   if (s->reason == R_DIVERGED_BREAKDOWN && s->ksp_rnorm > 0.0 && s->it == 0) return;
 #define HHd(a, b) hh[(size_t)(b) * ld + (a)]
-  if (HHd(it, it) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->done = 1; return; }
+  if (HHd(it, it) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->top.done = 1; return; }
   grs[it] = grs[it] / HHd(it, it);
   for (int ii = 1; ii <= it; ++ii) {
     const int k = it - ii;
     double t = grs[k];
     for (int j = k + 1; j <= it; ++j) t = t - HHd(k, j) * grs[j];
-    if (HHd(k, k) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->done = 1; return; }
+    if (HHd(k, k) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->top.done = 1; return; }
     grs[k] = t / HHd(k, k);
   }
 #undef HHd
@@ -506,8 +504,8 @@ __global__ void __launch_bounds__(256) gm_update_x_kernel(int64_t n, const KspSt
 __global__ void gm_cycle_end_kernel(KspState *s) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   s->itcount += s->it;
-  if (s->itcount >= s->max_it && !s->reason) s->reason = R_DIVERGED_ITS;
-  if (s->reason) s->done = 1;
+  if (s->itcount >= s->top.max_it && !s->reason) s->reason = R_DIVERGED_ITS;
+  if (s->reason) s->top.done = 1;
   s->guess_zero = 0;
 }
 
@@ -579,8 +577,8 @@ struct Events {
 
 void init_state(KspState &h, const mx_ksp_params &p, int normtype) {
   std::memset(&h, 0, sizeof(h));
-  h.rtol = p.rtol; h.atol = p.atol; h.dtol = p.dtol; h.haptol = p.haptol;
-  h.breakdowntol = p.breakdowntol; h.max_it = p.max_it; h.normtype = normtype;
+  h.rtol = p.rtol; h.top.atol = p.atol; h.top.dtol = p.dtol; h.haptol = p.haptol;
+  h.breakdowntol = p.breakdowntol; h.top.max_it = p.max_it; h.top.normtype = normtype;
   h.guess_zero = !p.guess_nonzero; h.max_k = p.restart; h.ksp_rnorm = -1.0;
 }
 
@@ -593,15 +591,19 @@ void read_state(hipStream_t st, const KspState *d, KspState &h) {
 
 // KSPSetUp work space: one device allocation per operator, grown on demand
 // and reused by later solves (no hipMalloc/hipFree inside a solve).
+// Consecutive vectors are skewed by g_knobs.ws_skew doubles so that equal
+// indices of different vectors do not sit at the same offset modulo the
+// large powers of two the HBM channel interleave repeats on.
+static size_t carve_step(size_t n) { return (n + 31) / 32 * 32 + (size_t)std::max(g_knobs.ws_skew, 0); }
 struct Carve {
   double *base;
   size_t off = 0;
   explicit Carve(double *b) : base(b) {}
-  double *take(size_t n) { double *p = base + off; off += (n + 31) / 32 * 32; return p; }
+  double *take(size_t n) { double *p = base + off; off += carve_step(n); return p; }
 };
 static size_t carve_size(std::initializer_list<size_t> parts) {
   size_t t = 0;
-  for (size_t n : parts) t += (n + 31) / 32 * 32;
+  for (size_t n : parts) t += carve_step(n);
   return t;
 }
 static double *workspace(Mat *A, size_t nd) {
@@ -643,7 +645,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     HIPCHECK(hipMemcpyAsync(r.p, b, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
   }
   KspState *s = sd.p;
-  double *red = reinterpret_cast<double *>(s);   // red[] is the first member
+  double *red = s->red;
   const int nv0 = p.guess_nonzero ? 6 : 3;
   if (nv0 == 6) cg_norms_kernel<6><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
   else cg_norms_kernel<3><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
@@ -657,43 +659,55 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   Poller poller(st);
   int i = 0;
   const unsigned egrid = grid_for(n, 256, 8192);
-  int *done = &s->done;
+  int *done = &s->top.done;
   double *hist_d = hist_host ? hist.p : nullptr;
   // fused: the direction update and the previous x step ride in the MatMult
   // (SPMV_CG); p ping-pongs between two buffers since neighbours read p_{i-1}
   // 1: direction update + x step inside the MatMult (SPMV_CG)
   // 2: x step deferred into the next direction update (cg_px_kernel)
-  // 3 (auto): 1 while r and p of the rank fit the 256 MB MALL (measured:
-  // -14% per iteration at 128^3, -8% at 64^3), else 0 (at 256^3 the
-  // two-vector gathers of mode 1 overflow the per-XCD L2, +10%, and mode 2's
-  // saved pass is repaid by a slower MatMult behind its two-vector writes)
-  const int fmode = g_knobs.cg_fuse == 3 ? (n <= (int64_t(8) << 20) ? 1 : 0) : g_knobs.cg_fuse;
+  // 3 (auto): 1 up to CG_FUSE_MAX_ROWS local rows, else 0.  Measured per
+  // iteration on 256 x 256 x nz ranks (tools/coll_ab.py): mode 1 -7% at nz 32,
+  // -4% at nz 64, but +5% at nz 128 and +10% at 256^3, where the two-vector
+  // gathers of mode 1 overflow the per-XCD L2; mode 2's saved pass is repaid
+  // by a slower MatMult behind its two-vector writes
+  const int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 0) : g_knobs.cg_fuse;
   const bool fuse_cg = fmode == 1;
   const bool defer_x = fmode != 0;
   // p_{-1} = -0.0: iteration 0's z + (+0)(-0) is exactly z (VecCopy)
   if (fuse_cg) vec_set(st, n, -0.0, pv2);
+  // in-launch folds: p.w into red1 (MatMult), [z.z, z.r, r.r] into red3 (update)
+  Fold fdot, fupd;
+  fdot.cnt = s->fold_dot; fdot.out = &s->red1;
+  fupd.cnt = s->fold_upd; fupd.out = s->top.red3;
+  fupd.ntotal = fupd.ncount = RED_BLOCKS;
+  const int fold_at = g_knobs.cg_fold;       // 0: fold kernels, 1: update in-launch, 2: both
+  const Fold *fdot_p = fold_at >= 2 ? &fdot : nullptr;
+  if (fold_at < 1) fupd.cnt = nullptr;
+  // per iteration: [first kernel: scalar top + p] -> MatMult (+ p.w) -> all-reduce
+  // -> update (alpha + x, r, z norms) -> all-reduce; the scalars are
+  // evaluated inside the vector kernels (mx_cg.hpp), no one-block kernels
   auto iteration = [&](int it) {
     int nb_spmv;
     if (fuse_cg) {
       CgFuse cg;
       cg.r = r.p; cg.pold = (it & 1) ? pv.p : pv2; cg.pnew = (it & 1) ? pv2 : pv.p;
-      cg.x = x; cg.coef = &s->pb; cg.jac = dinv;
+      cg.x = x; cg.st = s; cg.hist = hist_d; cg.jac = dinv;
       timer.begin();
-      nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg);
+      nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg, fdot_p);
       timer.end();
     } else {
-      if (defer_x) cg_px_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p, x);
-      else cg_p_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p);
+      if (defer_x) cg_px_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p, x, hist_d);
+      else cg_p_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p, hist_d);
       timer.begin();
-      nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done);
+      nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
     }
-    if (!fused) { finish_reduce(part.p, nb_spmv, 1, red, st, done); c->allreduce_sum(red, 1); }
-    cg_alpha_kernel<<<1, 256, 0, st>>>(s, part.p, nb_spmv, fused, defer_x);
+    if (!fdot_p) fold_kernel<1><<<1, 256, 0, st>>>(part.p, nb_spmv, &s->red1, done);
+    if (!fused) c->allreduce_sum(&s->red1, 1);
     const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : pv.p;
-    cg_update_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, part.p);
-    if (!fused) { finish_reduce(part.p, RED_BLOCKS, 3, red, st, done); c->allreduce_sum(red, 3); }
-    cg_conv_kernel<<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_d);
+    cg_update_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, part.p, fupd);
+    if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(part.p, RED_BLOCKS, s->top.red3, done);
+    if (!fused) c->allreduce_sum(s->top.red3, 3);
     HIPCHECK(hipGetLastError());
   };
   // a captured batch must start on an even iteration when p ping-pongs
@@ -703,7 +717,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   if (graph) {
     key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
            (uintptr_t)poll, (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt, (uintptr_t)g_knobs.spmv_grid,
-           (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode};
+           (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p,
+           (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;
@@ -747,6 +762,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       }
     }
   }
+  cg_tail_kernel<<<1, 64, 0, st>>>(s, hist_d);   // max_it launched without a stop
+  HIPCHECK(hipGetLastError());
   if (defer_x) {   // p is in place for mode 2: both buffer slots are pv
     cg_finish_x_kernel<<<egrid, 256, 0, st>>>(n, s, pv.p, fuse_cg ? pv2 : pv.p, x);
     HIPCHECK(hipGetLastError());
@@ -879,7 +896,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
     gm_cycle_end_kernel<<<1, 64, 0, st>>>(s);
     HIPCHECK(hipGetLastError());
     read_state(st, s, hs);
-    if (hs.done) break;
+    if (hs.top.done) break;
   }
   HIPCHECK(hipEventRecord(ev.b, st));
   HIPCHECK(hipEventSynchronize(ev.b));

@@ -19,6 +19,7 @@
 // slices with no ghost entries have width 0 and cost one scalar load.
 #include <algorithm>
 
+#include "mx_cg.hpp"
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 
@@ -204,8 +205,10 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o,
     const double *__restrict__ val_o, const double *__restrict__ x,
     const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
-    double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg) {
-  if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
+    double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold) {
+  CgTopIn top;
+  if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
+  else if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int s0, sstep, send;
@@ -227,9 +230,14 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
   double xa = 0.0;
   bool xpend = false;
   if constexpr (MODE == SPMV_CG) {
-    X = XCg<JM>{cg.r, cg.pold, cg.jac.d, cg.jac.c, cg.coef[0]};
-    xa = cg.coef[1];
-    xpend = cg.coef[2] != 0.0;
+    // the iteration's scalar top (convergence of i-1, b), committed by block 0
+    if (top.done) return;
+    const CgTop t = cg_top(top);
+    if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(cg.st, t, cg.hist);
+    if (t.reason) return;
+    X = XCg<JM>{cg.r, cg.pold, cg.jac.d, cg.jac.c, t.b};
+    xa = top.xa;
+    xpend = top.xpend != 0.0;
   } else {
     X = XPlain{x};
   }
@@ -293,13 +301,18 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
   }
   if (MODE == SPMV_DOT || MODE == SPMV_CG) {
     double v[1] = {dot};
-    block_sum_to_partials<1>(v, partials, gridDim.x);
+    block_partials<1>(v, partials, gridDim.x, fold);
   }
 }
 
-int spmv_blocks(const Mat *A) {
+// Grid of the main SpMV launch (an upper bound for every mode).  SPMV_CG
+// evaluates the iteration's scalar top in every workgroup, a dependent chain
+// of scalar loads paid once per workgroup generation, so it keeps >= 4 slices
+// per wave (tools/coll_ab.py: -6% per CG iteration at 2M rows per rank).
+int spmv_blocks(const Mat *A, int mode) {
   const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
   int64_t g = std::min<int64_t>(need, g_knobs.spmv_grid);
+  if (mode == SPMV_CG) g = std::min<int64_t>(g, std::max<int64_t>(2048, need / 4));
   if (g >= 64) g &= ~int64_t(7);   // multiple of 8: XCD grouping
   return (int)std::max<int64_t>(1, g);
 }
@@ -312,7 +325,7 @@ __global__ void __launch_bounds__(256) spmv_boundary_kernel(
     int64_t m, const int32_t *__restrict__ list, int nlist, const int64_t *__restrict__ sptr_o,
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o, const double *__restrict__ val_o,
     const double *__restrict__ x, const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
-    double *__restrict__ partials, const int *__restrict__ done) {
+    double *__restrict__ partials, const int *__restrict__ done, const Fold fold) {
   if (done && *done) return;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -330,7 +343,7 @@ __global__ void __launch_bounds__(256) spmv_boundary_kernel(
   }
   if (MODE == SPMV_DOT) {
     double v[1] = {dot};
-    block_sum_to_partials<1>(v, partials, gridDim.x);
+    block_partials<1>(v, partials, gridDim.x, fold);
   }
 }
 
@@ -344,8 +357,11 @@ __global__ void pack_kernel(int64_t n, const int32_t *__restrict__ idx, const do
 template <int JM>
 __global__ void pack_cg_kernel(int64_t n, const int32_t *__restrict__ idx, const CgFuse cg,
                                const int *__restrict__ done, double *__restrict__ buf) {
-  if (done && *done) return;
-  const XCg<JM> X{cg.r, cg.pold, cg.jac.d, cg.jac.c, cg.coef[0]};
+  const CgTopIn top = cg.st->top;
+  if (top.done) return;
+  const CgTop t = cg_top(top);                  // read-only: the MatMult commits it
+  if (t.reason) return;
+  const XCg<JM> X{cg.r, cg.pold, cg.jac.d, cg.jac.c, t.b};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) buf[k] = X(idx[k]);
 }
@@ -381,15 +397,15 @@ void halo_begin(Mat *A, const double *x) {
 }
 
 static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp) {
-  const unsigned grid = (unsigned)spmv_blocks(A);
+                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold) {
+  const unsigned grid = (unsigned)spmv_blocks(A, mode);
   const double *lvec = (A->nghost && !split) ? A->halo.lvec.p : nullptr;
   const int kd = A->sd.dia_k;
   const CgFuse cg = cgp ? *cgp : CgFuse{};
 #define SPMV_ARGS                                                                           \
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
       A->sd.mask.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac,   \
-      partials, done_flag, cg
+      partials, done_flag, cg, fold
 #define SPMV_KD(MODE, NT, SP)                                                                    \
   do {                                                                                           \
     switch (kd) {                                                                                \
@@ -436,20 +452,23 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
 
 void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                  int *done_flag) {
-  launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream, nullptr);
+  launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream, nullptr, Fold{});
 }
 
 constexpr int BND_BLOCKS = 64;
 
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                    int *done_flag, const CgFuse *cg) {
+                    int *done_flag, const CgFuse *cg, const Fold *fold) {
   Comm *c = A->comm;
   Halo &H = A->halo;
   hipStream_t st = c->stream;
+  const int nmain = spmv_blocks(A, mode);
   if (c->size == 1 || H.nbnd == 0 || !g_knobs.overlap) {
     if (c->size > 1) halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, st);
-    launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg);
-    return spmv_blocks(A);
+    Fold f;
+    if (fold) { f = *fold; f.ntotal = nmain; f.base = 0; f.ncount = nmain; }
+    launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg, f);
+    return nmain;
   }
   hipStream_t cs = c->comm_stream;
   if (!H.ev_x) {
@@ -463,15 +482,18 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
   halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, cs);
   HIPCHECK(hipEventRecord(H.ev_done, cs));
   // interior slices meanwhile; boundary slices after the exchange
-  const int nmain = spmv_blocks(A);
-  launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg);
+  launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{});
   HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
   const int nb = std::min(BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
-  double *pb = partials ? partials + nmain : nullptr;
+  // the boundary launch folds the partials of both launches (fold) or
+  // appends its own after the main launch's
+  Fold f;
+  if (fold) { f = *fold; f.ntotal = nmain + nb; f.base = nmain; f.ncount = nb; }
+  double *pb = partials ? (fold ? partials : partials + nmain) : nullptr;
   // the boundary rows' operand values were stored by the main kernel (CG)
   const double *xb = mode == SPMV_CG ? cg->pnew : x;
 #define BND(MODE) spmv_boundary_kernel<MODE><<<nb, 256, 0, st>>>(A->m, H.bnd_slices.p, H.nbnd, A->so.sptr.p, \
-      A->so.width.p, A->so.col.p, A->so.val.p, xb, H.lvec.p, y, jac, pb, done_flag)
+      A->so.width.p, A->so.col.p, A->so.val.p, xb, H.lvec.p, y, jac, pb, done_flag, f)
   switch (mode) {
     case SPMV_PLAIN: BND(SPMV_PLAIN); break;
     case SPMV_JACOBI: BND(SPMV_JACOBI); break;

@@ -16,19 +16,14 @@
 
 namespace mx {
 
-// one block per value: out[v] = sum_b partials[v][b], fixed order.
+// one block per value: out[v] = sum_b partials[v][b], fixed order (16 loads
+// in flight per thread; the same sums as the plain strided loop)
 __global__ void __launch_bounds__(256) finish_kernel(const double *__restrict__ partials,
                                                      int nblocks, double *__restrict__ out,
                                                      const int *done) {
   if (done && *done) return;
-  const double *p = partials + (size_t)blockIdx.x * nblocks;
-  double s = 0.0;
-  for (int i = threadIdx.x; i < nblocks; i += 256) s += p[i];
-  __shared__ double sh[4];
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) out[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  const double t = block_sum_array<16>(partials + (size_t)blockIdx.x * nblocks, nblocks);
+  if (threadIdx.x == 0) out[blockIdx.x] = t;
 }
 
 void finish_reduce(const double *partials, int nblocks, int nvals, double *out, hipStream_t s,
