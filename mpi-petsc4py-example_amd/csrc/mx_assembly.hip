@@ -18,7 +18,8 @@
 //   canonicalise rows: W-lane segments (W = 8..64) bitonic-sort (col, pos)
 //     pairs in registers with xor shuffles, then a segmented last-wins /
 //     ordered-fold dedupe with ballot compaction; rows longer than 64 go to a
-//     block-per-row LDS bitonic sort (<= 2048 entries);
+//     block-per-row LDS bitonic sort (<= 2048 entries), longer ones to a
+//     global chunk-sort + merge-pass sort (canon_huge_rows);
 //   split + ghost bitmap (atomicOr) -> scans -> bitmap popcount-scan gives
 //     garray and the A_o renumbering without any sort;
 //   SELL-64 copies of A_d and A_o for the SpMV;
@@ -307,15 +308,16 @@ __global__ void __launch_bounds__(256) canon_rows_block_kernel(
     const int64_t *__restrict__ rows_list, const int64_t *__restrict__ rowptr,
     const int64_t *__restrict__ col, const double *__restrict__ val,
     const int64_t *__restrict__ pos, int64_t N, int add, int64_t *__restrict__ ccol,
-    double *__restrict__ cval, int64_t *__restrict__ cnt_out, int *__restrict__ err) {
+    double *__restrict__ cval, int64_t *__restrict__ cnt_out, int *__restrict__ err,
+    int64_t *__restrict__ huge_rows, unsigned long long *__restrict__ nhuge) {
   __shared__ int64_t kc[LONG_ROW_MAX];
   __shared__ int64_t kp[LONG_ROW_MAX];
   __shared__ double kv[LONG_ROW_MAX];
   const int64_t row = rows_list[blockIdx.x];
   const int64_t start = rowptr[row];
   const int64_t len = rowptr[row + 1] - start;
-  if (len > LONG_ROW_MAX) {
-    if (threadIdx.x == 0) atomicOr(err, 2);
+  if (len > LONG_ROW_MAX) {                 // canon_huge_row below
+    if (threadIdx.x == 0) huge_rows[atomicAdd(nhuge, 1ULL)] = row;
     return;
   }
   int npad = 1;
@@ -361,6 +363,119 @@ __global__ void __launch_bounds__(256) canon_rows_block_kernel(
       }
     }
     cnt_out[row] = k;
+  }
+}
+
+// Rows longer than LONG_ROW_MAX: sorted in global scratch by the whole GPU --
+// LDS bitonic sorts of 2048-entry chunks, then merge passes that double the
+// run length (each entry finds its output slot by a binary search in the
+// partner run; ties go to the left run, so the merge is stable), then the
+// same sequential ordered dedupe.  (col, pos) keys are unique apart from the
+// dropped entries, which all sort last.
+struct SortKey { int64_t c, p; double v; };
+__device__ __forceinline__ bool key_less(const SortKey &a, const SortKey &b) {
+  return a.c < b.c || (a.c == b.c && a.p < b.p);
+}
+
+__global__ void __launch_bounds__(256) huge_chunk_sort_kernel(
+    int64_t start, int64_t len, const int64_t *__restrict__ col, const double *__restrict__ val,
+    const int64_t *__restrict__ pos, int64_t N, SortKey *__restrict__ out, int *__restrict__ err) {
+  __shared__ int64_t kc[LONG_ROW_MAX];
+  __shared__ int64_t kp[LONG_ROW_MAX];
+  __shared__ double kv[LONG_ROW_MAX];
+  const int64_t c0 = (int64_t)blockIdx.x * LONG_ROW_MAX;
+  const int cl = (int)min((int64_t)LONG_ROW_MAX, len - c0);
+  int npad = 1;
+  while (npad < cl) npad <<= 1;
+  for (int i = threadIdx.x; i < npad; i += 256) {
+    int64_t c = KEY_DROP, p = KEY_DROP;
+    double v = 0.0;
+    if (i < cl) {
+      const int64_t cc = col[start + c0 + i];
+      if (cc >= 0) {
+        if (cc >= N) atomicOr(err, 1);
+        c = cc; p = pos ? pos[start + c0 + i] : c0 + i; v = val[start + c0 + i];
+      }
+    }
+    kc[i] = c; kp[i] = p; kv[i] = v;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npad; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < npad; i += 256) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const bool greater = (kc[i] > kc[ixj]) || (kc[i] == kc[ixj] && kp[i] > kp[ixj]);
+          if (greater == up) {
+            int64_t tc = kc[i]; kc[i] = kc[ixj]; kc[ixj] = tc;
+            int64_t tp = kp[i]; kp[i] = kp[ixj]; kp[ixj] = tp;
+            double tv = kv[i]; kv[i] = kv[ixj]; kv[ixj] = tv;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < cl; i += 256) out[c0 + i] = SortKey{kc[i], kp[i], kv[i]};
+}
+
+__global__ void huge_merge_kernel(int64_t len, int64_t run, const SortKey *__restrict__ in,
+                                  SortKey *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += stride) {
+    const int64_t r = i / run, lo = (r >> 1) * 2 * run;
+    const int64_t mid = min(lo + run, len), hi = min(lo + 2 * run, len);
+    const SortKey k = in[i];
+    int64_t a, b, rank = 0;
+    if ((r & 1) == 0) {           // left run: count partner entries < k
+      a = mid; b = hi;
+      while (a < b) { const int64_t h = (a + b) >> 1; if (key_less(in[h], k)) a = h + 1; else b = h; }
+      rank = a - mid;
+      out[lo + (i - lo) + rank] = k;
+    } else {                      // right run: count partner entries <= k
+      a = lo; b = mid;
+      while (a < b) { const int64_t h = (a + b) >> 1; if (!key_less(k, in[h])) a = h + 1; else b = h; }
+      rank = a - lo;
+      out[lo + (i - mid) + rank] = k;
+    }
+  }
+}
+
+__global__ void huge_dedupe_kernel(int64_t row, int64_t start, int64_t len, int add,
+                                   const SortKey *__restrict__ in, int64_t *__restrict__ ccol,
+                                   double *__restrict__ cval, int64_t *__restrict__ cnt_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t k = 0;
+  for (int64_t i = 0; i < len && in[i].c != KEY_DROP; ++i) {
+    if (k > 0 && ccol[start + k - 1] == in[i].c) {
+      if (add) cval[start + k - 1] = cval[start + k - 1] + in[i].v;
+      else cval[start + k - 1] = in[i].v;
+    } else {
+      ccol[start + k] = in[i].c; cval[start + k] = in[i].v; ++k;
+    }
+  }
+  cnt_out[row] = k;
+}
+
+static void canon_huge_rows(const std::vector<int64_t> &rows, const int64_t *rowptr, const int64_t *col,
+                            const double *val, const int64_t *pos, int64_t N, int add, int64_t *ccol,
+                            double *cval, int64_t *cnt_out, int *err, hipStream_t st) {
+  for (int64_t row : rows) {
+    int64_t se[2];
+    HIPCHECK(hipMemcpy(se, rowptr + row, sizeof(se), hipMemcpyDeviceToHost));
+    const int64_t start = se[0], len = se[1] - se[0];
+    DBuf<SortKey> a((size_t)len), b((size_t)len);
+    huge_chunk_sort_kernel<<<(unsigned)cdiv(len, LONG_ROW_MAX), 256, 0, st>>>(start, len, col, val, pos, N, a.p, err);
+    HIPCHECK(hipGetLastError());
+    for (int64_t run = LONG_ROW_MAX; run < len; run *= 2) {
+      huge_merge_kernel<<<grid_for(len, 256, 8192), 256, 0, st>>>(len, run, a.p, b.p);
+      HIPCHECK(hipGetLastError());
+      std::swap(a, b);
+    }
+    huge_dedupe_kernel<<<1, 64, 0, st>>>(row, start, len, add, a.p, ccol, cval, cnt_out);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(st));
   }
 }
 
@@ -707,8 +822,20 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
       HIPCHECK(hipMemcpyAsync(&nl, &lmax.p[1], sizeof(nl), hipMemcpyDeviceToHost, st));
       HIPCHECK(hipStreamSynchronize(st));
       if (nl) {
-        canon_rows_block_kernel<<<(unsigned)nl, 256, 0, st>>>(long_rows.p, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, err.p);
+        DBuf<int64_t> huge((size_t)nl);
+        HIPCHECK(hipMemsetAsync(&lmax.p[0], 0, sizeof(unsigned long long), st));   // reused: huge-row count
+        canon_rows_block_kernel<<<(unsigned)nl, 256, 0, st>>>(long_rows.p, rowptr, col, val, pos, N, add, ccol.p,
+                                                              cval.p, cnt_out.p, err.p, huge.p, &lmax.p[0]);
         HIPCHECK(hipGetLastError());
+        if (Lh > LONG_ROW_MAX) {
+          unsigned long long nh = 0;
+          HIPCHECK(hipMemcpyAsync(&nh, &lmax.p[0], sizeof(nh), hipMemcpyDeviceToHost, st));
+          HIPCHECK(hipStreamSynchronize(st));
+          std::vector<int64_t> hrows((size_t)nh);
+          if (nh) HIPCHECK(hipMemcpy(hrows.data(), huge.p, sizeof(int64_t) * nh, hipMemcpyDeviceToHost));
+          std::sort(hrows.begin(), hrows.end());
+          canon_huge_rows(hrows, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, err.p, st);
+        }
       }
     }
   }
@@ -717,7 +844,6 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   HIPCHECK(hipStreamSynchronize(st));
   if (herr & 4) fail(MX_ERR_ARG, "row pointer array is not nondecreasing");
   if (herr & 1) fail(MX_ERR_OUTOFRANGE, "Column too large: max " + std::to_string(N - 1));
-  if (herr & 2) fail(MX_ERR_UNSUPPORTED, "row with more than 2048 entries (long-row sort not implemented)");
 
   // ---- split into A_d / A_o with a ghost bitmap
   const bool multi = c->size > 1;

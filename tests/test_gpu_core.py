@@ -61,6 +61,27 @@ def test_assembly_unsorted_duplicates(selfcomm, oracle_mod, add, maxlen):
     assert_csr_equal(A.csr(), O.csr())
 
 
+@pytest.mark.parametrize("add", [False, True])
+def test_assembly_huge_rows(selfcomm, oracle_mod, add):
+    """Rows beyond the LDS sort (> 2048 entries): chunk sorts + merge passes,
+    with duplicates, negative ids, zeros and rows of exactly 2048 / 2049."""
+    from mxsolve.core import DMat
+    rng = np.random.default_rng(11 + add)
+    M, N = 64, 50000
+    lens = rng.integers(0, 30, M)
+    lens[[3, 9, 17, 40, 63]] = [2048, 2049, 70001, 9000, 4096]
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nnz = int(ip[-1])
+    cols = rng.integers(-3, N, nnz).astype(np.int64)
+    s40 = slice(ip[40], ip[41])
+    cols[s40] = rng.integers(-1, 700, lens[40])      # many duplicates in one huge row
+    vals = rng.standard_normal(nnz)
+    vals[rng.random(nnz) < 0.05] = 0.0
+    A = DMat.from_csr(selfcomm, M, N, ip, cols, vals, add=add)
+    O = oracle_mod.OracleMat.from_csr(M, N, ip, cols, vals, P=1, add=add)
+    assert_csr_equal(A.csr(), O.csr())
+
+
 def test_assembly_coo(selfcomm, oracle_mod):
     from mxsolve.core import DMat
     rng = np.random.default_rng(3)
@@ -204,3 +225,4 @@ def test_gmres_reference_system(selfcomm, oracle_mod, golden):
     assert (r["its"], r["reason"]) == (o["its"], o["reason"])
     assert rel(x.cpu().numpy(), o["x"]) <= 1e-8
     assert np.allclose(x.cpu().numpy(), golden["sys_X"])       # test.py:149's check
+
