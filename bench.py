@@ -57,7 +57,7 @@ def cg_iter_bytes_design(m: int, nnz: int, nghost: int, mode: int) -> int:
 
 def fusion_mode(knob: int, m: int) -> int:
     """The mode cg_solve runs for knob 9 (3 = auto, mx_ksp.hip)."""
-    return (1 if m <= (6 << 20) else 0) if knob == 3 else knob
+    return (1 if m <= (6 << 20) else 2) if knob == 3 else knob
 
 
 def cpu_baseline(grid: int, budget_s: float, threads: int) -> dict:

@@ -195,7 +195,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        RCCL communicator (testing, default 0)
  * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
- *        1 for <= 6M local rows, else 0)
+ *        1 for <= 6M local rows, else 2)
  * key 10: where CG folds its per-workgroup partials: 0 one-block fold kernels;
  *        1 the update pass folds its own inside the launch (default); 2 the
  *        MatMult's too

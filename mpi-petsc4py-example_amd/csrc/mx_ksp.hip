@@ -176,44 +176,78 @@ __global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double 
   if (s->beta == 0.0) { stop(s, R_CONVERGED_ATOL); return; }
 }
 
+// ---- CG vector passes.  Rows go in pairs (16-B accesses when every vector
+// is 16-B aligned, VEC; the same arithmetic on scalars otherwise), and each
+// thread issues the loads of two pairs before the first use, so a workgroup
+// keeps enough bytes in flight to stream at HBM rate.  Every row's result is
+// the same expression as PETSc's loop; the order of the per-thread partial
+// sums (update pass) is fixed by the pair walk, independent of VEC.
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+template <bool VEC> __device__ __forceinline__ dbl2 ld2(const double *__restrict__ v, int64_t k) {
+  if constexpr (VEC) return reinterpret_cast<const dbl2 *>(v)[k];
+  else return dbl2{v[2 * k], v[2 * k + 1]};
+}
+template <bool VEC> __device__ __forceinline__ void st2(double *__restrict__ v, int64_t k, dbl2 t) {
+  if constexpr (VEC) reinterpret_cast<dbl2 *>(v)[k] = t;
+  else { v[2 * k] = t.x; v[2 * k + 1] = t.y; }
+}
+// PCApply_Jacobi by form (JM: 0 none, 1 vector d, 2 uniform scalar c)
+template <int JM> __device__ __forceinline__ double jac1(double r, double d, double c) {
+  if constexpr (JM == 1) return r * d;
+  else if constexpr (JM == 2) return r * c;
+  else return r;
+}
+constexpr int CG_VEC_BLOCKS = 4096;   // grid of the paired vector passes (grid-stride)
+
 // p = z + b p  (i == 0: p = z), z = d.*r recomputed, b = beta_i / beta_{i-1}
 // from the iteration's scalar top (cg_top), which this launch commits.  Every
 // iteration is the same launch sequence (graph replay): the index comes from
-// the device state.
-__global__ void cg_p_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
-                            const Jac jac, double *__restrict__ p, double *__restrict__ hist) {
+// the device state.  XD: also the previous iteration's deferred x step, read
+// from the same p_{i-1} before it is overwritten (mode 2).
+template <int JM, bool XD, bool VEC>
+__global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
+                                                   const double *__restrict__ dv, const double dc,
+                                                   double *__restrict__ p, double *__restrict__ x,
+                                                   double *__restrict__ hist) {
   const CgTopIn top = s->top;
   if (top.done) return;
   const CgTop t = cg_top(top);
   if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(s, t, hist);
   if (t.reason) return;
   const double b = t.b;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-    const double z = papply(jac, r[k], k);
-    p[k] = (b == 0.0) ? z : z + b * p[k];       // VecAYPX_Seq (b == 0 copies; i == 0: b = 0)
-  }
-}
-
-// cg_p_kernel plus the previous iteration's deferred x step, read from the
-// same p_{i-1} before it is overwritten: x += xa p_{i-1}; p = z + b p_{i-1}
-__global__ void cg_px_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
-                             const Jac jac, double *__restrict__ p, double *__restrict__ x,
-                             double *__restrict__ hist) {
-  const CgTopIn top = s->top;
-  if (top.done) return;
-  const CgTop t = cg_top(top);
-  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(s, t, hist);
-  if (t.reason) return;
-  const double b = t.b;
-  const bool xp = top.xpend != 0.0;
+  const bool xp = XD && top.xpend != 0.0;
   const double a = top.xa;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-    const double po = p[k];
-    const double z = papply(jac, r[k], k);
-    if (xp) x[k] = fma(a, po, x[k]);            // VecAXPY(X, a, P) of iteration i-1
-    p[k] = (b == 0.0) ? z : z + b * po;         // VecAYPX_Seq (b == 0 copies; i == 0: b = 0)
+  auto pnew = [&](double rr, double dd, double po) {
+    const double z = jac1<JM>(rr, dd, dc);
+    return (b == 0.0) ? z : z + b * po;          // VecAYPX_Seq (b == 0 copies; i == 0: b = 0)
+  };
+  auto xnew = [&](double po, double xx) { return fma(a, po, xx); };   // VecAXPY(X, a, P) of i-1
+  const int64_t np = n >> 1, stride = (int64_t)gridDim.x * 256;
+  int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; k < np; k += 2 * stride) {
+    const int64_t k2 = k + stride;
+    const bool two = k2 < np;
+    const dbl2 r0 = ld2<VEC>(r, k), p0 = ld2<VEC>(p, k);
+    const dbl2 d0 = JM == 1 ? ld2<VEC>(dv, k) : dbl2{0.0, 0.0};
+    const dbl2 x0 = XD && xp ? ld2<VEC>(x, k) : dbl2{0.0, 0.0};
+    dbl2 r1 = {0.0, 0.0}, p1 = {0.0, 0.0}, d1 = {0.0, 0.0}, x1 = {0.0, 0.0};
+    if (two) {
+      r1 = ld2<VEC>(r, k2); p1 = ld2<VEC>(p, k2);
+      if (JM == 1) d1 = ld2<VEC>(dv, k2);
+      if (XD && xp) x1 = ld2<VEC>(x, k2);
+    }
+    st2<VEC>(p, k, dbl2{pnew(r0.x, d0.x, p0.x), pnew(r0.y, d0.y, p0.y)});
+    if (XD && xp) st2<VEC>(x, k, dbl2{xnew(p0.x, x0.x), xnew(p0.y, x0.y)});
+    if (two) {
+      st2<VEC>(p, k2, dbl2{pnew(r1.x, d1.x, p1.x), pnew(r1.y, d1.y, p1.y)});
+      if (XD && xp) st2<VEC>(x, k2, dbl2{xnew(p1.x, x1.x), xnew(p1.y, x1.y)});
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {     // odd last row
+    const int64_t i = n - 1;
+    const double po = p[i];
+    if (XD && xp) x[i] = xnew(po, x[i]);
+    p[i] = pnew(r[i], JM == 1 ? dv[i] : 0.0, po);
   }
 }
 
@@ -239,14 +273,15 @@ __device__ __forceinline__ CgAlpha cg_alpha(const KspState *s) {
 }
 
 // x += a p, r -= a w (BLAS daxpy = fma), z = d.*r, [z.z, z.r, r.r] folded
-// into red3 inside the launch.  x == null: the x step is deferred (modes 1/2:
+// into red3 inside the launch.  XU false: the x step is deferred (modes 1/2:
 // applied by the next iteration's first kernel, or by cg_finish_x_kernel).
+template <int JM, bool XU, bool VEC>
 __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__restrict__ s,
                                                         const double *__restrict__ p,
                                                         const double *__restrict__ w,
                                                         double *__restrict__ x, double *__restrict__ r,
-                                                        const Jac jac, double *__restrict__ partials,
-                                                        const Fold fold) {
+                                                        const double *__restrict__ dv, const double dc,
+                                                        double *__restrict__ partials, const Fold fold) {
   if (s->top.done) return;
   const CgAlpha al = cg_alpha(s);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -257,20 +292,52 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
     } else {
       s->dpis[al.i & 1] = al.dpi;
       s->alpha = al.alpha;
-      if (!x) { s->top.xa = al.alpha; s->top.xpend = 1.0; s->xi = al.i; }
+      if (!XU) { s->top.xa = al.alpha; s->top.xpend = 1.0; s->xi = al.i; }
       s->top.it_u = al.i + 1;
     }
   }
   if (al.reason) return;
   const double a = al.alpha;
   double v[3] = {0.0, 0.0, 0.0};
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    if (x) x[i] = fma(a, p[i], x[i]);
-    const double ri = fma(-a, w[i], r[i]);
-    r[i] = ri;
-    const double zi = papply(jac, ri, i);
+  auto rnew = [&](double ww, double rr, double dd) {   // r - a w, then the partial sums
+    const double ri = fma(-a, ww, rr);
+    const double zi = jac1<JM>(ri, dd, dc);
     v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
+    return ri;
+  };
+  const int64_t np = n >> 1, stride = (int64_t)gridDim.x * 256;
+  int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; k < np; k += 2 * stride) {
+    const int64_t k2 = k + stride;
+    const bool two = k2 < np;
+    const dbl2 w0 = ld2<VEC>(w, k);
+    const dbl2 r0 = ld2<VEC>(r, k);
+    const dbl2 p0 = XU ? ld2<VEC>(p, k) : dbl2{0.0, 0.0};
+    const dbl2 x0 = XU ? ld2<VEC>(x, k) : dbl2{0.0, 0.0};
+    const dbl2 d0 = JM == 1 ? ld2<VEC>(dv, k) : dbl2{0.0, 0.0};
+    dbl2 w1 = {0.0, 0.0}, r1 = {0.0, 0.0}, p1 = {0.0, 0.0}, x1 = {0.0, 0.0}, d1 = {0.0, 0.0};
+    if (two) {
+      w1 = ld2<VEC>(w, k2); r1 = ld2<VEC>(r, k2);
+      if (XU) { p1 = ld2<VEC>(p, k2); x1 = ld2<VEC>(x, k2); }
+      if (JM == 1) d1 = ld2<VEC>(dv, k2);
+    }
+    if (XU) st2<VEC>(x, k, dbl2{fma(a, p0.x, x0.x), fma(a, p0.y, x0.y)});
+    {
+      const double ra = rnew(w0.x, r0.x, d0.x);
+      const double rb = rnew(w0.y, r0.y, d0.y);
+      st2<VEC>(r, k, dbl2{ra, rb});
+    }
+    if (two) {
+      if (XU) st2<VEC>(x, k2, dbl2{fma(a, p1.x, x1.x), fma(a, p1.y, x1.y)});
+      const double ra = rnew(w1.x, r1.x, d1.x);
+      const double rb = rnew(w1.y, r1.y, d1.y);
+      st2<VEC>(r, k2, dbl2{ra, rb});
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {     // odd last row
+    const int64_t i = n - 1;
+    if (XU) x[i] = fma(a, p[i], x[i]);
+    r[i] = rnew(w[i], r[i], JM == 1 ? dv[i] : 0.0);
   }
   block_partials<3>(v, partials, gridDim.x, fold);
 }
@@ -615,6 +682,45 @@ static KspState *state_buf(Mat *A) {
   return reinterpret_cast<KspState *>(A->ksp_state.p);
 }
 
+static bool aligned16(std::initializer_list<const void *> ptrs) {
+  for (const void *q : ptrs)
+    if (reinterpret_cast<uintptr_t>(q) & 15) return false;
+  return true;
+}
+static unsigned cg_vec_grid(int64_t n) { return grid_for(cdiv(n, 2), 256, CG_VEC_BLOCKS); }
+
+// direction update (+ the deferred x step when x != null)
+static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r, const Jac &j, double *p,
+                        double *x, double *hist) {
+  const bool vec = aligned16({r, p, x, j.d});
+  const unsigned g = cg_vec_grid(n);
+#define CGP(JM, XD, V) cg_p_kernel<JM, XD, V><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, p, x, hist)
+#define CGP_J(JM) do { if (x) { if (vec) CGP(JM, true, true); else CGP(JM, true, false); } \
+                       else { if (vec) CGP(JM, false, true); else CGP(JM, false, false); } } while (0)
+  switch (j.mode) { case 1: CGP_J(1); break; case 2: CGP_J(2); break; default: CGP_J(0); }
+#undef CGP_J
+#undef CGP
+  HIPCHECK(hipGetLastError());
+}
+
+// update pass; returns its grid (= partials per value)
+static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double *p, const double *w, double *x,
+                            double *r, const Jac &j, double *partials, const Fold &fold_in) {
+  const bool vec = aligned16({p, w, x, r, j.d});
+  const unsigned g = cg_vec_grid(n);
+  Fold f = fold_in;
+  f.ntotal = f.ncount = (int)g;
+  f.base = 0;
+#define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f)
+#define CGU_J(JM) do { if (x) { if (vec) CGU(JM, true, true); else CGU(JM, true, false); } \
+                       else { if (vec) CGU(JM, false, true); else CGU(JM, false, false); } } while (0)
+  switch (j.mode) { case 1: CGU_J(1); break; case 2: CGU_J(2); break; default: CGU_J(0); }
+#undef CGU_J
+#undef CGU
+  HIPCHECK(hipGetLastError());
+  return (int)g;
+}
+
 static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const double *b, double *x,
                      mx_ksp_result &res, double *hist_host) {
   Comm *c = A->comm;
@@ -664,13 +770,13 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // fused: the direction update and the previous x step ride in the MatMult
   // (SPMV_CG); p ping-pongs between two buffers since neighbours read p_{i-1}
   // 1: direction update + x step inside the MatMult (SPMV_CG)
-  // 2: x step deferred into the next direction update (cg_px_kernel)
-  // 3 (auto): 1 up to CG_FUSE_MAX_ROWS local rows, else 0.  Measured per
-  // iteration on 256 x 256 x nz ranks (tools/coll_ab.py): mode 1 -7% at nz 32,
-  // -4% at nz 64, but +5% at nz 128 and +10% at 256^3, where the two-vector
-  // gathers of mode 1 overflow the per-XCD L2; mode 2's saved pass is repaid
-  // by a slower MatMult behind its two-vector writes
-  const int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 0) : g_knobs.cg_fuse;
+  // 2: x step deferred into the next direction update (cg_p_kernel<XD = true>)
+  // 3 (auto): 1 up to CG_FUSE_MAX_ROWS local rows, else 2.  Measured per
+  // iteration on 256 x 256 x nz ranks (tools/cg_ab.py, interleaved): nz 32
+  // modes 0/1/2 within 1.3% (1 best); nz 128: 2 -3.4% and 1 +3.8% vs 0;
+  // 256^3: 2 -6%, 1 +2%.  Mode 1's two-vector gathers overflow the per-XCD
+  // L2 at large ranks
+  const int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
   const bool fuse_cg = fmode == 1;
   const bool defer_x = fmode != 0;
   // p_{-1} = -0.0: iteration 0's z + (+0)(-0) is exactly z (VecCopy)
@@ -679,7 +785,6 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   Fold fdot, fupd;
   fdot.cnt = s->fold_dot; fdot.out = &s->red1;
   fupd.cnt = s->fold_upd; fupd.out = s->top.red3;
-  fupd.ntotal = fupd.ncount = RED_BLOCKS;
   const int fold_at = g_knobs.cg_fold;       // 0: fold kernels, 1: update in-launch, 2: both
   const Fold *fdot_p = fold_at >= 2 ? &fdot : nullptr;
   if (fold_at < 1) fupd.cnt = nullptr;
@@ -696,8 +801,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg, fdot_p);
       timer.end();
     } else {
-      if (defer_x) cg_px_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p, x, hist_d);
-      else cg_p_kernel<<<egrid, 256, 0, st>>>(n, s, r.p, dinv, pv.p, hist_d);
+      cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
       timer.begin();
       nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
@@ -705,8 +809,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     if (!fdot_p) fold_kernel<1><<<1, 256, 0, st>>>(part.p, nb_spmv, &s->red1, done);
     if (!fused) c->allreduce_sum(&s->red1, 1);
     const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : pv.p;
-    cg_update_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, part.p, fupd);
-    if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(part.p, RED_BLOCKS, s->top.red3, done);
+    const int nb_upd = cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, part.p, fupd);
+    if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(part.p, nb_upd, s->top.red3, done);
     if (!fused) c->allreduce_sum(s->top.red3, 3);
     HIPCHECK(hipGetLastError());
   };
