@@ -200,6 +200,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        1 the update pass folds its own inside the launch (default); 2 the
  *        MatMult's too
  * key 11: skew (doubles) added between consecutive KSP work vectors
+ * key 12: grid of the CG vector passes (0 = default: row walk 8192 / 1024
+ *         workgroups for the direction / update pass, paired walk 4096)
+ * key 13: CG vector passes walk row pairs with 16-B accesses when every
+ *         vector is aligned (0/1, default 0: one row per thread per step)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

@@ -396,6 +396,8 @@ int mx_debug_set(int key, int value) {
     case 9: old = g_knobs.cg_fuse; g_knobs.cg_fuse = value; break;
     case 10: old = g_knobs.cg_fold; g_knobs.cg_fold = value; break;
     case 11: old = g_knobs.ws_skew; g_knobs.ws_skew = value; break;
+    case 12: old = g_knobs.cg_vec_grid; g_knobs.cg_vec_grid = value; break;
+    case 13: old = g_knobs.cg_vec; g_knobs.cg_vec = value; break;
     default: break;
   }
   return old;

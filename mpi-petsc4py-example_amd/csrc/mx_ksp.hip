@@ -222,6 +222,16 @@ __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restri
     return (b == 0.0) ? z : z + b * po;          // VecAYPX_Seq (b == 0 copies; i == 0: b = 0)
   };
   auto xnew = [&](double po, double xx) { return fma(a, po, xx); };   // VecAXPY(X, a, P) of i-1
+  if constexpr (!VEC) {          // row walk: one row per thread per step
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const double po = p[i];
+      const double z = pnew(r[i], JM == 1 ? dv[i] : 0.0, po);
+      if (XD && xp) x[i] = xnew(po, x[i]);
+      p[i] = z;
+    }
+    return;
+  }
   const int64_t np = n >> 1, stride = (int64_t)gridDim.x * 256;
   int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   for (; k < np; k += 2 * stride) {
@@ -305,6 +315,15 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
     v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
     return ri;
   };
+  if constexpr (!VEC) {          // row walk: one row per thread per step
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      if (XU) x[i] = fma(a, p[i], x[i]);
+      r[i] = rnew(w[i], r[i], JM == 1 ? dv[i] : 0.0);
+    }
+    block_partials<3>(v, partials, gridDim.x, fold);
+    return;
+  }
   const int64_t np = n >> 1, stride = (int64_t)gridDim.x * 256;
   int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   for (; k < np; k += 2 * stride) {
@@ -687,13 +706,18 @@ static bool aligned16(std::initializer_list<const void *> ptrs) {
     if (reinterpret_cast<uintptr_t>(q) & 15) return false;
   return true;
 }
-static unsigned cg_vec_grid(int64_t n) { return grid_for(cdiv(n, 2), 256, CG_VEC_BLOCKS); }
+// grid of a CG vector pass: the row walk by default (knob 13 = 0), the paired
+// walk (16-B accesses, knob 13 = 1) only when every vector is aligned
+static unsigned cg_vec_grid(int64_t n, bool paired, int dflt) {
+  const int cap = g_knobs.cg_vec_grid > 0 ? g_knobs.cg_vec_grid : dflt;
+  return grid_for(paired ? cdiv(n, 2) : n, 256, cap);
+}
 
 // direction update (+ the deferred x step when x != null)
 static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r, const Jac &j, double *p,
                         double *x, double *hist) {
-  const bool vec = aligned16({r, p, x, j.d});
-  const unsigned g = cg_vec_grid(n);
+  const bool vec = g_knobs.cg_vec && aligned16({r, p, x, j.d});
+  const unsigned g = cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : 8192);
 #define CGP(JM, XD, V) cg_p_kernel<JM, XD, V><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, p, x, hist)
 #define CGP_J(JM) do { if (x) { if (vec) CGP(JM, true, true); else CGP(JM, true, false); } \
                        else { if (vec) CGP(JM, false, true); else CGP(JM, false, false); } } while (0)
@@ -706,8 +730,8 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
 // update pass; returns its grid (= partials per value)
 static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double *p, const double *w, double *x,
                             double *r, const Jac &j, double *partials, const Fold &fold_in) {
-  const bool vec = aligned16({p, w, x, r, j.d});
-  const unsigned g = cg_vec_grid(n);
+  const bool vec = g_knobs.cg_vec && aligned16({p, w, x, r, j.d});
+  const unsigned g = cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : RED_BLOCKS);
   Fold f = fold_in;
   f.ntotal = f.ncount = (int)g;
   f.base = 0;
@@ -822,7 +846,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
            (uintptr_t)poll, (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt, (uintptr_t)g_knobs.spmv_grid,
            (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p,
-           (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p};
+           (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p, (uintptr_t)g_knobs.cg_vec_grid,
+           (uintptr_t)g_knobs.cg_vec};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;

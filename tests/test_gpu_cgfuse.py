@@ -35,6 +35,8 @@ def _mat(comm, oracle, kind):
         r0, r1 = oracle.split_ownership(M, comm.size)[comm.rank:comm.rank + 2]
         idx = np.arange(r0, r1)
         return DMat.from_coo(comm, M, M, idx, idx, d[r0:r1])
+    if kind == "odd":              # 13^3 = 2197 rows: the paired walk's tail row
+        return DMat.stencil(comm, "poisson3d", 13)
     return DMat.stencil(comm, kind, 14)
 
 
@@ -144,3 +146,23 @@ def test_fold_placement_ranks(oracle_mod, P):
     for k, v in outs.items():
         for a, b in zip(v, outs[0, 0]):
             _same(a, b)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("kind,kw", [("poisson3d", {}), ("varidiag", {}), ("poisson3d", {"guess": True}),
+                                     ("poisson3d", {"pc": "none", "max_it": 11}), ("odd", {}),
+                                     ("odd", {"pc": "none"})])
+def test_paired_vector_walk(selfcomm, oracle_mod, kind, kw, mode):
+    """The row-pair walk of the CG vector passes (knob 13, 16-B accesses; odd
+    row counts take a tail row) sums the partials in another order: same
+    iterations and reason, x within 1e-12 of the row walk."""
+    from mxsolve import _lib
+    L = _lib.load()
+    old = L.mx_debug_set(13, 1)
+    try:
+        a = _run(selfcomm, oracle_mod, kind, mode, **dict(kw))
+    finally:
+        L.mx_debug_set(13, old)
+    b = _run(selfcomm, oracle_mod, kind, mode, **dict(kw))
+    assert (a[0], a[1]) == (b[0], b[1])
+    assert np.linalg.norm(a[3] - b[3]) <= 1e-12 * np.linalg.norm(b[3])
