@@ -98,6 +98,18 @@ int mx_get_unique_id(void *out, size_t len);
 /* One process per GPU over RCCL/xGMI (replaces MPI_COMM_WORLD, test.py:55).   */
 int mx_comm_create_rccl(int rank, int size, int device, const void *uid, size_t uid_len,
                         mx_comm *out);
+/* Processes of one node that share GPUs (more ranks than devices, e.g.
+ * `mpiexec -n 2 python test.py` on a one-GPU machine; RCCL refuses two ranks
+ * on one device): device payloads staged through the POSIX shared-memory
+ * segment `name` (rank 0 creates it, the others open it; unlinked once all
+ * have mapped it), slot_kib KiB of staging per rank (<= 0: 64 MiB; larger
+ * exchanges run in rounds).  Host-ordered correctness
+ * transport; collectives fail with MX_ERR_COMM after mx_comm_abort on any rank.
+ * [collective]                                                                  */
+int mx_comm_create_shm(int rank, int size, int device, const char *name, int64_t slot_kib,
+                       mx_comm *out);
+/* Release peers blocked in a shared-memory collective (a failing rank calls it). */
+int mx_comm_abort(mx_comm c);
 /* Single-rank communicator (PETSC_COMM_SELF / MPI.COMM_WORLD of size 1).       */
 int mx_comm_create_self(int device, mx_comm *out);
 /* In-process virtual ranks that share one GPU (testing N>1 on a 1-GPU box):

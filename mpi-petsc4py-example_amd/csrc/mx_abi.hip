@@ -77,6 +77,16 @@ int mx_comm_create_rccl(int rank, int size, int device, const void *uid, size_t 
   });
 }
 
+int mx_comm_create_shm(int rank, int size, int device, const char *name, int64_t slot_kib, mx_comm *out) {
+  return guard([&] {
+    if (size < 1 || rank < 0 || rank >= size) fail(MX_ERR_ARG, "bad rank/size");
+    if (!name || name[0] != '/') fail(MX_ERR_ARG, "shared-memory name must start with '/'");
+    *out = new mx_comm_s{make_shm_comm(rank, size, device, name, slot_kib)};
+  });
+}
+
+int mx_comm_abort(mx_comm c) { return guard([&] { if (c && c->c) abort_shm_comm(c->c); }); }
+
 int mx_comm_create_self(int device, mx_comm *out) {
   return guard([&] { *out = new mx_comm_s{make_self_comm(device)}; });
 }

@@ -11,9 +11,20 @@
 //                moved by D2D copies ordered with events.  Used to exercise
 //                the N>1 path on a single-GPU box (RCCL refuses two ranks on
 //                one device).
+//   * ShmComm  : P processes of one node that may share GPUs (more ranks than
+//                devices, where RCCL refuses two ranks on one device): device
+//                payloads staged through a POSIX shared-memory segment, host
+//                ordered.  A correctness transport (mpiexec -n 2 of test.py on
+//                a one-GPU machine), not a fast path.
 //   * SelfComm : size 1.
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -232,6 +243,211 @@ struct LocalComm : Comm {
     w->barrier(rank, 5);
   }
 };
+
+// ------------------------------------------------------------------ shared memory (processes)
+// Segment: a header (barrier words, an abort flag, per-rank int64 scratch and
+// message directories) followed by one staging slot per rank.  Every
+// collective is a sequence of "write my slot -> barrier -> read peers' slots
+// -> barrier"; device data moves by synchronous copies on the rank's stream.
+constexpr int SHM_MAX = 64;
+constexpr int SHM_DIR = 2 * SHM_MAX;       // message directory entries per rank
+struct ShmDirEnt { int64_t peer, off, bytes; };
+struct ShmHeader {
+  std::atomic<int64_t> arrived, gen;
+  std::atomic<int> abort, opened;
+  int size, pad;
+  int64_t slot_bytes;
+  int64_t scratch[SHM_MAX][SHM_MAX];        // [rank][k]: small all-to-all / all-gather payloads
+  int64_t ndir[SHM_MAX];
+  ShmDirEnt dir[SHM_MAX][SHM_DIR];
+  int tags[SHM_MAX];
+};
+
+struct ShmComm : Comm {
+  ShmHeader *h = nullptr;
+  char *base = nullptr;
+  size_t map_bytes = 0;
+  std::vector<double> tmp;
+  ShmComm(int r, int s, int dev, const char *name, int64_t slot_kib) {
+    rank = r; size = s; device = dev;
+    capturable = false;
+    if (s < 1 || s > SHM_MAX) fail(MX_ERR_ARG, "shared-memory communicator size must be in [1, 64]");
+    if (slot_kib < 1) slot_kib = 64 << 10;
+    const int64_t slot = slot_kib << 10;
+    map_bytes = sizeof(ShmHeader) + (size_t)s * (size_t)slot;
+    int fd = -1;
+    if (r == 0) {
+      fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0) fail(MX_ERR_COMM, std::string("shm_open(create) failed for ") + name);
+      if (ftruncate(fd, (off_t)map_bytes) != 0) { close(fd); shm_unlink(name); fail(MX_ERR_MEM, "ftruncate of the shared segment failed"); }
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      while ((fd = shm_open(name, O_RDWR, 0600)) < 0) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+          fail(MX_ERR_COMM, std::string("shm_open timed out for ") + name);
+        usleep(1000);
+      }
+      // wait until rank 0 has sized it
+      const auto t1 = std::chrono::steady_clock::now();
+      for (;;) {
+        off_t sz = lseek(fd, 0, SEEK_END);
+        if (sz >= (off_t)map_bytes) break;
+        if (std::chrono::steady_clock::now() - t1 > std::chrono::seconds(120)) { close(fd); fail(MX_ERR_COMM, "shared segment never sized"); }
+        usleep(1000);
+      }
+    }
+    void *m = mmap(nullptr, map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) fail(MX_ERR_MEM, "mmap of the shared segment failed");
+    h = static_cast<ShmHeader *>(m);
+    base = static_cast<char *>(m) + sizeof(ShmHeader);
+    if (r == 0) {
+      h->size = s;
+      h->slot_bytes = slot;
+      h->arrived.store(0);
+      h->gen.store(0);
+      h->abort.store(0);
+      h->opened.store(1, std::memory_order_release);
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (h->opened.load(std::memory_order_acquire) < 1) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) fail(MX_ERR_COMM, "shared segment never initialised");
+        usleep(1000);
+      }
+      if (h->size != s || h->slot_bytes != slot) fail(MX_ERR_COMM, "shared segment size mismatch between ranks");
+      h->opened.fetch_add(1);
+    }
+    stream = new_stream(dev);
+    comm_stream = new_stream(dev);
+    wait_barrier(-1, 0);                    // everyone mapped it
+    if (r == 0) shm_unlink(name);           // the mappings keep it alive
+  }
+  ~ShmComm() override {
+    if (stream) (void)hipStreamDestroy(stream);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
+    if (h) munmap(h, map_bytes);
+  }
+  char *slot(int q) { return base + (size_t)q * (size_t)h->slot_bytes; }
+
+  // sense-free generation barrier; tag checks that every rank is in the same collective
+  void wait_barrier(int tag, int check) {
+    if (h->abort.load()) fail(MX_ERR_COMM, "shared-memory world: another rank failed");
+    if (check) h->tags[rank] = tag;
+    const int64_t g = h->gen.load(std::memory_order_acquire);
+    if (h->arrived.fetch_add(1, std::memory_order_acq_rel) == size - 1) {
+      h->arrived.store(0, std::memory_order_relaxed);
+      h->gen.fetch_add(1, std::memory_order_acq_rel);
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      int spins = 0;
+      while (h->gen.load(std::memory_order_acquire) == g) {
+        if (h->abort.load()) fail(MX_ERR_COMM, "shared-memory world: another rank failed");
+        if (++spins > 1000) {
+          sched_yield();
+          if ((spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600)) {
+            h->abort.store(1);
+            fail(MX_ERR_COMM, "shared-memory barrier timed out");
+          }
+        }
+      }
+    }
+    if (check)
+      for (int q = 0; q < size; ++q)
+        if (h->tags[q] != tag) { h->abort.store(1); fail(MX_ERR_COMM, "shared-memory world: ranks entered different collectives"); }
+  }
+
+  void allreduce_sum(double *dev, int n) override {
+    if (size == 1 || n <= 0) return;
+    if ((int64_t)n * 8 > h->slot_bytes) fail(MX_ERR_ARG, "all-reduce larger than the shared slot");
+    HIPCHECK(hipMemcpyAsync(slot(rank), dev, sizeof(double) * n, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    wait_barrier(1000 + n, 1);
+    tmp.assign((size_t)n, 0.0);
+    for (int j = 0; j < n; ++j) {                 // ranks in order: the same bits everywhere
+      double t = reinterpret_cast<double *>(slot(0))[j];
+      for (int q = 1; q < size; ++q) t = t + reinterpret_cast<double *>(slot(q))[j];
+      tmp[(size_t)j] = t;
+    }
+    wait_barrier(0, 0);                           // every rank has read every slot
+    HIPCHECK(hipMemcpyAsync(dev, tmp.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
+
+  // Each rank's messages form one byte stream staged slot_bytes at a time;
+  // all ranks run the same number of rounds (the largest stream decides).
+  void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs, hipStream_t st) override {
+    if (!st) st = stream;
+    HIPCHECK(hipStreamSynchronize(st));
+    if ((int)sends.size() > SHM_DIR) fail(MX_ERR_ARG, "too many messages for the shared-memory directory");
+    int64_t total = 0;
+    h->ndir[rank] = (int64_t)sends.size();
+    for (size_t i = 0; i < sends.size(); ++i) {
+      h->dir[rank][i] = ShmDirEnt{sends[i].peer, total, (int64_t)sends[i].bytes};
+      total += (int64_t)sends[i].bytes;
+    }
+    const int64_t cap = h->slot_bytes;
+    h->scratch[rank][0] = (total + cap - 1) / cap;
+    wait_barrier(2, 1);
+    int64_t rounds = 0;
+    for (int q = 0; q < size; ++q) rounds = std::max(rounds, h->scratch[q][0]);
+    for (const Msg &r : recvs) {                  // the sender must have one message for us, of this size
+      bool ok = false;
+      for (int64_t e = 0; e < h->ndir[r.peer]; ++e)
+        if (h->dir[r.peer][e].peer == rank) { ok = h->dir[r.peer][e].bytes == (int64_t)r.bytes; break; }
+      if (!ok) { h->abort.store(1); fail(MX_ERR_COMM, "shared-memory exchange: unmatched message"); }
+    }
+    for (int64_t rd = 0; rd < rounds; ++rd) {
+      const int64_t lo = rd * cap, hi = lo + cap;
+      for (size_t i = 0; i < sends.size(); ++i) {   // stage my part of this round
+        const ShmDirEnt &d = h->dir[rank][i];
+        const int64_t a = std::max(lo, d.off), b = std::min(hi, d.off + d.bytes);
+        if (a < b)
+          HIPCHECK(hipMemcpyAsync(slot(rank) + (a - lo), static_cast<const char *>(sends[i].buf) + (a - d.off),
+                                  (size_t)(b - a), hipMemcpyDeviceToHost, st));
+      }
+      HIPCHECK(hipStreamSynchronize(st));
+      wait_barrier(0, 0);
+      for (const Msg &r : recvs) {                  // collect what peers staged for me
+        for (int64_t e = 0; e < h->ndir[r.peer]; ++e) {
+          const ShmDirEnt &d = h->dir[r.peer][e];
+          if (d.peer != rank) continue;
+          const int64_t a = std::max(lo, d.off), b = std::min(hi, d.off + d.bytes);
+          if (a < b)
+            HIPCHECK(hipMemcpyAsync(static_cast<char *>(r.buf) + (a - d.off), slot(r.peer) + (a - lo),
+                                    (size_t)(b - a), hipMemcpyHostToDevice, st));
+          break;
+        }
+      }
+      HIPCHECK(hipStreamSynchronize(st));
+      wait_barrier(0, 0);
+    }
+  }
+
+  void alltoall_i64(const int64_t *send, int64_t *recv) override {
+    for (int q = 0; q < size; ++q) h->scratch[rank][q] = send[q];
+    wait_barrier(3, 1);
+    for (int q = 0; q < size; ++q) recv[q] = h->scratch[q][rank];
+    wait_barrier(0, 0);
+  }
+  void allgather_i64(int64_t v, int64_t *all) override {
+    h->scratch[rank][0] = v;
+    wait_barrier(4, 1);
+    for (int q = 0; q < size; ++q) all[q] = h->scratch[q][0];
+    wait_barrier(0, 0);
+  }
+  void barrier() override {
+    HIPCHECK(hipStreamSynchronize(stream));
+    wait_barrier(5, 1);
+  }
+  void abort_world() { if (h) h->abort.store(1); }
+};
+
+Comm *make_shm_comm(int rank, int size, int device, const char *name, int64_t slot_kib) {
+  return new ShmComm(rank, size, device, name, slot_kib);
+}
+void abort_shm_comm(Comm *c) {
+  if (auto *s = dynamic_cast<ShmComm *>(c)) s->abort_world();
+}
 
 void *make_local_world(int size) {
   if (size < 1 || size > LOCAL_MAX) fail(MX_ERR_ARG, "local world size must be in [1, 16]");

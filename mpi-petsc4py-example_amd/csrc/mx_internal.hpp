@@ -73,6 +73,8 @@ struct Comm {
 
 Comm *make_self_comm(int device);
 Comm *make_rccl_comm(int rank, int size, int device, const void *uid, size_t len);
+Comm *make_shm_comm(int rank, int size, int device, const char *name, int64_t slot_kib);
+void abort_shm_comm(Comm *c);
 void *make_local_world(int size);
 Comm *make_local_comm(void *world, int rank, int device);
 void destroy_local_world(void *world);

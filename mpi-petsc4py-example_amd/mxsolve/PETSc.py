@@ -194,15 +194,35 @@ def _mpi(comm):
     return comm
 
 
+def _transport(mc) -> str:
+    """RCCL when every rank of the node has a GPU of its own; the shared-memory
+    transport when ranks share GPUs (RCCL refuses two ranks on one device).
+    MXSOLVE_TRANSPORT=rccl|shm overrides.  Decided on rank 0, broadcast."""
+    choice = None
+    if mc.Get_rank() == 0:
+        choice = os.environ.get("MXSOLVE_TRANSPORT", "").lower()
+        if choice not in ("rccl", "shm"):
+            import torch
+            local = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", mc.Get_size())))
+            choice = "shm" if local > torch.cuda.device_count() else "rccl"
+    return mc.bcast(choice, root=0)
+
+
 def _device_comm(comm) -> core.DeviceComm:
     """One libmxsolve communicator per MPI communicator: self for one rank,
-    RCCL (unique id broadcast over the host control plane) otherwise."""
+    RCCL (unique id broadcast over the host control plane) or, when ranks
+    share GPUs, the node-local shared-memory transport."""
     mc = _mpi(comm)
     key = id(mc)
     dc = _DEVICE_COMMS.get(key)
     if dc is None:
         if mc.Get_size() == 1:
             dc = _guard(core.DeviceComm.self_comm)
+        elif _transport(mc) == "shm":
+            import secrets
+            name = f"/mxsolve_{os.getpid()}_{secrets.token_hex(6)}" if mc.Get_rank() == 0 else None
+            name = mc.bcast(name, root=0)
+            dc = _guard(core.DeviceComm.shm, mc.Get_rank(), mc.Get_size(), name)
         else:
             uid = _guard(core.unique_id) if mc.Get_rank() == 0 else None
             uid = mc.bcast(uid, root=0)

@@ -61,6 +61,8 @@ SIGNATURES = {
     "mx_get_unique_id": (C.c_int, [P, C.c_size_t]),
     "mx_comm_create_rccl": (C.c_int, [C.c_int, C.c_int, C.c_int, P, C.c_size_t, C.POINTER(P)]),
     "mx_comm_create_self": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "mx_comm_create_shm": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int64, C.POINTER(P)]),
+    "mx_comm_abort": (C.c_int, [P]),
     "mx_world_create_local": (C.c_int, [C.c_int, C.POINTER(P)]),
     "mx_comm_create_local": (C.c_int, [P, C.c_int, C.c_int, C.POINTER(P)]),
     "mx_world_destroy": (C.c_int, [P]),

@@ -80,6 +80,20 @@ class DeviceComm:
              b, len(uid), C.byref(h))
         return cls(h)
 
+    @classmethod
+    def shm(cls, rank: int, size: int, name: str, device: int | None = None, slot_kib: int | None = None):
+        """Node-local processes sharing GPUs: payloads staged through POSIX
+        shared memory `name` (rank 0 creates it; every rank passes the same name)."""
+        h = C.c_void_p()
+        kib = slot_kib if slot_kib is not None else int(os.environ.get("MXSOLVE_SHM_KIB", str(64 << 10)))
+        call("mx_comm_create_shm", rank, size, default_device() if device is None else device,
+             name.encode(), kib, C.byref(h))
+        return cls(h)
+
+    def abort(self):
+        if self.h:
+            call("mx_comm_abort", self.h)
+
     def barrier(self):
         call("mx_comm_barrier", self.h)
 
