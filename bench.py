@@ -132,9 +132,17 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-        uid = [unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = DeviceComm.rccl(rank, world, uid[0], device=local)
+        if os.environ.get("MXSOLVE_TRANSPORT", "").lower() == "shm":
+            # rehearsal of the N > 1 flow with ranks sharing a GPU (host-staged
+            # transport, not a measurement): the driver's runs use RCCL
+            import secrets
+            name = [f"/mxsolve_bench_{secrets.token_hex(6)}" if rank == 0 else None]
+            dist.broadcast_object_list(name, src=0)
+            comm = DeviceComm.shm(rank, world, name[0], device=local % torch.cuda.device_count())
+        else:
+            uid = [unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = DeviceComm.rccl(rank, world, uid[0], device=local)
     else:
         comm = DeviceComm.self_comm(local)
 
@@ -240,7 +248,7 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"3D 7-point Poisson {n}^3, CG + Jacobi, fp64, row-block partitioned",
                        "rows": info["M"], "nnz": int(7 * n**3 - 6 * n**2),
-                       "parallelism": f"row-block x{world} (RCCL halo + allreduce)" if world > 1 else "single GPU"},
+                       "parallelism": (f"row-block x{world} (" + ("shared-memory rehearsal" if os.environ.get("MXSOLVE_TRANSPORT", "").lower() == "shm" else "RCCL halo + allreduce") + ")") if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
