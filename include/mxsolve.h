@@ -216,6 +216,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         workgroups for the direction / update pass, paired walk 4096)
  * key 13: CG vector passes walk row pairs with 16-B accesses when every
  *         vector is aligned (0/1, default 0: one row per thread per step)
+ * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

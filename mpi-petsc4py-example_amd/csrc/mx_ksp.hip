@@ -198,6 +198,11 @@ template <int JM> __device__ __forceinline__ double jac1(double r, double d, dou
   else return r;
 }
 constexpr int CG_VEC_BLOCKS = 4096;   // grid of the paired vector passes (grid-stride)
+// store flavour of the row walk (knob 14): plain, or non-temporal (streamed past the caches)
+__device__ __forceinline__ void st1(double *q, double v, int nts) {
+  if (nts) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
 
 // p = z + b p  (i == 0: p = z), z = d.*r recomputed, b = beta_i / beta_{i-1}
 // from the iteration's scalar top (cg_top), which this launch commits.  Every
@@ -208,7 +213,7 @@ template <int JM, bool XD, bool VEC>
 __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
                                                    const double *__restrict__ dv, const double dc,
                                                    double *__restrict__ p, double *__restrict__ x,
-                                                   double *__restrict__ hist) {
+                                                   double *__restrict__ hist, const int nts) {
   const CgTopIn top = s->top;
   if (top.done) return;
   const CgTop t = cg_top(top);
@@ -227,8 +232,8 @@ __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restri
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
       const double po = p[i];
       const double z = pnew(r[i], JM == 1 ? dv[i] : 0.0, po);
-      if (XD && xp) x[i] = xnew(po, x[i]);
-      p[i] = z;
+      if (XD && xp) st1(x + i, xnew(po, x[i]), nts);
+      st1(p + i, z, nts);
     }
     return;
   }
@@ -291,7 +296,8 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
                                                         const double *__restrict__ w,
                                                         double *__restrict__ x, double *__restrict__ r,
                                                         const double *__restrict__ dv, const double dc,
-                                                        double *__restrict__ partials, const Fold fold) {
+                                                        double *__restrict__ partials, const Fold fold,
+                                                        const int nts) {
   if (s->top.done) return;
   const CgAlpha al = cg_alpha(s);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -318,8 +324,8 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
   if constexpr (!VEC) {          // row walk: one row per thread per step
     const int64_t stride = (int64_t)gridDim.x * 256;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-      if (XU) x[i] = fma(a, p[i], x[i]);
-      r[i] = rnew(w[i], r[i], JM == 1 ? dv[i] : 0.0);
+      if (XU) st1(x + i, fma(a, p[i], x[i]), nts);
+      st1(r + i, rnew(w[i], r[i], JM == 1 ? dv[i] : 0.0), nts);
     }
     block_partials<3>(v, partials, gridDim.x, fold);
     return;
@@ -718,7 +724,7 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
                         double *x, double *hist) {
   const bool vec = g_knobs.cg_vec && aligned16({r, p, x, j.d});
   const unsigned g = cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : 8192);
-#define CGP(JM, XD, V) cg_p_kernel<JM, XD, V><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, p, x, hist)
+#define CGP(JM, XD, V) cg_p_kernel<JM, XD, V><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, p, x, hist, g_knobs.cg_nts)
 #define CGP_J(JM) do { if (x) { if (vec) CGP(JM, true, true); else CGP(JM, true, false); } \
                        else { if (vec) CGP(JM, false, true); else CGP(JM, false, false); } } while (0)
   switch (j.mode) { case 1: CGP_J(1); break; case 2: CGP_J(2); break; default: CGP_J(0); }
@@ -735,7 +741,8 @@ static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double
   Fold f = fold_in;
   f.ntotal = f.ncount = (int)g;
   f.base = 0;
-#define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f)
+#define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f, \
+                                                                        g_knobs.cg_nts)
 #define CGU_J(JM) do { if (x) { if (vec) CGU(JM, true, true); else CGU(JM, true, false); } \
                        else { if (vec) CGU(JM, false, true); else CGU(JM, false, false); } } while (0)
   switch (j.mode) { case 1: CGU_J(1); break; case 2: CGU_J(2); break; default: CGU_J(0); }
@@ -847,7 +854,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
            (uintptr_t)poll, (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt, (uintptr_t)g_knobs.spmv_grid,
            (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p,
            (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p, (uintptr_t)g_knobs.cg_vec_grid,
-           (uintptr_t)g_knobs.cg_vec};
+           (uintptr_t)g_knobs.cg_vec, (uintptr_t)g_knobs.cg_nts};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;
