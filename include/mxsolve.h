@@ -217,6 +217,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 13: CG vector passes walk row pairs with 16-B accesses when every
  *         vector is aligned (0/1, default 0: one row per thread per step)
  * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
+ * key 15: grid cap of the halo-boundary SpMV launch (0 = default 2048)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

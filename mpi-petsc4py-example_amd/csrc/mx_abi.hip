@@ -409,6 +409,7 @@ int mx_debug_set(int key, int value) {
     case 12: old = g_knobs.cg_vec_grid; g_knobs.cg_vec_grid = value; break;
     case 13: old = g_knobs.cg_vec; g_knobs.cg_vec = value; break;
     case 14: old = g_knobs.cg_nts; g_knobs.cg_nts = value; break;
+    case 15: old = g_knobs.bnd_grid; g_knobs.bnd_grid = value; break;
     default: break;
   }
   return old;

@@ -455,7 +455,7 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *
   launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream, nullptr, Fold{});
 }
 
-constexpr int BND_BLOCKS = 64;
+constexpr int BND_BLOCKS = 2048;   // one boundary slice per wave: the launch runs after the interior, alone on the GPU
 
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                     int *done_flag, const CgFuse *cg, const Fold *fold) {
@@ -484,7 +484,7 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
   // interior slices meanwhile; boundary slices after the exchange
   launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{});
   HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
-  const int nb = std::min(BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
+  const int nb = std::min(g_knobs.bnd_grid > 0 ? g_knobs.bnd_grid : BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
   // the boundary launch folds the partials of both launches (fold) or
   // appends its own after the main launch's
   Fold f;
