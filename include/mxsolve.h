@@ -209,8 +209,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
  *        1 for <= 6M local rows, else 2)
  * key 10: where CG folds its per-workgroup partials: 0 one-block fold kernels;
- *        1 the update pass folds its own inside the launch (default); 2 the
- *        MatMult's too
+ *        1 the update pass folds its own inside the launch, and the MatMult's
+ *        halo-boundary launch when the product is split (default); 2 the
+ *        MatMult always
  * key 11: skew (doubles) added between consecutive KSP work vectors
  * key 12: grid of the CG vector passes (0 = default: row walk 8192 / 1024
  *         workgroups for the direction / update pass, paired walk 4096)

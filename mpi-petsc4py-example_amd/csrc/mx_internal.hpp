@@ -226,6 +226,9 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                     int *done_flag, const CgFuse *cg = nullptr, const Fold *fold = nullptr);
 int spmv_blocks(const Mat *A, int mode = SPMV_PLAIN);
+// true when matmult_overlap splits the product: interior launch || halo, then
+// a boundary launch (P > 1 with ghost entries and overlap on)
+bool matmult_splits(const Mat *A);
 void mat_mult(Mat *A, const double *x, double *y);
 
 // vector kernels (mx_vec.hip)

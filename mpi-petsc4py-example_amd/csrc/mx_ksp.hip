@@ -816,8 +816,11 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   Fold fdot, fupd;
   fdot.cnt = s->fold_dot; fdot.out = &s->red1;
   fupd.cnt = s->fold_upd; fupd.out = s->top.red3;
-  const int fold_at = g_knobs.cg_fold;       // 0: fold kernels, 1: update in-launch, 2: both
-  const Fold *fdot_p = fold_at >= 2 ? &fdot : nullptr;
+  // 0: fold kernels; 1 (default): the update pass folds in-launch, and so does
+  // the MatMult's halo-boundary launch when the product splits (a single
+  // workgroup generation, unlike the 8192-block interior launch); 2: always
+  const int fold_at = g_knobs.cg_fold;
+  const Fold *fdot_p = (fold_at >= 2 || (fold_at >= 1 && matmult_splits(A))) ? &fdot : nullptr;
   if (fold_at < 1) fupd.cnt = nullptr;
   // per iteration: [first kernel: scalar top + p] -> MatMult (+ p.w) -> all-reduce
   // -> update (alpha + x, r, z norms) -> all-reduce; the scalars are

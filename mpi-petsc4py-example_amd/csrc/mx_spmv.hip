@@ -457,6 +457,8 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *
 
 constexpr int BND_BLOCKS = 2048;   // one boundary slice per wave: the launch runs after the interior, alone on the GPU
 
+bool matmult_splits(const Mat *A) { return A->comm->size > 1 && A->halo.nbnd > 0 && g_knobs.overlap; }
+
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                     int *done_flag, const CgFuse *cg, const Fold *fold) {
   Comm *c = A->comm;
