@@ -410,6 +410,7 @@ int mx_debug_set(int key, int value) {
     case 13: old = g_knobs.cg_vec; g_knobs.cg_vec = value; break;
     case 14: old = g_knobs.cg_nts; g_knobs.cg_nts = value; break;
     case 15: old = g_knobs.bnd_grid; g_knobs.bnd_grid = value; break;
+    case 16: old = g_knobs.mdot_group; g_knobs.mdot_group = value; break;
     default: break;
   }
   return old;

@@ -112,7 +112,7 @@ struct Sell {
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
 struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
-                int bnd_grid = 0; };
+                int bnd_grid = 0; int mdot_group = 32; };
 extern Knobs g_knobs;
 
 struct Halo {

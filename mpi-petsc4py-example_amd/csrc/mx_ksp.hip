@@ -447,10 +447,11 @@ __global__ void scale_by_state_kernel(int64_t n, const KspState *__restrict__ s,
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = a * x[i];
 }
 
-// VecMDot: h_j = w . v_j for j in [j0, j0+NV), one pass over w
+// VecMDot: h_j = w . v_j for j in [j0, j0 + nv), nv <= NV, one pass over w
+// (restart 30: every step's k+1 dots in one launch)
 template <int NV>
 __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__restrict__ w,
-                                                   const double *__restrict__ V, int64_t ldv, int j0,
+                                                   const double *__restrict__ V, int64_t ldv, int j0, int nv,
                                                    double *__restrict__ partials, const int *__restrict__ stop_flag) {
   if (*stop_flag) return;
   double acc[NV];
@@ -460,7 +461,8 @@ __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__re
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const double wi = w[i];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] += wi * V[(int64_t)(j0 + k) * ldv + i];
+    for (int k = 0; k < NV; ++k)
+      if (k < nv) acc[k] += wi * V[(int64_t)(j0 + k) * ldv + i];
   }
   block_sum_to_partials<NV>(acc, partials + (size_t)j0 * gridDim.x, gridDim.x);
 }
@@ -921,25 +923,23 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
 }
 
 template <int NV>
-static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int j0,
+static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int j0, int k,
                         double *partials, const int *stop_flag) {
-  mdot_kernel<NV><<<RED_BLOCKS, 256, 0, st>>>(n, w, V, ldv, j0, partials, stop_flag);
+  mdot_kernel<NV><<<RED_BLOCKS, 256, 0, st>>>(n, w, V, ldv, j0, k, partials, stop_flag);
 }
 
+// partials rows [j0, j0 + NV) are written (rows >= nv with zeros): the
+// buffer holds max_k + 2 rows rounded up to 32; groups are gw wide (knob 16)
 static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
                  double *partials, const int *stop_flag) {
-  for (int j0 = 0; j0 < nv; j0 += 8) {
-    const int k = std::min(8, nv - j0);
-    switch (k) {
-      case 1: launch_mdot<1>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-      case 2: launch_mdot<2>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-      case 3: launch_mdot<3>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-      case 4: launch_mdot<4>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-      case 5: launch_mdot<5>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-      case 6: launch_mdot<6>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-      case 7: launch_mdot<7>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-      default: launch_mdot<8>(st, n, w, V, ldv, j0, partials, stop_flag); break;
-    }
+  const int gw = g_knobs.mdot_group == 16 || g_knobs.mdot_group == 32 || g_knobs.mdot_group == 4 ? g_knobs.mdot_group : 8;
+  for (int j0 = 0; j0 < nv; j0 += gw) {
+    const int k = std::min(gw, nv - j0);
+    if (k <= 2) launch_mdot<2>(st, n, w, V, ldv, j0, k, partials, stop_flag);
+    else if (k <= 4) launch_mdot<4>(st, n, w, V, ldv, j0, k, partials, stop_flag);
+    else if (k <= 8) launch_mdot<8>(st, n, w, V, ldv, j0, k, partials, stop_flag);
+    else if (k <= 16) launch_mdot<16>(st, n, w, V, ldv, j0, k, partials, stop_flag);
+    else launch_mdot<32>(st, n, w, V, ldv, j0, k, partials, stop_flag);
     HIPCHECK(hipGetLastError());
   }
 }
@@ -962,7 +962,8 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   const int ld = max_k + 2;
   const int64_t ldv = (std::max<int64_t>(n, 1) + 31) / 32 * 32;
   const size_t nV = (size_t)ldv * (max_k + 1), nh = (size_t)ld * (max_k + 1);
-  const size_t npart = (size_t)RED_BLOCKS * (max_k + 2) + (size_t)spmv_blocks(A) + 128;
+  const size_t prow = std::max<size_t>((size_t)max_k + 2, ((size_t)max_k + 1 + 31) / 32 * 32);   // MDot groups of 32
+  const size_t npart = (size_t)RED_BLOCKS * prow + (size_t)spmv_blocks(A) + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   const size_t k1 = (size_t)max_k + 1, k2 = (size_t)max_k + 2;
   Carve cv(workspace(A, carve_size({nV, (size_t)ldv, nh, k2, k1, k1, k1, k2, npart, nhist})));
