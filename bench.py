@@ -220,6 +220,14 @@ def main():
     del flush
     cold_ms = sorted(cold)[1]
 
+    # communication latency on the library stream (N > 1): the two CG
+    # all-reduces and the halo exchange, back to back; diagnostics for scaling
+    comm_lat = None
+    if world > 1:
+        comm_lat = {"allreduce_1_us": round(comm.comm_bench(0, 200), 2),
+                    "allreduce_3_us": round(comm.comm_bench(1, 200), 2),
+                    "halo_us": round(comm.comm_bench(2, 200, A), 2)}
+
     solve = None
     if not args.no_solve:
         x.zero_()
@@ -266,6 +274,7 @@ def main():
             "cg_fusion_mode": mode,
             "cg_iter_bytes_alg": cg_iter_bytes_design(m, nnz_loc, ng, mode),
             "cg_iter_GBps_alg": round(cg_iter_bytes_design(m, nnz_loc, ng, mode) * value / 1e9, 1),
+            "comm_latency": comm_lat,
             "solve": solve,
         }
         print(json.dumps(out), flush=True)

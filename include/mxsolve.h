@@ -226,6 +226,11 @@ int mx_debug_set(int key, int value);
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,
  * and writes one partial sum per workgroup to out_dev.                      */
 int mx_debug_stream_read(mx_comm c, const double *x_dev, int64_t n, int width_bytes, double *out_dev);
+/* Communication latency on the communicator's stream, iters back to back
+ * (device time per operation, microseconds): what 0 = all-reduce of 1 double,
+ * 1 = of 3 doubles (the CG reductions), 2 = the halo exchange of A (pack +
+ * send/recv, VecScatter).  [collective]                                       */
+int mx_debug_comm_bench(mx_comm c, mx_mat A, int what, int iters, double *us_per);
 
 #ifdef __cplusplus
 }

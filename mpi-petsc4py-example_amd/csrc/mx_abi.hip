@@ -306,6 +306,36 @@ int mx_mat_get_diagonal(mx_mat a, double *d) {
   });
 }
 
+int mx_debug_comm_bench(mx_comm c, mx_mat a, int what, int iters, double *us_per) {
+  return guard([&] {
+    Comm *cm = C(c);
+    hipStream_t st = cm->stream;
+    if (iters < 1) fail(MX_ERR_ARG, "iters must be positive");
+    if (what == 2 && !a) fail(MX_ERR_ARG, "halo bench needs a matrix");
+    if ((int)cm->red_scratch.n < 64) cm->red_scratch.alloc(64);
+    DBuf<double> xv;
+    if (what == 2) { xv.alloc((size_t)std::max<int64_t>(M(a)->m, 1)); HIPCHECK(hipMemsetAsync(xv.p, 0, sizeof(double) * xv.n, st)); }
+    auto once = [&] {
+      if (what == 2) halo_begin(M(a), xv.p);
+      else cm->allreduce_sum(cm->red_scratch.p, what == 1 ? 3 : 1);
+    };
+    once();                                  // warm (connections, buffers)
+    cm->barrier();
+    hipEvent_t e0, e1;
+    HIPCHECK(hipEventCreate(&e0));
+    HIPCHECK(hipEventCreate(&e1));
+    HIPCHECK(hipEventRecord(e0, st));
+    for (int k = 0; k < iters; ++k) once();
+    HIPCHECK(hipEventRecord(e1, st));
+    HIPCHECK(hipEventSynchronize(e1));
+    float t = 0.f;
+    HIPCHECK(hipEventElapsedTime(&t, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *us_per = 1e3 * (double)t / iters;
+  });
+}
+
 int mx_mat_bench_mult(mx_mat a, const double *x, double *y, int iters, double *spmv_ms, double *mult_ms) {
   return guard([&] {
     Mat *A = M(a);
