@@ -241,3 +241,46 @@ def test_failed_rank_releases_peers():
 
     with pytest.raises(KeyError):
         run_ranks(3, body)
+
+
+@pytest.mark.parametrize("P,M", [(8, 5), (4, 3), (3, 1)])
+def test_ranks_without_rows(oracle_mod, P, M):
+    """More ranks than rows (PetscSplitOwnership gives some ranks m = 0): the
+    split, the MatMult, CG and GMRES still match the oracle on every rank."""
+    from mxsolve.core import DMat
+    rng = np.random.default_rng(M + 10 * P)
+    dense = np.diag(4.0 + rng.random(M))
+    for i in range(M - 1):
+        dense[i, i + 1] = dense[i + 1, i] = -1.0
+    ip = np.concatenate([[0], np.cumsum((dense != 0).sum(1))]).astype(np.int64)
+    c = np.nonzero(dense)[1].astype(np.int64)
+    v = dense[dense != 0]
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+    ranges = oracle_mod.split_ownership(M, P)
+    b = rng.standard_normal(M)
+    o = {k: O.solve(b, ksp=k) for k in ("cg", "gmres")}
+    y_ref = O.mult(b)
+
+    def body(comm):
+        r = comm.rank
+        lip, lc, lv = local_csr(ip, c, v, ranges[r], ranges[r + 1])
+        A = DMat.from_csr(comm, M, M, lip, lc, lv)
+        m = ranges[r + 1] - ranges[r]
+        assert A.info()["m"] == m
+        bl = torch.from_numpy(b[ranges[r]:ranges[r + 1]].copy()).cuda()
+        y = torch.zeros(m, dtype=torch.float64, device="cuda")
+        A.mult(bl, y)
+        out = {"y": y.cpu().numpy()}
+        for k in ("cg", "gmres"):
+            x = torch.zeros(m, dtype=torch.float64, device="cuda")
+            rr = A.solve(bl, x, ksp=k)
+            out[k] = (rr["its"], rr["reason"], x.cpu().numpy())
+        A.destroy()
+        return out
+
+    res = run_ranks(P, body)
+    assert np.array_equal(np.concatenate([r["y"] for r in res]).view(np.uint64), y_ref.view(np.uint64))
+    for k in ("cg", "gmres"):
+        xs = np.concatenate([r[k][2] for r in res])
+        assert all((r[k][0], r[k][1]) == (o[k]["its"], o[k]["reason"]) for r in res), (k, [r[k][:2] for r in res])
+        assert np.linalg.norm(xs - o[k]["x"]) <= 1e-10 * np.linalg.norm(o[k]["x"])
