@@ -202,7 +202,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 5: uniform-diagonal Jacobi applied as one scalar (0/1, default 1)
  * key 6: halo exchange overlapping the interior slices when P > 1 (0/1, default 1)
  * key 7: CG iterations replayed from a captured hipGraph batch after one eager
- *        batch (0/1, default 1; equal at 256^3, 2% faster at 64^3 per rank)
+ *        batch: 0 never, 1 single-rank communicators (default; equal at 256^3,
+ *        2% faster at 64^3 per rank), 2 also multi-rank RCCL communicators
  * key 8: run the collective path (unfused folds + RCCL all-reduce) on a one-rank
  *        RCCL communicator (testing, default 0)
  * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the

@@ -851,8 +851,12 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     HIPCHECK(hipGetLastError());
   };
   // a captured batch must start on an even iteration when p ping-pongs
-  bool graph = g_knobs.graph && c->capturable && !p.profile && (!fuse_cg || (poll & 1) == 0) &&
-               !A->cg_graph_failed;
+  // graph replay: single-rank communicators by default (knob 7 = 1); with
+  // multi-rank RCCL communicators only when asked (knob 7 = 2) -- a batch of
+  // eager launches keeps the GPU busy there as well (measured within 2% of
+  // replay on one rank), and eager RCCL calls are the well-trodden path
+  bool graph = (g_knobs.graph >= 2 || (g_knobs.graph == 1 && c->size == 1)) && c->capturable && !p.profile &&
+               (!fuse_cg || (poll & 1) == 0) && !A->cg_graph_failed;
   std::vector<uintptr_t> key;
   if (graph) {
     key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
