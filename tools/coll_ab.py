@@ -20,6 +20,8 @@ nzs = [int(t) for t in (sys.argv[1] if len(sys.argv) > 1 else "32,64").split(","
 variants = [tuple(int(u) for u in t.split(":")) for t in (sys.argv[2] if len(sys.argv) > 2 else "0:1,1:1").split(",")]
 if os.environ.get("MX_GRID"):                 # SpMV grid (knob 3)
     L.mx_debug_set(3, int(os.environ["MX_GRID"]))
+if os.environ.get("MX_GRAPH"):                # graph replay policy (knob 7)
+    L.mx_debug_set(7, int(os.environ["MX_GRAPH"]))
 self_c = DeviceComm.self_comm(0)
 rc = DeviceComm.rccl(0, 1, unique_id(), device=0)
 
