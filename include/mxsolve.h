@@ -221,12 +221,19 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
  * key 15: grid cap of the halo-boundary SpMV launch (0 = default 2048)
  * key 16: GMRES VecMDot vectors per pass over w (4, 8, 16 or 32; default 32)
+ * key 18: library buffers >= 64 MiB physically contiguous when the driver can
+ *         provide them (hipDeviceMallocContiguous, else hipMalloc; 0/1, default 1)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,
  * and writes one partial sum per workgroup to out_dev.                      */
 int mx_debug_stream_read(mx_comm c, const double *x_dev, int64_t n, int width_bytes, double *out_dev);
+/* Device memory for vectors (what PETSc's VecCreate allocates): physically
+ * contiguous for >= 64 MiB when the driver can provide it (key 18), else
+ * hipMalloc; the shim wraps it as a torch tensor.                            */
+int mx_dev_alloc(int device, size_t bytes, void **ptr);
+int mx_dev_free(void *ptr);
 /* Communication latency on the communicator's stream, iters back to back
  * (device time per operation, microseconds): what 0 = all-reduce of 1 double,
  * 1 = of 3 doubles (the CG reductions), 2 = the halo exchange of A (pack +

@@ -423,6 +423,16 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
   return guard([&] { dense_lu_solve(C(c), n, indptr, cols, vals, b, x); });
 }
 
+int mx_dev_alloc(int device, size_t bytes, void **ptr) {
+  return guard([&] {
+    HIPCHECK(hipSetDevice(device));
+    *ptr = nullptr;
+    if (bytes && dev_malloc(ptr, bytes) != hipSuccess) { *ptr = nullptr; fail(MX_ERR_MEM, "device allocation failed"); }
+  });
+}
+
+int mx_dev_free(void *ptr) { return guard([&] { if (ptr) HIPCHECK(hipFree(ptr)); }); }
+
 int mx_debug_set(int key, int value) {
   int old = -1;
   switch (key) {
@@ -441,6 +451,7 @@ int mx_debug_set(int key, int value) {
     case 14: old = g_knobs.cg_nts; g_knobs.cg_nts = value; break;
     case 15: old = g_knobs.bnd_grid; g_knobs.bnd_grid = value; break;
     case 16: old = g_knobs.mdot_group; g_knobs.mdot_group = value; break;
+    case 18: old = g_knobs.contig; g_knobs.contig = value; break;
     default: break;
   }
   return old;

@@ -24,6 +24,10 @@ void hip_check(hipError_t e, const char *what, const char *file, int line);
 #define HIPCHECK(x) ::mx::hip_check((x), #x, __FILE__, __LINE__)
 
 // ---------------------------------------------------------------- device buffers
+// hipMalloc, or (knob 18) a physically contiguous allocation for large
+// buffers when the driver can provide one (falls back to hipMalloc)
+hipError_t dev_malloc(void **p, size_t bytes);
+
 // Owning device allocation (hipMalloc).  The library allocates matrix storage
 // and solver work vectors itself; user vectors arrive as raw device pointers.
 template <class T> struct DBuf {
@@ -40,7 +44,7 @@ template <class T> struct DBuf {
     reset();
     n = count;
     if (count) {
-      hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), count * sizeof(T));
+      hipError_t e = dev_malloc(reinterpret_cast<void **>(&p), count * sizeof(T));
       if (e != hipSuccess) { p = nullptr; n = 0; fail(MX_ERR_MEM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed"); }
     }
   }
@@ -112,7 +116,8 @@ struct Sell {
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
 struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
-                int bnd_grid = 0; int mdot_group = 32; };
+                int bnd_grid = 0; int mdot_group = 32;
+                int contig = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

@@ -16,6 +16,14 @@
 
 namespace mx {
 
+hipError_t dev_malloc(void **p, size_t bytes) {
+  if (g_knobs.contig && bytes >= ((size_t)64 << 20)) {
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+  }
+  return hipMalloc(p, bytes);
+}
+
 // one block per value: out[v] = sum_b partials[v][b], fixed order (16 loads
 // in flight per thread; the same sums as the plain strided loop)
 __global__ void __launch_bounds__(256) finish_kernel(const double *__restrict__ partials,

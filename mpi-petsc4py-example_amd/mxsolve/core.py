@@ -47,6 +47,38 @@ def unique_id() -> bytes:
     return buf.raw
 
 
+BIG_VECTOR_BYTES = 64 << 20
+
+
+class _DeviceBuffer:
+    """Library-allocated device memory exposed through __cuda_array_interface__;
+    the tensor made from it keeps this object (and so the memory) alive."""
+
+    def __init__(self, n: int, device: int):
+        self.ptr = C.c_void_p()
+        self.device = device
+        call("mx_dev_alloc", device, n * 8, C.byref(self.ptr))
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (self.ptr.value or 0, False),
+                                         "version": 2, "strides": None}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                _lib.load().mx_dev_free(self.ptr)
+                self.ptr = C.c_void_p()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def device_vector(n: int, device: int) -> torch.Tensor:
+    """A float64 vector in HBM: large ones in the library's (physically
+    contiguous when available) allocations, small ones from torch's cache."""
+    if n * 8 < BIG_VECTOR_BYTES:
+        return torch.empty(n, dtype=torch.float64, device=torch.device("cuda", device))
+    buf = _DeviceBuffer(n, device)
+    return torch.as_tensor(buf, device=torch.device("cuda", device))
+
+
 class DeviceComm:
     """One rank's communicator handle (self, RCCL, or in-process local)."""
 
@@ -106,10 +138,10 @@ class DeviceComm:
         call("mx_comm_barrier", self.h)
 
     def empty(self, n: int) -> torch.Tensor:
-        return torch.empty(max(int(n), 0), dtype=torch.float64, device=torch.device("cuda", self.device))
+        return device_vector(max(int(n), 0), self.device)
 
     def zeros(self, n: int) -> torch.Tensor:
-        return torch.zeros(max(int(n), 0), dtype=torch.float64, device=torch.device("cuda", self.device))
+        return device_vector(max(int(n), 0), self.device).zero_()
 
     def destroy(self):
         if self.h:
