@@ -212,7 +212,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 10: where CG folds its per-workgroup partials: 0 one-block fold kernels;
  *        1 the update pass folds its own inside the launch, and the MatMult's
  *        halo-boundary launch when the product is split (default); 2 the
- *        MatMult always
+ *        MatMult always; 3 as 1, and on one rank the update pass folds the
+ *        MatMult's partials in its prologue (no fold launch; measured equal)
  * key 11: skew (doubles) added between consecutive KSP work vectors
  * key 12: grid of the CG vector passes (0 = default: row walk 8192 / 1024
  *         workgroups for the direction / update pass, paired walk 4096)

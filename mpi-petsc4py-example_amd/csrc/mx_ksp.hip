@@ -269,10 +269,10 @@ __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restri
 // dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
 // Read-only; cg_update_kernel's workgroup 0 commits it.
 struct CgAlpha { int i, reason; double dpi, alpha; };
-__device__ __forceinline__ CgAlpha cg_alpha(const KspState *s) {
+__device__ __forceinline__ CgAlpha cg_alpha(const KspState *s, double dpi) {
   // every input loaded before the first branch
   const int i = s->it_k;
-  const double dpi = s->red1, d0 = s->dpis[0], d1 = s->dpis[1];
+  const double d0 = s->dpis[0], d1 = s->dpis[1];
   const double b0 = s->top.betas[0], b1 = s->top.betas[1];
   CgAlpha a;
   a.i = i;
@@ -297,11 +297,16 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
                                                         double *__restrict__ x, double *__restrict__ r,
                                                         const double *__restrict__ dv, const double dc,
                                                         double *__restrict__ partials, const Fold fold,
-                                                        const int nts) {
+                                                        const int nts, const double *__restrict__ dot_part,
+                                                        const int ndot) {
   if (s->top.done) return;
-  const CgAlpha al = cg_alpha(s);
+  // p.w: folded and all-reduced before this launch, or (one rank) folded here
+  // by every workgroup from the MatMult's partials, in fold_kernel's order
+  const double pw = ndot > 0 ? block_sum_array<16>(dot_part, ndot) : s->red1;
+  const CgAlpha al = cg_alpha(s, pw);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     s->dpi = al.dpi;
+    s->red1 = pw;
     s->top.xpend = 0.0;            // a deferred step of i-1 was applied by this iteration's first kernel
     if (al.reason) {
       stop(s, al.reason);
@@ -737,14 +742,15 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
 
 // update pass; returns its grid (= partials per value)
 static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double *p, const double *w, double *x,
-                            double *r, const Jac &j, double *partials, const Fold &fold_in) {
+                            double *r, const Jac &j, double *partials, const Fold &fold_in,
+                            const double *dot_part, int ndot) {
   const bool vec = g_knobs.cg_vec && aligned16({p, w, x, r, j.d});
   const unsigned g = cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : RED_BLOCKS);
   Fold f = fold_in;
   f.ntotal = f.ncount = (int)g;
   f.base = 0;
 #define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f, \
-                                                                        g_knobs.cg_nts)
+                                                                        g_knobs.cg_nts, dot_part, ndot)
 #define CGU_J(JM) do { if (x) { if (vec) CGU(JM, true, true); else CGU(JM, true, false); } \
                        else { if (vec) CGU(JM, false, true); else CGU(JM, false, false); } } while (0)
   switch (j.mode) { case 1: CGU_J(1); break; case 2: CGU_J(2); break; default: CGU_J(0); }
@@ -842,11 +848,16 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
     }
-    if (!fdot_p) fold_kernel<1><<<1, 256, 0, st>>>(part.p, nb_spmv, &s->red1, done);
+    // one rank: the update pass folds the MatMult's partials itself (knob 10 = 3)
+    const bool fold_in_update = !fdot_p && fused && fold_at == 3;
+    if (!fdot_p && !fold_in_update) fold_kernel<1><<<1, 256, 0, st>>>(part.p, nb_spmv, &s->red1, done);
     if (!fused) c->allreduce_sum(&s->red1, 1);
     const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : pv.p;
-    const int nb_upd = cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, part.p, fupd);
-    if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(part.p, nb_upd, s->top.red3, done);
+    // the update's own partials go after the MatMult's when it folds those
+    double *upart = fold_in_update ? part.p + ((nb_spmv + 63) / 64) * 64 : part.p;
+    const int nb_upd = cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, upart, fupd,
+                                        fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0);
+    if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(upart, nb_upd, s->top.red3, done);
     if (!fused) c->allreduce_sum(s->top.red3, 3);
     HIPCHECK(hipGetLastError());
   };

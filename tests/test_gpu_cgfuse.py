@@ -113,7 +113,7 @@ FOLD_CASES = [("poisson3d", {}), ("poisson3d", {"max_it": 7}), ("poisson3d", {"n
               ("varidiag", {}), ("indef", {"pc": "none"}), ("poisson3d", {"guess": True})]
 
 
-@pytest.mark.parametrize("fold", [0, 2])
+@pytest.mark.parametrize("fold", [0, 2, 3])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("kind,kw", FOLD_CASES)
 def test_fold_placement_one_rank(selfcomm, oracle_mod, kind, kw, mode, fold):
