@@ -88,7 +88,7 @@ def cpu_baseline(grid: int, budget_s: float, threads: int) -> dict:
     except (OSError, StopIteration):
         pass
     return {"value": round(r["its"] / dt, 3), "unit": "CG iterations/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "setup_s": round(setup, 2),
             "sample": f"{r['its']} CG+Jacobi iterations on the full {grid}^3 7-point system "
                       f"(oracle/petsc_oracle.c, PETSc-restatement not PETSc, 1 rank x {threads} OpenMP "
                       f"threads on {model}, nproc {os.cpu_count()}, {dt:.1f} s; matrix build {setup:.1f} s untimed)"}
@@ -246,6 +246,8 @@ def main():
         threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
         threads = max(1, min(threads, 16))
         cpu = cpu_baseline(n, args.cpu_seconds, threads)
+        if solve is not None:       # the converged solve's iterations at the CPU rate
+            cpu["time_to_solution_s_est"] = round(solve["its"] / cpu["value"] + cpu["setup_s"], 2)
 
     if rank == 0:
         traffic = load_traffic(n, world)
