@@ -224,6 +224,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 16: GMRES VecMDot vectors per pass over w (4, 8, 16 or 32; default 32)
  * key 18: library buffers >= 64 MiB physically contiguous when the driver can
  *         provide them (hipDeviceMallocContiguous, else hipMalloc; 0/1, default 1)
+ * key 19: one-byte row masks for aligned-offset slices when every slice has
+ *         <= 8 offsets (read at assembly; 0/1, default 1)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

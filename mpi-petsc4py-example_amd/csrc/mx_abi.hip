@@ -452,6 +452,7 @@ int mx_debug_set(int key, int value) {
     case 15: old = g_knobs.bnd_grid; g_knobs.bnd_grid = value; break;
     case 16: old = g_knobs.mdot_group; g_knobs.mdot_group = value; break;
     case 18: old = g_knobs.contig; g_knobs.contig = value; break;
+    case 19: old = g_knobs.mask8; g_knobs.mask8 = value; break;
     default: break;
   }
   return old;

@@ -598,7 +598,7 @@ __global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
                                  int64_t nslices, const int64_t *__restrict__ sptr,
                                  const int32_t *__restrict__ width, const int32_t *__restrict__ doff,
                                  int32_t *__restrict__ scol, double *__restrict__ sval,
-                                 uint32_t *__restrict__ mask) {
+                                 uint32_t *__restrict__ mask, uint8_t *__restrict__ mask8) {
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= nslices) return;
   const int lane = threadIdx.x & 63;
@@ -617,7 +617,8 @@ __global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
       sval[sell_slot(base, j, k, lane, PAIRED)] = hit ? cval[rs + cur] : 0.0;
       if (hit) { mk |= 1u << j; ++cur; }
     }
-    mask[row] = mk;
+    if (mask8) mask8[row] = (uint8_t)mk;
+    else mask[row] = mk;
     return;
   }
   const int w = wr;
@@ -636,8 +637,7 @@ static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *co
   S.width.alloc((size_t)std::max<int64_t>(ns, 1));
   S.sptr.alloc((size_t)std::max<int64_t>(ns, 1));
   S.doff.alloc((size_t)std::max<int64_t>(allow_dia ? ns * DIA_MAX : 1, 1));
-  S.mask.alloc((size_t)std::max<int64_t>(allow_dia ? ns * SLICE : 1, 1));
-  if (ns == 0) { S.slots = 0; return; }
+  if (ns == 0) { S.slots = 0; S.mask.alloc(1); return; }
   slice_format_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, ns, allow_dia ? 1 : 0, S.width.p,
                                                               S.sptr.p, S.doff.p);
   HIPCHECK(hipGetLastError());
@@ -650,14 +650,21 @@ static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *co
     for (int32_t w : wh)
       if (w < 0) { S.dia_slices++; hist[-w]++; }
     S.dia_k = 0;
-    for (int k = 1; k <= DIA_MAX; ++k)
+    int kmax = 0;
+    for (int k = 1; k <= DIA_MAX; ++k) {
       if (hist[k] > hist[S.dia_k]) S.dia_k = k;
+      if (hist[k]) kmax = k;
+    }
+    // presence masks: one byte per row when every aligned-offset slice has <= 8 offsets
+    if (S.dia_slices && kmax <= 8 && g_knobs.mask8) S.mask8.alloc((size_t)ns * SLICE);
+    else if (S.dia_slices) S.mask.alloc((size_t)ns * SLICE);
   }
+  if (!S.mask.p) S.mask.alloc(1);
   exclusive_scan_i64(S.sptr.p, S.sptr.p, ns, st, &S.slots);
   S.col.alloc((size_t)std::max<int64_t>(S.slots, 1));
   S.val.alloc((size_t)std::max<int64_t>(S.slots, 1));
   sell_fill_kernel<true><<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
-                                                                S.doff.p, S.col.p, S.val.p, S.mask.p);
+                                                                S.doff.p, S.col.p, S.val.p, S.mask.p, S.mask8.p);
   HIPCHECK(hipGetLastError());
 }
 

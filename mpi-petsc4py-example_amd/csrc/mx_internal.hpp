@@ -111,13 +111,14 @@ struct Sell {
   DBuf<double> val;      // [slots]
   DBuf<int32_t> doff;    // [nslices * DIA_MAX] offsets of aligned-offset slices
   DBuf<uint32_t> mask;   // [nslices * 64] slot-present bits of aligned-offset rows
+  DBuf<uint8_t> mask8;   // the same in one byte per row when every slice has <= 8 offsets
 };
 
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
 struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
                 int bnd_grid = 0; int mdot_group = 32;
-                int contig = 1; };
+                int contig = 1; int mask8 = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

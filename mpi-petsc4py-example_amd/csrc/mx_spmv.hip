@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     int64_t m, int64_t ncols, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
     const double *__restrict__ val_d, const int32_t *__restrict__ doff,
-    const uint32_t *__restrict__ dmask, const int64_t *__restrict__ sptr_o,
+    const uint32_t *__restrict__ dmask, const uint8_t *__restrict__ dmask8, const int64_t *__restrict__ sptr_o,
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o,
     const double *__restrict__ val_o, const double *__restrict__ x,
     const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     double sum;
     if (w < 0) {
       const int k = -w;
-      const uint32_t mk = dmask[row];
+      const uint32_t mk = dmask8 ? (uint32_t)dmask8[row] : dmask[row];
       const int32_t *__restrict__ off = doff + (int64_t)s * DIA_MAX;
       const int64_t srow = (int64_t)s * SLICE;
       int omin = off[0], omax = off[0];
@@ -404,7 +404,7 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
   const CgFuse cg = cgp ? *cgp : CgFuse{};
 #define SPMV_ARGS                                                                           \
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
-      A->sd.mask.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac,   \
+      A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
       partials, done_flag, cg, fold
 #define SPMV_KD(MODE, NT, SP)                                                                    \
   do {                                                                                           \
