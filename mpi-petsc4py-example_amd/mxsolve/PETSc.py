@@ -186,6 +186,12 @@ COMM_SELF = Comm(_MPI.COMM_SELF)
 _DEVICE_COMMS: dict[int, core.DeviceComm] = {}
 
 
+def _petsc_g(v) -> str:
+    """PETSc's "%g": a value that prints like an integer gets a trailing '.'."""
+    t = f"{float(v):g}"
+    return t if any(ch in t for ch in ".eEn") else t + "."
+
+
 def _mpi(comm):
     if comm is None:
         return _MPI.COMM_WORLD
@@ -539,9 +545,16 @@ class Vec:
                 petsc_io.write_vec(viewer._fh, np.concatenate(parts))
                 viewer._fh.flush()
             return
-        print(f"Vec Object: {self._comm.size} MPI process(es)\n  type: {'mpi' if self._comm.size > 1 else 'seq'}")
-        for v in arr:
-            print(f"{v:g}")
+        # VecView_MPI_ASCII default format: values per process, "%g"
+        P = mc.Get_size()
+        parts = mc.allgather(arr) if P > 1 else [arr]
+        if mc.Get_rank() == 0:
+            lines = [f"Vec Object: {P} MPI process{'es' if P > 1 else ''}", f"  type: {'mpi' if P > 1 else 'seq'}"]
+            for q, a in enumerate(parts):
+                if P > 1:
+                    lines.append(f"Process [{q}]")
+                lines += [_petsc_g(v) for v in a]
+            print("\n".join(lines), flush=True)
 
     def load(self, viewer):
         """VecLoad: the next Vec in a binary viewer, split by PetscSplitOwnership."""
@@ -841,10 +854,21 @@ class Mat:
                                    np.concatenate([p[2] for p in parts]))
                 viewer._fh.flush()
             return
-        i = self._info()
-        print(f"Mat Object: {self._comm.size} MPI process(es)\n  type: {self.getType()}\n"
-              f"  rows={i['M']}, cols={i['N']}, local nonzeros={i['nnz_d'] + i['nnz_o']} "
-              f"(diag {i['nnz_d']}, offdiag {i['nnz_o']}, ghosts {i['nghost']})")
+        # PETSC_VIEWER_STDOUT_WORLD, default ASCII format (MatView_MPIAIJ gathers
+        # the rows on rank 0, MatView_SeqAIJ_ASCII prints "row i: (j, v) ...")
+        mc = _mpi(self._comm)
+        part = self.getValuesCSR()
+        parts = mc.allgather(part) if mc.Get_size() > 1 else [part]
+        if mc.Get_rank() == 0:
+            P = mc.Get_size()
+            lines = [f"Mat Object: {P} MPI process{'es' if P > 1 else ''}", f"  type: {self.getType()}"]
+            r = 0
+            for ip, cj, vv in parts:
+                for k in range(len(ip) - 1):
+                    ents = "".join(f" ({int(cj[e])}, {_petsc_g(vv[e])}) " for e in range(ip[k], ip[k + 1]))
+                    lines.append(f"row {r}:{ents}")
+                    r += 1
+            print("\n".join(lines), flush=True)
 
     def destroy(self):
         if self._h is not None:

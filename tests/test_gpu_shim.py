@@ -159,3 +159,23 @@ def test_binary_viewer_roundtrip(PETSc, golden, tmp_path):
     for u, v in zip(A2.getValuesCSR(), A.getValuesCSR()):
         assert np.array_equal(u, v)
     assert np.array_equal(b2.array, golden["sys_B"])
+
+
+def test_ascii_view_petsc_format(PETSc, capsys):
+    """A.view() / b.view() (petsc_funcs.py:8, commented out in the reference)
+    print PETSc's default ASCII format: "row i: (j, v) ..." with "%g" values."""
+    ip = np.array([0, 2, 5, 7], dtype=np.int32)
+    cj = np.array([0, 1, 0, 1, 2, 1, 2], dtype=np.int32)
+    vv = np.array([2.0, -1.0, -1.0, 2.0, -1.0, -1.0, 2.5])
+    A = PETSc.Mat().createAIJ(size=(3, 3), csr=(ip, cj, vv))
+    A.assemble()
+    capsys.readouterr()
+    A.view()
+    out = capsys.readouterr().out.splitlines()
+    assert out == ["Mat Object: 1 MPI process", "  type: seqaij",
+                   "row 0: (0, 2.)  (1, -1.) ", "row 1: (0, -1.)  (1, 2.)  (2, -1.) ", "row 2: (1, -1.)  (2, 2.5) "]
+    x, b = A.getVecs()
+    b.setArray(np.array([1.0, 0.5, 3e-7]))
+    b.view()
+    out = capsys.readouterr().out.splitlines()
+    assert out == ["Vec Object: 1 MPI process", "  type: seq", "1.", "0.5", "3e-07"]
