@@ -226,6 +226,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         provide them (hipDeviceMallocContiguous, else hipMalloc; 0/1, default 1)
  * key 19: one-byte row masks for aligned-offset slices when every slice has
  *         <= 8 offsets (read at assembly; 0/1, default 1)
+ * key 21: CG vector passes issue four steps' loads together: 0 never, 1 always,
+ *         2 auto (default: up to 6M local rows)
+ * key 22: grid cap of the CG update pass (0 = default 1024 workgroups)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

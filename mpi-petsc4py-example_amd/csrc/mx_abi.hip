@@ -453,6 +453,8 @@ int mx_debug_set(int key, int value) {
     case 16: old = g_knobs.mdot_group; g_knobs.mdot_group = value; break;
     case 18: old = g_knobs.contig; g_knobs.contig = value; break;
     case 19: old = g_knobs.mask8; g_knobs.mask8 = value; break;
+    case 21: old = g_knobs.cg_unroll; g_knobs.cg_unroll = value; break;
+    case 22: old = g_knobs.cg_upd_grid; g_knobs.cg_upd_grid = std::min(value, 65536); break;
     default: break;
   }
   return old;

@@ -118,7 +118,8 @@ struct Sell {
 struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
                 int bnd_grid = 0; int mdot_group = 32;
-                int contig = 1; int mask8 = 1; };
+                int contig = 1; int mask8 = 1; int cg_unroll = 2;
+                int cg_upd_grid = 0; };
 extern Knobs g_knobs;
 
 struct Halo {

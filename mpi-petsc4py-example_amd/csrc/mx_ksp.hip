@@ -198,6 +198,7 @@ template <int JM> __device__ __forceinline__ double jac1(double r, double d, dou
   else return r;
 }
 constexpr int CG_VEC_BLOCKS = 4096;   // grid of the paired vector passes (grid-stride)
+constexpr int CG_MAX_VEC_GRID = 65536;  // cap on any vector-pass grid (partials buffer sizing)
 // store flavour of the row walk (knob 14): plain, or non-temporal (streamed past the caches)
 __device__ __forceinline__ void st1(double *q, double v, int nts) {
   if (nts) __builtin_nontemporal_store(v, q);
@@ -213,7 +214,7 @@ template <int JM, bool XD, bool VEC>
 __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
                                                    const double *__restrict__ dv, const double dc,
                                                    double *__restrict__ p, double *__restrict__ x,
-                                                   double *__restrict__ hist, const int nts) {
+                                                   double *__restrict__ hist, const int nts, const int unr) {
   const CgTopIn top = s->top;
   if (top.done) return;
   const CgTop t = cg_top(top);
@@ -229,6 +230,31 @@ __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restri
   auto xnew = [&](double po, double xx) { return fma(a, po, xx); };   // VecAXPY(X, a, P) of i-1
   if constexpr (!VEC) {          // row walk: one row per thread per step
     const int64_t stride = (int64_t)gridDim.x * 256;
+    if (unr) {                   // knob 21: four steps' loads issued together
+      int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+      for (; i + 3 * stride < n; i += 4 * stride) {
+        double po[4], rr[4], dd[4], xx[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          po[u] = p[i + u * stride];
+          rr[u] = r[i + u * stride];
+          dd[u] = JM == 1 ? dv[i + u * stride] : 0.0;
+          xx[u] = XD && xp ? x[i + u * stride] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (XD && xp) st1(x + i + u * stride, xnew(po[u], xx[u]), nts);
+          st1(p + i + u * stride, pnew(rr[u], dd[u], po[u]), nts);
+        }
+      }
+      for (; i < n; i += stride) {
+        const double po = p[i];
+        const double z = pnew(r[i], JM == 1 ? dv[i] : 0.0, po);
+        if (XD && xp) st1(x + i, xnew(po, x[i]), nts);
+        st1(p + i, z, nts);
+      }
+      return;
+    }
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
       const double po = p[i];
       const double z = pnew(r[i], JM == 1 ? dv[i] : 0.0, po);
@@ -298,7 +324,7 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
                                                         const double *__restrict__ dv, const double dc,
                                                         double *__restrict__ partials, const Fold fold,
                                                         const int nts, const double *__restrict__ dot_part,
-                                                        const int ndot) {
+                                                        const int ndot, const int unr) {
   if (s->top.done) return;
   // p.w: folded and all-reduced before this launch, or (one rank) folded here
   // by every workgroup from the MatMult's partials, in fold_kernel's order
@@ -328,7 +354,26 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
   };
   if constexpr (!VEC) {          // row walk: one row per thread per step
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (unr) {                   // knob 21: four steps' loads issued together, same sum order
+      for (; i + 3 * stride < n; i += 4 * stride) {
+        double pp[4], xx[4], ww[4], rr[4], dd[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          ww[u] = w[i + u * stride];
+          rr[u] = r[i + u * stride];
+          pp[u] = XU ? p[i + u * stride] : 0.0;
+          xx[u] = XU ? x[i + u * stride] : 0.0;
+          dd[u] = JM == 1 ? dv[i + u * stride] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (XU) st1(x + i + u * stride, fma(a, pp[u], xx[u]), nts);
+          st1(r + i + u * stride, rnew(ww[u], rr[u], dd[u]), nts);
+        }
+      }
+    }
+    for (; i < n; i += stride) {
       if (XU) st1(x + i, fma(a, p[i], x[i]), nts);
       st1(r + i, rnew(w[i], r[i], JM == 1 ? dv[i] : 0.0), nts);
     }
@@ -722,8 +767,14 @@ static bool aligned16(std::initializer_list<const void *> ptrs) {
 // grid of a CG vector pass: the row walk by default (knob 13 = 0), the paired
 // walk (16-B accesses, knob 13 = 1) only when every vector is aligned
 static unsigned cg_vec_grid(int64_t n, bool paired, int dflt) {
-  const int cap = g_knobs.cg_vec_grid > 0 ? g_knobs.cg_vec_grid : dflt;
+  const int cap = std::min(g_knobs.cg_vec_grid > 0 ? g_knobs.cg_vec_grid : dflt, CG_MAX_VEC_GRID);
   return grid_for(paired ? cdiv(n, 2) : n, 256, cap);
+}
+
+// four-step load batches in the row walk (knob 21): 2 = auto, on up to
+// CG_FUSE_MAX_ROWS rows (-3% per iteration at 2M rows/rank; +5% at 256^3)
+static int cg_unroll(int64_t n) {
+  return g_knobs.cg_unroll == 2 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 0) : g_knobs.cg_unroll;
 }
 
 // direction update (+ the deferred x step when x != null)
@@ -731,7 +782,8 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
                         double *x, double *hist) {
   const bool vec = g_knobs.cg_vec && aligned16({r, p, x, j.d});
   const unsigned g = cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : 8192);
-#define CGP(JM, XD, V) cg_p_kernel<JM, XD, V><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, p, x, hist, g_knobs.cg_nts)
+  const int unr = cg_unroll(n);
+#define CGP(JM, XD, V) cg_p_kernel<JM, XD, V><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, p, x, hist, g_knobs.cg_nts, unr)
 #define CGP_J(JM) do { if (x) { if (vec) CGP(JM, true, true); else CGP(JM, true, false); } \
                        else { if (vec) CGP(JM, false, true); else CGP(JM, false, false); } } while (0)
   switch (j.mode) { case 1: CGP_J(1); break; case 2: CGP_J(2); break; default: CGP_J(0); }
@@ -745,12 +797,14 @@ static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double
                             double *r, const Jac &j, double *partials, const Fold &fold_in,
                             const double *dot_part, int ndot) {
   const bool vec = g_knobs.cg_vec && aligned16({p, w, x, r, j.d});
-  const unsigned g = cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : RED_BLOCKS);
+  const unsigned g = g_knobs.cg_upd_grid > 0 ? grid_for(n, 256, g_knobs.cg_upd_grid)
+                                             : cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : RED_BLOCKS);
   Fold f = fold_in;
   f.ntotal = f.ncount = (int)g;
+  const int unr = cg_unroll(n);
   f.base = 0;
 #define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f, \
-                                                                        g_knobs.cg_nts, dot_part, ndot)
+                                                                        g_knobs.cg_nts, dot_part, ndot, unr)
 #define CGU_J(JM) do { if (x) { if (vec) CGU(JM, true, true); else CGU(JM, true, false); } \
                        else { if (vec) CGU(JM, false, true); else CGU(JM, false, false); } } while (0)
   switch (j.mode) { case 1: CGU_J(1); break; case 2: CGU_J(2); break; default: CGU_J(0); }
@@ -768,7 +822,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   const bool fused = c->size == 1 && !g_knobs.force_coll;
   int normtype = p.norm_type == MX_NORM_DEFAULT ? MX_NORM_PRECONDITIONED : p.norm_type;
   const size_t nv = (size_t)std::max<int64_t>(n, 1);
-  const size_t npart = (size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 64;
+  // MatMult partials (+ boundary launch), then the update pass's 3 per workgroup
+  const size_t npart = (size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 3 * (size_t)CG_MAX_VEC_GRID + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist})));
   struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
@@ -874,7 +929,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
            (uintptr_t)poll, (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt, (uintptr_t)g_knobs.spmv_grid,
            (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p,
            (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p, (uintptr_t)g_knobs.cg_vec_grid,
-           (uintptr_t)g_knobs.cg_vec, (uintptr_t)g_knobs.cg_nts};
+           (uintptr_t)g_knobs.cg_vec, (uintptr_t)g_knobs.cg_nts, (uintptr_t)g_knobs.cg_unroll,
+           (uintptr_t)g_knobs.cg_upd_grid};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;

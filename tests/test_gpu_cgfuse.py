@@ -166,3 +166,21 @@ def test_paired_vector_walk(selfcomm, oracle_mod, kind, kw, mode):
     b = _run(selfcomm, oracle_mod, kind, mode, **dict(kw))
     assert (a[0], a[1]) == (b[0], b[1])
     assert np.linalg.norm(a[3] - b[3]) <= 1e-12 * np.linalg.norm(b[3])
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("kind,kw", [("poisson3d", {}), ("varidiag", {}), ("odd", {"guess": True}),
+                                     ("poisson3d", {"max_it": 9})])
+def test_unrolled_row_walk_bitwise(selfcomm, oracle_mod, kind, kw, mode):
+    """Four-step load batches in the CG vector passes (knob 21) keep each
+    thread's sum order: bitwise the plain row walk."""
+    from mxsolve import _lib
+    L = _lib.load()
+    out = {}
+    for u in (0, 1):
+        old = L.mx_debug_set(21, u)
+        try:
+            out[u] = _run(selfcomm, oracle_mod, kind, mode, **dict(kw))
+        finally:
+            L.mx_debug_set(21, old)
+    _same(out[0], out[1])
