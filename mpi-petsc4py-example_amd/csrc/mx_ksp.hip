@@ -517,27 +517,34 @@ __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__re
   block_sum_to_partials<NV>(acc, partials + (size_t)j0 * gridDim.x, gridDim.x);
 }
 
-__global__ void __launch_bounds__(256) gm_orth_kernel(KspState *s, int k, double *red_k, double *lhh,
-                                                      double *hh, int ld) {
-  if (s->inner_stop) return;
-  if (threadIdx.x != 0) return;
-  for (int j = 0; j <= k; ++j) {
-    if (not_finite(red_k[j])) { stop(s, R_DIVERGED_NANORINF); return; }
-    lhh[j] = -red_k[j];
-  }
-  for (int j = 0; j <= k; ++j) hh[(size_t)k * ld + j] = 0.0 - lhh[j];
-}
-
-// VecMAXPY_Seq grouping (first nv%4 vectors, then groups of four), then ||w||^2
+// KSPGMRESClassicalGramSchmidtOrthogonalization after the MDot: the
+// coefficients -h_j (h = w.v_j, folded and all-reduced), the Hessenberg
+// column (hh[k][j] = 0 - (-h_j)) and the non-finite check, evaluated by every
+// workgroup (workgroup 0 commits), then VecMAXPY_Seq's grouping (first nv%4
+// vectors, then groups of four) and ||w||^2, folded in-launch (fold.cnt) or
+// as plain partials
 __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
-                                                         const double *__restrict__ alpha,
-                                                         double *__restrict__ partials,
-                                                         const int *__restrict__ stop_flag) {
-  if (*stop_flag) return;
+                                                         KspState *__restrict__ s, const double *__restrict__ red_k,
+                                                         double *__restrict__ hh, int ld,
+                                                         double *__restrict__ partials, const Fold fold) {
+  if (s->inner_stop) return;
   __shared__ double a[MAX_RESTART + 1];
-  for (int j = threadIdx.x; j < nv; j += 256) a[j] = alpha[j];
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
   __syncthreads();
+  for (int j = threadIdx.x; j < nv; j += 256) {
+    const double h = red_k[j];
+    if (not_finite(h)) bad = 1;
+    a[j] = -h;                                   // lhh[j] = -h_j
+  }
+  __syncthreads();
+  if (bad) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) stop(s, R_DIVERGED_NANORINF);
+    return;
+  }
+  if (blockIdx.x == 0)
+    for (int j = threadIdx.x; j < nv; j += 256) hh[(size_t)(nv - 1) * ld + j] = 0.0 - a[j];
   const int rem = nv & 3;
   double v[1] = {0.0};
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -553,7 +560,7 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
     w[i] = u;
     v[0] += u * u;
   }
-  block_sum_to_partials<1>(v, partials, gridDim.x);
+  block_partials<1>(v, partials, gridDim.x, fold);
 }
 
 // normalise vv[k+1], happy breakdown, KSPGMRESUpdateHessenberg, convergence
@@ -1037,10 +1044,10 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   const size_t npart = (size_t)RED_BLOCKS * prow + (size_t)spmv_blocks(A) + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   const size_t k1 = (size_t)max_k + 1, k2 = (size_t)max_k + 2;
-  Carve cv(workspace(A, carve_size({nV, (size_t)ldv, nh, k2, k1, k1, k1, k2, npart, nhist})));
+  Carve cv(workspace(A, carve_size({nV, (size_t)ldv, nh, k2, k1, k1, k2, npart, nhist})));
   struct B { double *p; size_t n; };
   B V{cv.take(nV), nV}, tmat{cv.take(ldv), (size_t)ldv}, hh{cv.take(nh), nh}, grs{cv.take(k2), k2},
-      cc{cv.take(k1), k1}, ss{cv.take(k1), k1}, lhh{cv.take(k1), k1}, red{cv.take(k2), k2},
+      cc{cv.take(k1), k1}, ss{cv.take(k1), k1}, red{cv.take(k2), k2},
       part{cv.take(npart), npart}, hist{cv.take(nhist), nhist};
   HIPCHECK(hipMemsetAsync(hh.p, 0, sizeof(double) * hh.n, st));
   struct { KspState *p; } sd{state_buf(A)};
@@ -1072,6 +1079,8 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   }
   int first = 1, launched = 0;
   int *istop = &s->inner_stop;
+  Fold fnorm;                      // ||w||^2 of the MAXPY pass, folded in-launch into s->red[0]
+  fnorm.cnt = s->fold_upd; fnorm.out = sred; fnorm.ntotal = fnorm.ncount = RED_BLOCKS;
   while (true) {
     // KSPInitialResidual: vv0 = B (b - A x)
     if (first && !p.guess_nonzero) {
@@ -1094,10 +1103,10 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       mdot(st, n, vk1, V.p, ldv, k + 1, part.p, istop);
       finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, RED_BLOCKS, red.p, istop);
       c->allreduce_sum(red.p, k + 1);
-      gm_orth_kernel<<<1, 64, 0, st>>>(s, k, red.p, lhh.p, hh.p, ld);
-      maxpy_norm_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, lhh.p, part.p, istop);
-      if (!fused) { finish_reduce(part.p, RED_BLOCKS, 1, sred, st, istop); c->allreduce_sum(sred, 1); }
-      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, fused, hh.p, ld, grs.p, cc.p, ss.p, hist_d);
+      // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
+      maxpy_norm_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, hh.p, ld, part.p, fnorm);
+      c->allreduce_sum(sred, 1);
+      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d);
       scale_by_state_kernel<<<egrid, 256, 0, st>>>(n, s, vk1, k + 1);
       HIPCHECK(hipGetLastError());
       ++launched;
