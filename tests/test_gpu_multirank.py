@@ -284,3 +284,54 @@ def test_ranks_without_rows(oracle_mod, P, M):
         xs = np.concatenate([r[k][2] for r in res])
         assert all((r[k][0], r[k][1]) == (o[k]["its"], o[k]["reason"]) for r in res), (k, [r[k][:2] for r in res])
         assert np.linalg.norm(xs - o[k]["x"]) <= 1e-10 * np.linalg.norm(o[k]["x"])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_structures(oracle_mod, seed):
+    """Random rectangular-free square structures across random rank counts:
+    empty rows, rows with only ghost entries, dense rows, wide bandwidth,
+    duplicates and negative ids (CSR, INSERT/ADD) -- split, garray and MatMult
+    bit-exact against the oracle on every rank."""
+    from mxsolve.core import DMat
+    rng = np.random.default_rng(1000 + seed)
+    P = int(rng.integers(2, 7))
+    M = int(rng.integers(P, 700))
+    add = bool(seed & 1)
+    lens = rng.integers(0, 12, M)
+    lens[rng.random(M) < 0.1] = 0                              # empty rows
+    if seed % 3 == 0:
+        lens[rng.integers(0, M)] = min(3000, 4 * M)            # one very long row
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nnz = int(ip[-1])
+    rows = np.repeat(np.arange(M), lens)
+    band = int(rng.integers(1, M))
+    c = np.clip(rows + rng.integers(-band, band + 1, nnz), -2, M - 1).astype(np.int64)
+    ghost_rows = rng.random(M) < 0.05                          # rows whose entries are all far away
+    sel = ghost_rows[rows]
+    c[sel] = (rows[sel] + M // 2) % M
+    v = rng.standard_normal(nnz)
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P, add=add)
+    ranges = oracle_mod.split_ownership(M, P)
+    x = rng.standard_normal(M)
+    y_ref = O.mult(x)
+
+    def body(comm):
+        r = comm.rank
+        lip, lc, lv = local_csr(ip, c, v, ranges[r], ranges[r + 1])
+        A = DMat.from_csr(comm, M, M, lip, lc, lv, add=add)
+        sp = A.split()
+        xl = torch.from_numpy(x[ranges[r]:ranges[r + 1]].copy()).cuda()
+        yl = torch.zeros(ranges[r + 1] - ranges[r], dtype=torch.float64, device="cuda")
+        A.mult(xl, yl)
+        out = (sp, yl.cpu().numpy())
+        A.destroy()
+        return out
+
+    res = run_ranks(P, body)
+    for r, (sp, yl) in enumerate(res):
+        ob = O.block(r)
+        for k in ("dptr", "dcol", "optr", "ocol", "garray"):
+            assert np.array_equal(sp[k], ob[k]), (seed, P, r, k)
+        for k in ("dval", "oval"):
+            assert np.array_equal(sp[k].view(np.uint64), ob[k].view(np.uint64)), (seed, P, r, k)
+        assert np.array_equal(yl.view(np.uint64), y_ref[ranges[r]:ranges[r + 1]].view(np.uint64)), (seed, P, r)
