@@ -335,3 +335,47 @@ def test_random_structures(oracle_mod, seed):
         for k in ("dval", "oval"):
             assert np.array_equal(sp[k].view(np.uint64), ob[k].view(np.uint64)), (seed, P, r, k)
         assert np.array_equal(yl.view(np.uint64), y_ref[ranges[r]:ranges[r + 1]].view(np.uint64)), (seed, P, r)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_ksp(oracle_mod, seed):
+    """Random diagonally dominant systems (SPD for CG, nonsymmetric for GMRES),
+    random rank counts and Jacobi on/off: iterations, reason and solution
+    (rel-L2 1e-10) against the oracle."""
+    from mxsolve.core import DMat
+    rng = np.random.default_rng(2000 + seed)
+    P = int(rng.integers(1, 6))
+    M = int(rng.integers(50, 900))
+    ksp = "cg" if seed % 2 == 0 else "gmres"
+    pc = "jacobi" if seed % 3 else "none"
+    k = 6
+    r = rng.integers(0, M, M * k)
+    cc = rng.integers(0, M, M * k)
+    vals = rng.uniform(-1, 1, M * k)
+    A = np.zeros((M, M))
+    np.add.at(A, (r, cc), vals)
+    if ksp == "cg":
+        A = A + A.T
+    A[np.arange(M), np.arange(M)] = np.abs(A).sum(1) + rng.uniform(0.5, 2.0, M)
+    ip = np.concatenate([[0], np.cumsum((A != 0).sum(1))]).astype(np.int64)
+    c = np.nonzero(A)[1].astype(np.int64)
+    v = A[A != 0]
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+    b = rng.standard_normal(M)
+    o = O.solve(b, ksp=ksp, pc=pc, rtol=1e-9)
+    ranges = oracle_mod.split_ownership(M, P)
+
+    def body(comm):
+        q = comm.rank
+        lip, lc, lv = local_csr(ip, c, v, ranges[q], ranges[q + 1])
+        Am = DMat.from_csr(comm, M, M, lip, lc, lv)
+        bl = torch.from_numpy(b[ranges[q]:ranges[q + 1]].copy()).cuda()
+        x = torch.zeros(ranges[q + 1] - ranges[q], dtype=torch.float64, device="cuda")
+        rr = Am.solve(bl, x, ksp=ksp, pc=pc, rtol=1e-9)
+        Am.destroy()
+        return rr["its"], rr["reason"], x.cpu().numpy()
+
+    res = run_ranks(P, body)
+    xs = np.concatenate([t[2] for t in res])
+    assert all((t[0], t[1]) == (o["its"], o["reason"]) for t in res), ([t[:2] for t in res], o["its"], o["reason"])
+    assert np.linalg.norm(xs - o["x"]) <= REL_TOL * np.linalg.norm(o["x"])
