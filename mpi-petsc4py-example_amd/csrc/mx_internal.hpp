@@ -206,7 +206,12 @@ __device__ __forceinline__ double papply(const Jac &J, double r, int64_t i) {
 }
 
 // SpMV (mx_spmv.hip)
-enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2, SPMV_CG = 3 };
+enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2, SPMV_CG = 3,
+                // the operand is s * x with s = *xscale: a GMRES basis vector kept
+                // unnormalised (VecScale applied at every read, the same bits)
+                SPMV_PLAIN_S = 4, SPMV_JACOBI_S = 5 };
+constexpr bool spmv_jac(int mode) { return mode == SPMV_JACOBI || mode == SPMV_JACOBI_S; }
+constexpr bool spmv_scaled(int mode) { return mode == SPMV_PLAIN_S || mode == SPMV_JACOBI_S; }
 // SPMV_CG: the CG direction update and the deferred solution update ride in
 // the MatMult.  The operand is p_i = z + b p_{i-1} (z = jac(r), i == 0: p = z),
 // formed on the fly wherever the product reads it and stored once for the
@@ -231,7 +236,8 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *
 // returns the number of partials written (DOT / CG mode).  fold != null: the
 // p.w partials are folded into fold->out inside the launch(es).
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                    int *done_flag, const CgFuse *cg = nullptr, const Fold *fold = nullptr);
+                    int *done_flag, const CgFuse *cg = nullptr, const Fold *fold = nullptr,
+                    const double *xscale = nullptr);
 int spmv_blocks(const Mat *A, int mode = SPMV_PLAIN);
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)

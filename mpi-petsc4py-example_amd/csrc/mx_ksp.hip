@@ -467,12 +467,14 @@ __global__ void __launch_bounds__(256) sumsq_kernel(int64_t n, const double *__r
 
 // cycle start: VecNormalize(vv0), restart consistency check, convergence test
 __global__ void __launch_bounds__(256) gm_start_kernel(KspState *s, const double *partials, int nblocks,
-                                                       int fused, double *grs, double *hist, double snorm) {
+                                                       int fused, double *grs, double *hist, double snorm,
+                                                       double *vscale) {
   if (!gather_red<1>(s, partials, nblocks, fused)) return;
   const double res = sqrt(s->red[0]);
   s->it = 0;
   s->res = res;
   s->scale = res != 0.0 ? 1.0 / res : 1.0;
+  vscale[0] = s->scale;       // VecNormalize(vv0), applied where vv0 is read
   if (not_finite(res)) { stop(s, R_DIVERGED_NANORINF); return; }
   if (s->ksp_rnorm > 0.0 && fabs(res - s->ksp_rnorm) > s->breakdowntol * s->gm_rnorm0) {
     stop(s, R_DIVERGED_BREAKDOWN); return;
@@ -487,32 +489,28 @@ __global__ void __launch_bounds__(256) gm_start_kernel(KspState *s, const double
   s->inner_stop = (s->its >= s->top.max_it) ? 1 : 0;
 }
 
-__global__ void scale_by_state_kernel(int64_t n, const KspState *__restrict__ s, double *__restrict__ x,
-                                      int expect_it) {
-  if (s->top.done && expect_it < 0) return;
-  if (expect_it >= 0 && s->it != expect_it) return;
-  if (s->res == 0.0 && expect_it < 0) return;
-  const double a = s->scale;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = a * x[i];
-}
-
 // VecMDot: h_j = w . v_j for j in [j0, j0 + nv), nv <= NV, one pass over w
 // (restart 30: every step's k+1 dots in one launch)
+// The basis vectors are stored unnormalised: v_j = vscale[j] * V_j, applied
+// at every read (fl(a * x), the bits VecScale would have stored)
 template <int NV>
 __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__restrict__ w,
                                                    const double *__restrict__ V, int64_t ldv, int j0, int nv,
+                                                   const double *__restrict__ vscale,
                                                    double *__restrict__ partials, const int *__restrict__ stop_flag) {
   if (*stop_flag) return;
-  double acc[NV];
+  double acc[NV], sc[NV];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) acc[k] = 0.0;
+  for (int k = 0; k < NV; ++k) {
+    acc[k] = 0.0;
+    sc[k] = k < nv ? vscale[j0 + k] : 0.0;
+  }
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const double wi = w[i];
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-      if (k < nv) acc[k] += wi * V[(int64_t)(j0 + k) * ldv + i];
+      if (k < nv) acc[k] += wi * (sc[k] * V[(int64_t)(j0 + k) * ldv + i]);
   }
   block_sum_to_partials<NV>(acc, partials + (size_t)j0 * gridDim.x, gridDim.x);
 }
@@ -526,10 +524,11 @@ __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__re
 __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
                                                          KspState *__restrict__ s, const double *__restrict__ red_k,
+                                                         const double *__restrict__ vscale,
                                                          double *__restrict__ hh, int ld,
                                                          double *__restrict__ partials, const Fold fold) {
   if (s->inner_stop) return;
-  __shared__ double a[MAX_RESTART + 1];
+  __shared__ double a[MAX_RESTART + 1], sc[MAX_RESTART + 1];
   __shared__ int bad;
   if (threadIdx.x == 0) bad = 0;
   __syncthreads();
@@ -537,6 +536,7 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
     const double h = red_k[j];
     if (not_finite(h)) bad = 1;
     a[j] = -h;                                   // lhh[j] = -h_j
+    sc[j] = vscale[j];
   }
   __syncthreads();
   if (bad) {
@@ -551,12 +551,12 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     double u = w[i];
     int j = 0;
-    if (rem == 1) { u = a[0] * V[i] + u; j = 1; }
-    else if (rem == 2) { u = u + (a[0] * V[i] + a[1] * V[ldv + i]); j = 2; }
-    else if (rem == 3) { u = u + ((a[0] * V[i] + a[1] * V[ldv + i]) + a[2] * V[2 * ldv + i]); j = 3; }
+    auto vj = [&](int j) { return sc[j] * V[(int64_t)j * ldv + i]; };
+    if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
+    else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
+    else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
     for (; j < nv; j += 4)
-      u = u + (((a[j] * V[(int64_t)j * ldv + i] + a[j + 1] * V[(int64_t)(j + 1) * ldv + i]) +
-                a[j + 2] * V[(int64_t)(j + 2) * ldv + i]) + a[j + 3] * V[(int64_t)(j + 3) * ldv + i]);
+      u = u + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
     w[i] = u;
     v[0] += u * u;
   }
@@ -566,11 +566,12 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
 // normalise vv[k+1], happy breakdown, KSPGMRESUpdateHessenberg, convergence
 __global__ void __launch_bounds__(256) gm_step_kernel(KspState *s, int k, const double *partials, int nblocks,
                                                       int fused, double *hh, int ld, double *grs, double *cc,
-                                                      double *ss, double *hist) {
+                                                      double *ss, double *hist, double *vscale) {
   if (s->inner_stop) return;
   if (!gather_red<1>(s, partials, nblocks, fused)) return;
   const double tt = sqrt(s->red[0]);
   s->scale = tt != 0.0 ? 1.0 / tt : 1.0;
+  vscale[k + 1] = s->scale;   // VecScale(vv[k+1], 1/tt), applied where it is read
   if (not_finite(tt)) { stop(s, R_DIVERGED_NANORINF); return; }
   double *h = hh + (size_t)k * ld;   // column k
   h[k + 1] = tt;
@@ -599,7 +600,7 @@ __global__ void __launch_bounds__(256) gm_step_kernel(KspState *s, int k, const 
   s->it = k + 1;
   s->its += 1;
   s->ksp_rnorm = res;
-  s->res = tt;          // the scale kernel reads s->scale; res kept nonzero for it
+  s->res = tt;
   if (hist) hist[s->its] = res;
   int reason = dev_converged(s, s->its, res, true, 0.0);
   if (hapend && !reason) reason = R_DIVERGED_BREAKDOWN;
@@ -631,23 +632,27 @@ __global__ void gm_buildsoln_kernel(KspState *s, const double *hh, int ld, doubl
 // x += sum_j nrs_j v_j  (VecMAXPY from zero, then VecAXPY(x, 1, TEMP))
 __global__ void __launch_bounds__(256) gm_update_x_kernel(int64_t n, const KspState *__restrict__ s,
                                                           const double *__restrict__ V, int64_t ldv,
+                                                          const double *__restrict__ vscale,
                                                           const double *__restrict__ nrs, double *__restrict__ x) {
   const int nv = s->nv;
   if (nv == 0) return;
-  __shared__ double a[MAX_RESTART + 1];
-  for (int j = threadIdx.x; j < nv; j += 256) a[j] = nrs[j];
+  __shared__ double a[MAX_RESTART + 1], sc[MAX_RESTART + 1];
+  for (int j = threadIdx.x; j < nv; j += 256) {
+    a[j] = nrs[j];
+    sc[j] = vscale[j];
+  }
   __syncthreads();
   const int rem = nv & 3;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     double u = 0.0;
     int j = 0;
-    if (rem == 1) { u = a[0] * V[i] + u; j = 1; }
-    else if (rem == 2) { u = u + (a[0] * V[i] + a[1] * V[ldv + i]); j = 2; }
-    else if (rem == 3) { u = u + ((a[0] * V[i] + a[1] * V[ldv + i]) + a[2] * V[2 * ldv + i]); j = 3; }
+    auto vj = [&](int j) { return sc[j] * V[(int64_t)j * ldv + i]; };
+    if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
+    else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
+    else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
     for (; j < nv; j += 4)
-      u = u + (((a[j] * V[(int64_t)j * ldv + i] + a[j + 1] * V[(int64_t)(j + 1) * ldv + i]) +
-                a[j + 2] * V[(int64_t)(j + 2) * ldv + i]) + a[j + 3] * V[(int64_t)(j + 3) * ldv + i]);
+      u = u + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
     x[i] = fma(1.0, u, x[i]);
   }
 }
@@ -1002,22 +1007,22 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
 
 template <int NV>
 static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int j0, int k,
-                        double *partials, const int *stop_flag) {
-  mdot_kernel<NV><<<RED_BLOCKS, 256, 0, st>>>(n, w, V, ldv, j0, k, partials, stop_flag);
+                        const double *vscale, double *partials, const int *stop_flag) {
+  mdot_kernel<NV><<<RED_BLOCKS, 256, 0, st>>>(n, w, V, ldv, j0, k, vscale, partials, stop_flag);
 }
 
 // partials rows [j0, j0 + NV) are written (rows >= nv with zeros): the
 // buffer holds max_k + 2 rows rounded up to 32; groups are gw wide (knob 16)
 static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
-                 double *partials, const int *stop_flag) {
+                 const double *vscale, double *partials, const int *stop_flag) {
   const int gw = g_knobs.mdot_group == 16 || g_knobs.mdot_group == 32 || g_knobs.mdot_group == 4 ? g_knobs.mdot_group : 8;
   for (int j0 = 0; j0 < nv; j0 += gw) {
     const int k = std::min(gw, nv - j0);
-    if (k <= 2) launch_mdot<2>(st, n, w, V, ldv, j0, k, partials, stop_flag);
-    else if (k <= 4) launch_mdot<4>(st, n, w, V, ldv, j0, k, partials, stop_flag);
-    else if (k <= 8) launch_mdot<8>(st, n, w, V, ldv, j0, k, partials, stop_flag);
-    else if (k <= 16) launch_mdot<16>(st, n, w, V, ldv, j0, k, partials, stop_flag);
-    else launch_mdot<32>(st, n, w, V, ldv, j0, k, partials, stop_flag);
+    if (k <= 2) launch_mdot<2>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
+    else if (k <= 4) launch_mdot<4>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
+    else if (k <= 8) launch_mdot<8>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
+    else if (k <= 16) launch_mdot<16>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
+    else launch_mdot<32>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
     HIPCHECK(hipGetLastError());
   }
 }
@@ -1044,11 +1049,12 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   const size_t npart = (size_t)RED_BLOCKS * prow + (size_t)spmv_blocks(A) + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   const size_t k1 = (size_t)max_k + 1, k2 = (size_t)max_k + 2;
-  Carve cv(workspace(A, carve_size({nV, (size_t)ldv, nh, k2, k1, k1, k2, npart, nhist})));
+  Carve cv(workspace(A, carve_size({nV, (size_t)ldv, nh, k2, k1, k1, k2, k2, npart, nhist})));
   struct B { double *p; size_t n; };
   B V{cv.take(nV), nV}, tmat{cv.take(ldv), (size_t)ldv}, hh{cv.take(nh), nh}, grs{cv.take(k2), k2},
-      cc{cv.take(k1), k1}, ss{cv.take(k1), k1}, red{cv.take(k2), k2},
+      cc{cv.take(k1), k1}, ss{cv.take(k1), k1}, red{cv.take(k2), k2}, vsc{cv.take(k2), k2},
       part{cv.take(npart), npart}, hist{cv.take(nhist), nhist};
+  vec_set(st, (int64_t)vsc.n, 1.0, vsc.p);
   HIPCHECK(hipMemsetAsync(hh.p, 0, sizeof(double) * hh.n, st));
   struct { KspState *p; } sd{state_buf(A)};
   KspState hs;
@@ -1091,28 +1097,27 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
     }
     sumsq_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, V.p, part.p, nullptr);
     if (!fused) { finish_reduce(part.p, RED_BLOCKS, 1, sred, st); c->allreduce_sum(sred, 1); }
-    gm_start_kernel<<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, grs.p, hist_d, first ? snorm : 0.0);
-    scale_by_state_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, -1);
+    gm_start_kernel<<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, grs.p, hist_d, first ? snorm : 0.0, vsc.p);
     HIPCHECK(hipGetLastError());
     first = 0;
     for (int k = 0; k < max_k; ++k) {
       double *vk = V.p + (int64_t)k * ldv, *vk1 = V.p + (int64_t)(k + 1) * ldv;
       timer.begin();
-      matmult_overlap(A, vk, vk1, dinv.mode ? SPMV_JACOBI : SPMV_PLAIN, dinv, nullptr, istop);
+      matmult_overlap(A, vk, vk1, dinv.mode ? SPMV_JACOBI_S : SPMV_PLAIN_S, dinv, nullptr, istop, nullptr,
+                      nullptr, vsc.p + k);
       timer.end();
-      mdot(st, n, vk1, V.p, ldv, k + 1, part.p, istop);
+      mdot(st, n, vk1, V.p, ldv, k + 1, vsc.p, part.p, istop);
       finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, RED_BLOCKS, red.p, istop);
       c->allreduce_sum(red.p, k + 1);
       // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
-      maxpy_norm_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, hh.p, ld, part.p, fnorm);
+      maxpy_norm_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
       c->allreduce_sum(sred, 1);
-      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d);
-      scale_by_state_kernel<<<egrid, 256, 0, st>>>(n, s, vk1, k + 1);
+      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p);
       HIPCHECK(hipGetLastError());
       ++launched;
     }
     gm_buildsoln_kernel<<<1, 64, 0, st>>>(s, hh.p, ld, grs.p);
-    gm_update_x_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, ldv, grs.p, x);
+    gm_update_x_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, ldv, vsc.p, grs.p, x);
     gm_cycle_end_kernel<<<1, 64, 0, st>>>(s);
     HIPCHECK(hipGetLastError());
     read_state(st, s, hs);

@@ -44,11 +44,16 @@ template <bool NT, class T> __device__ __forceinline__ T ld(const T *p) {
 // store -- yields the same bits as a separate update pass would.
 // at(base, lane) = value at base + lane for a wave-uniform base: the address
 // is one SGPR pair plus the lane's fixed byte offset, shared by every gather
-struct XPlain {
+template <bool S = false>
+struct XPlainT {
   const double *__restrict__ x;
-  __device__ __forceinline__ double operator()(int64_t j) const { return x[j]; }
-  __device__ __forceinline__ double at(int64_t base, int lane) const { return (x + base)[lane]; }
+  double s = 1.0;             // S: the operand is fl(s * x[j]) (a lazily normalised vector)
+  __device__ __forceinline__ double operator()(int64_t j) const { return S ? s * x[j] : x[j]; }
+  __device__ __forceinline__ double at(int64_t base, int lane) const {
+    return S ? s * (x + base)[lane] : (x + base)[lane];
+  }
 };
+using XPlain = XPlainT<false>;
 // JM = the Jacobi form, compile-time so every load is unconditional (a
 // runtime form turns each gather into a branch around the dinv load)
 template <int JM>
@@ -205,7 +210,8 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o,
     const double *__restrict__ val_o, const double *__restrict__ x,
     const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
-    double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold) {
+    double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
+    const double *__restrict__ xscale) {
   CgTopIn top;
   if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
   else if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
@@ -225,7 +231,9 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     send = (int)nslices;
   }
   // operand source
-  using XS = typename std::conditional<MODE == SPMV_CG, XCg<JM>, XPlain>::type;
+  constexpr bool SC = spmv_scaled(MODE);
+  using XS = typename std::conditional<MODE == SPMV_CG, XCg<JM>, XPlainT<SC>>::type;
+  const double xs = SC ? *xscale : 1.0;
   XS X;
   double xa = 0.0;
   bool xpend = false;
@@ -239,7 +247,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     xa = top.xa;
     xpend = top.xpend != 0.0;
   } else {
-    X = XPlain{x};
+    X = XPlainT<SC>{x, xs};
   }
   double dot = 0.0;
   for (int s = s0; s < send; s += sstep) {
@@ -290,10 +298,10 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       }
     } else if (lvec) {
       const int wo = wid_o[s];
-      if (wo) sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wo, sum, XPlain{lvec}, lane);
+      if (wo) sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wo, sum, XPlainT<SC>{lvec, xs}, lane);
     }
     if (row < m) {
-      if (MODE == SPMV_JACOBI) y[row] = papply(jac, sum, row);   // PCApply_Jacobi fused: w_i * d_i
+      if (spmv_jac(MODE)) y[row] = papply(jac, sum, row);   // PCApply_Jacobi fused: w_i * d_i
       else y[row] = sum;
       if (MODE == SPMV_DOT) dot += x[row] * sum;           // VecDot(p, w) partial, p = x
       if (MODE == SPMV_CG) dot += xr * sum;
@@ -325,8 +333,11 @@ __global__ void __launch_bounds__(256) spmv_boundary_kernel(
     int64_t m, const int32_t *__restrict__ list, int nlist, const int64_t *__restrict__ sptr_o,
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o, const double *__restrict__ val_o,
     const double *__restrict__ x, const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
-    double *__restrict__ partials, const int *__restrict__ done, const Fold fold) {
+    double *__restrict__ partials, const int *__restrict__ done, const Fold fold,
+    const double *__restrict__ xscale) {
   if (done && *done) return;
+  constexpr bool SC = spmv_scaled(MODE);
+  const double xs = SC ? *xscale : 1.0;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double dot = 0.0;
@@ -334,9 +345,9 @@ __global__ void __launch_bounds__(256) spmv_boundary_kernel(
     const int s = list[k];
     const int64_t row = (int64_t)s * SLICE + lane;
     double sum = row < m ? y[row] : 0.0;
-    sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wid_o[s], sum, XPlain{lvec}, lane);
+    sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wid_o[s], sum, XPlainT<SC>{lvec, xs}, lane);
     if (row < m) {
-      if (MODE == SPMV_JACOBI) y[row] = papply(jac, sum, row);
+      if (spmv_jac(MODE)) y[row] = papply(jac, sum, row);
       else y[row] = sum;
       if (MODE == SPMV_DOT) dot += x[row] * sum;
     }
@@ -397,7 +408,8 @@ void halo_begin(Mat *A, const double *x) {
 }
 
 static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold) {
+                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold,
+                        const double *xscale) {
   const unsigned grid = (unsigned)spmv_blocks(A, mode);
   const double *lvec = (A->nghost && !split) ? A->halo.lvec.p : nullptr;
   const int kd = A->sd.dia_k;
@@ -405,7 +417,7 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
 #define SPMV_ARGS                                                                           \
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
-      partials, done_flag, cg, fold
+      partials, done_flag, cg, fold, xscale
 #define SPMV_KD(MODE, NT, SP)                                                                    \
   do {                                                                                           \
     switch (kd) {                                                                                \
@@ -432,6 +444,8 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
   switch (mode) {
     case SPMV_PLAIN: SPMV_GO(SPMV_PLAIN); break;
     case SPMV_JACOBI: SPMV_GO(SPMV_JACOBI); break;
+    case SPMV_PLAIN_S: SPMV_GO(SPMV_PLAIN_S); break;
+    case SPMV_JACOBI_S: SPMV_GO(SPMV_JACOBI_S); break;
     case SPMV_DOT: SPMV_GO(SPMV_DOT); break;
     case SPMV_CG:   // always non-temporal; Jacobi form as a template argument
       if (!cgp) fail(MX_ERR_INTERNAL, "CG-fused SpMV without operands");
@@ -452,7 +466,7 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
 
 void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                  int *done_flag) {
-  launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream, nullptr, Fold{});
+  launch_main(A, x, y, mode, jac, partials, done_flag, false, A->comm->stream, nullptr, Fold{}, nullptr);
 }
 
 constexpr int BND_BLOCKS = 2048;   // one boundary slice per wave: the launch runs after the interior, alone on the GPU
@@ -460,7 +474,7 @@ constexpr int BND_BLOCKS = 2048;   // one boundary slice per wave: the launch ru
 bool matmult_splits(const Mat *A) { return A->comm->size > 1 && A->halo.nbnd > 0 && g_knobs.overlap; }
 
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                    int *done_flag, const CgFuse *cg, const Fold *fold) {
+                    int *done_flag, const CgFuse *cg, const Fold *fold, const double *xscale) {
   Comm *c = A->comm;
   Halo &H = A->halo;
   hipStream_t st = c->stream;
@@ -469,7 +483,7 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
     if (c->size > 1) halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, st);
     Fold f;
     if (fold) { f = *fold; f.ntotal = nmain; f.base = 0; f.ncount = nmain; }
-    launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg, f);
+    launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg, f, xscale);
     return nmain;
   }
   hipStream_t cs = c->comm_stream;
@@ -484,7 +498,7 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
   halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, cs);
   HIPCHECK(hipEventRecord(H.ev_done, cs));
   // interior slices meanwhile; boundary slices after the exchange
-  launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{});
+  launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{}, xscale);
   HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
   const int nb = std::min(g_knobs.bnd_grid > 0 ? g_knobs.bnd_grid : BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
   // the boundary launch folds the partials of both launches (fold) or
@@ -495,10 +509,12 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
   // the boundary rows' operand values were stored by the main kernel (CG)
   const double *xb = mode == SPMV_CG ? cg->pnew : x;
 #define BND(MODE) spmv_boundary_kernel<MODE><<<nb, 256, 0, st>>>(A->m, H.bnd_slices.p, H.nbnd, A->so.sptr.p, \
-      A->so.width.p, A->so.col.p, A->so.val.p, xb, H.lvec.p, y, jac, pb, done_flag, f)
+      A->so.width.p, A->so.col.p, A->so.val.p, xb, H.lvec.p, y, jac, pb, done_flag, f, xscale)
   switch (mode) {
     case SPMV_PLAIN: BND(SPMV_PLAIN); break;
     case SPMV_JACOBI: BND(SPMV_JACOBI); break;
+    case SPMV_PLAIN_S: BND(SPMV_PLAIN_S); break;
+    case SPMV_JACOBI_S: BND(SPMV_JACOBI_S); break;
     default: BND(SPMV_DOT); break;
   }
 #undef BND
