@@ -85,6 +85,9 @@ typedef struct {
   int nsend_peers, nrecv_peers;       /* halo neighbours                              */
   int64_t nsend, nrecv;               /* halo values per MatMult                      */
   int64_t dia_slices;                 /* A_d slices stored with aligned offsets       */
+  int64_t value_codes;                /* A_d values as 1-byte codes into a table of this
+                                         many distinct values (0: stored as fp64)       */
+  int64_t code_bytes;                 /* bytes of those codes                         */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */

@@ -235,6 +235,8 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->nrecv_peers = (int)A->halo.recv_peer.size();
     info->nsend = A->halo.nsend; info->nrecv = A->halo.nrecv;
     info->dia_slices = A->sd.dia_slices;
+    info->value_codes = A->sd.ntab;
+    info->code_bytes = A->sd.code_bytes;
   });
 }
 
@@ -437,7 +439,7 @@ int mx_debug_set(int key, int value) {
   int old = -1;
   switch (key) {
     case 1: old = g_knobs.spmv_nt; g_knobs.spmv_nt = value; break;
-    case 3: old = g_knobs.spmv_grid; if (value > 0) g_knobs.spmv_grid = value; break;
+    case 3: old = g_knobs.spmv_grid; if (value >= 0) g_knobs.spmv_grid = value; break;   // 0: resident grid
     case 4: old = g_knobs.dia; g_knobs.dia = value; break;
     case 5: old = g_knobs.jac_const; g_knobs.jac_const = value; break;
     case 6: old = g_knobs.overlap; g_knobs.overlap = value; break;
@@ -455,6 +457,10 @@ int mx_debug_set(int key, int value) {
     case 19: old = g_knobs.mask8; g_knobs.mask8 = value; break;
     case 21: old = g_knobs.cg_unroll; g_knobs.cg_unroll = value; break;
     case 22: old = g_knobs.cg_upd_grid; g_knobs.cg_upd_grid = std::min(value, 65536); break;
+    case 23: old = g_knobs.vcodes; g_knobs.vcodes = value; break;
+    case 24: old = g_knobs.spmv_unroll; g_knobs.spmv_unroll = value; break;
+    case 25: old = g_knobs.spmv_ynt; g_knobs.spmv_ynt = value; break;
+    case 26: old = g_knobs.spmv_bpc; g_knobs.spmv_bpc = value; break;
     default: break;
   }
   return old;

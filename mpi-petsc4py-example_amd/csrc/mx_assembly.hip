@@ -28,6 +28,8 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
+#include <unordered_map>
 
 #include "mx_internal.hpp"
 
@@ -630,8 +632,267 @@ __global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
   }
 }
 
-static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *col, const double *val,
-                       hipStream_t st, bool allow_dia) {
+// ---------------------------------------------------------------- offset patterns
+// The aligned-offset slices of a stencil share a handful of offset lists.
+// SpMV reads a slice's list right after its width, on the dependent path to
+// the gathers; one list per slice (128 B each) missed in the caches on every
+// slice, a shared table stays resident.  Slices are grouped by a hash of the
+// list, and every slice is checked against its group's list (any mismatch
+// keeps the per-slice lists).
+__global__ void dia_hash_kernel(int64_t ns, const int32_t *__restrict__ width, const int32_t *__restrict__ doff,
+                                unsigned long long *__restrict__ h) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= ns) return;
+  const int w = width[s];
+  unsigned long long x = 0xcbf29ce484222325ULL ^ (unsigned long long)(uint32_t)w;
+  if (w < 0)
+    for (int j = 0; j < -w; ++j) x = (x ^ (unsigned long long)(uint32_t)doff[s * DIA_MAX + j]) * 0x100000001b3ULL;
+  h[s] = w < 0 ? x : 0ULL;
+}
+
+__global__ void dia_pattern_gather_kernel(int npat, const int64_t *__restrict__ rep, const int32_t *__restrict__ doff,
+                                          int32_t *__restrict__ ptab) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)npat * DIA_MAX) return;
+  ptab[i] = doff[rep[i / DIA_MAX] * DIA_MAX + i % DIA_MAX];
+}
+
+__global__ void dia_pattern_check_kernel(int64_t ns, const int32_t *__restrict__ width, const int32_t *__restrict__ doff,
+                                         const int32_t *__restrict__ dpat, const int32_t *__restrict__ ptab,
+                                         int *__restrict__ bad) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= ns || width[s] >= 0) return;
+  for (int j = 0; j < -width[s]; ++j)
+    if (doff[s * DIA_MAX + j] != ptab[(int64_t)dpat[s] * DIA_MAX + j]) *bad = 1;
+}
+
+// bit DPAT_INB of dpat[s]: every gather of the slice (rows 64 s .. 64 s + 63,
+// present or not) lies inside the operand, so SpMV takes the unguarded body
+// without scanning the offsets
+__global__ void dia_inb_kernel(int64_t ns, int64_t ncols, const int32_t *__restrict__ width,
+                               const int32_t *__restrict__ ptab, int32_t *__restrict__ dpat) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= ns || width[s] >= 0) return;
+  const int32_t *off = ptab + (int64_t)dpat[s] * DIA_MAX;
+  int omin = off[0], omax = off[0];
+  for (int j = 1; j < -width[s]; ++j) { omin = min(omin, off[j]); omax = max(omax, off[j]); }
+  const int64_t srow = s * SLICE;
+  if (srow + omin >= 0 && srow + (SLICE - 1) + omax < ncols) dpat[s] |= DPAT_INB;
+}
+
+static void share_offset_patterns(Sell &S, const std::vector<int32_t> &wh, int64_t ncols, hipStream_t st) {
+  const int64_t ns = S.nslices;
+  S.dpat.alloc((size_t)ns);
+  std::vector<int32_t> pat((size_t)ns);
+  for (int64_t s = 0; s < ns; ++s) pat[s] = (int32_t)s;        // fallback: one list per slice
+  S.npat = ns;
+  {
+    DBuf<unsigned long long> hd((size_t)ns);
+    dia_hash_kernel<<<(unsigned)cdiv(ns, 256), 256, 0, st>>>(ns, S.width.p, S.doff.p, hd.p);
+    HIPCHECK(hipGetLastError());
+    std::vector<unsigned long long> hh((size_t)ns);
+    HIPCHECK(hipMemcpyAsync(hh.data(), hd.p, sizeof(unsigned long long) * ns, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    std::unordered_map<unsigned long long, int32_t> id;
+    std::vector<int64_t> rep;
+    std::vector<int32_t> p2((size_t)ns, 0);
+    unsigned long long last = 0;
+    int32_t last_id = -1;
+    for (int64_t s = 0; s < ns; ++s) {
+      if (wh[s] >= 0) continue;
+      if (last_id >= 0 && hh[s] == last) { p2[s] = last_id; continue; }
+      auto it = id.find(hh[s]);
+      if (it == id.end()) {
+        it = id.emplace(hh[s], (int32_t)rep.size()).first;
+        rep.push_back(s);
+      }
+      p2[s] = last_id = it->second;
+      last = hh[s];
+    }
+    if ((int64_t)rep.size() * 4 < ns) {
+      const int npat = (int)rep.size();
+      DBuf<int64_t> rd((size_t)npat);
+      DBuf<int32_t> ptab((size_t)npat * DIA_MAX);
+      DBuf<int> bad(1);
+      HIPCHECK(hipMemcpyAsync(rd.p, rep.data(), sizeof(int64_t) * npat, hipMemcpyHostToDevice, st));
+      HIPCHECK(hipMemcpyAsync(S.dpat.p, p2.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, st));
+      HIPCHECK(hipMemsetAsync(bad.p, 0, sizeof(int), st));
+      dia_pattern_gather_kernel<<<(unsigned)cdiv((int64_t)npat * DIA_MAX, 256), 256, 0, st>>>(npat, rd.p, S.doff.p,
+                                                                                                ptab.p);
+      dia_pattern_check_kernel<<<(unsigned)cdiv(ns, 256), 256, 0, st>>>(ns, S.width.p, S.doff.p, S.dpat.p, ptab.p,
+                                                                        bad.p);
+      HIPCHECK(hipGetLastError());
+      int hb = 0;
+      HIPCHECK(hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      if (!hb) {
+        S.doff = std::move(ptab);
+        S.npat = npat;
+        dia_inb_kernel<<<(unsigned)cdiv(ns, 256), 256, 0, st>>>(ns, ncols, S.width.p, S.doff.p, S.dpat.p);
+        HIPCHECK(hipGetLastError());
+        return;
+      }
+    }
+  }
+  HIPCHECK(hipMemcpyAsync(S.dpat.p, pat.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, st));
+  dia_inb_kernel<<<(unsigned)cdiv(ns, 256), 256, 0, st>>>(ns, ncols, S.width.p, S.doff.p, S.dpat.p);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(st));
+}
+
+// ---------------------------------------------------------------- value codes
+// A stencil or FEM block with few distinct coefficients streams one byte per
+// slot instead of eight: the distinct values (bit patterns) are collected in
+// an open-addressing table, and when there are at most VCODE_MAX of them every
+// slot stores its value's index.  SpMV reads the table from LDS, so the
+// product uses the very same doubles (bitwise results unchanged).
+constexpr int VDICT_SLOTS = 4096;
+constexpr unsigned long long VDICT_EMPTY = 0x7ff8dead5eed1e55ULL;   // a NaN payload; never a key
+
+__device__ __forceinline__ unsigned vdict_hash(unsigned long long k) {
+  return (unsigned)((k * 0x9E3779B97F4A7C15ULL) >> 52);   // 12 bits
+}
+
+__device__ __forceinline__ int vdict_find(const unsigned long long *__restrict__ tab, unsigned long long k) {
+  unsigned h = vdict_hash(k);
+  for (int probe = 0; probe < VDICT_SLOTS; ++probe) {
+    const unsigned long long c = tab[h];
+    if (c == k) return (int)h;
+    if (c == VDICT_EMPTY) return -1;
+    h = (h + 1) & (VDICT_SLOTS - 1);
+  }
+  return -1;
+}
+
+// one wave per slice, the slots a row stores (absent aligned-offset slots
+// and padding skipped).  st[0] = distinct values inserted, st[1] = overflow
+// (too many, or a value with the empty pattern).  A plain read that sees
+// EMPTY falls through to the CAS, which returns the slot's real content; keys
+// never leave a slot.
+__device__ __forceinline__ bool vdict_insert(unsigned long long *tab, int *st, unsigned long long k) {
+  if (k == VDICT_EMPTY) return false;
+  unsigned h = vdict_hash(k);
+  for (int probe = 0; probe < 64; ++probe) {
+    unsigned long long c = tab[h];
+    if (c == VDICT_EMPTY) {
+      c = atomicCAS(tab + h, VDICT_EMPTY, k);
+      if (c == VDICT_EMPTY) return atomicAdd(st, 1) < VCODE_ABSENT;
+    }
+    if (c == k) return true;
+    h = (h + 1) & (VDICT_SLOTS - 1);
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool slot_stored(int wr, uint32_t mk, const int32_t *__restrict__ col, int64_t t, int j) {
+  return wr < 0 ? ((mk >> j) & 1u) != 0 : col[t] >= 0;
+}
+
+__global__ void vdict_insert_kernel(int64_t ns, const int64_t *__restrict__ sptr, const int32_t *__restrict__ width,
+                                    const int32_t *__restrict__ col, const double *__restrict__ sval,
+                                    const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8,
+                                    unsigned long long *tab, int *st) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= ns || *(volatile int *)(st + 1)) return;
+  const int lane = threadIdx.x & 63;
+  const int wr = width[s];
+  const int w = wr < 0 ? -wr : wr;
+  const int64_t row = s * SLICE + lane;
+  const uint32_t mk = wr >= 0 ? 0u : (mask8 ? (uint32_t)mask8[row] : mask[row]);
+  for (int j = 0; j < w; ++j) {
+    const int64_t t = sell_slot(sptr[s], j, w, lane, true);
+    if (!slot_stored(wr, mk, col, t, j)) continue;
+    if (!vdict_insert(tab, st, (unsigned long long)__double_as_longlong(sval[t]))) { st[1] = 1; return; }
+  }
+}
+
+__global__ void code_bytes_kernel(int64_t ns, const int32_t *__restrict__ width, int64_t *__restrict__ cb) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= ns) return;
+  const int w = width[s] < 0 ? -width[s] : width[s];
+  cb[s] = (int64_t)((w + 7) / 8) * CODE_BATCH;
+}
+
+// one wave per slice: lane = row, 8 slots per 8-byte word; absent slots of
+// aligned-offset rows and slots past the width get VCODE_ABSENT (the table
+// holds 0.0 there)
+__global__ void code_fill_kernel(int64_t ns, const int64_t *__restrict__ sptr, const int32_t *__restrict__ width,
+                                 const int32_t *__restrict__ col,
+                                 const double *__restrict__ sval, const int64_t *__restrict__ cptr,
+                                 const unsigned long long *__restrict__ tab, const uint8_t *__restrict__ slot_code,
+                                 const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8,
+                                 uint8_t *__restrict__ code) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= ns) return;
+  const int lane = threadIdx.x & 63;
+  const int wr = width[s];
+  const int w = wr < 0 ? -wr : wr;
+  const int64_t base = sptr[s];
+  const int64_t row = s * SLICE + lane;
+  const uint32_t mk = wr >= 0 ? 0u : (mask8 ? (uint32_t)mask8[row] : mask[row]);
+  for (int b = 0; b < (w + 7) / 8; ++b) {
+    unsigned long long word = 0;
+    for (int q = 0; q < 8; ++q) {
+      const int j = 8 * b + q;
+      unsigned long long c = VCODE_ABSENT;
+      const int64_t t = j < w ? sell_slot(base, j, w, lane, true) : 0;
+      if (j < w && slot_stored(wr, mk, col, t, j)) {
+        const double v = sval[t];
+        const int h = vdict_find(tab, (unsigned long long)__double_as_longlong(v));
+        c = h >= 0 ? slot_code[h] : 0;
+      }
+      word |= c << (8 * q);
+    }
+    reinterpret_cast<unsigned long long *>(code + cptr[s] + (int64_t)b * CODE_BATCH)[lane] = word;
+  }
+}
+
+static void build_value_codes(Sell &S, hipStream_t st) {
+  S.ntab = 0;
+  if (S.slots == 0 || !g_knobs.vcodes) return;
+  DBuf<unsigned long long> tab(VDICT_SLOTS);
+  DBuf<int> stat(2);
+  std::vector<unsigned long long> th(VDICT_SLOTS, VDICT_EMPTY);
+  HIPCHECK(hipMemcpyAsync(tab.p, th.data(), sizeof(unsigned long long) * VDICT_SLOTS, hipMemcpyHostToDevice, st));
+  HIPCHECK(hipMemsetAsync(stat.p, 0, 2 * sizeof(int), st));
+  vdict_insert_kernel<<<(unsigned)cdiv(S.nslices, 4), 256, 0, st>>>(S.nslices, S.sptr.p, S.width.p, S.col.p, S.val.p,
+                                                                  S.mask.p, S.mask8.p, tab.p, stat.p);
+  HIPCHECK(hipGetLastError());
+  int sh[2];
+  HIPCHECK(hipMemcpyAsync(sh, stat.p, sizeof(sh), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  if (sh[1] || sh[0] > VCODE_ABSENT || sh[0] == 0) return;
+  HIPCHECK(hipMemcpyAsync(th.data(), tab.p, sizeof(unsigned long long) * VDICT_SLOTS, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  std::vector<unsigned long long> keys;
+  for (unsigned long long k : th)
+    if (k != VDICT_EMPTY) keys.push_back(k);
+  std::sort(keys.begin(), keys.end());
+  std::vector<uint8_t> slot_code(VDICT_SLOTS, 0);
+  for (int h = 0; h < VDICT_SLOTS; ++h)
+    if (th[h] != VDICT_EMPTY)
+      slot_code[h] = (uint8_t)(std::lower_bound(keys.begin(), keys.end(), th[h]) - keys.begin());
+  std::vector<double> vt(VCODE_MAX, 0.0);
+  for (size_t i = 0; i < keys.size(); ++i) std::memcpy(&vt[i], &keys[i], sizeof(double));
+  const int64_t ns = S.nslices;
+  S.cptr.alloc((size_t)ns);
+  code_bytes_kernel<<<(unsigned)cdiv(ns, 256), 256, 0, st>>>(ns, S.width.p, S.cptr.p);
+  HIPCHECK(hipGetLastError());
+  exclusive_scan_i64(S.cptr.p, S.cptr.p, ns, st, &S.code_bytes);
+  S.code.alloc((size_t)std::max<int64_t>(S.code_bytes, 8));
+  S.vtab.alloc(VCODE_MAX);
+  DBuf<uint8_t> sc(VDICT_SLOTS);
+  HIPCHECK(hipMemcpyAsync(sc.p, slot_code.data(), VDICT_SLOTS, hipMemcpyHostToDevice, st));
+  HIPCHECK(hipMemcpyAsync(S.vtab.p, vt.data(), sizeof(double) * vt.size(), hipMemcpyHostToDevice, st));
+  code_fill_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(ns, S.sptr.p, S.width.p, S.col.p, S.val.p, S.cptr.p, tab.p, sc.p,
+                                                          S.mask.p, S.mask8.p, S.code.p);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(st));   // tab / sc are freed on return
+  S.ntab = (int)keys.size();
+}
+
+static void build_sell(Sell &S, int64_t m, int64_t ncols, const int64_t *ptr, const int32_t *col,
+                       const double *val, hipStream_t st, bool allow_dia) {
   S.nslices = cdiv(m, SLICE);
   const int64_t ns = S.nslices;
   S.width.alloc((size_t)std::max<int64_t>(ns, 1));
@@ -641,8 +902,9 @@ static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *co
   slice_format_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, ns, allow_dia ? 1 : 0, S.width.p,
                                                               S.sptr.p, S.doff.p);
   HIPCHECK(hipGetLastError());
+  std::vector<int32_t> wh;
   if (allow_dia) {
-    std::vector<int32_t> wh((size_t)ns);
+    wh.resize((size_t)ns);
     HIPCHECK(hipMemcpyAsync(wh.data(), S.width.p, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, st));
     HIPCHECK(hipStreamSynchronize(st));
     S.dia_slices = 0;
@@ -666,6 +928,8 @@ static void build_sell(Sell &S, int64_t m, const int64_t *ptr, const int32_t *co
   sell_fill_kernel<true><<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
                                                                 S.doff.p, S.col.p, S.val.p, S.mask.p, S.mask8.p);
   HIPCHECK(hipGetLastError());
+  if (S.dia_slices) share_offset_patterns(S, wh, ncols, st);
+  else S.dpat.alloc(1);
 }
 
 // ---------------------------------------------------------------- halo plan
@@ -896,8 +1160,9 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   if (A->nghost) HIPCHECK(hipMemcpyAsync(A->garray_h.data(), A->garray.p, sizeof(int64_t) * A->nghost, hipMemcpyDeviceToHost, st));
 
   // ---- SpMV layouts
-  build_sell(A->sd, m, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
-  build_sell(A->so, m, A->optr.p, A->ocol.p, A->oval.p, st, false);
+  build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
+  build_value_codes(A->sd, st);
+  build_sell(A->so, m, A->nghost, A->optr.p, A->ocol.p, A->oval.p, st, false);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
 

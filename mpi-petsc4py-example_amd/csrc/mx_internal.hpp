@@ -102,6 +102,7 @@ constexpr int SLICE = 64;  // SELL-C with C = one wavefront
 // width[s] < 0 marks such a slice (k = -width[s]); the offsets live in
 // doff[s * DIA_MAX + j].  Per row: 8 k + 4 bytes instead of 12 w.
 constexpr int DIA_MAX = 32;
+constexpr int32_t DPAT_INB = 1 << 30;
 struct Sell {
   int64_t nslices = 0, slots = 0, dia_slices = 0;
   int dia_k = 0;         // most common aligned-offset width (kernel specialisation)
@@ -109,17 +110,32 @@ struct Sell {
   DBuf<int32_t> width;   // [nslices]  (< 0: aligned-offset slice with k = -width)
   DBuf<int32_t> col;     // [slots], -1 = padding (unused for aligned-offset slices)
   DBuf<double> val;      // [slots]
-  DBuf<int32_t> doff;    // [nslices * DIA_MAX] offsets of aligned-offset slices
+  DBuf<int32_t> doff;    // [npat * DIA_MAX] the distinct offset patterns of aligned-offset slices
+  DBuf<int32_t> dpat;    // [nslices] pattern of each aligned-offset slice (a stencil has a handful),
+                         // | DPAT_INB when all of the slice's gathers are in range
+  int64_t npat = 0;
   DBuf<uint32_t> mask;   // [nslices * 64] slot-present bits of aligned-offset rows
   DBuf<uint8_t> mask8;   // the same in one byte per row when every slice has <= 8 offsets
+  // value codes (diagonal block): when the block holds at most VCODE_MAX
+  // distinct values, code[cptr[s] + b * CODE_BATCH + 8 lane + q] is the index
+  // into vtab of slot 8 b + q of the lane's row (one byte per slot instead of 8)
+  int ntab = 0;          // 0: no codes
+  int64_t code_bytes = 0;
+  DBuf<uint8_t> code;
+  DBuf<int64_t> cptr;    // [nslices] byte offset of each slice's code block
+  DBuf<double> vtab;     // [ntab] the distinct values, ascending bit pattern
 };
+constexpr int VCODE_MAX = 256;      // table entries; code 255 marks an absent slot
+constexpr int VCODE_ABSENT = VCODE_MAX - 1;
+constexpr int CODE_BATCH = 8 * SLICE;   // bytes per 8-slot batch of a slice
+struct VCodes { const uint8_t *code; const int64_t *cptr; const double *tab; int ntab; };
 
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
-struct Knobs { int spmv_nt = 1; int spmv_grid = 8192; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
+struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
                 int bnd_grid = 0; int mdot_group = 32;
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
-                int cg_upd_grid = 0; };
+                int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; };
 extern Knobs g_knobs;
 
 struct Halo {

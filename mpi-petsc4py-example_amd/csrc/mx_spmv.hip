@@ -18,6 +18,7 @@
 // slots carry column -1 and are skipped.  A_o gets its own SELL structure;
 // slices with no ghost entries have width 0 and cost one scalar load.
 #include <algorithm>
+#include <unordered_map>
 
 #include "mx_cg.hpp"
 #include "mx_device.hpp"
@@ -78,6 +79,101 @@ struct XCg {
   }
 };
 
+// Matrix values of one slice: fp64 in the paired layout (slot j of a lane at
+// pair j / 2), or one-byte codes into the matrix's value table (copied to LDS
+// at kernel start): batch b = entries 8 b .. 8 b + 7 of every lane, one 8-B
+// load per lane = one 512-B wave load (SELL-64 code blocks, mx_assembly.hip).
+// A table entry is the stored value itself, so both give the same bits.
+template <bool NT>
+struct VDense {
+  const double *__restrict__ b;   // the slice's first slot
+  // entries 2 p0 .. 2 p0 + 7 (pairs p0 .. p0 + 3, those below np)
+  __device__ __forceinline__ void eight(int p0, int np, int lane, double v[8]) const {
+    const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(b) + lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = p0 + q;
+      const dbl2 t = p < np ? ld<NT>(vp + (int64_t)p * SLICE) : dbl2{0.0, 0.0};
+      v[2 * q] = t.x;
+      v[2 * q + 1] = t.y;
+    }
+  }
+  // the unpaired last entry 2 np of an odd width
+  __device__ __forceinline__ double last(int np, int lane) const { return ld<NT>(b + (int64_t)np * 2 * SLICE + lane); }
+  template <int K>
+  __device__ __forceinline__ void fixed(int lane, double v[K]) const {
+    constexpr int NP = K / 2;
+    const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(b) + lane;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const dbl2 t = ld<NT>(vp + p * SLICE);
+      v[2 * p] = t.x;
+      v[2 * p + 1] = t.y;
+    }
+    if constexpr (K & 1) v[K - 1] = ld<NT>(b + NP * 2 * SLICE + lane);
+  }
+  // two phases (loads of several slices in flight before the first use)
+  static constexpr bool kCodedPresence = false;   // presence comes from the row masks
+  template <int K> struct Raw { double v[K]; };
+  template <int K> __device__ __forceinline__ void fetch(int lane, Raw<K> &r) const { fixed<K>(lane, r.v); }
+  template <int K> __device__ __forceinline__ void decode(const Raw<K> &r, double v[K]) const {
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = r.v[j];
+  }
+};
+
+template <bool NT>
+struct VCoded {
+  const uint8_t *__restrict__ b;  // the slice's code block
+  const double *t;                // value table (LDS)
+  __device__ __forceinline__ uint64_t batch(int bi, int lane) const {
+    return ld<NT>(reinterpret_cast<const uint64_t *>(b + (int64_t)bi * CODE_BATCH) + lane);
+  }
+  __device__ __forceinline__ void eight(int p0, int, int lane, double v[8]) const {
+    const uint64_t c = batch(p0 >> 2, lane);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = t[(c >> (8 * q)) & 0xff];
+  }
+  __device__ __forceinline__ double last(int np, int lane) const {
+    const int j = 2 * np;
+    return t[b[(int64_t)(j >> 3) * CODE_BATCH + lane * 8 + (j & 7)]];
+  }
+  template <int K>
+  __device__ __forceinline__ void fixed(int lane, double v[K]) const {
+#pragma unroll
+    for (int bi = 0; bi < (K + 7) / 8; ++bi) {
+      const uint64_t c = batch(bi, lane);
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (8 * bi + q < K) v[8 * bi + q] = t[(c >> (8 * q)) & 0xff];
+    }
+  }
+  // the aligned-offset code blocks mark absent slots with VCODE_ABSENT, so
+  // the fixed-width body needs no presence-mask load
+  static constexpr bool kCodedPresence = true;
+  template <int K> struct Raw { uint64_t c[(K + 7) / 8]; };
+  template <int K> __device__ __forceinline__ bool present(const Raw<K> &r, int j) const {
+    return ((r.c[j >> 3] >> (8 * (j & 7))) & 0xff) != VCODE_ABSENT;
+  }
+  template <int K> __device__ __forceinline__ uint32_t presence(const Raw<K> &r) const {
+    uint32_t mk = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) mk |= present<K>(r, j) ? 1u << j : 0u;
+    return mk;
+  }
+  template <int K> __device__ __forceinline__ void fetch(int lane, Raw<K> &r) const {
+#pragma unroll
+    for (int bi = 0; bi < (K + 7) / 8; ++bi) r.c[bi] = batch(bi, lane);
+  }
+  template <int K> __device__ __forceinline__ void decode(const Raw<K> &r, double v[K]) const {
+#pragma unroll
+    for (int bi = 0; bi < (K + 7) / 8; ++bi)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (8 * bi + q < K) v[8 * bi + q] = t[(r.c[bi] >> (8 * q)) & 0xff];
+  }
+};
+
 // Every slice body below issues all of its loads before the first use, with
 // predicated (never branching) lanes: absent entries gather the always-valid
 // x[0] and are then skipped by a select, so the running sum sees exactly the
@@ -87,53 +183,56 @@ struct XCg {
 // inb: every gather of the slice lies inside x (wave-uniform), so the
 // absent entries can read their in-range neighbour and every gather uses the
 // uniform-base form; otherwise absent entries read x[0]
-template <int K, bool NT, class XS>
-__device__ __forceinline__ double dia_slice_fixed(const double *__restrict__ vbase, const int32_t *__restrict__ off,
-                                                  uint32_t mk, int64_t row, const XS &x, int lane, bool inb,
-                                                  int64_t srow) {
-  constexpr int NP = K / 2;
+template <int K, class VS, class XS, class MK>
+__device__ __forceinline__ double dia_slice_fixed(const VS &vs, const int32_t *__restrict__ off,
+                                                  const MK &mkload, int64_t row, const XS &x, int lane, bool inb,
+                                                  int64_t srow, double &xc, bool &hc) {
+  // values (or codes), then the gathers, then the code lookups: the
+  // scheduling barrier keeps the lookups (which wait for the codes) from being
+  // hoisted above the gathers, so both HBM trips are in flight together
+  // (the presence mask is loaded after the gathers when they do not need it).
+  // xc / hc: the operand at the slice's own rows when the middle offset is 0
+  // (symmetric stencils), reused by the DOT / CG epilogue instead of a reload
+  typename VS::template Raw<K> raw;
+  vs.template fetch<K>(lane, raw);
   double v[K], xv[K];
-  const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const dbl2 t = ld<NT>(vp + p * SLICE);
-    v[2 * p] = t.x;
-    v[2 * p + 1] = t.y;
-  }
-  if constexpr (K & 1) v[K - 1] = ld<NT>(vbase + NP * 2 * SLICE + lane);
+  uint32_t mk = 0;
   if (inb) {
 #pragma unroll
     for (int j = 0; j < K; ++j) xv[j] = x.at(srow + off[j], lane);
+    if constexpr (!VS::kCodedPresence) mk = mkload();
   } else {
+    if constexpr (VS::kCodedPresence) mk = vs.template presence<K>(raw);
+    else mk = mkload();
 #pragma unroll
     for (int j = 0; j < K; ++j) xv[j] = x(((mk >> j) & 1u) ? row + off[j] : 0);
   }
+  __builtin_amdgcn_sched_barrier(0);
+  hc = inb && off[K / 2] == 0;
+  xc = xv[K / 2];
+  vs.template decode<K>(raw, v);
   double sum = 0.0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const double t = sum + v[j] * xv[j];
-    sum = ((mk >> j) & 1u) ? t : sum;
+    bool p;
+    if constexpr (VS::kCodedPresence) p = inb ? vs.template present<K>(raw, j) : ((mk >> j) & 1u);
+    else p = (mk >> j) & 1u;
+    sum = p ? t : sum;
   }
   return sum;
 }
 
 // aligned-offset slice, runtime width: batches of 8 slots
-template <bool NT, class XS>
-__device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase, const int32_t *__restrict__ off,
+template <class VS, class XS>
+__device__ __forceinline__ double dia_slice_any(const VS &vs, const int32_t *__restrict__ off,
                                                 int k, uint32_t mk, int64_t row, const XS &x, int lane, bool inb,
                                                 int64_t srow) {
   const int np = k >> 1;
-  const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
   double sum = 0.0;
   for (int p0 = 0; p0 < np; p0 += 4) {
     double v[8], xv[8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int p = p0 + q;
-      const dbl2 t = p < np ? ld<NT>(vp + (int64_t)p * SLICE) : dbl2{0.0, 0.0};
-      v[2 * q] = t.x;
-      v[2 * q + 1] = t.y;
-    }
+    vs.eight(p0, np, lane, v);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int j = 2 * p0 + q;
@@ -149,7 +248,7 @@ __device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase
     }
   }
   if (k & 1) {
-    const double v = ld<NT>(vbase + (int64_t)np * 2 * SLICE + lane);
+    const double v = vs.last(np, lane);
     const bool ok = (mk >> (k - 1)) & 1u;
     const double xv = inb ? x.at(srow + off[k - 1], lane) : x(ok ? row + off[k - 1] : 0);
     const double t = sum + v * xv;
@@ -159,12 +258,11 @@ __device__ __forceinline__ double dia_slice_any(const double *__restrict__ vbase
 }
 
 // general SELL slice (paired layout), continuing `sum`: batches of 8 entries
-template <bool NT, class XS>
-__device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, const double *__restrict__ vbase,
+template <bool NT, class VS, class XS>
+__device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, const VS &vs,
                                              int w, double sum, const XS &x, int lane) {
   const int np = w >> 1;
   const int2v *__restrict__ cp = reinterpret_cast<const int2v *>(cbase) + lane;
-  const dbl2 *__restrict__ vp = reinterpret_cast<const dbl2 *>(vbase) + lane;
   for (int p0 = 0; p0 < np; p0 += 4) {
     int c[8];
     double v[8], xv[8];
@@ -172,10 +270,9 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
     for (int q = 0; q < 4; ++q) {
       const int p = p0 + q;
       const int2v cc = p < np ? ld<NT>(cp + (int64_t)p * SLICE) : int2v{-1, -1};
-      const dbl2 t = p < np ? ld<NT>(vp + (int64_t)p * SLICE) : dbl2{0.0, 0.0};
       c[2 * q] = cc.x; c[2 * q + 1] = cc.y;
-      v[2 * q] = t.x; v[2 * q + 1] = t.y;
     }
+    vs.eight(p0, np, lane, v);
 #pragma unroll
     for (int q = 0; q < 8; ++q) xv[q] = x(c[q] >= 0 ? c[q] : 0);
 #pragma unroll
@@ -187,7 +284,7 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
   if (w & 1) {
     const int64_t t = (int64_t)np * 2 * SLICE + lane;
     const int c = ld<NT>(cbase + t);
-    const double v = ld<NT>(vbase + t);
+    const double v = vs.last(np, lane);
     const double xv = x(c >= 0 ? c : 0);
     const double tt = sum + v * xv;
     sum = c >= 0 ? tt : sum;
@@ -201,17 +298,18 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
 // order, so the +-1 / +-n / +-n^2 re-reads of x stay in that XCD's 4 MB L2.
 // Placement only affects speed, never results.  KD > 0 specialises the
 // aligned-offset body for the matrix's dominant slice width.
-template <int MODE, bool NT, int KD, bool SPLIT, int JM = 0>
+template <int MODE, bool NT, int KD, bool SPLIT, int JM = 0, bool VC = false>
 __global__ void __launch_bounds__(256) spmv_sell_kernel(
     int64_t m, int64_t ncols, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
-    const double *__restrict__ val_d, const int32_t *__restrict__ doff,
+    const double *__restrict__ val_d, const int32_t *__restrict__ doff, const int32_t *__restrict__ dpat,
     const uint32_t *__restrict__ dmask, const uint8_t *__restrict__ dmask8, const int64_t *__restrict__ sptr_o,
     const int32_t *__restrict__ wid_o, const int32_t *__restrict__ col_o,
     const double *__restrict__ val_o, const double *__restrict__ x,
     const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
-    const double *__restrict__ xscale) {
+    const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
+    const double *__restrict__ vtab_g, int ntab, int ynt) {
   CgTopIn top;
   if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
   else if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
@@ -249,63 +347,83 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
   } else {
     X = XPlainT<SC>{x, xs};
   }
+  __shared__ double vtab[VC ? VCODE_MAX : 1];
+  if constexpr (VC) {   // every early return above is workgroup-uniform
+    for (int i = threadIdx.x; i < VCODE_MAX; i += 256) vtab[i] = vtab_g[i];   // [ntab, 256) zero
+    __syncthreads();
+  }
   double dot = 0.0;
-  for (int s = s0; s < send; s += sstep) {
+  using VS = typename std::conditional<VC, VCoded<NT>, VDense<NT>>::type;
+  auto vsrc = [&](int s) -> VS {
+    if constexpr (VC) return VCoded<NT>{vcode + vcptr[s], vtab};
+    else return VDense<NT>{val_d + sptr_d[s]};
+  };
+  // CG: p_{i-1} and x at the owned rows for the deferred VecAXPY, loaded with
+  // the slice's first loads so their latency overlaps the gathers
+  struct Own { double p = 0.0, x = 0.0; };
+  auto own_load = [&](int64_t row) {
+    Own o;
+    if constexpr (MODE == SPMV_CG) {
+      if (xpend) {
+        const int64_t rc = row < m ? row : 0;
+        o.p = cg.pold[rc];
+        o.x = cg.x[rc];
+      }
+    }
+    return o;
+  };
+  // everything after the diagonal-block sum of slice s; xc = the operand at
+  // the slice's own rows when hc (gathered by the body), else reloaded
+  auto finish = [&](int s, double sum, const Own &o, double xc, bool hc) {
     const int64_t row = (int64_t)s * SLICE + lane;
-    const int w = wid_d[s];
-    const int64_t base = sptr_d[s];
-    // CG: the owned row's r, p_{i-1}, x (and dinv) are loaded with the
-    // slice's first loads so their latency overlaps the gathers
-    double own_r = 0.0, own_p = 0.0, own_x = 0.0, own_d = 0.0;
     if constexpr (MODE == SPMV_CG) {
-      const int64_t rc = row < m ? row : 0;
-      own_r = cg.r[rc];
-      own_p = cg.pold[rc];
-      own_x = cg.x[rc];
-      if constexpr (JM == 1) own_d = cg.jac.d[rc];
-    }
-    double sum;
-    if (w < 0) {
-      const int k = -w;
-      const uint32_t mk = dmask8 ? (uint32_t)dmask8[row] : dmask[row];
-      const int32_t *__restrict__ off = doff + (int64_t)s * DIA_MAX;
-      const int64_t srow = (int64_t)s * SLICE;
-      int omin = off[0], omax = off[0];
-      for (int j = 1; j < k; ++j) { omin = min(omin, off[j]); omax = max(omax, off[j]); }
-      const bool inb = srow + omin >= 0 && srow + (SLICE - 1) + omax < ncols;
-      if (KD > 0 && k == KD) sum = dia_slice_fixed<(KD > 0 ? KD : 1), NT>(val_d + base, off, mk, row, X, lane, inb, srow);
-      else sum = dia_slice_any<NT>(val_d + base, off, k, mk, row, X, lane, inb, srow);
-    } else {
-      sum = sell_slice<NT>(col_d + base, val_d + base, w, 0.0, X, lane);
-    }
-    double xr = 0.0;   // operand at the owned row (DOT / CG)
-    if constexpr (MODE == SPMV_CG) {
-      double z = own_r;                         // same expression as XCg
-      if constexpr (JM == 1) z = own_r * own_d;
-      else if constexpr (JM == 2) z = own_r * cg.jac.c;
-      xr = z + X.b * own_p;
+      const double xr = hc ? xc : X(row < m ? row : 0);   // the same expression either way
       if (row < m) {
         cg.pnew[row] = xr;
-        if (xpend) cg.x[row] = fma(xa, own_p, own_x);   // VecAXPY(X, a, P) of the previous step
+        if (xpend) cg.x[row] = fma(xa, o.p, o.x);   // VecAXPY(X, a, P) of the previous step
       }
+      xc = xr;
     }
     if (SPLIT) {
       // slice with ghost entries: store the diagonal-block sum; the boundary
       // kernel continues it with A_o once the halo has arrived
       if (wid_o[s]) {
         if (row < m) y[row] = sum;
-        continue;
+        return;
       }
     } else if (lvec) {
       const int wo = wid_o[s];
-      if (wo) sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wo, sum, XPlainT<SC>{lvec, xs}, lane);
+      if (wo) sum = sell_slice<false>(col_o + sptr_o[s], VDense<false>{val_o + sptr_o[s]}, wo, sum, XPlainT<SC>{lvec, xs}, lane);
     }
     if (row < m) {
-      if (spmv_jac(MODE)) y[row] = papply(jac, sum, row);   // PCApply_Jacobi fused: w_i * d_i
-      else y[row] = sum;
-      if (MODE == SPMV_DOT) dot += x[row] * sum;           // VecDot(p, w) partial, p = x
-      if (MODE == SPMV_CG) dot += xr * sum;
+      const double out = spmv_jac(MODE) ? papply(jac, sum, row) : sum;   // PCApply_Jacobi fused: w_i * d_i
+      if (ynt) __builtin_nontemporal_store(out, y + row);   // keep L2 for the x re-reads
+      else y[row] = out;
+      if (MODE == SPMV_DOT) dot += (hc ? xc : x[row]) * sum;   // VecDot(p, w) partial, p = x
+      if (MODE == SPMV_CG) dot += xc * sum;
     }
+  };
+  for (int s = s0; s < send; s += sstep) {
+    const int64_t row = (int64_t)s * SLICE + lane;
+    const int w = wid_d[s];
+    const VS vs = vsrc(s);
+    const Own o = own_load(row);
+    double sum, xc = 0.0;
+    bool hc = false;
+    if (w < 0) {
+      const int k = -w;
+      auto mkload = [&]() -> uint32_t { return dmask8 ? (uint32_t)dmask8[row] : dmask[row]; };
+      const int dp = dpat[s];
+      const int32_t *__restrict__ off = doff + (int64_t)(dp & (DPAT_INB - 1)) * DIA_MAX;
+      const int64_t srow = (int64_t)s * SLICE;
+      const bool inb = (dp & DPAT_INB) != 0;
+      if (KD > 0 && k == KD)
+        sum = dia_slice_fixed<(KD > 0 ? KD : 1)>(vs, off, mkload, row, X, lane, inb, srow, xc, hc);
+      else sum = dia_slice_any(vs, off, k, mkload(), row, X, lane, inb, srow);
+    } else {
+      sum = sell_slice<NT>(col_d + sptr_d[s], vs, w, 0.0, X, lane);
+    }
+    finish(s, sum, o, xc, hc);
   }
   if (MODE == SPMV_DOT || MODE == SPMV_CG) {
     double v[1] = {dot};
@@ -313,14 +431,49 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
   }
 }
 
-// Grid of the main SpMV launch (an upper bound for every mode).  SPMV_CG
-// evaluates the iteration's scalar top in every workgroup, a dependent chain
-// of scalar loads paid once per workgroup generation, so it keeps >= 4 slices
-// per wave (tools/coll_ab.py: -6% per CG iteration at 2M rows per rank).
-int spmv_blocks(const Mat *A, int mode) {
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cus[dev]) HIPCHECK(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  return cus[dev];
+}
+
+// Upper bound of the main launch's grid (partial-sum buffers are sized by it)
+int spmv_blocks(const Mat *A, int) {
   const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
-  int64_t g = std::min<int64_t>(need, g_knobs.spmv_grid);
-  if (mode == SPMV_CG) g = std::min<int64_t>(g, std::max<int64_t>(2048, need / 4));
+  const int64_t cap = g_knobs.spmv_grid > 0 ? g_knobs.spmv_grid : 8 * (int64_t)device_cus();
+  return (int)std::max<int64_t>(1, std::min<int64_t>(need, std::max<int64_t>(cap, 8192)));
+}
+
+// Grid of the main SpMV launch: exactly the workgroups that are resident at
+// once (one generation).  Each XCD then walks its slices in one sweep with a
+// window of ~ the resident waves, so the x lines of the +-n^2 neighbours are
+// re-read from L2 (tools/pmc_spmv.sh: FETCH_SIZE = the compulsory bytes at
+// this grid, ~2x at a 4.6-generation grid) and no second generation leaves a
+// tail.  Blocks per CU: the occupancy API, capped at 6 (knob 26): the kernels
+// hold 106 SGPRs, which allow 6 waves per SIMD, while the API reports one
+// more at that count (MI355X guide, correctness boundaries).  SPMV_CG
+// evaluates the iteration's scalar top once per workgroup, so it keeps >= 4
+// slices per wave.  Knob 3 > 0 overrides the grid.
+static int main_grid(const Mat *A, int mode, const void *kf) {
+  const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
+  int64_t g;
+  if (g_knobs.spmv_grid > 0) {
+    g = g_knobs.spmv_grid;
+  } else {
+    static std::unordered_map<const void *, int> bpc_of;
+    auto it = bpc_of.find(kf);
+    if (it == bpc_of.end()) {
+      int b = 0;
+      HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kf, 256, 0));
+      it = bpc_of.emplace(kf, std::max(1, b)).first;
+    }
+    g = (int64_t)std::min(it->second, std::max(1, g_knobs.spmv_bpc)) * device_cus();
+  }
+  g = std::min<int64_t>(g, need);
+  if (mode == SPMV_CG) g = std::min<int64_t>(g, std::max<int64_t>(512, need / 4));
   if (g >= 64) g &= ~int64_t(7);   // multiple of 8: XCD grouping
   return (int)std::max<int64_t>(1, g);
 }
@@ -345,7 +498,7 @@ __global__ void __launch_bounds__(256) spmv_boundary_kernel(
     const int s = list[k];
     const int64_t row = (int64_t)s * SLICE + lane;
     double sum = row < m ? y[row] : 0.0;
-    sum = sell_slice<false>(col_o + sptr_o[s], val_o + sptr_o[s], wid_o[s], sum, XPlainT<SC>{lvec, xs}, lane);
+    sum = sell_slice<false>(col_o + sptr_o[s], VDense<false>{val_o + sptr_o[s]}, wid_o[s], sum, XPlainT<SC>{lvec, xs}, lane);
     if (row < m) {
       if (spmv_jac(MODE)) y[row] = papply(jac, sum, row);
       else y[row] = sum;
@@ -407,39 +560,43 @@ void halo_begin(Mat *A, const double *x) {
   halo_exchange(A, x, nullptr, nullptr, A->comm->stream);
 }
 
-static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
-                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold,
-                        const double *xscale) {
-  const unsigned grid = (unsigned)spmv_blocks(A, mode);
+// returns the grid; a fold (cnt set) counts all of its workgroups
+static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
+                       int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold_in,
+                       const double *xscale) {
   const double *lvec = (A->nghost && !split) ? A->halo.lvec.p : nullptr;
   const int kd = A->sd.dia_k;
   const CgFuse cg = cgp ? *cgp : CgFuse{};
+  // value codes (when the matrix has them; knob 23 = 0 reads the fp64 values)
+  const bool vcode = A->sd.ntab > 0 && g_knobs.vcodes;
+  const VCodes vc{A->sd.code.p, A->sd.cptr.p, A->sd.vtab.p, A->sd.ntab};
 #define SPMV_ARGS                                                                           \
-  A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, \
+  A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
-      partials, done_flag, cg, fold, xscale
-#define SPMV_KD(MODE, NT, SP)                                                                    \
-  do {                                                                                           \
-    switch (kd) {                                                                                \
-      case 5: spmv_sell_kernel<MODE, NT, 5, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
-      case 7: spmv_sell_kernel<MODE, NT, 7, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
-      case 27: spmv_sell_kernel<MODE, NT, 27, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;       \
-      default: spmv_sell_kernel<MODE, NT, 0, SP><<<grid, 256, 0, st>>>(SPMV_ARGS); break;        \
-    }                                                                                            \
+      partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt
+  using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
+  KFn kf = nullptr;
+#define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>
+#define SPMV_KD(MODE, NT, SP, JM, VC)                                                                 \
+  do {                                                                                                \
+    switch (kd) {                                                                                     \
+      case 5: SPMV_KDU(MODE, NT, SP, JM, VC, 5); break;                                               \
+      case 7: SPMV_KDU(MODE, NT, SP, JM, VC, 7); break;                                               \
+      case 27: SPMV_KDU(MODE, NT, SP, JM, VC, 27); break;                                             \
+      default: SPMV_KDU(MODE, NT, SP, JM, VC, 0); break;                                              \
+    }                                                                                                 \
   } while (0)
-#define SPMV_CGKD(JM, SP)                                                                                   \
-  do {                                                                                                      \
-    switch (kd) {                                                                                           \
-      case 5: spmv_sell_kernel<SPMV_CG, true, 5, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;           \
-      case 7: spmv_sell_kernel<SPMV_CG, true, 7, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;           \
-      case 27: spmv_sell_kernel<SPMV_CG, true, 27, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;         \
-      default: spmv_sell_kernel<SPMV_CG, true, 0, SP, JM><<<grid, 256, 0, st>>>(SPMV_ARGS); break;          \
-    }                                                                                                       \
+#define SPMV_CGKD(JM, SP)                                                  \
+  do {                                                                     \
+    if (vcode) SPMV_KD(SPMV_CG, true, SP, JM, true);                       \
+    else SPMV_KD(SPMV_CG, true, SP, JM, false);                            \
   } while (0)
+  // code blocks are always read non-temporally
 #define SPMV_GO(MODE)                                                         \
   do {                                                                        \
-    if (split) { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, true); else SPMV_KD(MODE, false, true); } \
-    else { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, false); else SPMV_KD(MODE, false, false); }     \
+    if (vcode) { if (split) SPMV_KD(MODE, true, true, 0, true); else SPMV_KD(MODE, true, false, 0, true); } \
+    else if (split) { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, true, 0, false); else SPMV_KD(MODE, false, true, 0, false); } \
+    else { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, false, 0, false); else SPMV_KD(MODE, false, false, 0, false); }     \
   } while (0)
   switch (mode) {
     case SPMV_PLAIN: SPMV_GO(SPMV_PLAIN); break;
@@ -457,11 +614,17 @@ static void launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, d
       break;
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
+  const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf));
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  kf<<<grid, 256, 0, st>>>(SPMV_ARGS);
 #undef SPMV_GO
 #undef SPMV_CGKD
 #undef SPMV_KD
+#undef SPMV_KDU
 #undef SPMV_ARGS
   HIPCHECK(hipGetLastError());
+  return grid;
 }
 
 void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
@@ -478,13 +641,9 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
   Comm *c = A->comm;
   Halo &H = A->halo;
   hipStream_t st = c->stream;
-  const int nmain = spmv_blocks(A, mode);
   if (c->size == 1 || H.nbnd == 0 || !g_knobs.overlap) {
     if (c->size > 1) halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, st);
-    Fold f;
-    if (fold) { f = *fold; f.ntotal = nmain; f.base = 0; f.ncount = nmain; }
-    launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg, f, xscale);
-    return nmain;
+    return launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg, fold ? *fold : Fold{}, xscale);
   }
   hipStream_t cs = c->comm_stream;
   if (!H.ev_x) {
@@ -498,7 +657,7 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
   halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, cs);
   HIPCHECK(hipEventRecord(H.ev_done, cs));
   // interior slices meanwhile; boundary slices after the exchange
-  launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{}, xscale);
+  const int nmain = launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{}, xscale);
   HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
   const int nb = std::min(g_knobs.bnd_grid > 0 ? g_knobs.bnd_grid : BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
   // the boundary launch folds the partials of both launches (fold) or

@@ -1,0 +1,139 @@
+"""Value codes: a diagonal block with at most 256 distinct values streams one
+byte per slot into an LDS value table (mx_assembly.hip build_value_codes).
+The product must stay bit-identical to the oracle, with codes, without them
+(more distinct values, or knob 23 = 0), on aligned-offset slices of every
+width class (fixed 5/7/27, runtime k, k > 8 = several code batches, odd k)
+and on general SELL slices (column ids + codes, odd widths)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def lib():
+    from mxsolve import _lib
+    return _lib.load()
+
+
+def mult_bits(comm, oracle_mod, M, ip, c, v, seed=3):
+    from mxsolve.core import DMat
+    A = DMat.from_csr(comm, M, M, ip, c, v)
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    x = np.random.default_rng(seed).standard_normal(M)
+    y = torch.zeros(M, dtype=torch.float64, device="cuda")
+    A.mult(torch.from_numpy(x).cuda(), y)
+    got = y.cpu().numpy().view(np.uint64)
+    return A.info(), got, O.mult(x).view(np.uint64)
+
+
+def banded(M, offsets, values, rng, drop=0.0):
+    """Rows with the given column offsets (clipped at the edges, some dropped)."""
+    ip, cols, vals = [0], [], []
+    for i in range(M):
+        for o in offsets:
+            j = i + o
+            if 0 <= j < M and (o == 0 or rng.random() >= drop):
+                cols.append(j)
+                vals.append(values[rng.integers(0, len(values))])
+        ip.append(len(cols))
+    return np.array(ip, np.int64), np.array(cols, np.int64), np.array(vals)
+
+
+@pytest.mark.parametrize("kind,n", [("poisson2d", 37), ("poisson3d", 19), ("poisson3d27", 9), ("convdiff3d", 13)])
+def test_stencils_use_codes(selfcomm, oracle_mod, kind, n):
+    ip, c, v = oracle_mod.stencil(kind, n)
+    info, got, exp = mult_bits(selfcomm, oracle_mod, ip.size - 1, ip, c, v)
+    assert 0 < info["value_codes"] <= 256
+    assert info["code_bytes"] > 0
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("offsets", [
+    (-3, -1, 0, 1, 3),                              # k = 5 (fixed body)
+    (-40, -7, -1, 0, 1, 7, 40),                     # k = 7
+    (-2, -1, 0, 1, 2, 5),                           # k = 6 (runtime body, one batch)
+    tuple(range(-6, 7)),                            # k = 13: two batches, odd
+    tuple(range(-8, 9)),                            # k = 17: three batches
+])
+@pytest.mark.parametrize("nvals", [1, 3, 255])
+def test_aligned_offset_slices(selfcomm, oracle_mod, offsets, nvals):
+    rng = np.random.default_rng(len(offsets) * 1000 + nvals)
+    values = np.unique(rng.standard_normal(nvals)) if nvals > 1 else np.array([-1.0])
+    assert values.size == nvals
+    ip, c, v = banded(1000, offsets, values, rng, drop=0.1)
+    info, got, exp = mult_bits(selfcomm, oracle_mod, 1000, ip, c, v)
+    assert info["value_codes"] == np.unique(v.view(np.uint64)).size   # stored values only
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("maxlen", [3, 9, 40])
+def test_general_slices(selfcomm, oracle_mod, maxlen):
+    """Irregular rows (general SELL, column ids) with few distinct values,
+    signed zeros among them."""
+    rng = np.random.default_rng(maxlen)
+    M = 777
+    lens = rng.integers(0, maxlen + 1, M)
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    cols = np.concatenate([np.sort(rng.choice(M, size=k, replace=False)) for k in lens]).astype(np.int64)
+    vals = np.array([0.5, -2.0, 0.0, -0.0, 3.25, 1e300])[rng.integers(0, 6, cols.size)]
+    info, got, exp = mult_bits(selfcomm, oracle_mod, M, ip, cols, vals)
+    assert info["value_codes"] > 0
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("nvals,coded", [(255, True), (256, False)])
+def test_table_limit(selfcomm, oracle_mod, nvals, coded):
+    """255 distinct values fit (code 255 marks absent slots), 256 do not."""
+    rng = np.random.default_rng(nvals)
+    values = np.unique(rng.standard_normal(nvals))
+    ip, c, v = banded(3000, (-2, -1, 0, 1, 2), values, rng, drop=0.05)
+    v[: values.size] = values                     # every value stored at least once
+    info, got, exp = mult_bits(selfcomm, oracle_mod, 3000, ip, c, v)
+    assert (info["value_codes"] == nvals) if coded else (info["value_codes"] == 0)
+    assert np.array_equal(got, exp)
+
+
+def test_too_many_values_falls_back(selfcomm, oracle_mod):
+    rng = np.random.default_rng(5)
+    values = np.unique(rng.standard_normal(400))
+    ip, c, v = banded(2000, (-1, 0, 1), values, rng)
+    assert np.unique(v).size > 256
+    info, got, exp = mult_bits(selfcomm, oracle_mod, 2000, ip, c, v)
+    assert info["value_codes"] == 0
+    assert np.array_equal(got, exp)
+
+
+def test_knob_off_same_bits(selfcomm, oracle_mod):
+    ip, c, v = oracle_mod.stencil("convdiff3d", 12)
+    L = lib()
+    old = L.mx_debug_set(23, 0)
+    try:
+        info0, got0, exp = mult_bits(selfcomm, oracle_mod, ip.size - 1, ip, c, v)
+    finally:
+        L.mx_debug_set(23, old)
+    info1, got1, _ = mult_bits(selfcomm, oracle_mod, ip.size - 1, ip, c, v)
+    assert info0["value_codes"] == 0 and info1["value_codes"] > 0
+    assert np.array_equal(got0, exp) and np.array_equal(got1, exp)
+
+
+def test_cg_with_and_without_codes(selfcomm):
+    """The whole CG solve: same iteration count and the same solution bits."""
+    from mxsolve.core import DMat, rhs_hash
+    L = lib()
+    res = []
+    for knob in (0, 1):
+        old = L.mx_debug_set(23, knob)
+        try:
+            A = DMat.stencil(selfcomm, "poisson3d", 32)
+            m = A.info()["m"]
+            b = selfcomm.empty(m)
+            rhs_hash(selfcomm, 0, b)
+            x = selfcomm.zeros(m)
+            r = A.solve(b, x, ksp="cg", rtol=1e-8)
+            res.append((r["its"], r["reason"], x.cpu().numpy().copy(), A.info()["value_codes"]))
+        finally:
+            L.mx_debug_set(23, old)
+    assert res[0][3] == 0 and res[1][3] > 0
+    assert res[0][:2] == res[1][:2]
+    assert np.array_equal(res[0][2].view(np.uint64), res[1][2].view(np.uint64))

@@ -39,11 +39,13 @@ res = {v: {"cg": [], "mult": []} for v in variants}
 for rnd in range(rounds):
     for v in (variants if rnd % 2 == 0 else variants[::-1]):
         A, b, x, y = ops[v]
+        old = setv(v)          # run-time knobs apply to the measurement as well
         A.solve(b, x, ksp="cg", rtol=0.0, max_it=32)
         torch.cuda.synchronize(); t0 = time.perf_counter()
         A.solve(b, x, ksp="cg", rtol=0.0, max_it=300)
         torch.cuda.synchronize(); res[v]["cg"].append((time.perf_counter() - t0) / 300 * 1e6)
         res[v]["mult"].append(A.bench_mult(b, y, 30)[0] * 1e3)
+        setv(old)
 print(json.dumps({"kind": kind, "n": n, **{v: {"cg_us": round(float(np.median(r["cg"])), 1),
                                               "mult_us": round(float(np.median(r["mult"])), 1)}
                                            for v, r in res.items()}}), flush=True)
