@@ -88,6 +88,7 @@ typedef struct {
   int64_t value_codes;                /* A_d values as 1-byte codes into a table of this
                                          many distinct values (0: stored as fp64)       */
   int64_t code_bytes;                 /* bytes of those codes                         */
+  int64_t pair_shape;                 /* row-pair SpMV layout: 5 / 7 / 27-point, 0 none */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */

@@ -237,6 +237,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->dia_slices = A->sd.dia_slices;
     info->value_codes = A->sd.ntab;
     info->code_bytes = A->sd.code_bytes;
+    info->pair_shape = A->sd.ntab > 0 ? A->sd.pair_shape : 0;
   });
 }
 
@@ -461,6 +462,8 @@ int mx_debug_set(int key, int value) {
     case 24: old = g_knobs.spmv_unroll; g_knobs.spmv_unroll = value; break;
     case 25: old = g_knobs.spmv_ynt; g_knobs.spmv_ynt = value; break;
     case 26: old = g_knobs.spmv_bpc; g_knobs.spmv_bpc = value; break;
+    case 27: old = g_knobs.spmv_pairs; g_knobs.spmv_pairs = value; break;
+    case 28: old = g_knobs.spmv_pair_bpc; g_knobs.spmv_pair_bpc = value; break;
     default: break;
   }
   return old;

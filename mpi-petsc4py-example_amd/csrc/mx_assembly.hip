@@ -726,6 +726,18 @@ static void share_offset_patterns(Sell &S, const std::vector<int32_t> &wh, int64
       HIPCHECK(hipMemcpyAsync(&hb, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
       HIPCHECK(hipStreamSynchronize(st));
       if (!hb) {
+        // the dominant pattern of the dominant width (row-pair layout, below)
+        std::vector<int64_t> cnt((size_t)npat, 0);
+        for (int64_t q = 0; q < ns; ++q)
+          if (wh[q] == -S.dia_k) cnt[p2[q]]++;
+        const int star = (int)(std::max_element(cnt.begin(), cnt.end()) - cnt.begin());
+        if (cnt[star] > 0) {
+          S.pat_star = star;
+          S.pat_star_off.resize((size_t)S.dia_k);
+          HIPCHECK(hipMemcpyAsync(S.pat_star_off.data(), ptab.p + (size_t)star * DIA_MAX, sizeof(int32_t) * S.dia_k,
+                                  hipMemcpyDeviceToHost, st));
+          HIPCHECK(hipStreamSynchronize(st));
+        }
         S.doff = std::move(ptab);
         S.npat = npat;
         dia_inb_kernel<<<(unsigned)cdiv(ns, 256), 256, 0, st>>>(ns, ncols, S.width.p, S.doff.p, S.dpat.p);
@@ -847,7 +859,73 @@ __global__ void code_fill_kernel(int64_t ns, const int64_t *__restrict__ sptr, c
   }
 }
 
-static void build_value_codes(Sell &S, hipStream_t st) {
+// ---------------------------------------------------------------- row pairs
+// Units of 128 rows (slices 2u, 2u+1) whose both slices carry the dominant
+// offset pattern, every gather in range and no ghost entries are stored a
+// second time as row pairs: lane l owns rows 128 u + 2 l and + 1, its codes
+// are [K codes of row 0][K codes of row 1] padded to PB bytes, so SpMV loads
+// x as 16-byte pairs -- one load per run of the pattern instead of one per
+// offset and row (mx_spmv.hip, pair body).  Shapes (sorted offsets):
+//   5:  a, -1, 0, 1, b          (2D 5-point)
+//   7:  a, b, -1, 0, 1, c, d    (3D 7-point)
+//   27: nine runs c-1, c, c+1   (3D 27-point)
+// with every singleton and run centre even (16-byte aligned pairs).
+static int pair_shape_of(const std::vector<int32_t> &o) {
+  const int k = (int)o.size();
+  auto even = [](int32_t v) { return (v & 1) == 0; };
+  auto tri = [&](int j) { return o[j + 1] == o[j] + 1 && o[j + 2] == o[j] + 2 && even(o[j + 1]); };
+  if (k == 5 && tri(1) && o[2] == 0 && even(o[0]) && even(o[4]) && o[0] < o[1] - 1 && o[4] > o[3] + 1) return 5;
+  if (k == 7 && tri(2) && o[3] == 0 && even(o[0]) && even(o[1]) && even(o[5]) && even(o[6]) &&
+      o[1] < o[2] - 1 && o[5] > o[4] + 1)
+    return 7;
+  if (k == 27) {
+    for (int t = 0; t < 9; ++t)
+      if (!tri(3 * t)) return 0;
+    return o[13] == 0 ? 27 : 0;
+  }
+  return 0;
+}
+
+constexpr int pair_bytes(int k) { return (2 * k + 15) / 16 * 16; }
+
+// one wave per unit; sets DPAT_PAIR on slice 2u and writes the unit's codes
+__global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star, const int64_t *__restrict__ sptr,
+                                 const int32_t *__restrict__ width, int32_t *__restrict__ dpat,
+                                 const int32_t *__restrict__ wid_o, const double *__restrict__ sval,
+                                 const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8,
+                                 const unsigned long long *__restrict__ tab, const uint8_t *__restrict__ slot_code,
+                                 uint8_t *__restrict__ pcode) {
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= nunits) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t s0 = 2 * u, s1 = s0 + 1;
+  auto ok = [&](int64_t sl) {
+    return width[sl] == -k && (dpat[sl] & DPAT_ID) == star && (dpat[sl] & DPAT_INB) &&
+           (!wid_o || wid_o[sl] == 0);
+  };
+  if (u * 128 + 127 >= m || !ok(s0) || !ok(s1)) return;   // wave-uniform
+  const int pb = pair_bytes(k);
+  uint8_t *dst = pcode + (u * 64 + lane) * pb;
+  for (int h = 0; h < 2; ++h) {
+    const int64_t row = u * 128 + 2 * lane + h;
+    const int64_t sl = row >> 6;
+    const int li = (int)(row & 63);
+    const uint32_t mk = mask8 ? (uint32_t)mask8[row] : mask[row];
+    for (int j = 0; j < k; ++j) {
+      int c = VCODE_ABSENT;
+      if ((mk >> j) & 1u) {
+        const double v = sval[sell_slot(sptr[sl], j, k, li, true)];
+        const int hh = vdict_find(tab, (unsigned long long)__double_as_longlong(v));
+        c = hh >= 0 ? slot_code[hh] : 0;
+      }
+      dst[h * k + j] = (uint8_t)c;
+    }
+  }
+  for (int j = 2 * k; j < pb; ++j) dst[j] = (uint8_t)VCODE_ABSENT;
+  if (lane == 0) dpat[s0] |= DPAT_PAIR;
+}
+
+static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, hipStream_t st) {
   S.ntab = 0;
   if (S.slots == 0 || !g_knobs.vcodes) return;
   DBuf<unsigned long long> tab(VDICT_SLOTS);
@@ -887,6 +965,16 @@ static void build_value_codes(Sell &S, hipStream_t st) {
   code_fill_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(ns, S.sptr.p, S.width.p, S.col.p, S.val.p, S.cptr.p, tab.p, sc.p,
                                                           S.mask.p, S.mask8.p, S.code.p);
   HIPCHECK(hipGetLastError());
+  S.pair_shape = g_knobs.spmv_pairs && S.pat_star >= 0 ? pair_shape_of(S.pat_star_off) : 0;
+  if (S.pair_shape) {
+    S.nunits = ns / 2;
+    S.pcode.alloc((size_t)std::max<int64_t>(S.nunits, 1) * 64 * pair_bytes(S.dia_k));
+    if (S.nunits)
+      pair_fill_kernel<<<(unsigned)cdiv(S.nunits, 4), 256, 0, st>>>(m, S.nunits, S.dia_k, S.pat_star, S.sptr.p,
+                                                                   S.width.p, S.dpat.p, wid_o, S.val.p, S.mask.p,
+                                                                   S.mask8.p, tab.p, sc.p, S.pcode.p);
+    HIPCHECK(hipGetLastError());
+  }
   HIPCHECK(hipStreamSynchronize(st));   // tab / sc are freed on return
   S.ntab = (int)keys.size();
 }
@@ -1161,8 +1249,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
 
   // ---- SpMV layouts
   build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
-  build_value_codes(A->sd, st);
   build_sell(A->so, m, A->nghost, A->optr.p, A->ocol.p, A->oval.p, st, false);
+  build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, st);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
 

@@ -103,6 +103,8 @@ constexpr int SLICE = 64;  // SELL-C with C = one wavefront
 // doff[s * DIA_MAX + j].  Per row: 8 k + 4 bytes instead of 12 w.
 constexpr int DIA_MAX = 32;
 constexpr int32_t DPAT_INB = 1 << 30;
+constexpr int32_t DPAT_PAIR = 1 << 29;   // on slice 2u: unit u is stored as row pairs
+constexpr int32_t DPAT_ID = DPAT_PAIR - 1;
 struct Sell {
   int64_t nslices = 0, slots = 0, dia_slices = 0;
   int dia_k = 0;         // most common aligned-offset width (kernel specialisation)
@@ -124,6 +126,12 @@ struct Sell {
   DBuf<uint8_t> code;
   DBuf<int64_t> cptr;    // [nslices] byte offset of each slice's code block
   DBuf<double> vtab;     // [ntab] the distinct values, ascending bit pattern
+  // row-pair copy of the codes (mx_assembly.hip, pair_fill_kernel)
+  int32_t pat_star = -1;              // the dominant pattern of width dia_k
+  std::vector<int32_t> pat_star_off;
+  int pair_shape = 0;                 // 0, 5, 7, 27
+  int64_t nunits = 0;
+  DBuf<uint8_t> pcode;
 };
 constexpr int VCODE_MAX = 256;      // table entries; code 255 marks an absent slot
 constexpr int VCODE_ABSENT = VCODE_MAX - 1;
@@ -135,7 +143,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
                 int bnd_grid = 0; int mdot_group = 32;
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
-                int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; };
+                int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4; };
 extern Knobs g_knobs;
 
 struct Halo {

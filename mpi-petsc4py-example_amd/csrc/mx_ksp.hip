@@ -942,7 +942,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
            (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p,
            (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p, (uintptr_t)g_knobs.cg_vec_grid,
            (uintptr_t)g_knobs.cg_vec, (uintptr_t)g_knobs.cg_nts, (uintptr_t)g_knobs.cg_unroll,
-           (uintptr_t)g_knobs.cg_upd_grid, (uintptr_t)g_knobs.vcodes, (uintptr_t)g_knobs.spmv_bpc,
+           (uintptr_t)g_knobs.cg_upd_grid, (uintptr_t)g_knobs.vcodes, (uintptr_t)g_knobs.spmv_bpc, (uintptr_t)g_knobs.spmv_pairs, (uintptr_t)g_knobs.spmv_pair_bpc,
            (uintptr_t)g_knobs.spmv_ynt};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }

@@ -292,13 +292,63 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
   return sum;
 }
 
+// Row-pair body (units of 128 rows, lane = rows 2 l and 2 l + 1; layout in
+// mx_assembly.hip pair_fill_kernel).  x is read as 16-byte pairs, one per run
+// of the pattern: a singleton offset o gives both rows' operand (x[r0+o],
+// x[r0+1+o]); a run c-1, c, c+1 loads the pair at c, and the two values that
+// fall outside it -- x[r0+c-1] for row 0, x[r0+c+2] for row 1 -- come from the
+// neighbouring lanes by a DPP wave shift (lanes 0 and 63 take the unit's edge
+// values, loaded once per unit).  Per unit: one code load, one load per run,
+// one 16-byte store, against two code loads, 2 K gathers and two stores for
+// two single-row slices.  Every row still sums its entries in ascending
+// column order, one rounding per multiply and add.
+template <int PS> struct PairShape;
+template <> struct PairShape<5> {     // a, -1, 0, 1, b
+  static constexpr int K = 5, NR = 3, CENTER_RUN = 1;
+  static constexpr int run(int j) { return j == 0 ? 0 : j == 4 ? 2 : 1; }
+  static constexpr int pos(int j) { return j >= 1 && j <= 3 ? j - 2 : 0; }
+  static constexpr bool tri(int r) { return r == 1; }
+  static constexpr int first(int r) { return r == 0 ? 0 : r == 1 ? 1 : 4; }
+};
+template <> struct PairShape<7> {     // a, b, -1, 0, 1, c, d
+  static constexpr int K = 7, NR = 5, CENTER_RUN = 2;
+  static constexpr int run(int j) { return j < 2 ? j : j <= 4 ? 2 : j - 2; }
+  static constexpr int pos(int j) { return j >= 2 && j <= 4 ? j - 3 : 0; }
+  static constexpr bool tri(int r) { return r == 2; }
+  static constexpr int first(int r) { return r < 2 ? r : r == 2 ? 2 : r + 2; }
+};
+template <> struct PairShape<27> {    // nine runs c-1, c, c+1
+  static constexpr int K = 27, NR = 9, CENTER_RUN = 4;
+  static constexpr int run(int j) { return j / 3; }
+  static constexpr int pos(int j) { return j % 3 - 1; }
+  static constexpr bool tri(int) { return true; }
+  static constexpr int first(int r) { return 3 * r; }
+};
+template <> struct PairShape<0> {
+  static constexpr int K = 1, NR = 1, CENTER_RUN = 0;
+  static constexpr int run(int) { return 0; }
+  static constexpr int pos(int) { return 0; }
+  static constexpr bool tri(int) { return false; }
+  static constexpr int first(int) { return 0; }
+};
+
+// lane i takes lane i - 1's value (UP) or lane i + 1's (!UP); the edge lane takes `edge`
+template <bool UP>
+__device__ __forceinline__ double wave_shift(double v, double edge) {
+  const long long b = __double_as_longlong(v), e = __double_as_longlong(edge);
+  constexpr int ctrl = UP ? 0x138 : 0x130;   // wave_shr:1 / wave_shl:1
+  const int lo = __builtin_amdgcn_update_dpp((int)e, (int)b, ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(b >> 32), ctrl, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // One wave sweeps slices; lane = row.  Grid-stride over a fixed grid whose
 // blocks are grouped by XCD (block b runs on XCD b % 8 under the observed
 // round-robin dispatch): each XCD walks one contiguous eighth of the slices in
 // order, so the +-1 / +-n / +-n^2 re-reads of x stay in that XCD's 4 MB L2.
 // Placement only affects speed, never results.  KD > 0 specialises the
 // aligned-offset body for the matrix's dominant slice width.
-template <int MODE, bool NT, int KD, bool SPLIT, int JM = 0, bool VC = false>
+template <int MODE, bool NT, int KD, bool SPLIT, int JM = 0, bool VC = false, int PS = 0>
 __global__ void __launch_bounds__(256) spmv_sell_kernel(
     int64_t m, int64_t ncols, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
@@ -309,24 +359,27 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
     const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
-    const double *__restrict__ vtab_g, int ntab, int ynt) {
+    const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star) {
+  static_assert(PS == 0 || (VC && MODE != SPMV_CG), "row pairs: coded values, plain operand");
   CgTopIn top;
   if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
   else if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // work items: slices, or with PS units of two slices
+  const int64_t nitems = PS ? (nslices + 1) / 2 : nslices;
   int s0, sstep, send;
   if ((gridDim.x & 7) == 0) {
     const int per = gridDim.x >> 3;                 // blocks per XCD group
     const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int chunk = (int)((nslices + 7) >> 3);
+    const int chunk = (int)((nitems + 7) >> 3);
     s0 = xcd * chunk + j * SPMV_WAVES + wid;
     sstep = per * SPMV_WAVES;
-    send = (int)min(nslices, (int64_t)(xcd + 1) * chunk);
+    send = (int)min(nitems, (int64_t)(xcd + 1) * chunk);
   } else {
     s0 = blockIdx.x * SPMV_WAVES + wid;
     sstep = gridDim.x * SPMV_WAVES;
-    send = (int)nslices;
+    send = (int)nitems;
   }
   // operand source
   constexpr bool SC = spmv_scaled(MODE);
@@ -403,7 +456,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       if (MODE == SPMV_CG) dot += xc * sum;
     }
   };
-  for (int s = s0; s < send; s += sstep) {
+  auto one_slice = [&](int s) {
     const int64_t row = (int64_t)s * SLICE + lane;
     const int w = wid_d[s];
     const VS vs = vsrc(s);
@@ -414,7 +467,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       const int k = -w;
       auto mkload = [&]() -> uint32_t { return dmask8 ? (uint32_t)dmask8[row] : dmask[row]; };
       const int dp = dpat[s];
-      const int32_t *__restrict__ off = doff + (int64_t)(dp & (DPAT_INB - 1)) * DIA_MAX;
+      const int32_t *__restrict__ off = doff + (int64_t)(dp & DPAT_ID) * DIA_MAX;
       const int64_t srow = (int64_t)s * SLICE;
       const bool inb = (dp & DPAT_INB) != 0;
       if (KD > 0 && k == KD)
@@ -424,6 +477,77 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       sum = sell_slice<NT>(col_d + sptr_d[s], vs, w, 0.0, X, lane);
     }
     finish(s, sum, o, xc, hc);
+  };
+  if constexpr (PS == 0) {
+    for (int s = s0; s < send; s += sstep) one_slice(s);
+  } else {
+    using SH = PairShape<PS>;
+    constexpr int K = SH::K, NR = SH::NR;
+    constexpr int PB = (2 * K + 15) / 16 * 16;      // code bytes per lane
+    // the dominant pattern's offsets, and each run's anchor (singleton / centre)
+    const int32_t *__restrict__ offs = doff + (int64_t)pat_star * DIA_MAX;
+    int64_t anchor[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) anchor[r] = offs[SH::first(r) + (SH::tri(r) ? 1 : 0)];
+    for (int u = s0; u < send; u += sstep) {
+      const int sa = 2 * u;
+      if (!(dpat[sa] & DPAT_PAIR)) {               // wave-uniform
+        one_slice(sa);
+        if (sa + 1 < nslices) one_slice(sa + 1);
+        continue;
+      }
+      const int64_t ubase = (int64_t)u * 128, r0 = ubase + 2 * lane;
+      // codes, then every x pair and edge value, then the lookups
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 cw[PB / 16];
+      const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)u * 64 + lane) * PB);
+#pragma unroll
+      for (int q = 0; q < PB / 16; ++q) cw[q] = ld<NT>(cp + q);
+      dbl2 L[NR];
+      double e_lo[NR], e_hi[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        L[r] = *reinterpret_cast<const dbl2 *>(x + r0 + anchor[r]);
+        if (SH::tri(r)) {
+          e_lo[r] = x[ubase + anchor[r] - 1];     // row 0 of lane 0: x[r0 + c - 1]
+          e_hi[r] = x[ubase + 128 + anchor[r]];   // row 1 of lane 63: x[r0 + 1 + c + 1]
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      auto code = [&](int i) -> int {            // code i of the lane (row 0: 0..K-1, row 1: K..2K-1)
+        return (cw[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xff;
+      };
+      double lo_m1[NR], hi_p1[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        if (SH::tri(r)) {
+          lo_m1[r] = wave_shift<true>(L[r].y, e_lo[r]);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
+          hi_p1[r] = wave_shift<false>(L[r].x, e_hi[r]);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
+        }
+      double sum0 = 0.0, sum1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int r = SH::run(j), p = SH::pos(j);
+        double a0, a1;                           // operand for row 0 / row 1
+        if (!SH::tri(r)) { a0 = L[r].x; a1 = L[r].y; }
+        else if (p < 0) { a0 = lo_m1[r]; a1 = L[r].x; }
+        else if (p == 0) { a0 = L[r].x; a1 = L[r].y; }
+        else { a0 = L[r].y; a1 = hi_p1[r]; }
+        if constexpr (SC) { a0 = xs * a0; a1 = xs * a1; }
+        const int c0 = code(j), c1 = code(K + j);
+        const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
+        sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
+        sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
+      }
+      double o0 = sum0, o1 = sum1;
+      if constexpr (spmv_jac(MODE)) { o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1); }
+      if (ynt) __builtin_nontemporal_store(dbl2{o0, o1}, reinterpret_cast<dbl2 *>(y + r0));
+      else *reinterpret_cast<dbl2 *>(y + r0) = dbl2{o0, o1};
+      if constexpr (MODE == SPMV_DOT) {          // x at the own rows = the centre run's pair
+        dot += L[SH::CENTER_RUN].x * sum0;
+        dot += L[SH::CENTER_RUN].y * sum1;
+      }
+    }
   }
   if (MODE == SPMV_DOT || MODE == SPMV_CG) {
     double v[1] = {dot};
@@ -454,10 +578,12 @@ int spmv_blocks(const Mat *A, int) {
 // this grid, ~2x at a 4.6-generation grid) and no second generation leaves a
 // tail.  Blocks per CU: the occupancy API, capped at 6 (knob 26): the kernels
 // hold 106 SGPRs, which allow 6 waves per SIMD, while the API reports one
-// more at that count (MI355X guide, correctness boundaries).  SPMV_CG
+// more at that count (MI355X guide, correctness boundaries).  The row-pair
+// kernels stream twice the rows per wave and do best at 4 (knob 28; 256^3:
+// 82 us at 4, 87 at 5, 93 at 6).  SPMV_CG
 // evaluates the iteration's scalar top once per workgroup, so it keeps >= 4
 // slices per wave.  Knob 3 > 0 overrides the grid.
-static int main_grid(const Mat *A, int mode, const void *kf) {
+static int main_grid(const Mat *A, int mode, const void *kf, bool pairs) {
   const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
   int64_t g;
   if (g_knobs.spmv_grid > 0) {
@@ -470,7 +596,12 @@ static int main_grid(const Mat *A, int mode, const void *kf) {
       HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kf, 256, 0));
       it = bpc_of.emplace(kf, std::max(1, b)).first;
     }
-    g = (int64_t)std::min(it->second, std::max(1, g_knobs.spmv_bpc)) * device_cus();
+    const int cap = pairs ? g_knobs.spmv_pair_bpc : g_knobs.spmv_bpc;
+    g = (int64_t)std::min(it->second, std::max(1, cap)) * device_cus();
+    // one workgroup fewer per XCD: a per-XCD wave count that is a multiple of
+    // 256 (grids of 1024 / 1536) puts the concurrent x streams on aliasing
+    // strides -- measured +35..+80% MatMult time (tools/op_ab.py)
+    if (g > 64) g -= 8;
   }
   g = std::min<int64_t>(g, need);
   if (mode == SPMV_CG) g = std::min<int64_t>(g, std::max<int64_t>(512, need / 4));
@@ -573,7 +704,8 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
 #define SPMV_ARGS                                                                           \
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
-      partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt
+      partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt, \
+      A->sd.pcode.p, A->sd.pat_star
   using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
   KFn kf = nullptr;
 #define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>
@@ -591,10 +723,18 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
     if (vcode) SPMV_KD(SPMV_CG, true, SP, JM, true);                       \
     else SPMV_KD(SPMV_CG, true, SP, JM, false);                            \
   } while (0)
-  // code blocks are always read non-temporally
+  // code blocks are always read non-temporally; row pairs when the matrix has them
+  const int ps = vcode && g_knobs.spmv_pairs ? A->sd.pair_shape : 0;
+#define SPMV_PS(MODE, SP)                                                                         \
+  do {                                                                                            \
+    if (ps == 5) kf = &spmv_sell_kernel<MODE, true, 5, SP, 0, true, 5>;                           \
+    else if (ps == 7) kf = &spmv_sell_kernel<MODE, true, 7, SP, 0, true, 7>;                      \
+    else kf = &spmv_sell_kernel<MODE, true, 27, SP, 0, true, 27>;                                 \
+  } while (0)
 #define SPMV_GO(MODE)                                                         \
   do {                                                                        \
-    if (vcode) { if (split) SPMV_KD(MODE, true, true, 0, true); else SPMV_KD(MODE, true, false, 0, true); } \
+    if (ps) { if (split) SPMV_PS(MODE, true); else SPMV_PS(MODE, false); }   \
+    else if (vcode) { if (split) SPMV_KD(MODE, true, true, 0, true); else SPMV_KD(MODE, true, false, 0, true); } \
     else if (split) { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, true, 0, false); else SPMV_KD(MODE, false, true, 0, false); } \
     else { if (g_knobs.spmv_nt) SPMV_KD(MODE, true, false, 0, false); else SPMV_KD(MODE, false, false, 0, false); }     \
   } while (0)
@@ -614,11 +754,12 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
       break;
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
-  const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf));
+  const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf), ps != 0 && mode != SPMV_CG);
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   kf<<<grid, 256, 0, st>>>(SPMV_ARGS);
 #undef SPMV_GO
+#undef SPMV_PS
 #undef SPMV_CGKD
 #undef SPMV_KD
 #undef SPMV_KDU

@@ -47,7 +47,7 @@ class MatInfo(C.Structure):
                 ("nnz_o", C.c_int64), ("nghost", C.c_int64), ("sell_slots_d", C.c_int64),
                 ("sell_slots_o", C.c_int64), ("nsend_peers", C.c_int), ("nrecv_peers", C.c_int),
                 ("nsend", C.c_int64), ("nrecv", C.c_int64), ("dia_slices", C.c_int64),
-                ("value_codes", C.c_int64), ("code_bytes", C.c_int64)]
+                ("value_codes", C.c_int64), ("code_bytes", C.c_int64), ("pair_shape", C.c_int64)]
 
 
 P = C.c_void_p
@@ -119,6 +119,10 @@ def load():
         fn.argtypes = args
     if lib.mx_version() != 1:
         raise ImportError("libmxsolve ABI version mismatch")
+    # diagnostics / A/B runs: MXSOLVE_KNOBS="27=0+3=8192" (mx_debug_set keys, include/mxsolve.h)
+    for kv in filter(None, os.environ.get("MXSOLVE_KNOBS", "").split("+")):
+        k, v = kv.split("=")
+        lib.mx_debug_set(int(k), int(v))
     _lib = lib
     return lib
 

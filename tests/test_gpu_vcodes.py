@@ -122,6 +122,7 @@ def test_cg_with_and_without_codes(selfcomm):
     from mxsolve.core import DMat, rhs_hash
     L = lib()
     res = []
+    old27 = L.mx_debug_set(27, 0)          # single-row layout in both (same dot grouping)
     for knob in (0, 1):
         old = L.mx_debug_set(23, knob)
         try:
@@ -134,6 +135,45 @@ def test_cg_with_and_without_codes(selfcomm):
             res.append((r["its"], r["reason"], x.cpu().numpy().copy(), A.info()["value_codes"]))
         finally:
             L.mx_debug_set(23, old)
+    L.mx_debug_set(27, old27)
     assert res[0][3] == 0 and res[1][3] > 0
     assert res[0][:2] == res[1][:2]
     assert np.array_equal(res[0][2].view(np.uint64), res[1][2].view(np.uint64))
+
+
+@pytest.mark.parametrize("kind,n,shape", [("poisson2d", 38, 5), ("poisson3d", 24, 7), ("poisson3d27", 24, 27),
+                                          ("convdiff3d", 12, 7), ("poisson3d", 19, 0)])
+def test_row_pairs(selfcomm, oracle_mod, kind, n, shape):
+    """Row-pair layout (even stencil offsets): MatMult bit-exact with pairs on
+    and off; n = 19 (odd offsets) keeps the single-row layout."""
+    ip, c, v = oracle_mod.stencil(kind, n)
+    L = lib()
+    old = L.mx_debug_set(27, 0)
+    try:
+        info0, got0, exp = mult_bits(selfcomm, oracle_mod, ip.size - 1, ip, c, v, seed=11)
+    finally:
+        L.mx_debug_set(27, old)
+    info1, got1, _ = mult_bits(selfcomm, oracle_mod, ip.size - 1, ip, c, v, seed=11)
+    assert info0["pair_shape"] == 0 and info1["pair_shape"] == shape
+    assert np.array_equal(got0, exp) and np.array_equal(got1, exp)
+
+
+@pytest.mark.parametrize("kind,n,ksp", [("poisson3d", 24, "cg"), ("poisson3d27", 24, "cg"),
+                                        ("poisson2d", 38, "cg"), ("convdiff3d", 12, "gmres")])
+def test_row_pairs_solve(selfcomm, oracle_mod, kind, n, ksp):
+    """CG (MatMult + dot) and GMRES (Jacobi-scaled, lazily normalised operand)
+    on the row-pair path against the oracle."""
+    from mxsolve.core import DMat
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+    assert A.info()["pair_shape"] > 0
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    b = np.random.default_rng(5).random(M)
+    bt = torch.from_numpy(b).cuda()
+    x = torch.zeros(M, dtype=torch.float64, device="cuda")
+    r = A.solve(bt, x, ksp=ksp, rtol=1e-8)
+    o = O.solve(b, ksp=ksp, rtol=1e-8)
+    assert r["reason"] == o["reason"] and abs(r["its"] - o["its"]) <= 1
+    xs = x.cpu().numpy()
+    assert np.linalg.norm(xs - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
