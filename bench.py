@@ -36,6 +36,18 @@ def spmv_bytes(m: int, nnz: int, nghost: int) -> int:
     return 12 * nnz + 4 * (m + 1) + 8 * (m + nghost) + 8 * m
 
 
+def spmv_format_bytes(info: dict, m: int, nnz: int, nghost: int) -> int:
+    """Algorithmic bytes of one SpMV in the layout the rank actually streams
+    (DESIGN.md §4): with value codes, one code byte per stored slot (8 B/row for
+    <= 8 offsets, 32 for 27) instead of 12 B/nnz, x (local + ghosts) read once,
+    y written once, 16 B of slice metadata per 64 rows, A_o as 12 B/nnz;
+    without codes, SURVEY.md §8d's CSR bytes."""
+    if not info.get("value_codes"):
+        return spmv_bytes(m, nnz, nghost)
+    return (info["code_bytes"] + 8 * (m + nghost) + 8 * m + 16 * ((m + 63) // 64)
+            + 12 * info["nnz_o"] + 4 * (m + 1) * (info["nnz_o"] > 0))
+
+
 def cg_iter_bytes(m: int, nnz: int, nghost: int) -> int:
     """SURVEY.md §8d's "fused minimum" CG iteration: SpMV + 88 B/row of vector traffic."""
     return spmv_bytes(m, nnz, nghost) + 88 * m
@@ -57,7 +69,7 @@ def cg_iter_bytes_design(m: int, nnz: int, nghost: int, mode: int) -> int:
 
 def fusion_mode(knob: int, m: int) -> int:
     """The mode cg_solve runs for knob 9 (3 = auto, mx_ksp.hip)."""
-    return (1 if m <= (6 << 20) else 2) if knob == 3 else knob
+    return (1 if m <= (3 << 20) else 2) if knob == 3 else knob
 
 
 def cpu_baseline(grid: int, budget_s: float, threads: int) -> dict:
@@ -199,9 +211,10 @@ def main():
     x.zero_()
     rp = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=min(args.steps, 100), profile=True)
     spmv_avg_ms = rp["spmv_ms"] / max(rp["spmv_count"], 1)
-    bytes_spmv = spmv_bytes(m, nnz_loc, ng)
+    bytes_csr = spmv_bytes(m, nnz_loc, ng)
+    bytes_spmv = spmv_format_bytes(info, m, nnz_loc, ng)
     mode = fusion_mode(fknob, m)
-    bytes_launch = cg_spmv_bytes(m, nnz_loc, ng) if mode == 1 else bytes_spmv
+    bytes_launch = bytes_spmv + (32 * m if mode == 1 else 0)   # SPMV_CG: + r, x r/w, p_i
     achieved = bytes_launch / (spmv_avg_ms * 1e-3) / 1e9
     # standalone SpMV timing (same kernel, back-to-back)
     y = comm.empty(m)
@@ -265,17 +278,23 @@ def main():
                          "traffic_detail": traffic,
                          "kernel": ("spmv_sell_kernel<SPMV_CG> (CG-fused MatMult" if mode == 1 else
                                     "spmv_sell_kernel<SPMV_DOT> (CG MatMult") + ", HIP events, rank 0)",
-                         "bytes_per_launch": bytes_launch, "avg_launch_ms": round(spmv_avg_ms, 5)},
+                         "bytes_per_launch": bytes_launch, "avg_launch_ms": round(spmv_avg_ms, 5),
+                         "format": ("value codes (" + str(info.get("value_codes")) + " distinct), " +
+                                    ("row pairs" if info.get("pair_shape") else "one row per lane"))
+                                   if info.get("value_codes") else "fp64 SELL-64",
+                         "csr_equiv_GBps": round((bytes_csr + (32 * m if mode == 1 else 0)) / (spmv_avg_ms * 1e-3) / 1e9, 1)},
             "cpu_baseline": cpu,
             "spmv_standalone": {"avg_ms": round(spmv_alone_ms, 5),
                                 "GBps": round(bytes_spmv / (spmv_alone_ms * 1e-3) / 1e9, 1),
+                                "csr_equiv_GBps": round(bytes_csr / (spmv_alone_ms * 1e-3) / 1e9, 1),
                                 "matmult_ms": round(mult_ms, 5),
                                 "cold_matmult_ms": round(cold_ms, 5),
                                 "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1)},
             "cg_iter_bytes_survey": cg_iter_bytes(m, nnz_loc, ng),
             "cg_fusion_mode": mode,
-            "cg_iter_bytes_alg": cg_iter_bytes_design(m, nnz_loc, ng, mode),
-            "cg_iter_GBps_alg": round(cg_iter_bytes_design(m, nnz_loc, ng, mode) * value / 1e9, 1),
+            "cg_iter_bytes_alg": cg_iter_bytes_design(m, nnz_loc, ng, mode) - bytes_csr + bytes_spmv,
+            "cg_iter_GBps_alg": round((cg_iter_bytes_design(m, nnz_loc, ng, mode) - bytes_csr + bytes_spmv)
+                                      * value / 1e9, 1),
             "comm_latency": comm_lat,
             "solve": solve,
         }

@@ -201,7 +201,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
 
 /* ---- measurement knobs (A/B runs only; defaults are the product path) -------
  * key 1: SpMV non-temporal matrix loads (0/1, default 1)
- * key 3: SpMV grid size in workgroups (default 8192)
+ * key 3: SpMV grid size in workgroups (0 = default: one resident generation,
+ *        see keys 26 / 28, one workgroup fewer per XCD)
  * key 4: aligned-offset (DIA-in-SELL) slices at assembly (0/1, default 1)
  * key 5: uniform-diagonal Jacobi applied as one scalar (0/1, default 1)
  * key 6: halo exchange overlapping the interior slices when P > 1 (0/1, default 1)
@@ -212,7 +213,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        RCCL communicator (testing, default 0)
  * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
- *        1 for <= 6M local rows, else 2)
+ *        1 for <= 3M local rows, else 2)
  * key 10: where CG folds its per-workgroup partials: 0 one-block fold kernels;
  *        1 the update pass folds its own inside the launch, and the MatMult's
  *        halo-boundary launch when the product is split (default); 2 the
@@ -233,6 +234,14 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 21: CG vector passes issue four steps' loads together: 0 never, 1 always,
  *         2 auto (default: up to 6M local rows)
  * key 22: grid cap of the CG update pass (0 = default 1024 workgroups)
+ * key 23: value codes -- one byte per slot into a table of <= 255 distinct
+ *         values -- for the diagonal block (read at assembly and at launch;
+ *         0/1, default 1)
+ * key 25: non-temporal y stores in the SpMV (0/1, default 0)
+ * key 26: resident workgroups per CU for the single-row SpMV grid (default 6)
+ * key 27: row-pair SpMV layout for 5/7/27-point patterns (read at assembly and
+ *         at launch; 0/1, default 1)
+ * key 28: resident workgroups per CU for the row-pair SpMV grid (default 4)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

@@ -37,7 +37,8 @@
 namespace mx {
 
 constexpr int MAX_RESTART = 1000;
-constexpr int64_t CG_FUSE_MAX_ROWS = int64_t(6) << 20;   // auto CG fusion: mode 1 up to here
+constexpr int64_t CG_FUSE_MAX_ROWS = int64_t(3) << 20;   // auto CG fusion: mode 1 up to here
+constexpr int64_t CG_UNROLL_MAX_ROWS = int64_t(6) << 20;  // auto 4-step load batching up to here
 
 // ------------------------------------------------------------------ shared scalar logic
 // KSPConvergedDefault (KSPConvergedSkip when the norm type is NONE).
@@ -784,9 +785,9 @@ static unsigned cg_vec_grid(int64_t n, bool paired, int dflt) {
 }
 
 // four-step load batches in the row walk (knob 21): 2 = auto, on up to
-// CG_FUSE_MAX_ROWS rows (-3% per iteration at 2M rows/rank; +5% at 256^3)
+// CG_UNROLL_MAX_ROWS rows (-3% per iteration at 2M rows/rank; +5% at 256^3)
 static int cg_unroll(int64_t n) {
-  return g_knobs.cg_unroll == 2 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 0) : g_knobs.cg_unroll;
+  return g_knobs.cg_unroll == 2 ? (n <= CG_UNROLL_MAX_ROWS ? 1 : 0) : g_knobs.cg_unroll;
 }
 
 // direction update (+ the deferred x step when x != null)
@@ -881,7 +882,9 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // iteration on 256 x 256 x nz ranks (tools/cg_ab.py, interleaved): nz 32
   // modes 0/1/2 within 1.3% (1 best); nz 128: 2 -3.4% and 1 +3.8% vs 0;
   // 256^3: 2 -6%, 1 +2%.  Mode 1's two-vector gathers overflow the per-XCD
-  // L2 at large ranks
+  // L2 at large ranks.  With the row-pair MatMult (value codes): nz 32 mode 1
+  // 55.6 / mode 2 56.8 us, nz 64 88.1 / 83.3, nz 128 151.5 / 137.0, 256^3
+  // 304 / 268 -- hence the 3M-row threshold
   const int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
   const bool fuse_cg = fmode == 1;
   const bool defer_x = fmode != 0;

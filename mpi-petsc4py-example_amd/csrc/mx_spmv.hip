@@ -53,6 +53,11 @@ struct XPlainT {
   __device__ __forceinline__ double at(int64_t base, int lane) const {
     return S ? s * (x + base)[lane] : (x + base)[lane];
   }
+  // the operand at i and i + 1 (i even: one 16-byte load)
+  __device__ __forceinline__ dbl2 pair(int64_t i) const {
+    const dbl2 v = *reinterpret_cast<const dbl2 *>(x + i);
+    return S ? dbl2{s * v.x, s * v.y} : v;
+  }
 };
 using XPlain = XPlainT<false>;
 // JM = the Jacobi form, compile-time so every load is unconditional (a
@@ -76,6 +81,11 @@ struct XCg {
   }
   __device__ __forceinline__ double at(int64_t base, int lane) const {
     return form((r + base)[lane], (p + base)[lane], JM == 1 ? (d + base)[lane] : 0.0);
+  }
+  __device__ __forceinline__ dbl2 pair(int64_t i) const {
+    const dbl2 rv = *reinterpret_cast<const dbl2 *>(r + i), pv = *reinterpret_cast<const dbl2 *>(p + i);
+    const dbl2 dv = JM == 1 ? *reinterpret_cast<const dbl2 *>(d + i) : dbl2{0.0, 0.0};
+    return dbl2{form(rv.x, pv.x, dv.x), form(rv.y, pv.y, dv.y)};
   }
 };
 
@@ -360,7 +370,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
     const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
     const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star) {
-  static_assert(PS == 0 || (VC && MODE != SPMV_CG), "row pairs: coded values, plain operand");
+  static_assert(PS == 0 || VC, "row pairs: coded values");
   CgTopIn top;
   if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
   else if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
@@ -507,10 +517,10 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       double e_lo[NR], e_hi[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
-        L[r] = *reinterpret_cast<const dbl2 *>(x + r0 + anchor[r]);
+        L[r] = X.pair(r0 + anchor[r]);           // the operand (scaled / formed as the mode has it)
         if (SH::tri(r)) {
-          e_lo[r] = x[ubase + anchor[r] - 1];     // row 0 of lane 0: x[r0 + c - 1]
-          e_hi[r] = x[ubase + 128 + anchor[r]];   // row 1 of lane 63: x[r0 + 1 + c + 1]
+          e_lo[r] = X(ubase + anchor[r] - 1);     // row 0 of lane 0: x[r0 + c - 1]
+          e_hi[r] = X(ubase + 128 + anchor[r]);   // row 1 of lane 63: x[r0 + 1 + c + 1]
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -533,7 +543,6 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         else if (p < 0) { a0 = lo_m1[r]; a1 = L[r].x; }
         else if (p == 0) { a0 = L[r].x; a1 = L[r].y; }
         else { a0 = L[r].y; a1 = hi_p1[r]; }
-        if constexpr (SC) { a0 = xs * a0; a1 = xs * a1; }
         const int c0 = code(j), c1 = code(K + j);
         const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
         sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
@@ -543,7 +552,17 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       if constexpr (spmv_jac(MODE)) { o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1); }
       if (ynt) __builtin_nontemporal_store(dbl2{o0, o1}, reinterpret_cast<dbl2 *>(y + r0));
       else *reinterpret_cast<dbl2 *>(y + r0) = dbl2{o0, o1};
-      if constexpr (MODE == SPMV_DOT) {          // x at the own rows = the centre run's pair
+      if constexpr (MODE == SPMV_CG) {
+        // p_i at the own rows is the centre run's pair: store it, and the
+        // previous step's deferred VecAXPY(X, a, P) on the own rows
+        *reinterpret_cast<dbl2 *>(cg.pnew + r0) = L[SH::CENTER_RUN];
+        if (xpend) {
+          const dbl2 po = *reinterpret_cast<const dbl2 *>(cg.pold + r0);
+          const dbl2 xo = *reinterpret_cast<const dbl2 *>(cg.x + r0);
+          *reinterpret_cast<dbl2 *>(cg.x + r0) = dbl2{fma(xa, po.x, xo.x), fma(xa, po.y, xo.y)};
+        }
+      }
+      if constexpr (MODE == SPMV_DOT || MODE == SPMV_CG) {   // operand at the own rows = the centre pair
         dot += L[SH::CENTER_RUN].x * sum0;
         dot += L[SH::CENTER_RUN].y * sum1;
       }
@@ -718,10 +737,13 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
       default: SPMV_KDU(MODE, NT, SP, JM, VC, 0); break;                                              \
     }                                                                                                 \
   } while (0)
-#define SPMV_CGKD(JM, SP)                                                  \
-  do {                                                                     \
-    if (vcode) SPMV_KD(SPMV_CG, true, SP, JM, true);                       \
-    else SPMV_KD(SPMV_CG, true, SP, JM, false);                            \
+#define SPMV_CGKD(JM, SP)                                                                    \
+  do {                                                                                       \
+    if (ps == 5) kf = &spmv_sell_kernel<SPMV_CG, true, 5, SP, JM, true, 5>;                  \
+    else if (ps == 7) kf = &spmv_sell_kernel<SPMV_CG, true, 7, SP, JM, true, 7>;             \
+    else if (ps == 27) kf = &spmv_sell_kernel<SPMV_CG, true, 27, SP, JM, true, 27>;          \
+    else if (vcode) SPMV_KD(SPMV_CG, true, SP, JM, true);                                    \
+    else SPMV_KD(SPMV_CG, true, SP, JM, false);                                              \
   } while (0)
   // code blocks are always read non-temporally; row pairs when the matrix has them
   const int ps = vcode && g_knobs.spmv_pairs ? A->sd.pair_shape : 0;
@@ -754,7 +776,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
       break;
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
-  const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf), ps != 0 && mode != SPMV_CG);
+  const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf), ps != 0);
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   kf<<<grid, 256, 0, st>>>(SPMV_ARGS);

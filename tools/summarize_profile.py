@@ -57,7 +57,11 @@ def main():
     m = grid ** 3 // ngpu
     nnz = 7 * grid ** 3 - 6 * grid ** 2
     ghosts = 0 if ngpu == 1 else (grid * grid * (1 if ngpu == 2 else 2))
-    spmv_alg = 12 * nnz // ngpu + 4 * (m + 1) + 8 * (m + ghosts) + 8 * m
+    # the streamed layout's bytes (bench.py spmv_format_bytes): value codes at one
+    # byte per slot (7 offsets -> 8 B/row), x once, y once, slice metadata, A_o;
+    # SURVEY.md §8d's CSR figure in csr_bytes
+    csr_bytes = 12 * nnz // ngpu + 4 * (m + 1) + 8 * (m + ghosts) + 8 * m
+    spmv_alg = 8 * m + 8 * (m + ghosts) + 8 * m + 16 * ((m + 63) // 64) + (12 * ghosts + 4 * (m + 1) if ghosts else 0)
     alg = spmv_alg + 32 * m          # SPMV_CG: + r read, x read/write, p_i write
     out = {}
     lines = [f"# {tag}: rocprofv3 summary (3D 7-pt Poisson {grid}^3, N={ngpu}, bench.py --steps 50)", "",
@@ -84,7 +88,7 @@ def main():
             "bytes_per_launch": round(traffic), "fetch_bytes_raw": round(fr), "write_bytes": round(wr),
             "fetch_correction": round(corr, 4), "calib_8B_per_lane": f8 and round(f8, 4),
             "calib_16B_per_lane": f16 and round(f16, 4), "algorithmic_bytes": alg,
-            "traffic_over_algorithmic": round(traffic / alg, 4), "kernel": sp,
+            "traffic_over_algorithmic": round(traffic / alg, 4), "kernel": sp, "csr_bytes": csr_bytes,
             "median_launch_us": round(statistics.median(durs[sp]), 1) if sp in durs else None,
             "source": f"profiles/{tag}_summary.md"}
         lines += ["", f"{sp} per launch: FETCH_SIZE {fr/1e6:.1f} MB raw x {corr:.3f} (calibrated, 16 B/lane NT stream; "
