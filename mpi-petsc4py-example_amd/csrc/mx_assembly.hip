@@ -811,10 +811,17 @@ __global__ void vdict_insert_kernel(int64_t ns, const int64_t *__restrict__ sptr
   const int w = wr < 0 ? -wr : wr;
   const int64_t row = s * SLICE + lane;
   const uint32_t mk = wr >= 0 ? 0u : (mask8 ? (uint32_t)mask8[row] : mask[row]);
+  unsigned long long last = VDICT_EMPTY;
   for (int j = 0; j < w; ++j) {
     const int64_t t = sell_slot(sptr[s], j, w, lane, true);
-    if (!slot_stored(wr, mk, col, t, j)) continue;
-    if (!vdict_insert(tab, st, (unsigned long long)__double_as_longlong(sval[t]))) { st[1] = 1; return; }
+    const bool stored = slot_stored(wr, mk, col, t, j);
+    const unsigned long long k = stored ? (unsigned long long)__double_as_longlong(sval[t]) : VDICT_EMPTY;
+    // a stencil slot holds one value across the wave: lane 0 alone inserts it
+    const unsigned long long k0 = __shfl(k, 0, 64);
+    const bool uniform = __all(k == k0 || !stored);
+    if (!stored || k == last || (uniform && lane != 0 && k0 != VDICT_EMPTY)) continue;
+    last = k;
+    if (!vdict_insert(tab, st, k)) { st[1] = 1; return; }
   }
 }
 
