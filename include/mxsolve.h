@@ -242,6 +242,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 27: row-pair SpMV layout for 5/7/27-point patterns (read at assembly and
  *         at launch; 0/1, default 1)
  * key 28: resident workgroups per CU for the row-pair SpMV grid (default 4)
+ * key 29: CG mode 2 applies the deferred x steps every B iterations from B
+ *         rotating direction buffers (1, 2 or 4; default 2)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

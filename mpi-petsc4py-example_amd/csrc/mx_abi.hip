@@ -464,6 +464,7 @@ int mx_debug_set(int key, int value) {
     case 26: old = g_knobs.spmv_bpc; g_knobs.spmv_bpc = value; break;
     case 27: old = g_knobs.spmv_pairs; g_knobs.spmv_pairs = value; break;
     case 28: old = g_knobs.spmv_pair_bpc; g_knobs.spmv_pair_bpc = value; break;
+    case 29: old = g_knobs.cg_xbatch; g_knobs.cg_xbatch = value; break;
     default: break;
   }
   return old;

@@ -41,6 +41,10 @@ struct CgTopIn {
   double betas[2];          // parity slots: beta_i in betas[i & 1]
   double ttol, atol, dtol, rnorm0;
   double xa, xpend;         // deferred x step (CG modes 1/2): x += xa p_{xi} while xpend != 0
+  // mode 2 with batched x steps (knob 29 = B > 1): the steps of directions
+  // [xlo, xhi) are pending, alpha_j in xal[j % B], p_j in buffer j % B
+  double xal[4];
+  int xlo, xhi;
 };
 
 // Device-resident solver state (one allocation, zeroed then parameterised at

@@ -293,6 +293,75 @@ __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restri
   }
 }
 
+// Mode 2 with the x steps batched over B iterations (knob 29): direction p_i
+// lives in buffer i % B, so p_{i-1} .. p_{i-B} are all still in memory when
+// p_i is formed; every B-th iteration (i % B == 0) applies the B pending steps
+// x = fma(a_{i-1}, p_{i-1}, ... fma(a_{i-B}, p_{i-B}, x)) -- the same FMAs in
+// the same order as one VecAXPY per iteration -- before p_i overwrites p_{i-B}.
+// x is read and written once per B iterations instead of every iteration.
+struct PBufs { double *b[4]; };
+template <int JM, int B>
+__global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
+                                                    const double *__restrict__ dv, const double dc,
+                                                    double *__restrict__ p0, double *__restrict__ p1,
+                                                    double *__restrict__ p2, double *__restrict__ p3,
+                                                    double *__restrict__ x, double *__restrict__ hist, const int unr) {
+  const CgTopIn top = s->top;
+  if (top.done) return;
+  const CgTop t = cg_top(top);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(s, t, hist);
+  if (t.reason) return;
+  const int i = t.i;
+  const double b = t.b;
+  // buffers picked by wave-uniform selects (pointers stay scalar; an indexed
+  // pointer array went through scratch and serialised the loop)
+  auto pick = [&](int k) -> double * { return k == 0 ? p0 : k == 1 ? p1 : k == 2 ? p2 : p3; };
+  auto row = [&](double rr, double dd, double po) {
+    const double z = jac1<JM>(rr, dd, dc);
+    return (b == 0.0) ? z : z + b * po;          // VecAYPX_Seq (b == 0 copies)
+  };
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // the pending steps are exactly [i - B, i) when i % B == 0 (the update pass
+  // keeps that invariant): p_{i-B+q} sits in buffer q, alpha in xal[q].  p_{i-B}
+  // is read through the output pointer before p_i is stored over it, so every
+  // pointer is distinct and __restrict__ holds
+  if ((i % B) == 0 && top.xhi == i && top.xlo == i - B) {
+    double al[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) al[q] = top.xal[q];
+    double *__restrict__ pout = p0;
+    const double *__restrict__ pprev = B == 4 ? p3 : p1;
+    for (; k < n; k += stride) {
+      const double po = pprev[k];
+      double xx = fma(al[0], pout[k], x[k]);     // x += a_{i-B} p_{i-B}, oldest first
+      if constexpr (B == 4) {
+        xx = fma(al[1], p1[k], xx);
+        xx = fma(al[2], p2[k], xx);
+      }
+      x[k] = fma(al[B - 1], po, xx);             // ... x += a_{i-1} p_{i-1}
+      pout[k] = row(r[k], JM == 1 ? dv[k] : 0.0, po);
+    }
+    return;
+  }
+  const double *__restrict__ pprev = pick((i + B - 1) % B);   // p_{i-1} (unused at i = 0: b = 0)
+  double *__restrict__ pout = pick(i % B);
+  if (unr) {                                     // four steps' loads issued together
+    for (; k + 3 * stride < n; k += 4 * stride) {
+      double po[4], rr[4], dd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        po[u] = pprev[k + u * stride];
+        rr[u] = r[k + u * stride];
+        dd[u] = JM == 1 ? dv[k + u * stride] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) pout[k + u * stride] = row(rr[u], dd[u], po[u]);
+    }
+  }
+  for (; k < n; k += stride) pout[k] = row(r[k], JM == 1 ? dv[k] : 0.0, pprev[k]);
+}
+
 // dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
 // Read-only; cg_update_kernel's workgroup 0 commits it.
 struct CgAlpha { int i, reason; double dpi, alpha; };
@@ -325,7 +394,7 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
                                                         const double *__restrict__ dv, const double dc,
                                                         double *__restrict__ partials, const Fold fold,
                                                         const int nts, const double *__restrict__ dot_part,
-                                                        const int ndot, const int unr) {
+                                                        const int ndot, const int unr, const int xb) {
   if (s->top.done) return;
   // p.w: folded and all-reduced before this launch, or (one rank) folded here
   // by every workgroup from the MatMult's partials, in fold_kernel's order
@@ -335,12 +404,19 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
     s->dpi = al.dpi;
     s->red1 = pw;
     s->top.xpend = 0.0;            // a deferred step of i-1 was applied by this iteration's first kernel
+    // batched x steps: this iteration's cg_pb applied [i - B, i) when i % B == 0
+    // (also when this pass stops the solve, so the finish pass does not repeat them)
+    if (xb > 1 && al.i % xb == 0) s->top.xlo = al.i;
     if (al.reason) {
       stop(s, al.reason);
     } else {
       s->dpis[al.i & 1] = al.dpi;
       s->alpha = al.alpha;
       if (!XU) { s->top.xa = al.alpha; s->top.xpend = 1.0; s->xi = al.i; }
+      if (xb > 1) {                // the step of direction i joins the pending batch
+        s->top.xal[al.i % xb] = al.alpha;
+        s->top.xhi = al.i + 1;
+      }
       s->top.it_u = al.i + 1;
     }
   }
@@ -445,6 +521,19 @@ __global__ void cg_finish_x_kernel(int64_t n, const KspState *__restrict__ s, co
   const double *__restrict__ p = (s->xi & 1) ? p1 : p0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = fma(a, p[i], x[i]);
+}
+
+// the batched x steps still pending when the solve stopped, oldest first
+__global__ void cg_finish_xb_kernel(int64_t n, const KspState *__restrict__ s, const PBufs pb, int B,
+                                    double *__restrict__ x) {
+  const int j0 = s->top.xlo, np = s->top.xhi - s->top.xlo;
+  if (np <= 0) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double xx = x[i];
+    for (int q = 0; q < np; ++q) xx = fma(s->top.xal[(j0 + q) % B], pb.b[(j0 + q) % B][i], xx);
+    x[i] = xx;
+  }
 }
 
 // ------------------------------------------------------------------ GMRES kernels
@@ -805,10 +894,23 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
   HIPCHECK(hipGetLastError());
 }
 
+static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r, const Jac &j, const PBufs &pb,
+                         int B, double *x, double *hist) {
+  const unsigned g = cg_vec_grid(n, false, 8192);
+  const int unr = cg_unroll(n);
+#define CGPB(JM, BB) cg_pb_kernel<JM, BB><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], pb.b[3], \
+                                                           x, hist, unr)
+#define CGPB_J(JM) do { if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
+  switch (j.mode) { case 1: CGPB_J(1); break; case 2: CGPB_J(2); break; default: CGPB_J(0); }
+#undef CGPB_J
+#undef CGPB
+  HIPCHECK(hipGetLastError());
+}
+
 // update pass; returns its grid (= partials per value)
 static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double *p, const double *w, double *x,
                             double *r, const Jac &j, double *partials, const Fold &fold_in,
-                            const double *dot_part, int ndot) {
+                            const double *dot_part, int ndot, int xb) {
   const bool vec = g_knobs.cg_vec && aligned16({p, w, x, r, j.d});
   const unsigned g = g_knobs.cg_upd_grid > 0 ? grid_for(n, 256, g_knobs.cg_upd_grid)
                                              : cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : RED_BLOCKS);
@@ -817,7 +919,7 @@ static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double
   const int unr = cg_unroll(n);
   f.base = 0;
 #define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f, \
-                                                                        g_knobs.cg_nts, dot_part, ndot, unr)
+                                                                        g_knobs.cg_nts, dot_part, ndot, unr, xb)
 #define CGU_J(JM) do { if (x) { if (vec) CGU(JM, true, true); else CGU(JM, true, false); } \
                        else { if (vec) CGU(JM, false, true); else CGU(JM, false, false); } } while (0)
   switch (j.mode) { case 1: CGU_J(1); break; case 2: CGU_J(2); break; default: CGU_J(0); }
@@ -838,9 +940,18 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // MatMult partials (+ boundary launch), then the update pass's 3 per workgroup
   const size_t npart = (size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 3 * (size_t)CG_MAX_VEC_GRID + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
-  Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist})));
+  // mode 2 batches B x steps (knob 29; 2 or 4 p buffers) when the batch of
+  // launched iterations (poll) is a multiple of B; 1 = the x step every iteration
+  const int poll = p.poll_every > 0 ? p.poll_every : 16;
+  const int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
+  const int xb = (fmode == 2 && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 4) && poll % g_knobs.cg_xbatch == 0)
+                     ? g_knobs.cg_xbatch : 1;
+  Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist, xb == 4 ? nv : 0, xb == 4 ? nv : 0})));
   struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
   double *pv2 = cv.take(nv);   // fused CG: p_i alternates between pv (i even) and pv2
+  double *pv3 = xb == 4 ? cv.take(nv) : pv.p;
+  double *pv4 = xb == 4 ? cv.take(nv) : pv2;
+  const PBufs pbs{{pv.p, pv2, pv3, pv4}};
   struct { KspState *p; } sd{state_buf(A)};
   KspState hs;
   init_state(hs, p, normtype);
@@ -868,7 +979,6 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   else cg_init_kernel<3><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
   HIPCHECK(hipGetLastError());
 
-  const int poll = p.poll_every > 0 ? p.poll_every : 16;
   Poller poller(st);
   int i = 0;
   const unsigned egrid = grid_for(n, 256, 8192);
@@ -885,7 +995,6 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // L2 at large ranks.  With the row-pair MatMult (value codes): nz 32 mode 1
   // 55.6 / mode 2 56.8 us, nz 64 88.1 / 83.3, nz 128 151.5 / 137.0, 256^3
   // 304 / 268 -- hence the 3M-row threshold
-  const int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
   const bool fuse_cg = fmode == 1;
   const bool defer_x = fmode != 0;
   // p_{-1} = -0.0: iteration 0's z + (+0)(-0) is exactly z (VecCopy)
@@ -912,6 +1021,11 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       timer.begin();
       nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg, fdot_p);
       timer.end();
+    } else if (xb > 1) {
+      cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d);
+      timer.begin();
+      nb_spmv = matmult_overlap(A, pbs.b[it % xb], w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
+      timer.end();
     } else {
       cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
       timer.begin();
@@ -922,11 +1036,11 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     const bool fold_in_update = !fdot_p && fused && fold_at == 3;
     if (!fdot_p && !fold_in_update) fold_kernel<1><<<1, 256, 0, st>>>(part.p, nb_spmv, &s->red1, done);
     if (!fused) c->allreduce_sum(&s->red1, 1);
-    const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : pv.p;
+    const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : xb > 1 ? pbs.b[it % xb] : pv.p;
     // the update's own partials go after the MatMult's when it folds those
     double *upart = fold_in_update ? part.p + ((nb_spmv + 63) / 64) * 64 : part.p;
     const int nb_upd = cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, upart, fupd,
-                                        fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0);
+                                        fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb);
     if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(upart, nb_upd, s->top.red3, done);
     if (!fused) c->allreduce_sum(s->top.red3, 3);
     HIPCHECK(hipGetLastError());
@@ -946,7 +1060,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
            (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p, (uintptr_t)g_knobs.cg_vec_grid,
            (uintptr_t)g_knobs.cg_vec, (uintptr_t)g_knobs.cg_nts, (uintptr_t)g_knobs.cg_unroll,
            (uintptr_t)g_knobs.cg_upd_grid, (uintptr_t)g_knobs.vcodes, (uintptr_t)g_knobs.spmv_bpc, (uintptr_t)g_knobs.spmv_pairs, (uintptr_t)g_knobs.spmv_pair_bpc,
-           (uintptr_t)g_knobs.spmv_ynt};
+           (uintptr_t)g_knobs.spmv_ynt, (uintptr_t)xb, (uintptr_t)pv3, (uintptr_t)pv4};
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;
@@ -992,7 +1106,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   }
   cg_tail_kernel<<<1, 64, 0, st>>>(s, hist_d);   // max_it launched without a stop
   HIPCHECK(hipGetLastError());
-  if (defer_x) {   // p is in place for mode 2: both buffer slots are pv
+  if (xb > 1) {
+    cg_finish_xb_kernel<<<egrid, 256, 0, st>>>(n, s, pbs, xb, x);
+    HIPCHECK(hipGetLastError());
+  } else if (defer_x) {   // p is in place for mode 2: both buffer slots are pv
     cg_finish_x_kernel<<<egrid, 256, 0, st>>>(n, s, pv.p, fuse_cg ? pv2 : pv.p, x);
     HIPCHECK(hipGetLastError());
   }

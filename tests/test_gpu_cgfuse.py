@@ -196,3 +196,21 @@ def test_unrolled_row_walk_bitwise(selfcomm, oracle_mod, kind, kw, mode):
         finally:
             L.mx_debug_set(21, old)
     _same(out[0], out[1])
+
+
+@pytest.mark.parametrize("B", [2, 4])
+@pytest.mark.parametrize("kind,kw", [("poisson3d", {}), ("poisson3d", {"max_it": 7}), ("poisson3d", {"max_it": 9}),
+                                     ("poisson3d", {"max_it": 16}), ("varidiag", {}), ("poisson3d", {"guess": True}),
+                                     ("indef", {"pc": "none"}), ("poisson3d27", {}), ("odd", {})])
+def test_batched_x_steps_equal_separate(selfcomm, oracle_mod, kind, kw, B):
+    """Mode 2 with the x steps applied every B iterations (knob 29): the same
+    FMAs in the same order, so x and the history are identical to mode 0 for
+    every stop position relative to the batch (max_it 7, 9, 16, convergence)."""
+    from mxsolve import _lib
+    L = _lib.load()
+    old = L.mx_debug_set(29, B)
+    try:
+        a = _run(selfcomm, oracle_mod, kind, 2, **dict(kw))
+    finally:
+        L.mx_debug_set(29, old)
+    _same(a, _run(selfcomm, oracle_mod, kind, 0, **dict(kw)))
