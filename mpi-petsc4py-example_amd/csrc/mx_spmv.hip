@@ -26,7 +26,10 @@
 
 namespace mx {
 
-constexpr int SPMV_WAVES = 4;  // 256-thread workgroups, one slice per wave at a time
+constexpr int SPMV_WAVES = 4;
+#ifndef SPMV_PAIR_PHASES
+#define SPMV_PAIR_PHASES 1   // 27-point unit in 1 phase: 3 phases measured +1% (tools/lib_ab.py)
+#endif  // 256-thread workgroups, one slice per wave at a time
 Knobs g_knobs;
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -480,7 +483,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       const int32_t *__restrict__ off = doff + (int64_t)(dp & DPAT_ID) * DIA_MAX;
       const int64_t srow = (int64_t)s * SLICE;
       const bool inb = (dp & DPAT_INB) != 0;
-      if (KD > 0 && k == KD)
+      if (KD > 0 && k == KD && (PS == 0 || KD <= 8))   // pair kernels: rare fallback slices take the lean runtime-width body
         sum = dia_slice_fixed<(KD > 0 ? KD : 1)>(vs, off, mkload, row, X, lane, inb, srow, xc, hc);
       else sum = dia_slice_any(vs, off, k, mkload(), row, X, lane, inb, srow);
     } else {
@@ -513,40 +516,47 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)u * 64 + lane) * PB);
 #pragma unroll
       for (int q = 0; q < PB / 16; ++q) cw[q] = ld<NT>(cp + q);
-      dbl2 L[NR];
-      double e_lo[NR], e_hi[NR];
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        L[r] = X.pair(r0 + anchor[r]);           // the operand (scaled / formed as the mode has it)
-        if (SH::tri(r)) {
-          e_lo[r] = X(ubase + anchor[r] - 1);     // row 0 of lane 0: x[r0 + c - 1]
-          e_hi[r] = X(ubase + 128 + anchor[r]);   // row 1 of lane 63: x[r0 + 1 + c + 1]
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
       auto code = [&](int i) -> int {            // code i of the lane (row 0: 0..K-1, row 1: K..2K-1)
         return (cw[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xff;
       };
-      double lo_m1[NR], hi_p1[NR];
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-        if (SH::tri(r)) {
-          lo_m1[r] = wave_shift<true>(L[r].y, e_lo[r]);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
-          hi_p1[r] = wave_shift<false>(L[r].x, e_hi[r]);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
-        }
+      // runs in phases (27-point: SPMV_PAIR_PHASES of them) so that one
+      // phase's x pairs are live at a time -- more waves per SIMD for one more
+      // memory round trip per phase
+      constexpr int NPH = NR > 5 ? SPMV_PAIR_PHASES : 1, RPP = (NR + NPH - 1) / NPH;
+      dbl2 L[NR];
+      double e_lo[NR], e_hi[NR];
       double sum0 = 0.0, sum1 = 0.0;
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int r = SH::run(j), p = SH::pos(j);
-        double a0, a1;                           // operand for row 0 / row 1
-        if (!SH::tri(r)) { a0 = L[r].x; a1 = L[r].y; }
-        else if (p < 0) { a0 = lo_m1[r]; a1 = L[r].x; }
-        else if (p == 0) { a0 = L[r].x; a1 = L[r].y; }
-        else { a0 = L[r].y; a1 = hi_p1[r]; }
-        const int c0 = code(j), c1 = code(K + j);
-        const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
-        sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
-        sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
+      for (int ph = 0; ph < NPH; ++ph) {
+#pragma unroll
+        for (int r = ph * RPP; r < NR && r < (ph + 1) * RPP; ++r) {
+          L[r] = X.pair(r0 + anchor[r]);         // the operand (scaled / formed as the mode has it)
+          if (SH::tri(r)) {
+            e_lo[r] = X(ubase + anchor[r] - 1);   // row 0 of lane 0: x[r0 + c - 1]
+            e_hi[r] = X(ubase + 128 + anchor[r]); // row 1 of lane 63: x[r0 + 1 + c + 1]
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double lo_m1 = 0.0, hi_p1 = 0.0;         // the current run's shifted neighbours
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int r = SH::run(j), p = SH::pos(j);
+          if (r < ph * RPP || r >= (ph + 1) * RPP) continue;
+          if (SH::tri(r) && p < 0) {
+            lo_m1 = wave_shift<true>(L[r].y, e_lo[r]);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
+            hi_p1 = wave_shift<false>(L[r].x, e_hi[r]);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
+          }
+          double a0, a1;                         // operand for row 0 / row 1
+          if (!SH::tri(r)) { a0 = L[r].x; a1 = L[r].y; }
+          else if (p < 0) { a0 = lo_m1; a1 = L[r].x; }
+          else if (p == 0) { a0 = L[r].x; a1 = L[r].y; }
+          else { a0 = L[r].y; a1 = hi_p1; }
+          const int c0 = code(j), c1 = code(K + j);
+          const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
+          sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
+          sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
+        }
+        if (ph + 1 < NPH) __builtin_amdgcn_sched_barrier(0);
       }
       double o0 = sum0, o1 = sum1;
       if constexpr (spmv_jac(MODE)) { o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1); }
