@@ -27,6 +27,9 @@
 namespace mx {
 
 constexpr int SPMV_WAVES = 4;
+#ifndef SPMV_EDGE_VMEM
+#define SPMV_EDGE_VMEM 0   // 1: edge values by a two-lane vector load (measured +6% on 27-pt CG, +1% on 7-pt)
+#endif
 #ifndef SPMV_PAIR_PHASES
 #define SPMV_PAIR_PHASES 1   // 27-point unit in 1 phase: 3 phases measured +1% (tools/lib_ab.py)
 #endif  // 256-thread workgroups, one slice per wave at a time
@@ -532,8 +535,19 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         for (int r = ph * RPP; r < NR && r < (ph + 1) * RPP; ++r) {
           L[r] = X.pair(r0 + anchor[r]);         // the operand (scaled / formed as the mode has it)
           if (SH::tri(r)) {
+#if SPMV_EDGE_VMEM
+            // lanes 0 and 63 fetch the unit's two edge values with one 16-byte
+            // load (two active lanes); the shifts read them as their old operand
+            const bool edge = lane == 0 || lane == 63;
+            const int64_t ei = lane == 0 ? ubase + anchor[r] - 2 : ubase + 128 + anchor[r];
+            dbl2 ev = {0.0, 0.0};
+            if (edge) ev = X.pair(ei);
+            e_lo[r] = ev.y;                       // lane 0: x[ubase + c - 1]
+            e_hi[r] = ev.x;                       // lane 63: x[ubase + 128 + c]
+#else
             e_lo[r] = X(ubase + anchor[r] - 1);   // row 0 of lane 0: x[r0 + c - 1]
             e_hi[r] = X(ubase + 128 + anchor[r]); // row 1 of lane 63: x[r0 + 1 + c + 1]
+#endif
           }
         }
         __builtin_amdgcn_sched_barrier(0);
