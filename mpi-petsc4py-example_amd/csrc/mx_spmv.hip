@@ -17,6 +17,12 @@
 // own row sequentially -- which is exactly the order PETSc sums in.  Padding
 // slots carry column -1 and are skipped.  A_o gets its own SELL structure;
 // slices with no ghost entries have width 0 and cost one scalar load.
+// On top of that (mx_assembly.hip): aligned-offset slices with a
+// shared offset-pattern table, one-byte value codes into an LDS table when
+// the block has <= 255 distinct values, and a row-pair copy of the codes for
+// 5/7/27-point patterns (two rows per lane, x read as 16-byte pairs, +-1
+// neighbours by DPP wave shifts).  Every variant sums each row in the same
+// order, so all give the same bits.
 #include <algorithm>
 #include <unordered_map>
 
