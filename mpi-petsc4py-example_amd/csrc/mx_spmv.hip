@@ -24,6 +24,7 @@
 // neighbours by DPP wave shifts).  Every variant sums each row in the same
 // order, so all give the same bits.
 #include <algorithm>
+#include <mutex>
 #include <unordered_map>
 
 #include "mx_cg.hpp"
@@ -604,11 +605,15 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
   }
 }
 
+// launch-geometry caches, shared by the host threads of in-process ranks
+static std::mutex g_geom_mu;
+
 static int device_cus() {
   static int cus[64] = {0};
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return 256;
+  std::lock_guard<std::mutex> lk(g_geom_mu);
   if (!cus[dev]) HIPCHECK(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
   return cus[dev];
 }
@@ -639,14 +644,19 @@ static int main_grid(const Mat *A, int mode, const void *kf, bool pairs) {
     g = g_knobs.spmv_grid;
   } else {
     static std::unordered_map<const void *, int> bpc_of;
-    auto it = bpc_of.find(kf);
-    if (it == bpc_of.end()) {
-      int b = 0;
-      HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kf, 256, 0));
-      it = bpc_of.emplace(kf, std::max(1, b)).first;
+    int bpc;
+    {
+      std::lock_guard<std::mutex> lk(g_geom_mu);
+      auto it = bpc_of.find(kf);
+      if (it == bpc_of.end()) {
+        int b = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kf, 256, 0));
+        it = bpc_of.emplace(kf, std::max(1, b)).first;
+      }
+      bpc = it->second;
     }
     const int cap = pairs ? g_knobs.spmv_pair_bpc : g_knobs.spmv_bpc;
-    g = (int64_t)std::min(it->second, std::max(1, cap)) * device_cus();
+    g = (int64_t)std::min(bpc, std::max(1, cap)) * device_cus();
     // one workgroup fewer per XCD: a per-XCD wave count that is a multiple of
     // 256 (grids of 1024 / 1536) puts the concurrent x streams on aliasing
     // strides -- measured +35..+80% MatMult time (tools/op_ab.py)
