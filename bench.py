@@ -41,10 +41,15 @@ def spmv_format_bytes(info: dict, m: int, nnz: int, nghost: int) -> int:
     (DESIGN.md §4): with value codes, one code byte per stored slot (8 B/row for
     <= 8 offsets, 32 for 27) instead of 12 B/nnz, x (local + ghosts) read once,
     y written once, 16 B of slice metadata per 64 rows, A_o as 12 B/nnz;
-    without codes, SURVEY.md §8d's CSR bytes."""
+    row-pair units whose code blocks come from the block dictionary stream a
+    4-byte block index per 128 rows and the dictionary once instead of their
+    codes; without codes, SURVEY.md §8d's CSR bytes."""
     if not info.get("value_codes"):
         return spmv_bytes(m, nnz, nghost)
-    return (info["code_bytes"] + 8 * (m + nghost) + 8 * m + 16 * ((m + 63) // 64)
+    codes = info["code_bytes"]
+    if info.get("pair_blocks"):
+        codes += (4 - info["pair_block_bytes"]) * info["pair_units"] + info["pair_blocks"] * info["pair_block_bytes"]
+    return (codes + 8 * (m + nghost) + 8 * m + 16 * ((m + 63) // 64)
             + 12 * info["nnz_o"] + 4 * (m + 1) * (info["nnz_o"] > 0))
 
 
@@ -280,7 +285,8 @@ def main():
                                     "spmv_sell_kernel<SPMV_DOT> (CG MatMult") + ", HIP events, rank 0)",
                          "bytes_per_launch": bytes_launch, "avg_launch_ms": round(spmv_avg_ms, 5),
                          "format": ("value codes (" + str(info.get("value_codes")) + " distinct), " +
-                                    ("row pairs" if info.get("pair_shape") else "one row per lane"))
+                                    ("row pairs" if info.get("pair_shape") else "one row per lane") +
+                                    (f", {info['pair_blocks']} distinct code blocks" if info.get("pair_blocks") else ""))
                                    if info.get("value_codes") else "fp64 SELL-64",
                          "csr_equiv_GBps": round((bytes_csr + (32 * m if mode == 1 else 0)) / (spmv_avg_ms * 1e-3) / 1e9, 1)},
             "cpu_baseline": cpu,

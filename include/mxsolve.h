@@ -89,6 +89,11 @@ typedef struct {
                                          many distinct values (0: stored as fp64)       */
   int64_t code_bytes;                 /* bytes of those codes                         */
   int64_t pair_shape;                 /* row-pair SpMV layout: 5 / 7 / 27-point, 0 none */
+  int64_t pair_units;                 /* 128-row units stored as row pairs (all units
+                                         when pair_blocks is 0)                        */
+  int64_t pair_blocks;                /* distinct unit code blocks streamed from the
+                                         dictionary (0: one block per unit)           */
+  int64_t pair_block_bytes;           /* bytes of one unit's code block               */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */

@@ -932,6 +932,121 @@ __global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star,
   if (lane == 0) dpat[s0] |= DPAT_PAIR;
 }
 
+// Code-block dictionary of the row-pair layout.  A unit's code block (64
+// lanes x pair_bytes) depends only on which slots of its 128 rows are present
+// and on their value codes, so a stencil block has a few dozen distinct blocks
+// (the x-line position of the unit, the y/z boundary class, the coefficient
+// class) however many units it has.  Distinct blocks are found by a 64-bit
+// hash per unit (host map), copied to a dictionary, and every unit is then
+// compared byte for byte with its dictionary block on the device; a hash
+// collision, or more distinct blocks than fit comfortably in L2, keeps one
+// block per unit.  SpMV then reads 4 bytes per 128 rows plus L2-resident
+// dictionary lines instead of pair_bytes per row pair from HBM.
+__global__ void pair_hash_kernel(int64_t nunits, int pb, const int32_t *__restrict__ dpat,
+                                 const uint8_t *__restrict__ pcode, unsigned long long *__restrict__ h) {
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= nunits) return;
+  const int lane = threadIdx.x & 63;
+  if (!(dpat[2 * u] & DPAT_PAIR)) {                 // wave-uniform: no code block
+    if (lane == 0) h[u] = 0;
+    return;
+  }
+  const unsigned long long *w = reinterpret_cast<const unsigned long long *>(pcode + (u * 64 + lane) * pb);
+  unsigned long long a = 0x9E3779B97F4A7C15ull * (unsigned long long)(lane + 1);
+  for (int q = 0; q < pb / 8; ++q) {
+    a ^= w[q] + 0x632BE59BD9B4E019ull * (unsigned long long)(q + 1);
+    a ^= a >> 31; a *= 0xBF58476D1CE4E5B9ull; a ^= a >> 29; a *= 0x94D049BB133111EBull; a ^= a >> 32;
+  }
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+  if (lane == 0) h[u] = a | 1ull;
+}
+
+__global__ void pair_gather_kernel(int64_t nblocks, int pb, const int64_t *__restrict__ rep,
+                                   const uint8_t *__restrict__ pcode, uint8_t *__restrict__ dict) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nblocks) return;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long *src = reinterpret_cast<const unsigned long long *>(pcode + (rep[b] * 64 + lane) * pb);
+  unsigned long long *dst = reinterpret_cast<unsigned long long *>(dict + (b * 64 + lane) * pb);
+  for (int q = 0; q < pb / 8; ++q) dst[q] = src[q];
+}
+
+__global__ void pair_verify_kernel(int64_t nunits, int pb, const int32_t *__restrict__ dpat,
+                                   const uint8_t *__restrict__ pcode, const int32_t *__restrict__ blk,
+                                   const uint8_t *__restrict__ dict, int *__restrict__ bad) {
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= nunits) return;
+  const int lane = threadIdx.x & 63;
+  if (!(dpat[2 * u] & DPAT_PAIR)) return;
+  const unsigned long long *a = reinterpret_cast<const unsigned long long *>(pcode + (u * 64 + lane) * pb);
+  const unsigned long long *d = reinterpret_cast<const unsigned long long *>(dict + ((int64_t)blk[u] * 64 + lane) * pb);
+  bool same = true;
+  for (int q = 0; q < pb / 8; ++q) same = same && a[q] == d[q];
+  if (!same) bad[lane] = 1;
+}
+
+constexpr int64_t PAIR_DICT_MAX_BYTES = 2 << 20;   // 2 MiB: well inside one XCD's 4 MB L2
+
+static void dedupe_pair_blocks(Sell &S, hipStream_t st) {
+  const int64_t nu = S.nunits;
+  const int pb = pair_bytes(S.dia_k);
+  S.pair_blocks = 0;
+  S.pair_used = 0;
+  std::vector<int32_t> blk((size_t)std::max<int64_t>(nu, 1));
+  for (int64_t u = 0; u < nu; ++u) blk[(size_t)u] = (int32_t)u;
+  S.pblk.alloc(blk.size());
+  auto identity = [&] {
+    for (int64_t u = 0; u < nu; ++u) blk[(size_t)u] = (int32_t)u;
+    HIPCHECK(hipMemcpyAsync(S.pblk.p, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice, st));
+    HIPCHECK(hipStreamSynchronize(st));
+  };
+  if (nu == 0 || !g_knobs.pdict || nu > INT32_MAX) { identity(); return; }
+  DBuf<unsigned long long> hd((size_t)nu);
+  pair_hash_kernel<<<(unsigned)cdiv(nu, 4), 256, 0, st>>>(nu, pb, S.dpat.p, S.pcode.p, hd.p);
+  HIPCHECK(hipGetLastError());
+  std::vector<unsigned long long> hh((size_t)nu);
+  HIPCHECK(hipMemcpyAsync(hh.data(), hd.p, sizeof(unsigned long long) * (size_t)nu, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  const int64_t max_blocks = PAIR_DICT_MAX_BYTES / (64 * pb);
+  std::unordered_map<unsigned long long, int32_t> ids;
+  std::vector<int64_t> rep;
+  int64_t used = 0;
+  for (int64_t u = 0; u < nu; ++u) {
+    // knob 30 = 2 (tests): every unit hashes alike, so the byte comparison
+    // below must reject the dictionary
+    const unsigned long long k = g_knobs.pdict == 2 && hh[(size_t)u] ? 1ull : hh[(size_t)u];
+    if (!k) { blk[(size_t)u] = 0; continue; }       // not a pair unit: never read
+    ++used;
+    auto it = ids.find(k);
+    if (it == ids.end()) {
+      if ((int64_t)rep.size() >= max_blocks) { identity(); return; }
+      it = ids.emplace(k, (int32_t)rep.size()).first;
+      rep.push_back(u);
+    }
+    blk[(size_t)u] = it->second;
+  }
+  const int64_t nb = (int64_t)rep.size();
+  if (nb == 0 || (4 * nb > nu && g_knobs.pdict != 2)) { identity(); return; }   // too few repeats to pay for the indirection
+  DBuf<int64_t> repd((size_t)nb);
+  DBuf<uint8_t> dict((size_t)nb * 64 * pb);
+  DBuf<int> bad(64);
+  HIPCHECK(hipMemcpyAsync(repd.p, rep.data(), sizeof(int64_t) * (size_t)nb, hipMemcpyHostToDevice, st));
+  HIPCHECK(hipMemcpyAsync(S.pblk.p, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice, st));
+  HIPCHECK(hipMemsetAsync(bad.p, 0, 64 * sizeof(int), st));
+  pair_gather_kernel<<<(unsigned)cdiv(nb, 4), 256, 0, st>>>(nb, pb, repd.p, S.pcode.p, dict.p);
+  HIPCHECK(hipGetLastError());
+  pair_verify_kernel<<<(unsigned)cdiv(nu, 4), 256, 0, st>>>(nu, pb, S.dpat.p, S.pcode.p, S.pblk.p, dict.p, bad.p);
+  HIPCHECK(hipGetLastError());
+  std::vector<int> bh(64);
+  HIPCHECK(hipMemcpyAsync(bh.data(), bad.p, 64 * sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  for (int v : bh)
+    if (v) { identity(); return; }                  // hash collision: keep every block
+  S.pcode = std::move(dict);
+  S.pair_blocks = nb;
+  S.pair_used = used;
+}
+
 static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, hipStream_t st) {
   S.ntab = 0;
   if (S.slots == 0 || !g_knobs.vcodes) return;
@@ -981,6 +1096,7 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, hipStrea
                                                                    S.width.p, S.dpat.p, wid_o, S.val.p, S.mask.p,
                                                                    S.mask8.p, tab.p, sc.p, S.pcode.p);
     HIPCHECK(hipGetLastError());
+    dedupe_pair_blocks(S, st);
   }
   HIPCHECK(hipStreamSynchronize(st));   // tab / sc are freed on return
   S.ntab = (int)keys.size();

@@ -131,7 +131,13 @@ struct Sell {
   std::vector<int32_t> pat_star_off;
   int pair_shape = 0;                 // 0, 5, 7, 27
   int64_t nunits = 0;
-  DBuf<uint8_t> pcode;
+  DBuf<uint8_t> pcode;    // unit code blocks (64 * pair_bytes per unit), or the distinct ones
+  // unit u's codes are block pblk[u] of pcode: u itself, or (pair_blocks > 0)
+  // an index into the dictionary of the distinct blocks (a stencil has a few
+  // dozen: boundary classes x value classes), which then stays in L2
+  DBuf<int32_t> pblk;     // [nunits]
+  int64_t pair_blocks = 0;
+  int64_t pair_used = 0;   // units stored as row pairs (known when the dictionary is built)
 };
 constexpr int VCODE_MAX = 256;      // table entries; code 255 marks an absent slot
 constexpr int VCODE_ABSENT = VCODE_MAX - 1;
@@ -144,7 +150,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int bnd_grid = 0; int mdot_group = 32;
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
-                int cg_xbatch = 2; };
+                int cg_xbatch = 2; int pdict = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

@@ -382,7 +382,8 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     const double *__restrict__ lvec, double *__restrict__ y, const Jac jac,
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
     const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
-    const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star) {
+    const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star,
+    const int32_t *__restrict__ pblk, int pdict) {
   static_assert(PS == 0 || VC, "row pairs: coded values");
   CgTopIn top;
   if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
@@ -523,9 +524,18 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       // codes, then every x pair and edge value, then the lookups
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       u32x4 cw[PB / 16];
-      const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)u * 64 + lane) * PB);
+      // the unit's code block: its own (streamed non-temporally), or a
+      // dictionary block shared with every unit of the same boundary/value
+      // class (cached: the dictionary stays in L2)
+      if (pdict) {                                // kernel-uniform
+        const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)pblk[u] * 64 + lane) * PB);
 #pragma unroll
-      for (int q = 0; q < PB / 16; ++q) cw[q] = ld<NT>(cp + q);
+        for (int q = 0; q < PB / 16; ++q) cw[q] = cp[q];
+      } else {
+        const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)u * 64 + lane) * PB);
+#pragma unroll
+        for (int q = 0; q < PB / 16; ++q) cw[q] = ld<NT>(cp + q);
+      }
       auto code = [&](int i) -> int {            // code i of the lane (row 0: 0..K-1, row 1: K..2K-1)
         return (cw[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xff;
       };
@@ -764,7 +774,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
       partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt, \
-      A->sd.pcode.p, A->sd.pat_star
+      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, A->sd.pair_blocks > 0 ? 1 : 0
   using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
   KFn kf = nullptr;
 #define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>

@@ -177,3 +177,58 @@ def test_row_pairs_solve(selfcomm, oracle_mod, kind, n, ksp):
     assert r["reason"] == o["reason"] and abs(r["its"] - o["its"]) <= 1
     xs = x.cpu().numpy()
     assert np.linalg.norm(xs - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
+
+
+def _with_knob(L, key, value, fn):
+    old = L.mx_debug_set(key, value)
+    try:
+        return fn()
+    finally:
+        L.mx_debug_set(key, old)
+
+
+@pytest.mark.parametrize("kind,n,shape", [("poisson2d", 256, 5), ("poisson3d", 64, 7), ("poisson3d27", 48, 27),
+                                          ("convdiff3d", 64, 7)])
+def test_pair_code_dictionary(selfcomm, oracle_mod, kind, n, shape):
+    """Row-pair code blocks deduplicated into a dictionary (knob 30 = 1, the
+    default): a few distinct blocks, MatMult bit-exact against the oracle and
+    against the one-block-per-unit layout (knob 30 = 0); knob 30 = 2 makes
+    every unit hash alike, so the byte-for-byte check must refuse the
+    dictionary and keep the per-unit blocks (unless there is only one)."""
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    L = lib()
+    info1, got1, exp = mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=13)
+    info0, got0, _ = _with_knob(L, 30, 0, lambda: mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=13))
+    info2, got2, _ = _with_knob(L, 30, 2, lambda: mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=13))
+    assert info1["pair_shape"] == shape and info0["pair_shape"] == shape
+    assert 0 < info1["pair_blocks"] <= info1["pair_units"] // 4
+    assert info0["pair_blocks"] == 0
+    # one distinct block (3D 64^3: every pair unit is two interior x-lines;
+    # the y-boundary slices carry another offset pattern) is the one case the
+    # forced collision cannot break
+    assert info2["pair_blocks"] == (1 if info1["pair_blocks"] == 1 else 0)
+    for got in (got0, got1, got2):
+        assert np.array_equal(got, exp)
+
+
+def test_pair_code_dictionary_cg(selfcomm):
+    """CG on 3D 7-point 64^3 with and without the code dictionary: same
+    iteration count, same solution bits."""
+    from mxsolve.core import DMat, rhs_hash
+    L = lib()
+
+    def run():
+        A = DMat.stencil(selfcomm, "poisson3d", 64)
+        m = A.info()["m"]
+        b = selfcomm.empty(m)
+        rhs_hash(selfcomm, 0, b)
+        x = selfcomm.zeros(m)
+        r = A.solve(b, x, ksp="cg", pc="jacobi")
+        return r["its"], r["reason"], x.cpu().numpy().copy(), A.info()["pair_blocks"]
+
+    on = run()
+    off = _with_knob(L, 30, 0, run)
+    assert on[3] > 0 and off[3] == 0
+    assert on[:2] == off[:2]
+    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
