@@ -33,13 +33,10 @@
 
 namespace mx {
 
-constexpr int SPMV_WAVES = 4;
-#ifndef SPMV_EDGE_VMEM
-#define SPMV_EDGE_VMEM 0   // 1: edge values by a two-lane vector load (measured +6% on 27-pt CG, +1% on 7-pt)
+constexpr int SPMV_WAVES = 4;  // 256-thread workgroups, one slice per wave at a time
+#ifndef SPMV_PAIR_TWO
+#define SPMV_PAIR_TWO 1   // 5/7-point row pairs: two units' loads in flight per wave
 #endif
-#ifndef SPMV_PAIR_PHASES
-#define SPMV_PAIR_PHASES 1   // 27-point unit in 1 phase: 3 phases measured +1% (tools/lib_ab.py)
-#endif  // 256-thread workgroups, one slice per wave at a time
 Knobs g_knobs;
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -383,7 +380,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
     const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
     const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star,
-    const int32_t *__restrict__ pblk, int pdict) {
+    const int32_t *__restrict__ pblk, int pdict, int rev) {
   static_assert(PS == 0 || VC, "row pairs: coded values");
   CgTopIn top;
   if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
@@ -480,7 +477,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       if (MODE == SPMV_CG) dot += xc * sum;
     }
   };
-  auto one_slice = [&](int s) {
+  auto one_slice = [&](int s) __attribute__((always_inline)) {
     const int64_t row = (int64_t)s * SLICE + lane;
     const int w = wid_d[s];
     const VS vs = vsrc(s);
@@ -502,92 +499,71 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     }
     finish(s, sum, o, xc, hc);
   };
+  // rev: the sweep runs from the last item down (each XCD's range stays
+  // contiguous), so the rows the previous kernel wrote last -- still in the
+  // memory-side cache -- are read first
+  auto item = [&](int i) -> int { return rev ? (int)(nitems - 1) - i : i; };
   if constexpr (PS == 0) {
-    for (int s = s0; s < send; s += sstep) one_slice(s);
+    for (int s = s0; s < send; s += sstep) one_slice(item(s));
   } else {
     using SH = PairShape<PS>;
     constexpr int K = SH::K, NR = SH::NR;
     constexpr int PB = (2 * K + 15) / 16 * 16;      // code bytes per lane
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     // the dominant pattern's offsets, and each run's anchor (singleton / centre)
     const int32_t *__restrict__ offs = doff + (int64_t)pat_star * DIA_MAX;
     int64_t anchor[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) anchor[r] = offs[SH::first(r) + (SH::tri(r) ? 1 : 0)];
-    for (int u = s0; u < send; u += sstep) {
-      const int sa = 2 * u;
-      if (!(dpat[sa] & DPAT_PAIR)) {               // wave-uniform
-        one_slice(sa);
-        if (sa + 1 < nslices) one_slice(sa + 1);
-        continue;
-      }
+    // one unit's loads: its code block, every x pair and the edge values
+    struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e_lo[NR], e_hi[NR]; };
+    auto unit_load = [&](int u, Unit &t) __attribute__((always_inline)) {
       const int64_t ubase = (int64_t)u * 128, r0 = ubase + 2 * lane;
-      // codes, then every x pair and edge value, then the lookups
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      u32x4 cw[PB / 16];
       // the unit's code block: its own (streamed non-temporally), or a
       // dictionary block shared with every unit of the same boundary/value
       // class (cached: the dictionary stays in L2)
       if (pdict) {                                // kernel-uniform
         const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)pblk[u] * 64 + lane) * PB);
 #pragma unroll
-        for (int q = 0; q < PB / 16; ++q) cw[q] = cp[q];
+        for (int q = 0; q < PB / 16; ++q) t.cw[q] = cp[q];
       } else {
         const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)u * 64 + lane) * PB);
 #pragma unroll
-        for (int q = 0; q < PB / 16; ++q) cw[q] = ld<NT>(cp + q);
+        for (int q = 0; q < PB / 16; ++q) t.cw[q] = ld<NT>(cp + q);
       }
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        t.L[r] = X.pair(r0 + anchor[r]);         // the operand (scaled / formed as the mode has it)
+        if (SH::tri(r)) {
+          t.e_lo[r] = X(ubase + anchor[r] - 1);   // row 0 of lane 0: x[r0 + c - 1]
+          t.e_hi[r] = X(ubase + 128 + anchor[r]); // row 1 of lane 63: x[r0 + 1 + c + 1]
+        }
+      }
+    };
+    // the lookups, the two row sums and everything stored after them
+    auto unit_finish = [&](int u, const Unit &t) __attribute__((always_inline)) {
+      const int64_t r0 = (int64_t)u * 128 + 2 * lane;
       auto code = [&](int i) -> int {            // code i of the lane (row 0: 0..K-1, row 1: K..2K-1)
-        return (cw[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xff;
+        return (t.cw[i >> 4][(i >> 2) & 3] >> (8 * (i & 3))) & 0xff;
       };
-      // runs in phases (27-point: SPMV_PAIR_PHASES of them) so that one
-      // phase's x pairs are live at a time -- more waves per SIMD for one more
-      // memory round trip per phase
-      constexpr int NPH = NR > 5 ? SPMV_PAIR_PHASES : 1, RPP = (NR + NPH - 1) / NPH;
-      dbl2 L[NR];
-      double e_lo[NR], e_hi[NR];
       double sum0 = 0.0, sum1 = 0.0;
+      double lo_m1 = 0.0, hi_p1 = 0.0;           // the current run's shifted neighbours
 #pragma unroll
-      for (int ph = 0; ph < NPH; ++ph) {
-#pragma unroll
-        for (int r = ph * RPP; r < NR && r < (ph + 1) * RPP; ++r) {
-          L[r] = X.pair(r0 + anchor[r]);         // the operand (scaled / formed as the mode has it)
-          if (SH::tri(r)) {
-#if SPMV_EDGE_VMEM
-            // lanes 0 and 63 fetch the unit's two edge values with one 16-byte
-            // load (two active lanes); the shifts read them as their old operand
-            const bool edge = lane == 0 || lane == 63;
-            const int64_t ei = lane == 0 ? ubase + anchor[r] - 2 : ubase + 128 + anchor[r];
-            dbl2 ev = {0.0, 0.0};
-            if (edge) ev = X.pair(ei);
-            e_lo[r] = ev.y;                       // lane 0: x[ubase + c - 1]
-            e_hi[r] = ev.x;                       // lane 63: x[ubase + 128 + c]
-#else
-            e_lo[r] = X(ubase + anchor[r] - 1);   // row 0 of lane 0: x[r0 + c - 1]
-            e_hi[r] = X(ubase + 128 + anchor[r]); // row 1 of lane 63: x[r0 + 1 + c + 1]
-#endif
-          }
+      for (int j = 0; j < K; ++j) {
+        const int r = SH::run(j), p = SH::pos(j);
+        if (SH::tri(r) && p < 0) {
+          lo_m1 = wave_shift<true>(t.L[r].y, t.e_lo[r]);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
+          hi_p1 = wave_shift<false>(t.L[r].x, t.e_hi[r]);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
         }
-        __builtin_amdgcn_sched_barrier(0);
-        double lo_m1 = 0.0, hi_p1 = 0.0;         // the current run's shifted neighbours
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const int r = SH::run(j), p = SH::pos(j);
-          if (r < ph * RPP || r >= (ph + 1) * RPP) continue;
-          if (SH::tri(r) && p < 0) {
-            lo_m1 = wave_shift<true>(L[r].y, e_lo[r]);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
-            hi_p1 = wave_shift<false>(L[r].x, e_hi[r]);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
-          }
-          double a0, a1;                         // operand for row 0 / row 1
-          if (!SH::tri(r)) { a0 = L[r].x; a1 = L[r].y; }
-          else if (p < 0) { a0 = lo_m1; a1 = L[r].x; }
-          else if (p == 0) { a0 = L[r].x; a1 = L[r].y; }
-          else { a0 = L[r].y; a1 = hi_p1; }
-          const int c0 = code(j), c1 = code(K + j);
-          const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
-          sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
-          sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
-        }
-        if (ph + 1 < NPH) __builtin_amdgcn_sched_barrier(0);
+        double a0, a1;                           // operand for row 0 / row 1
+        if (!SH::tri(r)) { a0 = t.L[r].x; a1 = t.L[r].y; }
+        else if (p < 0) { a0 = lo_m1; a1 = t.L[r].x; }
+        else if (p == 0) { a0 = t.L[r].x; a1 = t.L[r].y; }
+        else { a0 = t.L[r].y; a1 = hi_p1; }
+        const int c0 = code(j), c1 = code(K + j);
+        const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
+        sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
+        sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
       }
       double o0 = sum0, o1 = sum1;
       if constexpr (spmv_jac(MODE)) { o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1); }
@@ -596,7 +572,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       if constexpr (MODE == SPMV_CG) {
         // p_i at the own rows is the centre run's pair: store it, and the
         // previous step's deferred VecAXPY(X, a, P) on the own rows
-        *reinterpret_cast<dbl2 *>(cg.pnew + r0) = L[SH::CENTER_RUN];
+        *reinterpret_cast<dbl2 *>(cg.pnew + r0) = t.L[SH::CENTER_RUN];
         if (xpend) {
           const dbl2 po = *reinterpret_cast<const dbl2 *>(cg.pold + r0);
           const dbl2 xo = *reinterpret_cast<const dbl2 *>(cg.x + r0);
@@ -604,10 +580,43 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         }
       }
       if constexpr (MODE == SPMV_DOT || MODE == SPMV_CG) {   // operand at the own rows = the centre pair
-        dot += L[SH::CENTER_RUN].x * sum0;
-        dot += L[SH::CENTER_RUN].y * sum1;
+        dot += t.L[SH::CENTER_RUN].x * sum0;
+        dot += t.L[SH::CENTER_RUN].y * sum1;
+      }
+    };
+    auto one_unit = [&](int u) __attribute__((always_inline)) {
+      if (!(dpat[2 * u] & DPAT_PAIR)) {           // wave-uniform
+        one_slice(2 * u);
+        if (2 * u + 1 < nslices) one_slice(2 * u + 1);
+        return;
+      }
+      Unit t;
+      unit_load(u, t);
+      __builtin_amdgcn_sched_barrier(0);          // every load issued before the first lookup
+      unit_finish(u, t);
+    };
+    int u = s0;
+    // SPMV_PAIR_TWO: a wave takes its next two units together, both units'
+    // loads in flight before the first lookup (twice the bytes in flight per
+    // wave at the same occupancy); the units still finish in sweep order, so
+    // the per-lane dot partial sums in the same order
+    if constexpr (SPMV_PAIR_TWO && PS != 27 && MODE != SPMV_CG) {
+      for (; u + sstep < send; u += 2 * sstep) {
+        const int ua = item(u), ub = item(u + sstep);
+        if ((dpat[2 * ua] & DPAT_PAIR) && (dpat[2 * ub] & DPAT_PAIR)) {   // wave-uniform
+          Unit ta, tb;
+          unit_load(ua, ta);
+          unit_load(ub, tb);
+          __builtin_amdgcn_sched_barrier(0);
+          unit_finish(ua, ta);
+          unit_finish(ub, tb);
+        } else {
+          one_unit(ua);
+          one_unit(ub);
+        }
       }
     }
+    for (; u < send; u += sstep) one_unit(item(u));
   }
   if (MODE == SPMV_DOT || MODE == SPMV_CG) {
     double v[1] = {dot};
@@ -774,7 +783,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
       partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt, \
-      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, A->sd.pair_blocks > 0 ? 1 : 0
+      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, A->sd.pair_blocks > 0 ? 1 : 0, g_knobs.spmv_rev
   using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
   KFn kf = nullptr;
 #define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>

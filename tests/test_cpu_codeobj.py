@@ -1,0 +1,56 @@
+"""The built library's gfx950 code objects: no hot kernel may use scratch
+(private segment).  A lambda the compiler declined to inline once put a
+row-pair unit's registers on the stack (432 bytes per lane) and halved the
+SpMV's speed with every parity test still green; this check catches that
+class of regression on the CPU, from the kernel descriptors' metadata."""
+import os
+import re
+import shutil
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "mpi-petsc4py-example_amd", "lib", "libmxsolve.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+HOT = re.compile(r"spmv_sell_kernel|cg_|mdot|maxpy|fold_kernel")
+
+
+def code_objects(fatbin: bytes):
+    """gfx950 ELF images of every offload bundle in a .hip_fatbin section."""
+    i = fatbin.find(MAGIC)
+    while i >= 0:
+        n = struct.unpack_from("<Q", fatbin, i + 24)[0]
+        p = i + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", fatbin, p)
+            triple = fatbin[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" in triple:
+                yield fatbin[i + off:i + off + size]
+        i = fatbin.find(MAGIC, i + 1)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not os.path.exists(os.path.join(LLVM, "llvm-readelf")),
+                    reason="library not built or no ROCm llvm tools")
+def test_hot_kernels_use_no_scratch(tmp_path):
+    fb = tmp_path / "fatbin"
+    subprocess.check_call([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", f".hip_fatbin={fb}", LIB,
+                           str(tmp_path / "lib.copy")])
+    kernels = {}
+    for j, elf in enumerate(code_objects(fb.read_bytes())):
+        co = tmp_path / f"co{j}.elf"
+        co.write_bytes(elf)
+        notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", str(co)],
+                               capture_output=True, text=True, check=True).stdout
+        for blk in re.split(r"\n\s+- \.", notes):
+            m = re.search(r"\.name:\s+(\S+)", blk)
+            ps = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+            if m and ps:
+                kernels[m.group(1)] = int(ps.group(1))
+    hot = {k: v for k, v in kernels.items() if HOT.search(k)}
+    assert any("spmv_sell_kernel" in k for k in hot), "no SpMV kernel found in the code objects"
+    bad = {k: v for k, v in hot.items() if v}
+    assert not bad, f"hot kernels with scratch: {bad}"

@@ -79,6 +79,15 @@ def main():
         next((k for k in fetch if k.startswith("spmv_sell_kernel<2,")), None)
     if sp and not sp.startswith("spmv_sell_kernel<3,"):
         alg = spmv_alg
+    # the profiled bench's own figure (bench.py spmv_format_bytes: code-block
+    # dictionary, value codes) when its JSON line is in the trace log
+    try:
+        with open(os.path.join(src, "trace.log")) as f:
+            js = [json.loads(ln) for ln in f if ln.startswith("{")]
+        if js and js[-1].get("roofline", {}).get("bytes_per_launch"):
+            alg = js[-1]["roofline"]["bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
     if sp in fetch and sp in write:
         fr = statistics.median(fetch[sp]) * 1024
         wr = statistics.median(write[sp]) * 1024
