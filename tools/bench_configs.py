@@ -45,7 +45,8 @@ def main():
         rec = {"config": tag, "kind": kind, "dims": [nx, ny, nz], "ksp": ksp, "rows": m, "nnz": nnz,
                "assembly_s": round(t_asm, 4), "its": r["its"], "reason": r["reason"], "solve_s": round(ts, 4),
                "its_per_s": round(r["its"] / ts, 1), "spmv_ms": round(spmv_ms, 4),
-               "spmv_alg_GBps": round(alg / spmv_ms / 1e6, 1), "dia_slices": info["dia_slices"]}
+               "spmv_alg_GBps": round(alg / spmv_ms / 1e6, 1), "dia_slices": info["dia_slices"],
+               "pair_shape": info["pair_shape"], "pair_blocks": info["pair_blocks"]}
         print(json.dumps(rec), flush=True)
         out.append(rec)
         A.destroy()
