@@ -517,13 +517,13 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     for (int r = 0; r < NR; ++r) anchor[r] = offs[SH::first(r) + (SH::tri(r) ? 1 : 0)];
     // one unit's loads: its code block, every x pair and the edge values
     struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e_lo[NR], e_hi[NR]; };
-    auto unit_load = [&](int u, Unit &t) __attribute__((always_inline)) {
+    auto unit_load = [&](int u, int blk, Unit &t) __attribute__((always_inline)) {
       const int64_t ubase = (int64_t)u * 128, r0 = ubase + 2 * lane;
       // the unit's code block: its own (streamed non-temporally), or a
       // dictionary block shared with every unit of the same boundary/value
       // class (cached: the dictionary stays in L2)
       if (pdict) {                                // kernel-uniform
-        const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)pblk[u] * 64 + lane) * PB);
+        const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)blk * 64 + lane) * PB);
 #pragma unroll
         for (int q = 0; q < PB / 16; ++q) t.cw[q] = cp[q];
       } else {
@@ -591,7 +591,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         return;
       }
       Unit t;
-      unit_load(u, t);
+      unit_load(u, pdict ? pblk[u] : 0, t);
       __builtin_amdgcn_sched_barrier(0);          // every load issued before the first lookup
       unit_finish(u, t);
     };
@@ -600,19 +600,37 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     // loads in flight before the first lookup (twice the bytes in flight per
     // wave at the same occupancy); the units still finish in sweep order, so
     // the per-lane dot partial sums in the same order
+    // The step's metadata (pair flags, dictionary block ids) is loaded one
+    // step ahead, behind the current step's vector loads, so the branch and
+    // the code-block address never wait on a scalar round trip of their own.
     if constexpr (SPMV_PAIR_TWO && PS != 27 && MODE != SPMV_CG) {
+      struct Meta { int32_t da = 0, db = 0, ba = 0, bb = 0; };
+      auto meta = [&](int v) __attribute__((always_inline)) {   // step starting at sweep index v
+        Meta q;
+        if (v + sstep < send) {
+          const int va = item(v), vb = item(v + sstep);
+          q.da = dpat[2 * va];
+          q.db = dpat[2 * vb];
+          if (pdict) { q.ba = pblk[va]; q.bb = pblk[vb]; }
+        }
+        return q;
+      };
+      Meta cur = meta(u);
       for (; u + sstep < send; u += 2 * sstep) {
         const int ua = item(u), ub = item(u + sstep);
-        if ((dpat[2 * ua] & DPAT_PAIR) && (dpat[2 * ub] & DPAT_PAIR)) {   // wave-uniform
+        if ((cur.da & DPAT_PAIR) && (cur.db & DPAT_PAIR)) {   // wave-uniform
           Unit ta, tb;
-          unit_load(ua, ta);
-          unit_load(ub, tb);
+          unit_load(ua, cur.ba, ta);
+          unit_load(ub, cur.bb, tb);
+          const Meta nxt = meta(u + 2 * sstep);
           __builtin_amdgcn_sched_barrier(0);
           unit_finish(ua, ta);
           unit_finish(ub, tb);
+          cur = nxt;
         } else {
           one_unit(ua);
           one_unit(ub);
+          cur = meta(u + 2 * sstep);
         }
       }
     }
