@@ -470,6 +470,7 @@ int mx_debug_set(int key, int value) {
     case 29: old = g_knobs.cg_xbatch; g_knobs.cg_xbatch = value; break;
     case 30: old = g_knobs.pdict; g_knobs.pdict = value; break;
     case 31: old = g_knobs.spmv_rev; g_knobs.spmv_rev = value; break;
+    case 32: old = g_knobs.cg_ntl; g_knobs.cg_ntl = value; break;
     default: break;
   }
   return old;

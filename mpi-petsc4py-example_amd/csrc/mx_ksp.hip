@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstring>
 #include <initializer_list>
+#include <type_traits>
 
 #include "mx_cg.hpp"
 #include "mx_device.hpp"
@@ -332,34 +333,54 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
     for (int q = 0; q < B; ++q) al[q] = top.xal[q];
     double *__restrict__ pout = p0;
     const double *__restrict__ pprev = B == 4 ? p3 : p1;
-    for (; k < n; k += stride) {
-      const double po = pprev[k];
-      double xx = fma(al[0], pout[k], x[k]);     // x += a_{i-B} p_{i-B}, oldest first
-      if constexpr (B == 4) {
-        xx = fma(al[1], p1[k], xx);
-        xx = fma(al[2], p2[k], xx);
+    auto batch = [&](auto ntc) __attribute__((always_inline)) {   // non-temporal reads: see walk below
+      constexpr bool NTL = decltype(ntc)::value;
+      auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
+        if constexpr (NTL) return __builtin_nontemporal_load(q);
+        else return *q;
+      };
+      for (; k < n; k += stride) {
+        const double po = ldv(pprev + k);
+        double xx = fma(al[0], ldv(pout + k), ldv(x + k));   // x += a_{i-B} p_{i-B}, oldest first
+        if constexpr (B == 4) {
+          xx = fma(al[1], ldv(p1 + k), xx);
+          xx = fma(al[2], ldv(p2 + k), xx);
+        }
+        x[k] = fma(al[B - 1], po, xx);             // ... x += a_{i-1} p_{i-1}
+        pout[k] = row(ldv(r + k), JM == 1 ? dv[k] : 0.0, po);
       }
-      x[k] = fma(al[B - 1], po, xx);             // ... x += a_{i-1} p_{i-1}
-      pout[k] = row(r[k], JM == 1 ? dv[k] : 0.0, po);
-    }
+    };
+    if (unr & 2) batch(std::true_type{});
+    else batch(std::false_type{});
     return;
   }
   const double *__restrict__ pprev = pick((i + B - 1) % B);   // p_{i-1} (unused at i = 0: b = 0)
   double *__restrict__ pout = pick(i % B);
-  if (unr) {                                     // four steps' loads issued together
-    for (; k + 3 * stride < n; k += 4 * stride) {
-      double po[4], rr[4], dd[4];
+  // unr bit 1 (knob 32): r and p_{i-1} read non-temporally, so the memory-side
+  // cache keeps more of the p_i just written for the MatMult that reads it next
+  auto walk = [&](auto ntc) __attribute__((always_inline)) {
+    constexpr bool NTL = decltype(ntc)::value;
+    auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
+      if constexpr (NTL) return __builtin_nontemporal_load(q);
+      else return *q;
+    };
+    if (unr & 1) {                               // four steps' loads issued together
+      for (; k + 3 * stride < n; k += 4 * stride) {
+        double po[4], rr[4], dd[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        po[u] = pprev[k + u * stride];
-        rr[u] = r[k + u * stride];
-        dd[u] = JM == 1 ? dv[k + u * stride] : 0.0;
+        for (int u = 0; u < 4; ++u) {
+          po[u] = ldv(pprev + k + u * stride);
+          rr[u] = ldv(r + k + u * stride);
+          dd[u] = JM == 1 ? dv[k + u * stride] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pout[k + u * stride] = row(rr[u], dd[u], po[u]);
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) pout[k + u * stride] = row(rr[u], dd[u], po[u]);
     }
-  }
-  for (; k < n; k += stride) pout[k] = row(r[k], JM == 1 ? dv[k] : 0.0, pprev[k]);
+    for (; k < n; k += stride) pout[k] = row(ldv(r + k), JM == 1 ? dv[k] : 0.0, ldv(pprev + k));
+  };
+  if (unr & 2) walk(std::true_type{});
+  else walk(std::false_type{});
 }
 
 // dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
@@ -432,28 +453,39 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
   if constexpr (!VEC) {          // row walk: one row per thread per step
     const int64_t stride = (int64_t)gridDim.x * 256;
     int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (unr) {                   // knob 21: four steps' loads issued together, same sum order
-      for (; i + 3 * stride < n; i += 4 * stride) {
-        double pp[4], xx[4], ww[4], rr[4], dd[4];
+    // unr bit 1 (knob 32): w and r read non-temporally, so the memory-side
+    // cache keeps the r written here for the direction update that reads it
+    auto walk = [&](auto ntc) __attribute__((always_inline)) {
+      constexpr bool NTL = decltype(ntc)::value;
+      auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
+        if constexpr (NTL) return __builtin_nontemporal_load(q);
+        else return *q;
+      };
+      if (unr & 1) {             // knob 21: four steps' loads issued together, same sum order
+        for (; i + 3 * stride < n; i += 4 * stride) {
+          double pp[4], xx[4], ww[4], rr[4], dd[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          ww[u] = w[i + u * stride];
-          rr[u] = r[i + u * stride];
-          pp[u] = XU ? p[i + u * stride] : 0.0;
-          xx[u] = XU ? x[i + u * stride] : 0.0;
-          dd[u] = JM == 1 ? dv[i + u * stride] : 0.0;
-        }
+          for (int u = 0; u < 4; ++u) {
+            ww[u] = ldv(w + i + u * stride);
+            rr[u] = ldv(r + i + u * stride);
+            pp[u] = XU ? p[i + u * stride] : 0.0;
+            xx[u] = XU ? x[i + u * stride] : 0.0;
+            dd[u] = JM == 1 ? dv[i + u * stride] : 0.0;
+          }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (XU) st1(x + i + u * stride, fma(a, pp[u], xx[u]), nts);
-          st1(r + i + u * stride, rnew(ww[u], rr[u], dd[u]), nts);
+          for (int u = 0; u < 4; ++u) {
+            if (XU) st1(x + i + u * stride, fma(a, pp[u], xx[u]), nts);
+            st1(r + i + u * stride, rnew(ww[u], rr[u], dd[u]), nts);
+          }
         }
       }
-    }
-    for (; i < n; i += stride) {
-      if (XU) st1(x + i, fma(a, p[i], x[i]), nts);
-      st1(r + i, rnew(w[i], r[i], JM == 1 ? dv[i] : 0.0), nts);
-    }
+      for (; i < n; i += stride) {
+        if (XU) st1(x + i, fma(a, p[i], x[i]), nts);
+        st1(r + i, rnew(ldv(w + i), ldv(r + i), JM == 1 ? dv[i] : 0.0), nts);
+      }
+    };
+    if (unr & 2) walk(std::true_type{});
+    else walk(std::false_type{});
     block_partials<3>(v, partials, gridDim.x, fold);
     return;
   }
@@ -909,7 +941,7 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
 static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r, const Jac &j, const PBufs &pb,
                          int B, double *x, double *hist) {
   const unsigned g = cg_vec_grid(n, false, 8192);
-  const int unr = cg_unroll(n);
+  const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 1) ? 2 : 0);
 #define CGPB(JM, BB) cg_pb_kernel<JM, BB><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], pb.b[3], \
                                                            x, hist, unr)
 #define CGPB_J(JM) do { if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
@@ -928,7 +960,7 @@ static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double
                                              : cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : RED_BLOCKS);
   Fold f = fold_in;
   f.ntotal = f.ncount = (int)g;
-  const int unr = cg_unroll(n);
+  const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 2) ? 2 : 0);
   f.base = 0;
 #define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f, \
                                                                         g_knobs.cg_nts, dot_part, ndot, unr, xb)
