@@ -611,6 +611,18 @@ __global__ void __launch_bounds__(256) gm_start_kernel(KspState *s, const double
   s->inner_stop = (s->its >= s->top.max_it) ? 1 : 0;
 }
 
+// Basis-vector reads of MDot and MAXPY (GM_NTL): non-temporal, so the
+// memory-side cache keeps w -- written by the MatMult and read by the MDot,
+// then rewritten by the MAXPY and read by the next MatMult -- instead of the
+// basis, which is far larger than that cache anyway
+#ifndef GM_NTL
+#define GM_NTL 1
+#endif
+__device__ __forceinline__ double gm_ld(const double *q) {
+  if constexpr (GM_NTL) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+
 // VecMDot: h_j = w . v_j for j in [j0, j0 + nv), nv <= NV, one pass over w
 // (restart 30: every step's k+1 dots in one launch)
 // The basis vectors are stored unnormalised: v_j = vscale[j] * V_j, applied
@@ -639,7 +651,7 @@ __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__re
     const double wi = w[i];
     double v[NV];
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = vk[k][i];
+    for (int k = 0; k < NV; ++k) v[k] = gm_ld(vk[k] + i);
 #pragma unroll
     for (int k = 0; k < NV; ++k) acc[k] += wi * (sc[k] * v[k]);
   }
@@ -685,7 +697,7 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     double u = w[i];
     int j = 0;
-    auto vj = [&](int j) { return sc[j] * V[(int64_t)j * ldv + i]; };
+    auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
     if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
     else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
     else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
@@ -781,7 +793,7 @@ __global__ void __launch_bounds__(256) gm_update_x_kernel(int64_t n, const KspSt
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     double u = 0.0;
     int j = 0;
-    auto vj = [&](int j) { return sc[j] * V[(int64_t)j * ldv + i]; };
+    auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
     if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
     else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
     else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
