@@ -300,6 +300,9 @@ __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restri
 // x = fma(a_{i-1}, p_{i-1}, ... fma(a_{i-B}, p_{i-B}, x)) -- the same FMAs in
 // the same order as one VecAXPY per iteration -- before p_i overwrites p_{i-B}.
 // x is read and written once per B iterations instead of every iteration.
+#ifndef CG_X_NTS
+#define CG_X_NTS 1   // batched x steps: x stored non-temporally (with knob 32 bit 0)
+#endif
 struct PBufs { double *b[4]; };
 template <int JM, int B>
 __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
@@ -346,7 +349,11 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
           xx = fma(al[1], ldv(p1 + k), xx);
           xx = fma(al[2], ldv(p2 + k), xx);
         }
-        x[k] = fma(al[B - 1], po, xx);             // ... x += a_{i-1} p_{i-1}
+        // ... x += a_{i-1} p_{i-1}; x is next read B iterations on, so with
+        // CG_X_NTS its store bypasses the memory-side cache (p_i keeps it)
+        const double xn = fma(al[B - 1], po, xx);
+        if constexpr (NTL && CG_X_NTS) __builtin_nontemporal_store(xn, x + k);
+        else x[k] = xn;
         pout[k] = row(ldv(r + k), JM == 1 ? dv[k] : 0.0, po);
       }
     };
