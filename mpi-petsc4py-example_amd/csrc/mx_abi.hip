@@ -238,7 +238,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->value_codes = A->sd.ntab;
     info->code_bytes = A->sd.code_bytes;
     info->pair_shape = A->sd.ntab > 0 ? A->sd.pair_shape : 0;
-    info->pair_units = info->pair_shape ? (A->sd.pair_blocks ? A->sd.pair_used : A->sd.nunits) : 0;
+    info->pair_units = info->pair_shape ? A->sd.pair_used : 0;
     info->pair_blocks = info->pair_shape ? A->sd.pair_blocks : 0;
     info->pair_block_bytes = info->pair_shape ? 64 * (int64_t)((2 * A->sd.dia_k + 15) / 16 * 16) : 0;
   });

@@ -867,12 +867,17 @@ __global__ void code_fill_kernel(int64_t ns, const int64_t *__restrict__ sptr, c
 }
 
 // ---------------------------------------------------------------- row pairs
-// Units of 128 rows (slices 2u, 2u+1) whose both slices carry the dominant
-// offset pattern, every gather in range and no ghost entries are stored a
+// Units of 128 rows (slices 2u, 2u+1) whose both slices are aligned-offset
+// slices with an offset pattern contained in the dominant one are stored a
 // second time as row pairs: lane l owns rows 128 u + 2 l and + 1, its codes
-// are [K codes of row 0][K codes of row 1] padded to PB bytes, so SpMV loads
-// x as 16-byte pairs -- one load per run of the pattern instead of one per
-// offset and row (mx_spmv.hip, pair body).  Shapes (sorted offsets):
+// are [K codes of row 0][K codes of row 1] in the dominant pattern's slot
+// order, padded to PB bytes; a slot whose offset the row does not store is
+// VCODE_ABSENT.  SpMV loads x as 16-byte pairs -- one load per run of the
+// pattern instead of one per offset and row (mx_spmv.hip, pair body) --
+// through buffer loads that read 0 outside the operand, so the boundary
+// units of a stencil (first/last planes, lines, and the planes next to
+// another rank's rows, whose A_o entries the boundary kernel adds) are pair
+// units too.  Shapes (sorted offsets):
 //   5:  a, -1, 0, 1, b          (2D 5-point)
 //   7:  a, b, -1, 0, 1, c, d    (3D 7-point)
 //   27: nine runs c-1, c, c+1   (3D 27-point)
@@ -898,7 +903,7 @@ constexpr int pair_bytes(int k) { return (2 * k + 15) / 16 * 16; }
 // one wave per unit; sets DPAT_PAIR on slice 2u and writes the unit's codes
 __global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star, const int64_t *__restrict__ sptr,
                                  const int32_t *__restrict__ width, int32_t *__restrict__ dpat,
-                                 const int32_t *__restrict__ wid_o, const double *__restrict__ sval,
+                                 const int32_t *__restrict__ doff, const double *__restrict__ sval,
                                  const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8,
                                  const unsigned long long *__restrict__ tab, const uint8_t *__restrict__ slot_code,
                                  uint8_t *__restrict__ pcode) {
@@ -906,9 +911,24 @@ __global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star,
   if (u >= nunits) return;
   const int lane = threadIdx.x & 63;
   const int64_t s0 = 2 * u, s1 = s0 + 1;
+  const int32_t *__restrict__ so = doff + (int64_t)star * DIA_MAX;
+  // slot j of the dominant pattern -> slot of slice sl's own pattern, or -1
+  auto slot_of = [&](int64_t sl, int j) -> int {
+    const int32_t *__restrict__ po = doff + (int64_t)(dpat[sl] & DPAT_ID) * DIA_MAX;
+    for (int q = 0; q < -width[sl]; ++q)
+      if (po[q] == so[j]) return q;
+    return -1;
+  };
+  // every offset of the slice's pattern is one of the dominant pattern's
   auto ok = [&](int64_t sl) {
-    return width[sl] == -k && (dpat[sl] & DPAT_ID) == star && (dpat[sl] & DPAT_INB) &&
-           (!wid_o || wid_o[sl] == 0);
+    if (width[sl] >= 0) return false;
+    const int32_t *__restrict__ po = doff + (int64_t)(dpat[sl] & DPAT_ID) * DIA_MAX;
+    for (int q = 0; q < -width[sl]; ++q) {
+      bool in = false;
+      for (int j = 0; j < k; ++j) in = in || po[q] == so[j];
+      if (!in) return false;
+    }
+    return true;
   };
   if (u * 128 + 127 >= m || !ok(s0) || !ok(s1)) return;   // wave-uniform
   const int pb = pair_bytes(k);
@@ -917,11 +937,13 @@ __global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star,
     const int64_t row = u * 128 + 2 * lane + h;
     const int64_t sl = row >> 6;
     const int li = (int)(row & 63);
+    const int kw = -width[sl];
     const uint32_t mk = mask8 ? (uint32_t)mask8[row] : mask[row];
     for (int j = 0; j < k; ++j) {
       int c = VCODE_ABSENT;
-      if ((mk >> j) & 1u) {
-        const double v = sval[sell_slot(sptr[sl], j, k, li, true)];
+      const int q = slot_of(sl, j);
+      if (q >= 0 && ((mk >> q) & 1u)) {
+        const double v = sval[sell_slot(sptr[sl], q, kw, li, true)];
         const int hh = vdict_find(tab, (unsigned long long)__double_as_longlong(v));
         c = hh >= 0 ? slot_code[hh] : 0;
       }
@@ -930,6 +952,29 @@ __global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star,
   }
   for (int j = 2 * k; j < pb; ++j) dst[j] = (uint8_t)VCODE_ABSENT;
   if (lane == 0) dpat[s0] |= DPAT_PAIR;
+}
+
+__global__ void pair_count_kernel(int64_t nunits, const int32_t *__restrict__ dpat, unsigned long long *__restrict__ cnt) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool p = u < nunits && (dpat[2 * u] & DPAT_PAIR);
+  const unsigned long long b = __ballot(p);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(cnt, (unsigned long long)__popcll(b));
+}
+
+// pblk flags of the pair units whose slices hold off-diagonal (A_o) entries:
+// SpMV stores their diagonal-block sums and the boundary kernel finishes them
+__global__ void pair_ghost_flags_kernel(int64_t nunits, int64_t nslices, const int32_t *__restrict__ dpat,
+                                        const int32_t *__restrict__ wid_o, int32_t *__restrict__ pblk,
+                                        int *__restrict__ any) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nunits || !(dpat[2 * u] & DPAT_PAIR)) return;
+  uint32_t f = 0;
+  if (wid_o[2 * u]) f |= PBLK_GHOST_LO;
+  if (2 * u + 1 < nslices && wid_o[2 * u + 1]) f |= PBLK_GHOST_HI;
+  if (f) {
+    pblk[u] = (int32_t)((uint32_t)pblk[u] | f);
+    *any = 1;
+  }
 }
 
 // Code-block dictionary of the row-pair layout.  A unit's code block (64
@@ -991,7 +1036,6 @@ static void dedupe_pair_blocks(Sell &S, hipStream_t st) {
   const int64_t nu = S.nunits;
   const int pb = pair_bytes(S.dia_k);
   S.pair_blocks = 0;
-  S.pair_used = 0;
   std::vector<int32_t> blk((size_t)std::max<int64_t>(nu, 1));
   for (int64_t u = 0; u < nu; ++u) blk[(size_t)u] = (int32_t)u;
   S.pblk.alloc(blk.size());
@@ -1010,13 +1054,11 @@ static void dedupe_pair_blocks(Sell &S, hipStream_t st) {
   const int64_t max_blocks = PAIR_DICT_MAX_BYTES / (64 * pb);
   std::unordered_map<unsigned long long, int32_t> ids;
   std::vector<int64_t> rep;
-  int64_t used = 0;
   for (int64_t u = 0; u < nu; ++u) {
     // knob 30 = 2 (tests): every unit hashes alike, so the byte comparison
     // below must reject the dictionary
     const unsigned long long k = g_knobs.pdict == 2 && hh[(size_t)u] ? 1ull : hh[(size_t)u];
     if (!k) { blk[(size_t)u] = 0; continue; }       // not a pair unit: never read
-    ++used;
     auto it = ids.find(k);
     if (it == ids.end()) {
       if ((int64_t)rep.size() >= max_blocks) { identity(); return; }
@@ -1044,10 +1086,9 @@ static void dedupe_pair_blocks(Sell &S, hipStream_t st) {
     if (v) { identity(); return; }                  // hash collision: keep every block
   S.pcode = std::move(dict);
   S.pair_blocks = nb;
-  S.pair_used = used;
 }
 
-static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, hipStream_t st) {
+static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st) {
   S.ntab = 0;
   if (S.slots == 0 || !g_knobs.vcodes) return;
   DBuf<unsigned long long> tab(VDICT_SLOTS);
@@ -1087,16 +1128,42 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, hipStrea
   code_fill_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(ns, S.sptr.p, S.width.p, S.col.p, S.val.p, S.cptr.p, tab.p, sc.p,
                                                           S.mask.p, S.mask8.p, S.code.p);
   HIPCHECK(hipGetLastError());
-  S.pair_shape = g_knobs.spmv_pairs && S.pat_star >= 0 ? pair_shape_of(S.pat_star_off) : 0;
+  // row pairs read the operand through buffer loads with 32-bit byte offsets
+  S.pair_shape = g_knobs.spmv_pairs && S.pat_star >= 0 && m < PAIR_MAX_ROWS && ncols < PAIR_MAX_ROWS
+                     ? pair_shape_of(S.pat_star_off) : 0;
   if (S.pair_shape) {
     S.nunits = ns / 2;
     S.pcode.alloc((size_t)std::max<int64_t>(S.nunits, 1) * 64 * pair_bytes(S.dia_k));
     if (S.nunits)
       pair_fill_kernel<<<(unsigned)cdiv(S.nunits, 4), 256, 0, st>>>(m, S.nunits, S.dia_k, S.pat_star, S.sptr.p,
-                                                                   S.width.p, S.dpat.p, wid_o, S.val.p, S.mask.p,
+                                                                   S.width.p, S.dpat.p, S.doff.p, S.val.p, S.mask.p,
                                                                    S.mask8.p, tab.p, sc.p, S.pcode.p);
     HIPCHECK(hipGetLastError());
+    {
+      DBuf<unsigned long long> cnt(1);
+      HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long), st));
+      pair_count_kernel<<<(unsigned)cdiv(std::max<int64_t>(S.nunits, 1), 256), 256, 0, st>>>(S.nunits, S.dpat.p, cnt.p);
+      HIPCHECK(hipGetLastError());
+      unsigned long long hc = 0;
+      HIPCHECK(hipMemcpyAsync(&hc, cnt.p, sizeof(hc), hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      S.pair_used = (int64_t)hc;
+    }
     dedupe_pair_blocks(S, st);
+    S.pair_ghosts = false;
+    if (wid_o && S.nunits) {
+      DBuf<int> any(1);
+      HIPCHECK(hipMemsetAsync(any.p, 0, sizeof(int), st));
+      pair_ghost_flags_kernel<<<(unsigned)cdiv(S.nunits, 256), 256, 0, st>>>(S.nunits, ns, S.dpat.p, wid_o, S.pblk.p,
+                                                                             any.p);
+      HIPCHECK(hipGetLastError());
+      int ha = 0;
+      HIPCHECK(hipMemcpyAsync(&ha, any.p, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPCHECK(hipStreamSynchronize(st));
+      S.pair_ghosts = ha != 0;
+    }
+    // every full unit a pair unit: SpMV reads no per-unit pattern word
+    S.pair_all = S.pair_used == m / 128;
   }
   HIPCHECK(hipStreamSynchronize(st));   // tab / sc are freed on return
   S.ntab = (int)keys.size();
@@ -1373,7 +1440,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   // ---- SpMV layouts
   build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
   build_sell(A->so, m, A->nghost, A->optr.p, A->ocol.p, A->oval.p, st, false);
-  build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, st);
+  build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, A->n, st);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
 

@@ -142,21 +142,27 @@ struct LocalWorld {
   std::vector<double *> red_ptr;
   std::vector<std::vector<Msg>> posted;
   std::vector<int64_t> slots;
-  std::vector<int> tags;        // collective each rank entered (mismatch = error, not a race)
+  // collective each rank entered, one row per generation parity: a rank
+  // released from generation g may enter g+1 (and write its tag there) while
+  // a slower one still checks the tags of g; g+2 cannot start before every
+  // rank has left g.  Unchecked barriers record tag 0, so a checked barrier
+  // meeting an unchecked one fails too (mismatch = error, not a race).
+  std::vector<int> tags[2];
   bool broken = false;          // a rank failed: every barrier throws instead of waiting
-  explicit LocalWorld(int s) : size(s), red_ptr(s), posted(s), slots((size_t)s * s), tags(s) {}
-  // tag: which collective the caller is in; all ranks must agree
-  void barrier(int rank = -1, int tag = 0) {
+  explicit LocalWorld(int s) : size(s), red_ptr(s), posted(s), slots((size_t)s * s) { tags[0].resize(s); tags[1].resize(s); }
+  // tag: which collective the caller is in (0: not checked); all ranks must agree
+  void barrier(int rank, int tag = 0) {
     std::unique_lock<std::mutex> lk(mu);
     if (broken) fail(MX_ERR_COMM, "local world: another rank failed");
-    if (rank >= 0) tags[rank] = tag;
     long g = gen;
+    std::vector<int> &tg = tags[g & 1];
+    tg[rank] = tag;
     if (++arrived == size) { arrived = 0; gen++; cv.notify_all(); }
     else cv.wait(lk, [&] { return gen != g || broken; });
     if (broken) fail(MX_ERR_COMM, "local world: another rank failed");
-    if (rank >= 0)
+    if (tag != 0)
       for (int q = 0; q < size; ++q)
-        if (tags[q] != tag) {
+        if (tg[q] != tag) {
           broken = true;
           cv.notify_all();
           fail(MX_ERR_COMM, "local world: ranks entered different collectives");
@@ -207,7 +213,7 @@ struct LocalComm : Comm {
     local_sum_kernel<<<grid_for(n, 256), 256, 0, stream>>>(pk, size, n, tmp.p);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(stream));
-    w->barrier();                  // every rank has read every dev
+    w->barrier(rank);              // every rank has read every dev
     HIPCHECK(hipMemcpyAsync(dev, tmp.p, sizeof(double) * n, hipMemcpyDeviceToDevice, stream));
   }
 
@@ -223,20 +229,20 @@ struct LocalComm : Comm {
       if (r.bytes) HIPCHECK(hipMemcpyAsync(r.buf, src->buf, r.bytes, hipMemcpyDeviceToDevice, st));
     }
     HIPCHECK(hipStreamSynchronize(st));
-    w->barrier();                  // the senders' buffers may be overwritten now
+    w->barrier(rank);              // the senders' buffers may be overwritten now
   }
 
   void alltoall_i64(const int64_t *send, int64_t *recv) override {
     for (int q = 0; q < size; ++q) w->slots[(size_t)rank * size + q] = send[q];
     w->barrier(rank, 3);
     for (int q = 0; q < size; ++q) recv[q] = w->slots[(size_t)q * size + rank];
-    w->barrier();
+    w->barrier(rank);
   }
   void allgather_i64(int64_t v, int64_t *all) override {
     w->slots[rank] = v;
     w->barrier(rank, 4);
     for (int q = 0; q < size; ++q) all[q] = w->slots[q];
-    w->barrier();
+    w->barrier(rank);
   }
   void barrier() override {
     HIPCHECK(hipStreamSynchronize(stream));
@@ -260,7 +266,7 @@ struct ShmHeader {
   int64_t scratch[SHM_MAX][SHM_MAX];        // [rank][k]: small all-to-all / all-gather payloads
   int64_t ndir[SHM_MAX];
   ShmDirEnt dir[SHM_MAX][SHM_DIR];
-  int tags[SHM_MAX];
+  int tags[2][SHM_MAX];                      // by generation parity (see LocalWorld)
 };
 
 struct ShmComm : Comm {
@@ -329,11 +335,16 @@ struct ShmComm : Comm {
   }
   char *slot(int q) { return base + (size_t)q * (size_t)h->slot_bytes; }
 
-  // sense-free generation barrier; tag checks that every rank is in the same collective
+  // sense-free generation barrier; tag checks that every rank is in the same
+  // collective.  Tags live in one row per generation parity (a rank released
+  // early may already write its next tag while a slower one checks these);
+  // unchecked barriers record tag 0.  The generation cannot move between the
+  // load below and this rank's arrival, which it needs.
   void wait_barrier(int tag, int check) {
     if (h->abort.load()) fail(MX_ERR_COMM, "shared-memory world: another rank failed");
-    if (check) h->tags[rank] = tag;
     const int64_t g = h->gen.load(std::memory_order_acquire);
+    int *tg = h->tags[g & 1];
+    tg[rank] = check ? tag : 0;
     if (h->arrived.fetch_add(1, std::memory_order_acq_rel) == size - 1) {
       h->arrived.store(0, std::memory_order_relaxed);
       h->gen.fetch_add(1, std::memory_order_acq_rel);
@@ -353,7 +364,7 @@ struct ShmComm : Comm {
     }
     if (check)
       for (int q = 0; q < size; ++q)
-        if (h->tags[q] != tag) { h->abort.store(1); fail(MX_ERR_COMM, "shared-memory world: ranks entered different collectives"); }
+        if (tg[q] != tag) { h->abort.store(1); fail(MX_ERR_COMM, "shared-memory world: ranks entered different collectives"); }
   }
 
   void allreduce_sum(double *dev, int n) override {
@@ -421,6 +432,8 @@ struct ShmComm : Comm {
       HIPCHECK(hipStreamSynchronize(st));
       wait_barrier(0, 0);
     }
+    // no rounds: peers may still read this rank's directory and round count
+    if (rounds == 0) wait_barrier(0, 0);
   }
 
   void alltoall_i64(const int64_t *send, int64_t *recv) override {

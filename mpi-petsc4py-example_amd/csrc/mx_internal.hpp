@@ -135,10 +135,16 @@ struct Sell {
   // unit u's codes are block pblk[u] of pcode: u itself, or (pair_blocks > 0)
   // an index into the dictionary of the distinct blocks (a stencil has a few
   // dozen: boundary classes x value classes), which then stays in L2
-  DBuf<int32_t> pblk;     // [nunits]
+  DBuf<int32_t> pblk;     // [nunits] | PBLK_GHOST_LO/HI: the unit's first/second slice has A_o entries
   int64_t pair_blocks = 0;
-  int64_t pair_used = 0;   // units stored as row pairs (known when the dictionary is built)
+  int64_t pair_used = 0;   // units stored as row pairs
+  bool pair_ghosts = false;  // some pair unit has A_o entries (SpMV then always splits)
+  bool pair_all = false;     // every full unit is a pair unit
 };
+constexpr uint32_t PBLK_GHOST_LO = 1u << 30;
+constexpr uint32_t PBLK_GHOST_HI = 1u << 31;
+constexpr uint32_t PBLK_ID = PBLK_GHOST_LO - 1;
+constexpr int64_t PAIR_MAX_ROWS = int64_t(1) << 28;   // operand byte offsets (unsigned 32-bit voffset, bound n * 8 < 2^31)
 constexpr int VCODE_MAX = 256;      // table entries; code 255 marks an absent slot
 constexpr int VCODE_ABSENT = VCODE_MAX - 1;
 constexpr int CODE_BATCH = 8 * SLICE;   // bytes per 8-slot batch of a slice

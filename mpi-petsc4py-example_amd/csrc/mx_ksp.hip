@@ -1117,55 +1117,61 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
                (!fuse_cg || (poll & 1) == 0) && !A->cg_graph_failed;
   std::vector<uintptr_t> key;
   if (graph) {
+    // the whole knob block is part of the key: every knob a captured kernel
+    // could have baked in (template choice, launch geometry, argument) counts
     key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
-           (uintptr_t)poll, (uintptr_t)g_knobs.overlap, (uintptr_t)g_knobs.spmv_nt, (uintptr_t)g_knobs.spmv_grid,
-           (uintptr_t)g_knobs.force_coll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p,
-           (uintptr_t)w.p, (uintptr_t)pv2, (uintptr_t)part.p, (uintptr_t)g_knobs.cg_vec_grid,
-           (uintptr_t)g_knobs.cg_vec, (uintptr_t)g_knobs.cg_nts, (uintptr_t)g_knobs.cg_unroll,
-           (uintptr_t)g_knobs.cg_upd_grid, (uintptr_t)g_knobs.vcodes, (uintptr_t)g_knobs.spmv_bpc, (uintptr_t)g_knobs.spmv_pairs, (uintptr_t)g_knobs.spmv_pair_bpc,
-           (uintptr_t)g_knobs.spmv_ynt, (uintptr_t)xb, (uintptr_t)pv3, (uintptr_t)pv4};
+           (uintptr_t)poll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p, (uintptr_t)w.p, (uintptr_t)pv2,
+           (uintptr_t)part.p, (uintptr_t)xb, (uintptr_t)pv3, (uintptr_t)pv4};
+    const int *kw = reinterpret_cast<const int *>(&g_knobs);
+    for (size_t q = 0; q < sizeof(Knobs) / sizeof(int); ++q) key.push_back((uintptr_t)(uint32_t)kw[q]);
     std::memcpy(&key[5], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;
-  // Eager until a graph for exactly this configuration exists: the first
-  // batch of the first solve also warms every RCCL connection it uses, so the
-  // capture that follows records only steady-state collective calls.
+  // A capture records a batch of `poll` iterations without running them. A
+  // single-rank communicator captures before its first iteration (so a short
+  // first solve -- KSPSetUp, a warmup -- leaves the graph for the next one);
+  // a multi-rank one after its first eager batch, which also warms every RCCL
+  // connection the batch uses, so the capture holds only steady-state calls.
+  // A batch shorter than `poll` (the max_it remainder) runs eagerly: replaying
+  // a whole batch would launch iterations that only test the done flag.
+  auto capture = [&]() {
+    if (A->cg_graph) { HIPCHECK(hipGraphExecDestroy(A->cg_graph)); A->cg_graph = nullptr; }
+    // A capture that fails (a runtime or collective library that cannot
+    // record some call) leaves the iterations un-run: drop the graph for
+    // this operator and carry on eagerly from the same state.
+    hipGraph_t g = nullptr;
+    try {
+      HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      for (int k = 0; k < poll; ++k) iteration(i + k);
+      HIPCHECK(hipStreamEndCapture(st, &g));
+      HIPCHECK(hipGraphInstantiate(&A->cg_graph, g, nullptr, nullptr, 0));
+      HIPCHECK(hipGraphDestroy(g));
+      A->cg_key = key;
+      use_graph = true;
+    } catch (const Error &) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        hipGraph_t junk = nullptr;
+        (void)hipStreamEndCapture(st, &junk);
+        if (junk) (void)hipGraphDestroy(junk);
+      }
+      if (g) (void)hipGraphDestroy(g);
+      if (A->cg_graph) { (void)hipGraphExecDestroy(A->cg_graph); A->cg_graph = nullptr; }
+      (void)hipGetLastError();
+      A->cg_graph_failed = true;
+      graph = false;
+    }
+  };
+  if (graph && !use_graph && c->size == 1 && p.max_it > 0) capture();
   for (; i < p.max_it;) {
-    if (use_graph) {
+    if (use_graph && p.max_it - i >= poll) {
       HIPCHECK(hipGraphLaunch(A->cg_graph, st));
       i += poll;
     } else {
       for (int k = 0; k < poll && i < p.max_it; ++k, ++i) iteration(i);
     }
     if (poller.batch(done)) break;
-    if (graph && !use_graph && i < p.max_it) {
-      if (A->cg_graph) { HIPCHECK(hipGraphExecDestroy(A->cg_graph)); A->cg_graph = nullptr; }
-      // A capture that fails (a runtime or collective library that cannot
-      // record some call) leaves the iterations un-run: drop the graph for
-      // this operator and carry on eagerly from the same state.
-      hipGraph_t g = nullptr;
-      try {
-        HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-        for (int k = 0; k < poll; ++k) iteration(i + k);
-        HIPCHECK(hipStreamEndCapture(st, &g));
-        HIPCHECK(hipGraphInstantiate(&A->cg_graph, g, nullptr, nullptr, 0));
-        HIPCHECK(hipGraphDestroy(g));
-        A->cg_key = key;
-        use_graph = true;
-      } catch (const Error &) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
-          hipGraph_t junk = nullptr;
-          (void)hipStreamEndCapture(st, &junk);
-          if (junk) (void)hipGraphDestroy(junk);
-        }
-        if (g) (void)hipGraphDestroy(g);
-        if (A->cg_graph) { (void)hipGraphExecDestroy(A->cg_graph); A->cg_graph = nullptr; }
-        (void)hipGetLastError();
-        A->cg_graph_failed = true;
-        graph = false;
-      }
-    }
+    if (graph && !use_graph && i < p.max_it) capture();
   }
   cg_tail_kernel<<<1, 64, 0, st>>>(s, hist_d);   // max_it launched without a stop
   HIPCHECK(hipGetLastError());

@@ -99,6 +99,47 @@ struct XCg {
   }
 };
 
+// Buffer-load forms of the operand sources for the row-pair body: 32-bit
+// element indices, and a read outside the vector (an absent slot of a
+// boundary unit: its offset points before row 0 or past the last row)
+// returns 0 by the hardware range check instead of faulting, so no unit
+// needs an in-range test.  Bound: n * 8 < 2^31 (PAIR_MAX_ROWS); a negative
+// index wraps to an offset >= 2^31, outside every vector.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double *p, int64_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), 0, (int)(n * 8), 0x00020000);
+}
+__device__ __forceinline__ dbl2 bload2(__amdgpu_buffer_rsrc_t r, int i) {
+  return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)((unsigned)i * 8u), 0, 0));
+}
+__device__ __forceinline__ double bload1(__amdgpu_buffer_rsrc_t r, int i) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)((unsigned)i * 8u), 0, 0));
+}
+template <class XS> struct XBuf;
+template <bool S> struct XBuf<XPlainT<S>> {
+  __amdgpu_buffer_rsrc_t x;
+  double s;
+  __device__ __forceinline__ XBuf(const XPlainT<S> &X, int64_t n) : x(vec_rsrc(X.x, n)), s(X.s) {}
+  __device__ __forceinline__ double operator()(int i) const { const double v = bload1(x, i); return S ? s * v : v; }
+  __device__ __forceinline__ dbl2 pair(int i) const {
+    const dbl2 v = bload2(x, i);
+    return S ? dbl2{s * v.x, s * v.y} : v;
+  }
+};
+template <int JM> struct XBuf<XCg<JM>> {
+  __amdgpu_buffer_rsrc_t r, p, d;
+  XCg<JM> f;
+  __device__ __forceinline__ XBuf(const XCg<JM> &X, int64_t n)
+      : r(vec_rsrc(X.r, n)), p(vec_rsrc(X.p, n)), d(vec_rsrc(JM == 1 ? X.d : X.r, n)), f(X) {}
+  __device__ __forceinline__ double operator()(int i) const {
+    return f.form(bload1(r, i), bload1(p, i), JM == 1 ? bload1(d, i) : 0.0);
+  }
+  __device__ __forceinline__ dbl2 pair(int i) const {
+    const dbl2 rv = bload2(r, i), pv = bload2(p, i);
+    const dbl2 dv = JM == 1 ? bload2(d, i) : dbl2{0.0, 0.0};
+    return dbl2{f.form(rv.x, pv.x, dv.x), f.form(rv.y, pv.y, dv.y)};
+  }
+};
+
 // Matrix values of one slice: fp64 in the paired layout (slot j of a lane at
 // pair j / 2), or one-byte codes into the matrix's value table (copied to LDS
 // at kernel start): batch b = entries 8 b .. 8 b + 7 of every lane, one 8-B
@@ -512,31 +553,37 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     // the dominant pattern's offsets, and each run's anchor (singleton / centre)
     const int32_t *__restrict__ offs = doff + (int64_t)pat_star * DIA_MAX;
-    int64_t anchor[NR];
+    int anchor[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) anchor[r] = offs[SH::first(r) + (SH::tri(r) ? 1 : 0)];
+    const XBuf<XS> XB(X, MODE == SPMV_CG ? m : ncols);
+    // pdict bits: 1 = code blocks from the dictionary (cached), 2 = read pblk
+    // (dictionary ids and/or ghost flags), 4 = every full unit is a pair unit
+    const bool use_pblk = (pdict & 3) != 0;
     // one unit's loads: its code block, every x pair and the edge values
-    struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e_lo[NR], e_hi[NR]; };
-    auto unit_load = [&](int u, int blk, Unit &t) __attribute__((always_inline)) {
-      const int64_t ubase = (int64_t)u * 128, r0 = ubase + 2 * lane;
+    struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e_lo[NR], e_hi[NR]; uint32_t fl; };
+    auto unit_load = [&](int u, int32_t blkw, Unit &t) __attribute__((always_inline)) {
+      const int ubase = u * 128, r0 = ubase + 2 * lane;
+      const uint32_t bw = (uint32_t)blkw;
+      t.fl = bw & ~PBLK_ID;
       // the unit's code block: its own (streamed non-temporally), or a
       // dictionary block shared with every unit of the same boundary/value
       // class (cached: the dictionary stays in L2)
-      if (pdict) {                                // kernel-uniform
-        const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)blk * 64 + lane) * PB);
+      const int64_t blk = use_pblk ? (int64_t)(bw & PBLK_ID) : (int64_t)u;
+      const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + (blk * 64 + lane) * PB);
+      if (pdict & 1) {                            // kernel-uniform
 #pragma unroll
         for (int q = 0; q < PB / 16; ++q) t.cw[q] = cp[q];
       } else {
-        const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + ((int64_t)u * 64 + lane) * PB);
 #pragma unroll
         for (int q = 0; q < PB / 16; ++q) t.cw[q] = ld<NT>(cp + q);
       }
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
-        t.L[r] = X.pair(r0 + anchor[r]);         // the operand (scaled / formed as the mode has it)
+        t.L[r] = XB.pair(r0 + anchor[r]);        // the operand (scaled / formed as the mode has it)
         if (SH::tri(r)) {
-          t.e_lo[r] = X(ubase + anchor[r] - 1);   // row 0 of lane 0: x[r0 + c - 1]
-          t.e_hi[r] = X(ubase + 128 + anchor[r]); // row 1 of lane 63: x[r0 + 1 + c + 1]
+          t.e_lo[r] = XB(ubase + anchor[r] - 1);   // row 0 of lane 0: x[r0 + c - 1]
+          t.e_hi[r] = XB(ubase + 128 + anchor[r]); // row 1 of lane 63: x[r0 + 1 + c + 1]
         }
       }
     };
@@ -565,8 +612,13 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
         sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
       }
+      // SPLIT: rows of a slice with A_o entries store the diagonal-block sum;
+      // the boundary kernel continues it (and applies the epilogue)
+      const bool gh = SPLIT && (t.fl & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
       double o0 = sum0, o1 = sum1;
-      if constexpr (spmv_jac(MODE)) { o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1); }
+      if constexpr (spmv_jac(MODE)) {
+        if (!gh) { o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1); }
+      }
       if (ynt) __builtin_nontemporal_store(dbl2{o0, o1}, reinterpret_cast<dbl2 *>(y + r0));
       else *reinterpret_cast<dbl2 *>(y + r0) = dbl2{o0, o1};
       if constexpr (MODE == SPMV_CG) {
@@ -580,18 +632,24 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         }
       }
       if constexpr (MODE == SPMV_DOT || MODE == SPMV_CG) {   // operand at the own rows = the centre pair
-        dot += t.L[SH::CENTER_RUN].x * sum0;
-        dot += t.L[SH::CENTER_RUN].y * sum1;
+        if (!gh) {
+          dot += t.L[SH::CENTER_RUN].x * sum0;
+          dot += t.L[SH::CENTER_RUN].y * sum1;
+        }
       }
     };
+    // is unit v stored as row pairs (wave-uniform)
+    auto is_pair = [&](int v) -> bool {
+      return (pdict & 4) ? (int64_t)v * 128 + 127 < m : (dpat[2 * v] & DPAT_PAIR) != 0;
+    };
     auto one_unit = [&](int u) __attribute__((always_inline)) {
-      if (!(dpat[2 * u] & DPAT_PAIR)) {           // wave-uniform
+      if (!is_pair(u)) {
         one_slice(2 * u);
         if (2 * u + 1 < nslices) one_slice(2 * u + 1);
         return;
       }
       Unit t;
-      unit_load(u, pdict ? pblk[u] : 0, t);
+      unit_load(u, use_pblk ? pblk[u] : 0, t);
       __builtin_amdgcn_sched_barrier(0);          // every load issued before the first lookup
       unit_finish(u, t);
     };
@@ -609,9 +667,9 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         Meta q;
         if (v + sstep < send) {
           const int va = item(v), vb = item(v + sstep);
-          q.da = dpat[2 * va];
-          q.db = dpat[2 * vb];
-          if (pdict) { q.ba = pblk[va]; q.bb = pblk[vb]; }
+          q.da = is_pair(va) ? DPAT_PAIR : 0;
+          q.db = is_pair(vb) ? DPAT_PAIR : 0;
+          if (use_pblk) { q.ba = pblk[va]; q.bb = pblk[vb]; }
         }
         return q;
       };
@@ -787,6 +845,12 @@ void halo_begin(Mat *A, const double *x) {
   halo_exchange(A, x, nullptr, nullptr, A->comm->stream);
 }
 
+// the pair body's pdict argument (see the kernel)
+static int pair_flags(const Mat *A) {
+  const Sell &S = A->sd;
+  return (S.pair_blocks > 0 ? 1 : 0) | (S.pair_blocks > 0 || S.pair_ghosts ? 2 : 0) | (S.pair_all ? 4 : 0);
+}
+
 // returns the grid; a fold (cnt set) counts all of its workgroups
 static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold_in,
@@ -801,7 +865,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
       partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt, \
-      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, A->sd.pair_blocks > 0 ? 1 : 0, g_knobs.spmv_rev
+      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, pair_flags(A), g_knobs.spmv_rev
   using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
   KFn kf = nullptr;
 #define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>
@@ -874,31 +938,43 @@ void spmv_launch(Mat *A, const double *x, double *y, int mode, Jac jac, double *
 
 constexpr int BND_BLOCKS = 2048;   // one boundary slice per wave: the launch runs after the interior, alone on the GPU
 
-bool matmult_splits(const Mat *A) { return A->comm->size > 1 && A->halo.nbnd > 0 && g_knobs.overlap; }
+// The product splits (diagonal-block launch, then the boundary kernel adds
+// A_o) when the halo overlaps the interior, and always when some row-pair
+// unit has A_o entries: the pair body has no A_o continuation of its own.
+static bool pair_forces_split(const Mat *A) { return A->sd.pair_ghosts && A->sd.ntab > 0 && g_knobs.vcodes && g_knobs.spmv_pairs; }
+bool matmult_splits(const Mat *A) {
+  return A->comm->size > 1 && A->halo.nbnd > 0 && (g_knobs.overlap || pair_forces_split(A));
+}
 
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                     int *done_flag, const CgFuse *cg, const Fold *fold, const double *xscale) {
   Comm *c = A->comm;
   Halo &H = A->halo;
   hipStream_t st = c->stream;
-  if (c->size == 1 || H.nbnd == 0 || !g_knobs.overlap) {
+  if (!matmult_splits(A)) {
     if (c->size > 1) halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, st);
     return launch_main(A, x, y, mode, jac, partials, done_flag, false, st, cg, fold ? *fold : Fold{}, xscale);
   }
-  hipStream_t cs = c->comm_stream;
-  if (!H.ev_x) {
-    HIPCHECK(hipEventCreateWithFlags(&H.ev_x, hipEventDisableTiming));
-    HIPCHECK(hipEventCreateWithFlags(&H.ev_done, hipEventDisableTiming));
+  int nmain;
+  if (g_knobs.overlap) {
+    hipStream_t cs = c->comm_stream;
+    if (!H.ev_x) {
+      HIPCHECK(hipEventCreateWithFlags(&H.ev_x, hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&H.ev_done, hipEventDisableTiming));
+    }
+    // halo on the comm stream, after the operand's inputs are final on the
+    // compute stream; the CG operand's inputs (r, p_{i-1}) are only read by both
+    HIPCHECK(hipEventRecord(H.ev_x, st));
+    HIPCHECK(hipStreamWaitEvent(cs, H.ev_x, 0));
+    halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, cs);
+    HIPCHECK(hipEventRecord(H.ev_done, cs));
+    // interior slices meanwhile; boundary slices after the exchange
+    nmain = launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{}, xscale);
+    HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
+  } else {                      // no overlap: exchange, split product, boundary pass
+    halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, st);
+    nmain = launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{}, xscale);
   }
-  // halo on the comm stream, after the operand's inputs are final on the
-  // compute stream; the CG operand's inputs (r, p_{i-1}) are only read by both
-  HIPCHECK(hipEventRecord(H.ev_x, st));
-  HIPCHECK(hipStreamWaitEvent(cs, H.ev_x, 0));
-  halo_exchange(A, x, mode == SPMV_CG ? cg : nullptr, done_flag, cs);
-  HIPCHECK(hipEventRecord(H.ev_done, cs));
-  // interior slices meanwhile; boundary slices after the exchange
-  const int nmain = launch_main(A, x, y, mode, jac, partials, done_flag, true, st, cg, Fold{}, xscale);
-  HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
   const int nb = std::min(g_knobs.bnd_grid > 0 ? g_knobs.bnd_grid : BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
   // the boundary launch folds the partials of both launches (fold) or
   // appends its own after the main launch's

@@ -442,7 +442,7 @@ class Vec:
         stash and reach their owner at assemblyEnd (negative indices skipped)."""
         gidx = np.atleast_1d(np.asarray(indices, dtype=np.int64))
         val = np.broadcast_to(np.asarray(values, dtype=np.float64), gidx.shape)
-        add = addv in (InsertMode.ADD_VALUES, InsertMode.ADD, True)
+        add = _is_add(addv)
         mode = getattr(self, "_vmode", None)
         if mode is not None and mode != add:
             raise Error(PETSC_ERR_ARG_WRONG, "You have already added values; you cannot now insert")
@@ -585,6 +585,14 @@ class InsertMode:
     NOT_SET_VALUES = 0
 
 
+def _is_add(addv) -> bool:
+    """petsc4py's InsertMode argument: None/False insert, True adds, an int is
+    compared against ADD_VALUES only (INSERT_VALUES == 1 == True must not add)."""
+    if addv is None or isinstance(addv, bool):
+        return addv is True
+    return int(addv) == InsertMode.ADD_VALUES
+
+
 # ------------------------------------------------------------------ Mat
 class Mat:
     """Row-partitioned AIJ matrix (MATSEQAIJ / MATMPIAIJ)."""
@@ -692,7 +700,7 @@ class Mat:
         rows = np.atleast_1d(np.asarray(rows, dtype=np.int64))
         cols = np.atleast_1d(np.asarray(cols, dtype=np.int64))
         vals = np.asarray(values, dtype=np.float64).reshape(rows.size, cols.size)
-        mode = InsertMode.ADD_VALUES if addv in (InsertMode.ADD_VALUES, True) else InsertMode.INSERT_VALUES
+        mode = InsertMode.ADD_VALUES if _is_add(addv) else InsertMode.INSERT_VALUES
         if self._mode is not None and mode != self._mode:
             raise Error(PETSC_ERR_ARG_WRONG, "You cannot mix add values and insert values")
         self._mode = mode
@@ -707,7 +715,7 @@ class Mat:
         I = np.asarray(I, dtype=np.int64)
         rstart = self.getOwnershipRange()[0] if self._h else _split(self._size[1], self._comm.size, self._comm.rank)[0]
         rows = np.repeat(np.arange(I.size - 1, dtype=np.int64) + rstart, np.diff(I))
-        mode = InsertMode.ADD_VALUES if addv in (InsertMode.ADD_VALUES, True) else InsertMode.INSERT_VALUES
+        mode = InsertMode.ADD_VALUES if _is_add(addv) else InsertMode.INSERT_VALUES
         self._mode = self._mode or mode
         self._stash.append((rows, np.asarray(J, dtype=np.int64), np.asarray(V, dtype=np.float64)))
 
@@ -1087,7 +1095,7 @@ class KSP:
         if kt == "preonly" and pct == "lu":
             from . import direct
             t0 = time.perf_counter()
-            direct.lu_solve(self._A, b, x)
+            _guard(direct.lu_solve, self._A, b, x)
             self._its, self._reason, self._rnorm = 1, 4, 0.0
             self._timing = {"KSPSolve": time.perf_counter() - t0}
             self._report()

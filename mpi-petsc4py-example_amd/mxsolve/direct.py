@@ -12,6 +12,7 @@ import ctypes as C
 import numpy as np
 
 from . import core
+from . import _lib
 from ._lib import call
 
 
@@ -36,13 +37,28 @@ def lu_solve(A, b, x):
         n = gb.size
         gx = np.zeros(n)
         dc = A._dc
-        call("mx_lu_solve_csr", dc.h, n, C.c_void_p(gip.ctypes.data), C.c_void_p(gcj.ctypes.data),
-             C.c_void_p(gvv.ctypes.data), C.c_void_p(gb.ctypes.data), C.c_void_p(gx.ctypes.data))
-        counts = [p[3].size for p in parts]
-        starts = np.concatenate([[0], np.cumsum(counts)])
-        chunks = [gx[starts[r]:starts[r + 1]] for r in range(len(parts))]
+        try:
+            call("mx_lu_solve_csr", dc.h, n, C.c_void_p(gip.ctypes.data), C.c_void_p(gcj.ctypes.data),
+                 C.c_void_p(gvv.ctypes.data), C.c_void_p(gb.ctypes.data), C.c_void_p(gx.ctypes.data))
+        except Exception as e:       # every rank raises the same error instead of waiting in bcast
+            if mc.Get_size() == 1:
+                raise
+            chunks = ("error", getattr(e, "code", None), getattr(e, "msg", str(e)))
+            err = e
+        else:
+            counts = [p[3].size for p in parts]
+            starts = np.concatenate([[0], np.cumsum(counts)])
+            chunks = [gx[starts[r]:starts[r + 1]] for r in range(len(parts))]
     else:
         chunks = None
-    xl = mc.bcast(chunks, root=0)[mc.Get_rank()] if mc.Get_size() > 1 else chunks[0]
+    if mc.Get_size() > 1:
+        chunks = mc.bcast(chunks, root=0)
+        if isinstance(chunks, tuple) and chunks[:1] == ("error",):
+            if mc.Get_rank() == 0:
+                raise err
+            if chunks[1] is None:
+                raise RuntimeError(chunks[2])
+            raise _lib.MxError(chunks[1], chunks[2])
+    xl = chunks[mc.Get_rank()]
     x.setArray(xl)
     return x

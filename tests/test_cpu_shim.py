@@ -34,6 +34,16 @@ def test_size_forms():
     assert [_split(100, 3, r) for r in range(3)] == [(0, 34), (34, 33), (67, 33)]
 
 
+def test_insert_mode_mapping():
+    """petsc4py's addv: None/False/INSERT_VALUES insert, True/ADD_VALUES add
+    (INSERT_VALUES == 1 == True must not be taken as ADD)."""
+    from mxsolve.PETSc import InsertMode, _is_add
+    assert not _is_add(None) and not _is_add(False)
+    assert not _is_add(InsertMode.INSERT_VALUES) and not _is_add(InsertMode.INSERT)
+    assert not _is_add(1) and not _is_add(InsertMode.NOT_SET_VALUES)
+    assert _is_add(True) and _is_add(InsertMode.ADD_VALUES) and _is_add(InsertMode.ADD) and _is_add(2)
+
+
 def test_ksp_options_override_without_gpu():
     """setFromOptions applies after explicit setters (test.py:38-46)."""
     from mxsolve import PETSc

@@ -423,3 +423,31 @@ def test_distributed_row_pairs(oracle_mod, P, kind, n, fuse):
     assert all(r[0] == o["its"] and r[1] == o["reason"] for r in res), ([r[:2] for r in res], o["its"])
     xs = np.concatenate([r[2] for r in res])
     assert np.linalg.norm(xs - o["x"]) / np.linalg.norm(o["x"]) <= REL_TOL
+
+
+def test_local_barrier_then_collectives_skewed():
+    """LocalComm: barrier() immediately followed by an all-reduce, with skewed
+    rank threads (the per-generation tag rows keep a released rank's next tag
+    from being read as the previous collective's)."""
+    import random
+    import time
+    from mxsolve.core import LocalWorld, vdot
+    W = LocalWorld(4)
+
+    def body(c):
+        x = c.empty(1000)
+        x.fill_(1.0)
+        rng = random.Random(c.rank)
+        t = 0.0
+        for _ in range(300):
+            if rng.random() < 0.5:
+                time.sleep(rng.random() * 2e-4)
+            c.barrier()
+            t += vdot(c, x, x)
+        return t
+
+    try:
+        out = W.run(body)
+    finally:
+        W.destroy()
+    assert out == [300 * 4000.0] * 4

@@ -179,3 +179,33 @@ def test_ascii_view_petsc_format(PETSc, capsys):
     b.view()
     out = capsys.readouterr().out.splitlines()
     assert out == ["Vec Object: 1 MPI process", "  type: seq", "1.", "0.5", "3e-07"]
+
+
+def test_insert_values_explicit_over_existing(PETSc):
+    """An explicit INSERT_VALUES replaces existing entries (Vec and Mat re-assembly);
+    ADD_VALUES sums into them."""
+    from mxsolve import MPI
+    v = PETSc.Vec().createMPI(4, comm=MPI.COMM_WORLD)
+    v.set(1.0)
+    v.setValues([0, 2], [5.0, 7.0], PETSc.InsertMode.INSERT_VALUES)
+    v.assemble()
+    assert np.array_equal(v.getArray(), [5.0, 1.0, 7.0, 1.0])
+    w = PETSc.Vec().createMPI(4, comm=MPI.COMM_WORLD)
+    w.set(1.0)
+    w.setValues([1], [2.5], PETSc.InsertMode.ADD_VALUES)
+    w.assemble()
+    assert np.array_equal(w.getArray(), [1.0, 3.5, 1.0, 1.0])
+
+    A = PETSc.Mat().create(comm=MPI.COMM_WORLD)
+    A.setSizes((3, 3))
+    A.setUp()
+    for i in range(3):
+        A.setValues([i], [i], [[2.0]], PETSc.InsertMode.INSERT_VALUES)
+    A.assemble()
+    A.setValues([1], [1], [[9.0]], PETSc.InsertMode.INSERT_VALUES)
+    A.setValuesCSR([0, 1, 1, 1], [0], [4.0], PETSc.InsertMode.INSERT_VALUES)
+    A.assemble()
+    assert np.array_equal(A.getDiagonal().getArray(), [4.0, 9.0, 2.0])
+    A.setValues([2], [2], [[1.5]], PETSc.InsertMode.ADD_VALUES)
+    A.assemble()
+    assert np.array_equal(A.getDiagonal().getArray(), [4.0, 9.0, 3.5])

@@ -77,3 +77,23 @@ def test_shm_distributed_solve(P, kind, n, ksp):
     assert res["rows_ok"]
     assert (res["its"], res["reason"]) == (res["oracle_its"], res["oracle_reason"]), res
     assert res["rel"] <= 1e-10, res
+
+
+def test_shm_barrier_then_collectives_skewed():
+    """barrier() followed at once by all-reduces / halo exchanges, ranks
+    skewed: no false 'ranks entered different collectives' (tags are kept
+    per barrier generation), results exact."""
+    name = f"/mxsolve_test_{os.getpid()}_{secrets.token_hex(4)}"
+    outs = launch(3, [os.path.join("tests", "_shm_stress_worker.py"), "barrier", name], timeout=200)
+    for o in outs:
+        res = json.loads(o.strip().splitlines()[-1])
+        assert res["total"] == res["expect"], res
+
+
+def test_lu_singular_two_ranks_all_raise():
+    """preonly + LU on a singular matrix with 2 processes: rank 0's factorisation
+    error reaches every rank as PETSc.Error (no rank left waiting in bcast)."""
+    outs = launch(2, [os.path.join("tests", "_shm_stress_worker.py"), "lu_singular", "-"], timeout=120)
+    for o in outs:
+        res = json.loads(o.strip().splitlines()[-1])
+        assert res["raised"], res

@@ -1,0 +1,370 @@
+// Ceiling probe for the 256^3 7-point MatMult (not product code): how fast can
+// y = A x with x read and y written once run on this GPU, by access scheme?
+//   copy      : y = x, 16 B per lane (the stream ceiling for 268 MB)
+//   pairs<U>  : matrix-free 7-point, two rows per lane, U units per wave step,
+//               each XCD sweeping one contiguous eighth (the product's order)
+//   zmarch    : 2.5D: a workgroup owns a y-tile of lines and marches z,
+//               keeping planes in LDS (x read once from HBM per tile)
+// hipcc --offload-arch=gfx950 -O3 -o /tmp/stencil_probe tools/stencil_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+constexpr int N = 256;
+constexpr int64_t NN = (int64_t)N * N, M = NN * N;
+
+__global__ void copy_kernel(const dbl2 *__restrict__ x, dbl2 *__restrict__ y, int64_t n2) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = __builtin_nontemporal_load(x + i);
+}
+
+template <bool UP>
+__device__ __forceinline__ double wave_shift(double v, double edge) {
+  const long long b = __double_as_longlong(v), e = __double_as_longlong(edge);
+  constexpr int ctrl = UP ? 0x138 : 0x130;
+  const int lo = __builtin_amdgcn_update_dpp((int)e, (int)b, ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(b >> 32), ctrl, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double xat(const double *x, int64_t i) { return (i >= 0 && i < M) ? x[i] : 0.0; }
+__device__ __forceinline__ dbl2 xpair(const double *x, int64_t i) {
+  return (i >= 0 && i + 1 < M) ? *reinterpret_cast<const dbl2 *>(x + i) : dbl2{0.0, 0.0};
+}
+
+// one 128-row unit: lane = rows r0, r0 + 1
+struct UnitL { dbl2 zm, ym, c, yp, zp; double elo, ehi; };
+__device__ __forceinline__ void unit_load(const double *x, int64_t u, int lane, UnitL &t) {
+  const int64_t ub = u * 128, r0 = ub + 2 * lane;
+  t.zm = xpair(x, r0 - NN); t.ym = xpair(x, r0 - N); t.c = xpair(x, r0);
+  t.yp = xpair(x, r0 + N); t.zp = xpair(x, r0 + NN);
+  t.elo = xat(x, ub - 1); t.ehi = xat(x, ub + 128);
+}
+__device__ __forceinline__ void unit_finish(double *y, int64_t u, int lane, const UnitL &t) {
+  const int64_t r0 = u * 128 + 2 * lane;
+  const double lo = wave_shift<true>(t.c.y, t.elo), hi = wave_shift<false>(t.c.x, t.ehi);
+  const double s0 = 6.0 * t.c.x - t.zm.x - t.ym.x - lo - t.c.y - t.yp.x - t.zp.x;
+  const double s1 = 6.0 * t.c.y - t.zm.y - t.ym.y - t.c.x - hi - t.yp.y - t.zp.y;
+  *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) pairs_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits) {
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t chunk = (nunits + 7) >> 3;
+  const int64_t s0 = xcd * chunk + (int64_t)j * 4 + wid, step = (int64_t)per * 4;
+  const int64_t send = min(nunits, (xcd + 1) * chunk);
+  int64_t u = s0;
+  for (; u + (U - 1) * step < send; u += U * step) {
+    UnitL t[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) unit_load(x, u + k * step, lane, t[k]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) unit_finish(y, u + k * step, lane, t[k]);
+  }
+  for (; u < send; u += step) { UnitL t; unit_load(x, u, lane, t); unit_finish(y, u, lane, t); }
+}
+
+// the product's row-pair scheme with its coded values: per unit a 16-B code
+// block per lane from a small dictionary (L2), codes -> values through an LDS
+// table, absent slots skipped by select; optional p.w dot partial (DOT)
+constexpr int ABSENT = 255;
+template <int U, bool DOT, bool META>
+__global__ void __launch_bounds__(256) pcodes_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                     const uint8_t *__restrict__ dict, const int32_t *__restrict__ pblk,
+                                                     const double *__restrict__ vtab_g, double *__restrict__ part) {
+  __shared__ double vtab[256];
+  for (int i = threadIdx.x; i < 256; i += 256) vtab[i] = vtab_g[i];
+  __syncthreads();
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t chunk = (nunits + 7) >> 3;
+  const int64_t s0 = xcd * chunk + (int64_t)j * 4 + wid, step = (int64_t)per * 4;
+  const int64_t send = min(nunits, (xcd + 1) * chunk);
+  double dot = 0.0;
+  struct T { UnitL l; u32x4 cw; };
+  auto ld = [&](int64_t u, T &t) {
+    unit_load(x, u, lane, t.l);
+    const int blk = META ? pblk[u] : (int)(u & 1);
+    t.cw = *reinterpret_cast<const u32x4 *>(dict + ((int64_t)blk * 64 + lane) * 16);
+  };
+  auto fin = [&](int64_t u, const T &t) {
+    const int64_t r0 = u * 128 + 2 * lane;
+    auto code = [&](int i) -> int { return (t.cw[(i >> 2) & 3] >> (8 * (i & 3))) & 0xff; };
+    const double lo = wave_shift<true>(t.l.c.y, t.l.elo), hi = wave_shift<false>(t.l.c.x, t.l.ehi);
+    const double a0[7] = {t.l.zm.x, t.l.ym.x, lo, t.l.c.x, t.l.c.y, t.l.yp.x, t.l.zp.x};
+    const double a1[7] = {t.l.zm.y, t.l.ym.y, t.l.c.x, t.l.c.y, hi, t.l.yp.y, t.l.zp.y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int c0 = code(k), c1 = code(7 + k);
+      const double q0 = s0 + vtab[c0] * a0[k], q1 = s1 + vtab[c1] * a1[k];
+      s0 = c0 != ABSENT ? q0 : s0;
+      s1 = c1 != ABSENT ? q1 : s1;
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    if (DOT) { dot += t.l.c.x * s0; dot += t.l.c.y * s1; }
+  };
+  int64_t u = s0;
+  for (; u + (U - 1) * step < send; u += U * step) {
+    T t[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) ld(u + k * step, t[k]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) fin(u + k * step, t[k]);
+  }
+  for (; u < send; u += step) { T t; ld(u, t); fin(u, t); }
+  if (DOT) {
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+    if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+  }
+}
+
+// pcodes with buffer loads (out-of-range reads return 0: no bounds logic) and
+// the dictionary block ids of the wave's next 64 steps in one vector load,
+// read per step by readlane (no dependent scalar load per unit)
+template <int U, bool DOT>
+__global__ void __launch_bounds__(256) pbuf_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                   const uint8_t *__restrict__ dict, const int32_t *__restrict__ pblk,
+                                                   const double *__restrict__ vtab_g, double *__restrict__ part) {
+  __shared__ double vtab[256];
+  for (int i = threadIdx.x; i < 256; i += 256) vtab[i] = vtab_g[i];
+  __syncthreads();
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t chunk = (nunits + 7) >> 3;
+  const int64_t s0 = xcd * chunk + (int64_t)j * 4 + wid, step = (int64_t)per * 4;
+  const int64_t send = min(nunits, (xcd + 1) * chunk);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, (int)(M * 8), 0x00020000);
+  double dot = 0.0;
+  struct T { dbl2 zm, ym, c, yp, zp; double elo, ehi; u32x4 cw; };
+  auto ldp = [&](int64_t i) -> dbl2 {
+    return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(i * 8), 0, 0));
+  };
+  auto lds = [&](int64_t i) -> double {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (int)(i * 8), 0, 0));
+  };
+  auto ld = [&](int64_t u, int blk, T &t) {
+    const int64_t ub = u * 128, r0 = ub + 2 * lane;
+    t.zm = ldp(r0 - NN); t.ym = ldp(r0 - N); t.c = ldp(r0); t.yp = ldp(r0 + N); t.zp = ldp(r0 + NN);
+    t.elo = lds(ub - 1); t.ehi = lds(ub + 128);
+    t.cw = *reinterpret_cast<const u32x4 *>(dict + ((int64_t)blk * 64 + lane) * 16);
+  };
+  auto fin = [&](int64_t u, const T &t) {
+    const int64_t r0 = u * 128 + 2 * lane;
+    auto code = [&](int i) -> int { return (t.cw[(i >> 2) & 3] >> (8 * (i & 3))) & 0xff; };
+    const double lo = wave_shift<true>(t.c.y, t.elo), hi = wave_shift<false>(t.c.x, t.ehi);
+    const double a0[7] = {t.zm.x, t.ym.x, lo, t.c.x, t.c.y, t.yp.x, t.zp.x};
+    const double a1[7] = {t.zm.y, t.ym.y, t.c.x, t.c.y, hi, t.yp.y, t.zp.y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int c0 = code(k), c1 = code(7 + k);
+      const double q0 = s0 + vtab[c0] * a0[k], q1 = s1 + vtab[c1] * a1[k];
+      s0 = c0 != ABSENT ? q0 : s0;
+      s1 = c1 != ABSENT ? q1 : s1;
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    if (DOT) { dot += t.c.x * s0; dot += t.c.y * s1; }
+  };
+  int64_t u = s0;
+  int kstep = 64;
+  int bv = 0;
+  for (; u + (U - 1) * step < send; u += U * step) {
+    if (kstep + U > 64) {                  // refill: block ids of the next 64 steps
+      const int64_t uu = u + lane * step;
+      bv = uu < send ? pblk[uu] : 0;
+      kstep = 0;
+    }
+    T t[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) ld(u + k * step, __builtin_amdgcn_readlane(bv, kstep + k), t[k]);
+    kstep += U;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) fin(u + k * step, t[k]);
+  }
+  for (; u < send; u += step) { T t; ld(u, pblk[u], t); fin(u, t); }
+  if (DOT) {
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+    if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+  }
+}
+
+// 2.5D z-march: workgroup = (tile of TY lines in y) x (z range of ZR planes),
+// 256 threads = one line's columns, PER = TY values per thread per plane plus
+// the two y-halo values.  Planes live in a 4-slot register ring (static slot
+// indices: the z loop is unrolled by 4), loaded two planes ahead; x+-1 and
+// y+-1 neighbours come from the current plane staged in LDS.
+template <int TY, int ZR>
+__global__ void __launch_bounds__(256) zmarch_kernel(const double *__restrict__ x, double *__restrict__ y) {
+  static_assert(ZR % 4 == 0, "ring");
+  constexpr int PER = TY + 2;                    // [0] halo y0-1, [1..TY] tile lines, [TY+1] halo y0+TY
+  __shared__ double pl[2][(TY + 2) * N + 2];
+  const int ntile = N / TY;
+  const int tile = blockIdx.x % ntile, zb = blockIdx.x / ntile;
+  const int y0 = tile * TY, z0 = zb * ZR;
+  const int t = threadIdx.x;
+  double ring[4][PER];
+  auto load = [&](int z, double *dst) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int yy = y0 - 1 + k;
+      const bool ok = z >= 0 && z < N && yy >= 0 && yy < N;
+      const int64_t g = ok ? (int64_t)z * NN + (int64_t)yy * N + t : 0;
+      const double v = (k == 0 || k == PER - 1) ? x[g] : __builtin_nontemporal_load(x + g);
+      dst[k] = ok ? v : 0.0;
+    }
+  };
+  load(z0 - 1, ring[3]);
+  load(z0, ring[0]);
+  load(z0 + 1, ring[1]);
+  for (int zz = z0; zz < z0 + ZR; zz += 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int z = zz + q;
+      double *prev = ring[(q + 3) & 3], *cur = ring[q], *next = ring[(q + 1) & 3];
+      load(z + 2, ring[(q + 2) & 3]);            // overwrites plane z - 2's slot
+      double *P = pl[q & 1];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) P[1 + k * N + t] = cur[k];
+      if (t == 0) { P[0] = 0.0; P[(TY + 2) * N + 1] = 0.0; }
+      __syncthreads();
+#pragma unroll
+      for (int k = 1; k <= TY; ++k) {
+        const int li = 1 + k * N + t;
+        const double xm = t > 0 ? P[li - 1] : 0.0, xp = t < N - 1 ? P[li + 1] : 0.0;
+        const double s = 6.0 * cur[k] - prev[k] - P[li - N] - xm - xp - P[li + N] - next[k];
+        y[(int64_t)z * NN + (int64_t)(y0 + k - 1) * N + t] = s;
+      }
+    }
+  }
+}
+
+__global__ void ref_kernel(const double *__restrict__ x, double *__restrict__ y) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const int c = i % N, r = (i / N) % N, z = i / NN;
+  double s = 6.0 * x[i];
+  if (z > 0) s -= x[i - NN];
+  if (r > 0) s -= x[i - N];
+  if (c > 0) s -= x[i - 1];
+  if (c < N - 1) s -= x[i + 1];
+  if (r < N - 1) s -= x[i + N];
+  if (z < N - 1) s -= x[i + NN];
+  y[i] = s;
+}
+
+int main(int argc, char **argv) {
+  double *x, *y, *yr, *flush;
+  CK(hipMalloc(&x, M * 8)); CK(hipMalloc(&y, M * 8)); CK(hipMalloc(&yr, M * 8)); CK(hipMalloc(&flush, 512ull << 20));
+  std::vector<double> h(M);
+  for (int64_t i = 0; i < M; ++i) h[i] = (double)((i * 2654435761ull) % 1000) / 1000.0;
+  CK(hipMemcpy(x, h.data(), M * 8, hipMemcpyHostToDevice));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  const double bytes = 2.0 * M * 8;
+  auto timeit = [&](const char *name, auto launch, bool check) {
+    for (int w = 0; w < 3; ++w) launch();
+    CK(hipDeviceSynchronize());
+    const int it = 50;
+    CK(hipEventRecord(a));
+    for (int k = 0; k < it; ++k) launch();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    const double us = ms * 1e3 / it;
+    // cold: flush caches first
+    float cold = 0;
+    for (int k = 0; k < 3; ++k) {
+      CK(hipMemsetAsync(flush, k, 512ull << 20));
+      CK(hipEventRecord(a)); launch(); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+      float t; CK(hipEventElapsedTime(&t, a, b)); cold += t * 1e3f / 3;
+    }
+    double err = 0;
+    if (check) {
+      std::vector<double> g(M), r(M);
+      CK(hipMemcpy(g.data(), y, M * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(r.data(), yr, M * 8, hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < M; ++i) err = fmax(err, fabs(g[i] - r[i]));
+    }
+    printf("%-22s %8.1f us  %7.0f GB/s  (%.3f of 8 TB/s)  cold %7.1f us  maxerr %.1e\n", name, us, bytes / us * 1e-3,
+           bytes / us * 1e-3 / 8000, cold, err);
+  };
+  ref_kernel<<<(M + 255) / 256, 256>>>(x, yr);
+  CK(hipDeviceSynchronize());
+  int cus = 256;
+  for (int g : {8192})
+    timeit((std::string("copy g") + std::to_string(g)).c_str(), [&] { copy_kernel<<<g, 256>>>((const dbl2 *)x, (dbl2 *)y, M / 2); }, false);
+  timeit("ref (naive)", [&] { ref_kernel<<<(M + 255) / 256, 256>>>(x, y); }, true);
+  for (int wpc : {2, 3, 4}) {
+    const int g = cus * wpc - 8;
+    char nm[64];
+    snprintf(nm, sizeof nm, "pairs<1> %d/CU", wpc);
+    timeit(nm, [&] { pairs_kernel<1><<<g, 256>>>(x, y, M / 128); }, wpc == 4);
+    snprintf(nm, sizeof nm, "pairs<2> %d/CU", wpc);
+    timeit(nm, [&] { pairs_kernel<2><<<g, 256>>>(x, y, M / 128); }, wpc == 4);
+    snprintf(nm, sizeof nm, "pairs<4> %d/CU", wpc);
+    timeit(nm, [&] { pairs_kernel<4><<<g, 256>>>(x, y, M / 128); }, wpc == 4);
+  }
+  // dictionary: block 0 = lane 0 row 0 lacks the -1 entry, block 1 = lane 63 row 1 lacks +1
+  std::vector<uint8_t> hd(2 * 64 * 16, 0);
+  for (int b = 0; b < 2; ++b)
+    for (int l = 0; l < 64; ++l) {
+      uint8_t *c = &hd[(b * 64 + l) * 16];
+      for (int r = 0; r < 2; ++r)
+        for (int k = 0; k < 7; ++k) c[7 * r + k] = k == 3 - r + r * 1 ? 0 : 1;   // centre -> 6.0 (code 0), else -1.0 (code 1)
+      // row 0 centre is slot 3, row 1 centre is slot 4 (a1 order)
+      for (int k = 0; k < 7; ++k) { c[k] = k == 3 ? 0 : 1; c[7 + k] = k == 3 ? 0 : 1; }
+      if (b == 0 && l == 0) c[2] = ABSENT;
+      if (b == 1 && l == 63) c[7 + 4] = ABSENT;
+      c[14] = c[15] = ABSENT;
+    }
+  uint8_t *dict; int32_t *pblk; double *vt, *part;
+  CK(hipMalloc(&dict, hd.size())); CK(hipMemcpy(dict, hd.data(), hd.size(), hipMemcpyHostToDevice));
+  std::vector<int32_t> hb(M / 128); for (size_t u = 0; u < hb.size(); ++u) hb[u] = (int)(u & 1);
+  CK(hipMalloc(&pblk, hb.size() * 4)); CK(hipMemcpy(pblk, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  std::vector<double> hv(256, 0.0); hv[0] = 6.0; hv[1] = -1.0;
+  CK(hipMalloc(&vt, 256 * 8)); CK(hipMemcpy(vt, hv.data(), 256 * 8, hipMemcpyHostToDevice));
+  CK(hipMalloc(&part, 1 << 20));
+  for (int wpc : {2, 3, 4, 5}) {
+    const int g = cus * wpc - 8;
+    char nm[64];
+    snprintf(nm, sizeof nm, "pcodes<1> %d/CU", wpc);
+    timeit(nm, [&] { pcodes_kernel<1, false, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pcodes<2> %d/CU", wpc);
+    timeit(nm, [&] { pcodes_kernel<2, false, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pcodes<2>+meta %d/CU", wpc);
+    timeit(nm, [&] { pcodes_kernel<2, false, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pbuf<1>+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<1, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pbuf<2>+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<2, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pbuf<3>+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<3, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pbuf<2> %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<2, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pcodes<2>+meta+dot %d/CU", wpc);
+    timeit(nm, [&] { pcodes_kernel<2, true, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+  }
+  timeit("zmarch TY4 ZR16", [&] { zmarch_kernel<4, 16><<<(N / 4) * (N / 16), 256>>>(x, y); }, true);
+  timeit("zmarch TY4 ZR32", [&] { zmarch_kernel<4, 32><<<(N / 4) * (N / 32), 256>>>(x, y); }, true);
+  timeit("zmarch TY2 ZR32", [&] { zmarch_kernel<2, 32><<<(N / 2) * (N / 32), 256>>>(x, y); }, true);
+  timeit("zmarch TY8 ZR16", [&] { zmarch_kernel<8, 16><<<(N / 8) * (N / 16), 256>>>(x, y); }, true);
+  timeit("zmarch TY4 ZR64", [&] { zmarch_kernel<4, 64><<<(N / 4) * (N / 64), 256>>>(x, y); }, true);
+  return 0;
+}
