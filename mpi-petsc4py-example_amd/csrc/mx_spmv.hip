@@ -561,14 +561,23 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     // (dictionary ids and/or ghost flags), 4 = every full unit is a pair unit
     const bool use_pblk = (pdict & 3) != 0;
     // one unit's loads: its code block, every x pair and the edge values
-    struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e_lo[NR], e_hi[NR]; uint32_t fl; };
+    struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e[NR]; uint32_t fl; };
     auto unit_load = [&](int u, int32_t blkw, Unit &t) __attribute__((always_inline)) {
       const int ubase = u * 128, r0 = ubase + 2 * lane;
       const uint32_t bw = (uint32_t)blkw;
       t.fl = bw & ~PBLK_ID;
-      // the unit's code block: its own (streamed non-temporally), or a
-      // dictionary block shared with every unit of the same boundary/value
-      // class (cached: the dictionary stays in L2)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        t.L[r] = XB.pair(r0 + anchor[r]);        // the operand (scaled / formed as the mode has it)
+        // the run's two edge values in one load: lane 0 reads x[r0 + c - 1]
+        // (its row 0's left neighbour), every other lane x[ubase + 128 + c]
+        // (lane 63's row 1's right neighbour; one line for the wave)
+        if (SH::tri(r)) t.e[r] = XB(lane == 0 ? ubase + anchor[r] - 1 : ubase + 128 + anchor[r]);
+      }
+      // the unit's code block (after the operand loads: its address waits on
+      // the block id): its own (streamed non-temporally), or a dictionary
+      // block shared with every unit of the same boundary/value class (cached:
+      // the dictionary stays in L2)
       const int64_t blk = use_pblk ? (int64_t)(bw & PBLK_ID) : (int64_t)u;
       const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + (blk * 64 + lane) * PB);
       if (pdict & 1) {                            // kernel-uniform
@@ -577,14 +586,6 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       } else {
 #pragma unroll
         for (int q = 0; q < PB / 16; ++q) t.cw[q] = ld<NT>(cp + q);
-      }
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        t.L[r] = XB.pair(r0 + anchor[r]);        // the operand (scaled / formed as the mode has it)
-        if (SH::tri(r)) {
-          t.e_lo[r] = XB(ubase + anchor[r] - 1);   // row 0 of lane 0: x[r0 + c - 1]
-          t.e_hi[r] = XB(ubase + 128 + anchor[r]); // row 1 of lane 63: x[r0 + 1 + c + 1]
-        }
       }
     };
     // the lookups, the two row sums and everything stored after them
@@ -599,8 +600,8 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       for (int j = 0; j < K; ++j) {
         const int r = SH::run(j), p = SH::pos(j);
         if (SH::tri(r) && p < 0) {
-          lo_m1 = wave_shift<true>(t.L[r].y, t.e_lo[r]);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
-          hi_p1 = wave_shift<false>(t.L[r].x, t.e_hi[r]);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
+          lo_m1 = wave_shift<true>(t.L[r].y, t.e[r]);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
+          hi_p1 = wave_shift<false>(t.L[r].x, t.e[r]);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
         }
         double a0, a1;                           // operand for row 0 / row 1
         if (!SH::tri(r)) { a0 = t.L[r].x; a1 = t.L[r].y; }
@@ -673,23 +674,25 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         }
         return q;
       };
-      Meta cur = meta(u);
+      // block ids two steps ahead: a wave sweeps only ~16 steps, so the
+      // first steps' scalar round trips must not sit in front of their loads
+      Meta cur = meta(u), nx1 = meta(u + 2 * sstep);
       for (; u + sstep < send; u += 2 * sstep) {
         const int ua = item(u), ub = item(u + sstep);
+        const Meta nx2 = meta(u + 4 * sstep);
         if ((cur.da & DPAT_PAIR) && (cur.db & DPAT_PAIR)) {   // wave-uniform
           Unit ta, tb;
           unit_load(ua, cur.ba, ta);
           unit_load(ub, cur.bb, tb);
-          const Meta nxt = meta(u + 2 * sstep);
           __builtin_amdgcn_sched_barrier(0);
           unit_finish(ua, ta);
           unit_finish(ub, tb);
-          cur = nxt;
         } else {
           one_unit(ua);
           one_unit(ub);
-          cur = meta(u + 2 * sstep);
         }
+        cur = nx1;
+        nx1 = nx2;
       }
     }
     for (; u < send; u += sstep) one_unit(item(u));

@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(256) pcodes_kernel(const double *__restrict__ 
 // pcodes with buffer loads (out-of-range reads return 0: no bounds logic) and
 // the dictionary block ids of the wave's next 64 steps in one vector load,
 // read per step by readlane (no dependent scalar load per unit)
-template <int U, bool DOT>
+template <int U, bool DOT, int META = 1, bool BUF = true>
 __global__ void __launch_bounds__(256) pbuf_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
                                                    const uint8_t *__restrict__ dict, const int32_t *__restrict__ pblk,
                                                    const double *__restrict__ vtab_g, double *__restrict__ part) {
@@ -153,9 +153,11 @@ __global__ void __launch_bounds__(256) pbuf_kernel(const double *__restrict__ x,
   double dot = 0.0;
   struct T { dbl2 zm, ym, c, yp, zp; double elo, ehi; u32x4 cw; };
   auto ldp = [&](int64_t i) -> dbl2 {
+    if (!BUF) return xpair(x, i);
     return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(i * 8), 0, 0));
   };
   auto lds = [&](int64_t i) -> double {
+    if (!BUF) return xat(x, i);
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (int)(i * 8), 0, 0));
   };
   auto ld = [&](int64_t u, int blk, T &t) {
@@ -185,20 +187,153 @@ __global__ void __launch_bounds__(256) pbuf_kernel(const double *__restrict__ x,
   int kstep = 64;
   int bv = 0;
   for (; u + (U - 1) * step < send; u += U * step) {
-    if (kstep + U > 64) {                  // refill: block ids of the next 64 steps
+    if (META && kstep + U > 64) {          // refill: block ids of the next 64 steps
       const int64_t uu = u + lane * step;
       bv = uu < send ? pblk[uu] : 0;
       kstep = 0;
     }
     T t[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) ld(u + k * step, __builtin_amdgcn_readlane(bv, kstep + k), t[k]);
+    for (int k = 0; k < U; ++k) ld(u + k * step, META ? __builtin_amdgcn_readlane(bv, kstep + k) : (int)((u + k * step) & 1), t[k]);
     kstep += U;
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < U; ++k) fin(u + k * step, t[k]);
   }
   for (; u < send; u += step) { T t; ld(u, pblk[u], t); fin(u, t); }
+  if (DOT) {
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+    if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+  }
+}
+
+// wave-blocked sweep: each wave owns a CONTIGUOUS run of C units (XCD-major
+// numbering, so an XCD's waves cover one contiguous eighth and the +-n^2
+// neighbours 512 units away are 16 waves over, on the same XCD at the same
+// step); the run's dictionary block ids come in with ONE vector load
+template <int U, bool DOT, int META>
+__global__ void __launch_bounds__(256) pblk_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                   const uint8_t *__restrict__ dict, const int32_t *__restrict__ pblk,
+                                                   const double *__restrict__ vtab_g, double *__restrict__ part) {
+  __shared__ double vtab[256];
+  for (int i = threadIdx.x; i < 256; i += 256) vtab[i] = vtab_g[i];
+  __syncthreads();
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t C = (nunits + nw - 1) / nw;
+  const int64_t w = (int64_t)xcd * per * 4 + j * 4 + wid;    // XCD-major wave number
+  const int64_t u0 = w * C, u1 = min(nunits, u0 + C);
+  double dot = 0.0;
+  int bv = 0;
+  if (META == 1) bv = (u0 + lane < u1) ? pblk[u0 + lane] : 0;
+  struct T { UnitL l; u32x4 cw; };
+  auto ld = [&](int64_t u, int blk, T &t) {
+    unit_load(x, u, lane, t.l);
+    t.cw = *reinterpret_cast<const u32x4 *>(dict + ((int64_t)blk * 64 + lane) * 16);
+  };
+  auto fin = [&](int64_t u, const T &t) {
+    const int64_t r0 = u * 128 + 2 * lane;
+    auto code = [&](int i) -> int { return (t.cw[(i >> 2) & 3] >> (8 * (i & 3))) & 0xff; };
+    const double lo = wave_shift<true>(t.l.c.y, t.l.elo), hi = wave_shift<false>(t.l.c.x, t.l.ehi);
+    const double a0[7] = {t.l.zm.x, t.l.ym.x, lo, t.l.c.x, t.l.c.y, t.l.yp.x, t.l.zp.x};
+    const double a1[7] = {t.l.zm.y, t.l.ym.y, t.l.c.x, t.l.c.y, hi, t.l.yp.y, t.l.zp.y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int c0 = code(k), c1 = code(7 + k);
+      const double q0 = s0 + vtab[c0] * a0[k], q1 = s1 + vtab[c1] * a1[k];
+      s0 = c0 != ABSENT ? q0 : s0;
+      s1 = c1 != ABSENT ? q1 : s1;
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    if (DOT) { dot += t.l.c.x * s0; dot += t.l.c.y * s1; }
+  };
+  auto blk_of = [&](int64_t u) -> int {
+    if (META == 1) return __builtin_amdgcn_readlane(bv, (int)(u - u0));
+    if (META == 2) return pblk[u];
+    return (int)(u & 1);
+  };
+  int64_t u = u0;
+  for (; u + U - 1 < u1; u += U) {
+    T t[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) ld(u + k, blk_of(u + k), t[k]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) fin(u + k, t[k]);
+  }
+  for (; u < u1; ++u) { T t; ld(u, blk_of(u), t); fin(u, t); }
+  if (DOT) {
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+    if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+  }
+}
+
+// pcodes with the prologue overlapped: the value table's global load and the
+// first step's x loads are issued before the table is written to LDS and the
+// workgroup barrier; block ids by scalar loads one step ahead (META 1) or
+// from the unit index (META 0)
+template <bool DOT, int META>
+__global__ void __launch_bounds__(256) pov_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                  const uint8_t *__restrict__ dict, const int32_t *__restrict__ pblk,
+                                                  const double *__restrict__ vtab_g, double *__restrict__ part) {
+  __shared__ double vtab[256];
+  const double vt_reg = vtab_g[threadIdx.x];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t chunk = (nunits + 7) >> 3;
+  const int64_t s0 = xcd * chunk + (int64_t)j * 4 + wid, step = (int64_t)per * 4;
+  const int64_t send = min(nunits, (xcd + 1) * chunk);
+  double dot = 0.0;
+  struct T { UnitL l; u32x4 cw; };
+  auto ldx = [&](int64_t u, T &t) { unit_load(x, u, lane, t.l); };
+  auto ldc = [&](int blk, T &t) { t.cw = *reinterpret_cast<const u32x4 *>(dict + ((int64_t)blk * 64 + lane) * 16); };
+  auto fin = [&](int64_t u, const T &t) {
+    const int64_t r0 = u * 128 + 2 * lane;
+    auto code = [&](int i) -> int { return (t.cw[(i >> 2) & 3] >> (8 * (i & 3))) & 0xff; };
+    const double lo = wave_shift<true>(t.l.c.y, t.l.elo), hi = wave_shift<false>(t.l.c.x, t.l.ehi);
+    const double a0[7] = {t.l.zm.x, t.l.ym.x, lo, t.l.c.x, t.l.c.y, t.l.yp.x, t.l.zp.x};
+    const double a1[7] = {t.l.zm.y, t.l.ym.y, t.l.c.x, t.l.c.y, hi, t.l.yp.y, t.l.zp.y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int c0 = code(k), c1 = code(7 + k);
+      const double q0 = s0 + vtab[c0] * a0[k], q1 = s1 + vtab[c1] * a1[k];
+      s0 = c0 != ABSENT ? q0 : s0;
+      s1 = c1 != ABSENT ? q1 : s1;
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    if (DOT) { dot += t.l.c.x * s0; dot += t.l.c.y * s1; }
+  };
+  auto mb = [&](int64_t u) -> int { return u < send ? (META ? pblk[u] : (int)(u & 1)) : 0; };
+  int64_t u = s0;
+  int ba = mb(u), bb = mb(u + step);
+  bool first = true;
+  while (true) {
+    const bool two = u + step < send, one = u < send;
+    T ta, tb;
+    if (one) ldx(u, ta);
+    if (two) ldx(u + step, tb);
+    if (one) ldc(ba, ta);
+    if (two) ldc(bb, tb);
+    const int na = mb(u + 2 * step), nb = mb(u + 3 * step);   // next step's block ids, behind this step's loads
+    __builtin_amdgcn_sched_barrier(0);
+    if (first) {                         // the table lands while the first loads are in flight
+      vtab[threadIdx.x] = vt_reg;
+      __syncthreads();
+      first = false;
+    }
+    if (!one) break;
+    fin(u, ta);
+    if (two) fin(u + step, tb);
+    u += 2 * step;
+    ba = na; bb = nb;
+  }
   if (DOT) {
     for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
     if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
@@ -278,7 +413,9 @@ int main(int argc, char **argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   const double bytes = 2.0 * M * 8;
+  const std::string only = argc > 1 ? std::string(";") + argv[1] + ";" : std::string();
   auto timeit = [&](const char *name, auto launch, bool check) {
+    if (!only.empty() && only.find(std::string(";") + name + ";") == std::string::npos) return;
     for (int w = 0; w < 3; ++w) launch();
     CK(hipDeviceSynchronize());
     const int it = 50;
@@ -356,6 +493,27 @@ int main(int argc, char **argv) {
     timeit(nm, [&] { pbuf_kernel<2, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pbuf<3>+dot %d/CU", wpc);
     timeit(nm, [&] { pbuf_kernel<3, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pcodes<2>+dot %d/CU", wpc);
+    timeit(nm, [&] { pcodes_kernel<2, true, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "glob+batchmeta+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<2, true, 1, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "buf+nometa+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<2, true, 0, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "glob+nometa+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<2, true, 0, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    for (int U2 : {1, 2, 4}) {
+      for (int me : {0, 1, 2}) {
+        snprintf(nm, sizeof nm, "blk<%d>+meta%d+dot %d/CU", U2, me, wpc);
+        auto go = [&](auto kern) { timeit(nm, [&] { kern<<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false); };
+        if (U2 == 1) { if (me == 0) go(pblk_kernel<1, true, 0>); else if (me == 1) go(pblk_kernel<1, true, 1>); else go(pblk_kernel<1, true, 2>); }
+        if (U2 == 2) { if (me == 0) go(pblk_kernel<2, true, 0>); else if (me == 1) go(pblk_kernel<2, true, 1>); else go(pblk_kernel<2, true, 2>); }
+        if (U2 == 4) { if (me == 0) go(pblk_kernel<4, true, 0>); else if (me == 1) go(pblk_kernel<4, true, 1>); else go(pblk_kernel<4, true, 2>); }
+      }
+    }
+    snprintf(nm, sizeof nm, "pov+meta0+dot %d/CU", wpc);
+    timeit(nm, [&] { pov_kernel<true, 0><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pov+meta1+dot %d/CU", wpc);
+    timeit(nm, [&] { pov_kernel<true, 1><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pbuf<2> %d/CU", wpc);
     timeit(nm, [&] { pbuf_kernel<2, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pcodes<2>+meta+dot %d/CU", wpc);
