@@ -98,6 +98,9 @@ typedef struct {
 
 /* ---- library ---------------------------------------------------------------- */
 int mx_version(void);
+/* PetscFinalize: waits for all device work the library queued.  Handles must
+ * be destroyed before (or not used after) this call.                        */
+int mx_finalize(void);
 int mx_last_error(char *buf, size_t len);
 
 /* ---- communicators (the comm= argument of createAIJ / KSP().create:
@@ -188,6 +191,15 @@ int mx_vec_pointwise_mult(mx_comm c, int64_t n, const double *x_dev, const doubl
                           double *w_dev);
 int mx_vec_scale(mx_comm c, int64_t n, double alpha, double *x_dev);
 int mx_vec_set(mx_comm c, int64_t n, double alpha, double *x_dev);
+/* VecMDot (GMRES orthogonalisation): out_host[k] = x . y_k for
+ * the nv device vectors listed in the host array y; one all-reduce of nv
+ * values.  [collective]                                                      */
+int mx_vec_mdot(mx_comm c, int64_t n, const double *x_dev, int nv, const double *const *y_dev_list,
+                double *out_host);
+/* VecMAXPY: y += sum_k alpha[k] x_k (alpha on the host), PETSc's VecMAXPY_Seq
+ * grouping: the first nv % 4 vectors together, then groups of four.          */
+int mx_vec_maxpy(mx_comm c, int64_t n, double *y_dev, int nv, const double *alpha_host,
+                 const double *const *x_dev_list);
 /* b_i = (splitmix64(i + 42 phi) >> 11) 2^-53 for global i in [i0, i0+n) */
 int mx_vec_rhs_hash(mx_comm c, int64_t i0, int64_t n, double *b_dev);
 
@@ -196,6 +208,11 @@ int mx_vec_rhs_hash(mx_comm c, int64_t i0, int64_t n, double *b_dev);
 int mx_ksp_solve(mx_mat A, const mx_ksp_params *p, const double *b_dev, double *x_dev,
                  mx_ksp_result *res, double *history_host /* NULL or max_it+2 */);
 void mx_ksp_default_params(mx_ksp_params *p);
+/* KSPDestroy / KSPReset (test.py's ksp object going away): releases the solver
+ * state kept on operator A between solves -- KSPSetUp work space, the device
+ * convergence state, the captured CG iteration graph and the PCSetUp_Jacobi
+ * result.  A stays usable; the next solve sets them up again.              */
+int mx_ksp_destroy(mx_mat A);
 
 /* ---- direct solve: replaces KSPPREONLY + PCLU (+ MUMPS) of test.py:38-43,138
  *      (SURVEY.md §8f F1).  The caller gathers the whole square system (global

@@ -405,6 +405,38 @@ int mx_vec_scale(mx_comm c, int64_t n, double a, double *x) {
 int mx_vec_set(mx_comm c, int64_t n, double a, double *x) {
   return guard([&] { Comm *k = C(c); vec_set(k->stream, n, a, x); HIPCHECK(hipStreamSynchronize(k->stream)); });
 }
+int mx_vec_mdot(mx_comm c, int64_t n, const double *x, int nv, const double *const *y, double *out) {
+  return guard([&] {
+    if (nv < 0 || (nv > 0 && (!y || !out))) fail(MX_ERR_ARG, "VecMDot: bad vector list");
+    host_mdot(C(c), n, x, nv, y, out);
+  });
+}
+int mx_vec_maxpy(mx_comm c, int64_t n, double *y, int nv, const double *alpha, const double *const *x) {
+  return guard([&] {
+    if (nv < 0 || (nv > 0 && (!x || !alpha))) fail(MX_ERR_ARG, "VecMAXPY: bad vector list");
+    Comm *k = C(c);
+    vec_maxpy(k->stream, n, y, nv, alpha, x);
+    HIPCHECK(hipStreamSynchronize(k->stream));
+  });
+}
+int mx_ksp_destroy(mx_mat a) {
+  return guard([&] {
+    Mat *A = M(a);
+    (void)hipSetDevice(A->comm->device);
+    HIPCHECK(hipStreamSynchronize(A->comm->stream));
+    A->release_ksp();
+  });
+}
+int mx_finalize(void) {
+  return guard([&] {
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess) nd = 0;
+    for (int d = 0; d < nd; ++d) {
+      if (hipSetDevice(d) == hipSuccess) HIPCHECK(hipDeviceSynchronize());
+    }
+    (void)hipGetLastError();
+  });
+}
 int mx_vec_rhs_hash(mx_comm c, int64_t i0, int64_t n, double *b) {
   return guard([&] { Comm *k = C(c); vec_rhs_hash(k->stream, i0, n, b); HIPCHECK(hipStreamSynchronize(k->stream)); });
 }

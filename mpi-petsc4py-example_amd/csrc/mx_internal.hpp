@@ -208,9 +208,14 @@ struct Mat {
   hipGraphExec_t cg_graph = nullptr;
   std::vector<uintptr_t> cg_key;
   bool cg_graph_failed = false;     // capture failed once: this operator stays eager
-  ~Mat() {
-    if (cg_graph) (void)hipGraphExecDestroy(cg_graph);
-  }
+  // per-solve host resources, created at the first solve and kept: the
+  // pinned convergence-flag slots the host polls and the solve's timing
+  // events (a pinned allocation per solve costs more than a short solve)
+  int *poll_pinned = nullptr;
+  hipEvent_t poll_ev[2] = {nullptr, nullptr};
+  hipEvent_t solve_ev[2] = {nullptr, nullptr};
+  void release_ksp();               // KSPReset: work space, state, graph, Jacobi setup
+  ~Mat() { release_ksp(); }
 };
 
 // assembly entry (mx_assembly.hip)
@@ -286,6 +291,10 @@ constexpr int RED_BLOCKS = 1024;   // fixed grid of the reduction kernels
 void finish_reduce(const double *partials, int nblocks, int nvals, double *out, hipStream_t s,
                    int *done_flag = nullptr);
 double host_dot(Comm *c, int64_t n, const double *x, const double *y);
+// VecMDot: out_host[k] = x . y[k] (collective); VecMAXPY: y += sum_k alpha[k] x[k]
+// with PETSc's grouping (VecMAXPY_Seq)
+void host_mdot(Comm *c, int64_t n, const double *x, int nv, const double *const *y, double *out_host);
+void vec_maxpy(hipStream_t s, int64_t n, double *y, int nv, const double *alpha, const double *const *x);
 void vec_axpy(hipStream_t s, int64_t n, double a, const double *x, double *y);
 void vec_aypx(hipStream_t s, int64_t n, double a, const double *x, double *y);
 void vec_pmult(hipStream_t s, int64_t n, const double *x, const double *y, double *w);

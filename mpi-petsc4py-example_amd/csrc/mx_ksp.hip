@@ -821,23 +821,27 @@ __global__ void gm_cycle_end_kernel(KspState *s) {
 // ------------------------------------------------------------------ host drivers
 namespace {
 
+// the operator's pinned flag slots and events (Mat::poll_*), made once
+static void solve_resources(Mat *A) {
+  if (A->poll_pinned) return;
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&A->poll_pinned), 2 * sizeof(int), hipHostMallocDefault));
+  A->poll_pinned[0] = A->poll_pinned[1] = 0;
+  for (auto &e : A->poll_ev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto &e : A->solve_ev) HIPCHECK(hipEventCreate(&e));
+}
+
 struct Poller {
   hipStream_t st;
-  int *pinned = nullptr;
-  hipEvent_t ev[2];
+  int *pinned;
+  hipEvent_t *ev;
   int pending = 0;  // batches enqueued
-  explicit Poller(hipStream_t s) : st(s) {
-    HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&pinned), 2 * sizeof(int), hipHostMallocDefault));
+  Poller(Mat *A, hipStream_t s) : st(s) {
+    solve_resources(A);
+    pinned = A->poll_pinned;
+    ev = A->poll_ev;
     pinned[0] = pinned[1] = 0;
-    HIPCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
-    HIPCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
   }
-  ~Poller() {
-    (void)hipStreamSynchronize(st);
-    (void)hipHostFree(pinned);
-    (void)hipEventDestroy(ev[0]);
-    (void)hipEventDestroy(ev[1]);
-  }
+  ~Poller() { (void)hipStreamSynchronize(st); }
   // enqueue the flag copy for this batch; return true if the PREVIOUS batch saw done
   bool batch(const int *dev_done) {
     const int slot = pending & 1;
@@ -880,8 +884,7 @@ struct SpmvTimer {
 
 struct Events {
   hipEvent_t a, b;
-  Events() { HIPCHECK(hipEventCreate(&a)); HIPCHECK(hipEventCreate(&b)); }
-  ~Events() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
+  explicit Events(Mat *A) { solve_resources(A); a = A->solve_ev[0]; b = A->solve_ev[1]; }
 };
 
 void init_state(KspState &h, const mx_ksp_params &p, int normtype) {
@@ -897,6 +900,21 @@ void read_state(hipStream_t st, const KspState *d, KspState &h) {
 }
 
 }  // namespace
+
+void Mat::release_ksp() {
+  if (cg_graph) (void)hipGraphExecDestroy(cg_graph);
+  cg_graph = nullptr;
+  cg_key.clear();
+  cg_graph_failed = false;
+  ksp_ws = DBuf<double>();
+  ksp_state = DBuf<char>();
+  jac_dinv = DBuf<double>();
+  jac_mode = -1;
+  if (poll_pinned) (void)hipHostFree(poll_pinned);
+  poll_pinned = nullptr;
+  for (auto &e : poll_ev) { if (e) (void)hipEventDestroy(e); e = nullptr; }
+  for (auto &e : solve_ev) { if (e) (void)hipEventDestroy(e); e = nullptr; }
+}
 
 // KSPSetUp work space: one device allocation per operator, grown on demand
 // and reused by later solves (no hipMalloc/hipFree inside a solve).
@@ -1019,7 +1037,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   KspState hs;
   init_state(hs, p, normtype);
   HIPCHECK(hipMemcpyAsync(sd.p, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
-  Events ev;
+  Events ev(A);
   SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
   HIPCHECK(hipEventRecord(ev.a, st));
 
@@ -1042,7 +1060,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   else cg_init_kernel<3><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
   HIPCHECK(hipGetLastError());
 
-  Poller poller(st);
+  Poller poller(A, st);
   int i = 0;
   const unsigned egrid = grid_for(n, 256, 8192);
   int *done = &s->top.done;
@@ -1257,7 +1275,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   double *sred = reinterpret_cast<double *>(s);
   const bool fused = c->size == 1;
   double *hist_d = hist_host ? hist.p : nullptr;
-  Events ev;
+  Events ev(A);
   SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
   HIPCHECK(hipEventRecord(ev.a, st));
   const unsigned egrid = grid_for(n, 256, 8192);

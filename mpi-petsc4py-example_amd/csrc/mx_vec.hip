@@ -11,6 +11,8 @@
 // and finish_reduce sums the partials in a fixed order.  Results are therefore
 // bitwise reproducible run to run (the order differs from PETSc's BLAS ddot,
 // which is itself unspecified).
+#include <algorithm>
+
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 
@@ -61,6 +63,91 @@ double host_dot(Comm *c, int64_t n, const double *x, const double *y) {
   HIPCHECK(hipMemcpyAsync(&h, out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   return h;
+}
+
+// ------------------------------------------------------------- VecMDot / VecMAXPY on arbitrary vectors
+constexpr int VGROUP = 8;   // vectors per pass
+struct VPtrs { const double *p[VGROUP]; double a[VGROUP]; };
+
+// partials[k][b] for the k < nv vectors of this pass (rows in the fixed
+// grid-stride order, the deterministic two-level fold of dot_partials_kernel)
+__global__ void __launch_bounds__(256) mdot_ptrs_kernel(int64_t n, const double *__restrict__ x, VPtrs y, int nv,
+                                                        double *__restrict__ partials) {
+  double v[VGROUP];
+#pragma unroll
+  for (int k = 0; k < VGROUP; ++k) v[k] = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const double xi = x[i];
+#pragma unroll
+    for (int k = 0; k < VGROUP; ++k)
+      if (k < nv) v[k] += xi * y.p[k][i];
+  }
+  block_sum_to_partials<VGROUP>(v, partials, gridDim.x);
+}
+
+void host_mdot(Comm *c, int64_t n, const double *x, int nv, const double *const *y, double *out_host) {
+  if (nv <= 0) return;
+  const size_t need = (size_t)VGROUP * RED_BLOCKS + (size_t)nv + 64;
+  if (c->red_scratch.n < need) c->red_scratch.alloc(need);
+  double *part = c->red_scratch.p, *out = c->red_scratch.p + (size_t)VGROUP * RED_BLOCKS;
+  for (int j0 = 0; j0 < nv; j0 += VGROUP) {
+    VPtrs pk{};
+    const int k = std::min(VGROUP, nv - j0);
+    for (int q = 0; q < VGROUP; ++q) pk.p[q] = y[j0 + std::min(q, k - 1)];
+    mdot_ptrs_kernel<<<RED_BLOCKS, 256, 0, c->stream>>>(n, x, pk, k, part);
+    HIPCHECK(hipGetLastError());
+    finish_reduce(part, RED_BLOCKS, k, out + j0, c->stream);
+  }
+  c->allreduce_sum(out, nv);
+  HIPCHECK(hipMemcpyAsync(out_host, out, sizeof(double) * (size_t)nv, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+}
+
+// VecMAXPY_Seq: the first nv % 4 vectors in one PetscKernelAXPY{,2,3} step,
+// then groups of four, u = u + (((a0 x0 + a1 x1) + a2 x2) + a3 x3); a pass
+// holds whole groups, so storing u between passes changes no bit
+template <int REM>
+__global__ void __launch_bounds__(256) maxpy_ptrs_kernel(int64_t n, double *__restrict__ y, VPtrs x, int nv) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double u = y[i];
+    if constexpr (REM == 1) u = x.a[0] * x.p[0][i] + u;
+    else if constexpr (REM == 2) u = u + (x.a[0] * x.p[0][i] + x.a[1] * x.p[1][i]);
+    else if constexpr (REM == 3) u = u + ((x.a[0] * x.p[0][i] + x.a[1] * x.p[1][i]) + x.a[2] * x.p[2][i]);
+#pragma unroll
+    for (int g = REM; g + 3 < VGROUP; g += 4)
+      if (g < nv)
+        u = u + (((x.a[g] * x.p[g][i] + x.a[g + 1] * x.p[g + 1][i]) + x.a[g + 2] * x.p[g + 2][i]) + x.a[g + 3] * x.p[g + 3][i]);
+    y[i] = u;
+  }
+}
+
+void vec_maxpy(hipStream_t s, int64_t n, double *y, int nv, const double *alpha, const double *const *x) {
+  if (nv <= 0 || n <= 0) return;
+  int j0 = 0;
+  bool first = true;
+  while (j0 < nv) {
+    // first pass: the remainder plus whole groups; later passes whole groups
+    const int rem = first ? nv % 4 : 0;
+    const int cnt = first ? std::min(nv, rem + (rem ? 4 : VGROUP)) : std::min(VGROUP, nv - j0);
+    VPtrs pk{};
+    for (int q = 0; q < VGROUP; ++q) {
+      const int src = j0 + std::min(q, cnt - 1);
+      pk.p[q] = x[src];
+      pk.a[q] = q < cnt ? alpha[src] : 0.0;
+    }
+    const unsigned g = grid_for(n, 256, 8192);
+    switch (rem) {
+      case 1: maxpy_ptrs_kernel<1><<<g, 256, 0, s>>>(n, y, pk, cnt); break;
+      case 2: maxpy_ptrs_kernel<2><<<g, 256, 0, s>>>(n, y, pk, cnt); break;
+      case 3: maxpy_ptrs_kernel<3><<<g, 256, 0, s>>>(n, y, pk, cnt); break;
+      default: maxpy_ptrs_kernel<0><<<g, 256, 0, s>>>(n, y, pk, cnt); break;
+    }
+    HIPCHECK(hipGetLastError());
+    j0 += cnt;
+    first = false;
+  }
 }
 
 // ------------------------------------------------------------- element-wise

@@ -1153,7 +1153,17 @@ class KSP:
               f"  tolerances: relative={self._rtol:g}, absolute={self._atol:g}, divergence={self._dtol:g}\n"
               f"PC Object:\n  type: {self._params()}")
 
+    def reset(self):
+        """KSPReset: the solver state kept on the operator (work space, device
+        convergence state, captured CG graph, PCSetUp_Jacobi) is released."""
+        h = self._A.getDeviceHandle() if self._A is not None else None
+        if h is not None and h.h:
+            _guard(h.ksp_reset)
+        return self
+
     def destroy(self):
+        self.reset()
+        self._A = None
         return self
 
 

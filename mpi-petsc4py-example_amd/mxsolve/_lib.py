@@ -92,6 +92,10 @@ SIGNATURES = {
     "mx_vec_scale": (C.c_int, [P, I64, C.c_double, P]),
     "mx_vec_set": (C.c_int, [P, I64, C.c_double, P]),
     "mx_vec_rhs_hash": (C.c_int, [P, I64, I64, P]),
+    "mx_vec_mdot": (C.c_int, [P, I64, P, C.c_int, C.POINTER(P), DP]),
+    "mx_vec_maxpy": (C.c_int, [P, I64, P, C.c_int, DP, C.POINTER(P)]),
+    "mx_ksp_destroy": (C.c_int, [P]),
+    "mx_finalize": (C.c_int, []),
     "mx_ksp_solve": (C.c_int, [P, C.POINTER(KSPParams), P, P, C.POINTER(KSPResult), P]),
     "mx_ksp_default_params": (None, [C.POINTER(KSPParams)]),
     "mx_lu_solve_csr": (C.c_int, [P, I64, P, P, P, P, P]),

@@ -323,6 +323,11 @@ class DMat:
             out["history"] = h[: r.its + 1]
         return out
 
+    def ksp_reset(self):
+        """KSPDestroy/KSPReset: drop the solver state kept on this operator."""
+        if self.h:
+            call("mx_ksp_destroy", self.h)
+
     def destroy(self):
         if self.h:
             call("mx_mat_destroy", self.h)
@@ -366,6 +371,21 @@ def vscale(comm, a, x):
 
 def vset(comm, a, x):
     call("mx_vec_set", comm.h, x.numel(), float(a), _ptr(x))
+
+
+def vmdot(comm: DeviceComm, x, ys) -> np.ndarray:
+    """VecMDot: [x . y for y in ys] (collective)."""
+    arr = (C.c_void_p * max(len(ys), 1))(*[_ptr(y).value for y in ys])
+    out = np.zeros(len(ys))
+    call("mx_vec_mdot", comm.h, x.numel(), _ptr(x), len(ys), arr, out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
+
+
+def vmaxpy(comm: DeviceComm, y, alphas, xs):
+    """VecMAXPY: y += sum_k alphas[k] xs[k] (PETSc's grouping)."""
+    arr = (C.c_void_p * max(len(xs), 1))(*[_ptr(v).value for v in xs])
+    a = np.ascontiguousarray(alphas, dtype=np.float64)
+    call("mx_vec_maxpy", comm.h, y.numel(), _ptr(y), len(xs), a.ctypes.data_as(C.POINTER(C.c_double)), arr)
 
 
 def rhs_hash(comm, i0: int, out: torch.Tensor):

@@ -69,6 +69,9 @@ def lib():
         L.or_stencil.argtypes = [C.c_int, C.c_int64, C.c_int64, C.c_int64, P, P, P]
         L.or_stencil.restype = C.c_int64
         L.or_rhs_hash.argtypes = [C.c_int64, C.c_int64, f64p]
+        dp = C.POINTER(C.c_double)
+        L.or_vec_maxpy.argtypes = [C.c_int64, C.c_int, dp, C.POINTER(dp), dp]
+        L.or_vec_mdot.argtypes = [C.c_int64, dp, C.c_int, C.POINTER(dp), dp]
         _lib = L
     return _lib
 
@@ -216,3 +219,25 @@ def rhs_hash(i0: int, n: int) -> np.ndarray:
     b = np.zeros(n)
     lib().or_rhs_hash(i0, n, b)
     return b
+
+
+def vec_maxpy(y, alphas, xs):
+    """VecMAXPY_Seq restated: returns y + sum alphas[k] xs[k] with PETSc's grouping."""
+    out = np.ascontiguousarray(y, dtype=np.float64).copy()
+    xs = [np.ascontiguousarray(v, dtype=np.float64) for v in xs]
+    a = np.ascontiguousarray(alphas, dtype=np.float64)
+    f64p = C.POINTER(C.c_double)
+    arr = (f64p * max(len(xs), 1))(*[v.ctypes.data_as(f64p) for v in xs])
+    lib().or_vec_maxpy(out.size, len(xs), a.ctypes.data_as(f64p), arr, out.ctypes.data_as(f64p))
+    return out
+
+
+def vec_mdot(x, ys):
+    """VecMDot, sequential sums."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    ys = [np.ascontiguousarray(v, dtype=np.float64) for v in ys]
+    f64p = C.POINTER(C.c_double)
+    arr = (f64p * max(len(ys), 1))(*[v.ctypes.data_as(f64p) for v in ys])
+    out = np.zeros(len(ys))
+    lib().or_vec_mdot(x.size, x.ctypes.data_as(f64p), len(ys), arr, out.ctypes.data_as(f64p))
+    return out

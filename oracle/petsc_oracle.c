@@ -746,3 +746,15 @@ void or_rhs_hash(int64_t i0, int64_t n, double *b) {
   for (int64_t i = 0; i < n; ++i)
     b[i] = (double)(splitmix64((uint64_t)(i0 + i) + seed) >> 11) * 0x1.0p-53;
 }
+
+/* exported forms of the VecMAXPY_Seq restatement above and of VecMDot (plain
+ * sequential sums: PETSc leaves the dot order to BLAS) */
+void or_vec_maxpy(int64_t n, int nv, const double *alpha, double *const *x, double *y) { vmaxpy(n, nv, alpha, x, y); }
+
+void or_vec_mdot(int64_t n, const double *x, int nv, const double *const *y, double *out) {
+  for (int k = 0; k < nv; ++k) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += x[i] * y[k][i];
+    out[k] = s;
+  }
+}

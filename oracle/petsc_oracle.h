@@ -101,6 +101,10 @@ int64_t or_stencil(int kind, int64_t nx, int64_t ny, int64_t nz, int64_t *indptr
 /* b_i = (splitmix64(i + 42*phi) >> 11) * 2^-53 for i in [i0, i0+n). */
 void or_rhs_hash(int64_t i0, int64_t n, double *b);
 
+/* VecMAXPY_Seq (PETSc's grouping) and a sequential VecMDot, for the Vec ABI tests */
+void or_vec_maxpy(int64_t n, int nv, const double *alpha, double *const *x, double *y);
+void or_vec_mdot(int64_t n, const double *x, int nv, const double *const *y, double *out);
+
 #ifdef __cplusplus
 }
 #endif

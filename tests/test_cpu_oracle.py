@@ -165,3 +165,25 @@ def test_convergence_reasons(oracle_mod):
     ind = oracle_mod.OracleMat.from_csr(2, 2, np.array([0, 1, 2]), np.array([0, 1]), np.array([1.0, -1.0]))
     assert ind.solve(np.ones(2), ksp="cg", pc="none")["reason"] == -10    # p.Ap == 0: DIVERGED_INDEFINITE_MAT
     assert A.solve(np.ones(M), ksp="preonly")["its"] == 1
+
+
+def test_oracle_maxpy_grouping(oracle_mod):
+    """The oracle's VecMAXPY_Seq restatement: the first nv % 4 vectors, then
+    groups of four, each summed left to right before it is added to y."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    for nv in (1, 2, 3, 4, 5, 6, 9):
+        xs = [rng.standard_normal(257) for _ in range(nv)]
+        y = rng.standard_normal(257)
+        a = rng.standard_normal(nv)
+        u = y.copy()
+        r = nv % 4
+        if r == 1:
+            u = a[0] * xs[0] + u
+        elif r == 2:
+            u = u + (a[0] * xs[0] + a[1] * xs[1])
+        elif r == 3:
+            u = u + ((a[0] * xs[0] + a[1] * xs[1]) + a[2] * xs[2])
+        for j in range(r, nv, 4):
+            u = u + (((a[j] * xs[j] + a[j + 1] * xs[j + 1]) + a[j + 2] * xs[j + 2]) + a[j + 3] * xs[j + 3])
+        assert np.array_equal(oracle_mod.vec_maxpy(y, a, xs), u)

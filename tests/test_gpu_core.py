@@ -226,3 +226,41 @@ def test_gmres_reference_system(selfcomm, oracle_mod, golden):
     assert rel(x.cpu().numpy(), o["x"]) <= 1e-8
     assert np.allclose(x.cpu().numpy(), golden["sys_X"])       # test.py:149's check
 
+
+
+@pytest.mark.parametrize("nv", [1, 2, 3, 4, 5, 7, 8, 11, 13, 30])
+def test_vec_maxpy_mdot(selfcomm, oracle_mod, nv):
+    """mx_vec_maxpy: bit-exact with VecMAXPY_Seq's grouping (first nv % 4, then
+    groups of four) for every remainder and pass split; mx_vec_mdot: VecMDot
+    within rounding of sequential sums (PETSc leaves the dot order to BLAS)."""
+    from mxsolve.core import vmaxpy, vmdot
+    rng = np.random.default_rng(nv)
+    n = 100_003
+    xs_h = [rng.standard_normal(n) for _ in range(nv)]
+    y_h = rng.standard_normal(n)
+    a = rng.standard_normal(nv)
+    xs = [torch.from_numpy(v).cuda() for v in xs_h]
+    y = torch.from_numpy(y_h).cuda()
+    vmaxpy(selfcomm, y, a, xs)
+    got = y.cpu().numpy()
+    assert np.array_equal(got.view(np.uint64), oracle_mod.vec_maxpy(y_h, a, xs_h).view(np.uint64))
+    d = vmdot(selfcomm, y, xs)
+    e = oracle_mod.vec_mdot(got, xs_h)
+    assert np.allclose(d, e, rtol=1e-12, atol=1e-9)
+
+
+def test_ksp_destroy_then_solve(selfcomm, oracle_mod):
+    """mx_ksp_destroy (KSPReset) releases the operator's solver state; the next
+    solve sets it up again and gives the same bits."""
+    from mxsolve.core import DMat, rhs_hash
+    A = DMat.stencil(selfcomm, "poisson3d", 16)
+    m = A.info()["m"]
+    b = selfcomm.empty(m)
+    rhs_hash(selfcomm, 0, b)
+    x1, x2 = selfcomm.zeros(m), selfcomm.zeros(m)
+    r1 = A.solve(b, x1, ksp="cg", pc="jacobi")
+    A.ksp_reset()
+    A.ksp_reset()                      # idempotent
+    r2 = A.solve(b, x2, ksp="cg", pc="jacobi")
+    assert r1["its"] == r2["its"] and torch.equal(x1, x2)
+    A.destroy()
