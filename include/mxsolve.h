@@ -266,6 +266,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 28: resident workgroups per CU for the row-pair SpMV grid (default 4)
  * key 29: CG mode 2 applies the deferred x steps every B iterations from B
  *         rotating direction buffers (1, 2 or 4; default 2)
+ * key 33: deadline in ms of a host wait on an RCCL communicator's work; past
+ *         it (or on an RCCL asynchronous error) the communicator is aborted
+ *         and the call fails with MX_ERR_COMM (default 120000)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with
@@ -282,6 +285,10 @@ int mx_dev_free(void *ptr);
  * 1 = of 3 doubles (the CG reductions), 2 = the halo exchange of A (pack +
  * send/recv, VecScatter).  [collective]                                       */
 int mx_debug_comm_bench(mx_comm c, mx_mat A, int what, int iters, double *us_per);
+/* Failure-detection test hook: enqueues ~stall_us of device time on the
+ * communicator's stream (a bounded spin) and waits for it through the
+ * communicator's watched wait (key 33 deadline, RCCL async-error polling).  */
+int mx_debug_comm_stall(mx_comm c, int stall_us);
 
 #ifdef __cplusplus
 }

@@ -405,6 +405,13 @@ int mx_vec_scale(mx_comm c, int64_t n, double a, double *x) {
 int mx_vec_set(mx_comm c, int64_t n, double a, double *x) {
   return guard([&] { Comm *k = C(c); vec_set(k->stream, n, a, x); HIPCHECK(hipStreamSynchronize(k->stream)); });
 }
+int mx_debug_comm_stall(mx_comm c, int stall_us) {
+  return guard([&] {
+    Comm *k = C(c);
+    debug_stall(k->stream, stall_us);
+    k->wait_stream(k->stream);
+  });
+}
 int mx_vec_mdot(mx_comm c, int64_t n, const double *x, int nv, const double *const *y, double *out) {
   return guard([&] {
     if (nv < 0 || (nv > 0 && (!y || !out))) fail(MX_ERR_ARG, "VecMDot: bad vector list");
@@ -503,6 +510,7 @@ int mx_debug_set(int key, int value) {
     case 30: old = g_knobs.pdict; g_knobs.pdict = value; break;
     case 31: old = g_knobs.spmv_rev; g_knobs.spmv_rev = value; break;
     case 32: old = g_knobs.cg_ntl; g_knobs.cg_ntl = value; break;
+    case 33: old = g_knobs.comm_timeout_ms; if (value > 0) g_knobs.comm_timeout_ms = value; break;
     default: break;
   }
   return old;

@@ -92,10 +92,12 @@ struct RcclComm : Comm {
   }
   void allreduce_sum(double *dev, int n) override {
     if ((size == 1 && !g_knobs.force_coll) || n <= 0) return;
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     NCCLCHECK(ncclAllReduce(dev, dev, (size_t)n, ncclDouble, ncclSum, nc, stream));
   }
   void exchange(const std::vector<Msg> &sends, const std::vector<Msg> &recvs, hipStream_t s) override {
     if (sends.empty() && recvs.empty()) return;
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     if (!s) s = stream;
     NCCLCHECK(ncclGroupStart());
     for (const Msg &m : sends) NCCLCHECK(ncclSend(m.buf, m.bytes, ncclUint8, m.peer, nc, s));
@@ -111,18 +113,56 @@ struct RcclComm : Comm {
     }
     NCCLCHECK(ncclGroupEnd());
     HIPCHECK(hipMemcpyAsync(recv, i64buf.p + size, sizeof(int64_t) * size, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+    wait_stream(stream);
   }
   void allgather_i64(int64_t v, int64_t *all) override {
     HIPCHECK(hipMemcpyAsync(i64buf.p, &v, sizeof(int64_t), hipMemcpyHostToDevice, stream));
     NCCLCHECK(ncclAllGather(i64buf.p, i64buf.p + size, 1, ncclInt64, nc, stream));
     HIPCHECK(hipMemcpyAsync(all, i64buf.p + size, sizeof(int64_t) * size, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+    wait_stream(stream);
   }
   void barrier() override {
     HIPCHECK(hipMemsetAsync(i64buf.p, 0, sizeof(int64_t), stream));
     NCCLCHECK(ncclAllReduce(i64buf.p, i64buf.p, 1, ncclInt64, ncclSum, nc, stream));
-    HIPCHECK(hipStreamSynchronize(stream));
+    wait_stream(stream);
+  }
+  // Failure detection: poll the device work and RCCL's
+  // asynchronous error state; past the deadline (knob 33, default 120 s) or on
+  // an RCCL error, abort the communicator so this rank fails with MX_ERR_COMM
+  // rather than waiting forever on a peer that died or took another path.
+  template <class Q> void watch(Q query, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spins = 0;; ++spins) {
+      const hipError_t e = query();
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) HIPCHECK(e);
+      ncclResult_t ar = ncclSuccess;
+      if (nc && ncclCommGetAsyncError(nc, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress) {
+        abort_comm();
+        fail(MX_ERR_COMM, std::string(what) + ": RCCL asynchronous error: " + ncclGetErrorString(ar));
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(g_knobs.comm_timeout_ms)) {
+        abort_comm();
+        fail(MX_ERR_COMM, std::string(what) + ": no progress for " + std::to_string(g_knobs.comm_timeout_ms) +
+                              " ms; RCCL communicator aborted");
+      }
+      if (spins > 200) usleep(50); else sched_yield();
+    }
+  }
+  void abort_comm() {
+    if (nc) (void)ncclCommAbort(nc);
+    nc = nullptr;
+    aborted = true;
+  }
+  bool aborted = false;
+  void wait_stream(hipStream_t s) override {
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
+    hipStream_t q = s ? s : stream;
+    watch([&] { return hipStreamQuery(q); }, "stream wait");
+  }
+  void wait_event(hipEvent_t ev) override {
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
+    watch([&] { return hipEventQuery(ev); }, "event wait");
   }
 };
 

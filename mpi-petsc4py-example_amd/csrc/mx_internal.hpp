@@ -73,6 +73,12 @@ struct Comm {
   // Host all-gather of one int64 per rank (setup only; synchronous).
   virtual void allgather_i64(int64_t v, int64_t *all) = 0;
   virtual void barrier() = 0;
+  // Host waits for device work that may include this communicator's
+  // collectives.  RCCL communicators poll the stream/event together with
+  // ncclCommGetAsyncError under a deadline and abort the communicator
+  // (MX_ERR_COMM) instead of hanging on a peer that never arrives.
+  virtual void wait_stream(hipStream_t s) { HIPCHECK(hipStreamSynchronize(s ? s : stream)); }
+  virtual void wait_event(hipEvent_t e) { HIPCHECK(hipEventSynchronize(e)); }
 };
 
 Comm *make_self_comm(int device);
@@ -156,7 +162,8 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int bnd_grid = 0; int mdot_group = 32;
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
-                int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3; };
+                int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
+                int comm_timeout_ms = 120000; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -301,6 +308,7 @@ void vec_pmult(hipStream_t s, int64_t n, const double *x, const double *y, doubl
 void vec_scale(hipStream_t s, int64_t n, double a, double *x);
 void vec_set(hipStream_t s, int64_t n, double a, double *x);
 void vec_rhs_hash(hipStream_t s, int64_t i0, int64_t n, double *b);
+void debug_stall(hipStream_t s, int stall_us);
 void debug_stream_read(hipStream_t s, const double *x, int64_t n, int width, double *out);
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t s,
                         int64_t *total_host);

@@ -832,10 +832,11 @@ static void solve_resources(Mat *A) {
 
 struct Poller {
   hipStream_t st;
+  Comm *c;
   int *pinned;
   hipEvent_t *ev;
   int pending = 0;  // batches enqueued
-  Poller(Mat *A, hipStream_t s) : st(s) {
+  Poller(Mat *A, hipStream_t s) : st(s), c(A->comm) {
     solve_resources(A);
     pinned = A->poll_pinned;
     ev = A->poll_ev;
@@ -850,7 +851,7 @@ struct Poller {
     ++pending;
     if (pending >= 2) {
       const int prev = (pending - 2) & 1;
-      HIPCHECK(hipEventSynchronize(ev[prev]));
+      c->wait_event(ev[prev]);
       if (pinned[prev]) return true;
     }
     return false;
@@ -894,9 +895,9 @@ void init_state(KspState &h, const mx_ksp_params &p, int normtype) {
   h.guess_zero = !p.guess_nonzero; h.max_k = p.restart; h.ksp_rnorm = -1.0;
 }
 
-void read_state(hipStream_t st, const KspState *d, KspState &h) {
+void read_state(Comm *c, hipStream_t st, const KspState *d, KspState &h) {
   HIPCHECK(hipMemcpyAsync(&h, d, sizeof(KspState), hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipStreamSynchronize(st));
+  c->wait_stream(st);
 }
 
 }  // namespace
@@ -1201,7 +1202,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     HIPCHECK(hipGetLastError());
   }
   HIPCHECK(hipEventRecord(ev.b, st));
-  read_state(st, s, hs);
+  read_state(c, st, s, hs);
   float ms = 0.f;
   HIPCHECK(hipEventElapsedTime(&ms, ev.a, ev.b));
   res.its = hs.its;
@@ -1288,7 +1289,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
     finish_reduce(part.p, RED_BLOCKS, 1, red.p, st);
     c->allreduce_sum(red.p, 1);
     HIPCHECK(hipMemcpyAsync(&snorm, red.p, sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
+    c->wait_stream(st);
     snorm = std::sqrt(snorm);
   }
   int first = 1, launched = 0;
@@ -1328,11 +1329,11 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
     gm_update_x_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, ldv, vsc.p, grs.p, x);
     gm_cycle_end_kernel<<<1, 64, 0, st>>>(s);
     HIPCHECK(hipGetLastError());
-    read_state(st, s, hs);
+    read_state(c, st, s, hs);
     if (hs.top.done) break;
   }
   HIPCHECK(hipEventRecord(ev.b, st));
-  HIPCHECK(hipEventSynchronize(ev.b));
+  c->wait_event(ev.b);
   float ms = 0.f;
   HIPCHECK(hipEventElapsedTime(&ms, ev.a, ev.b));
   res.its = hs.its;

@@ -339,4 +339,24 @@ void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t 
   HIPCHECK(hipStreamSynchronize(s));
 }
 
+// ------------------------------------------------------------- failure-detection test hook
+// one lane spins for about stall_us microseconds of device time, then exits
+// (a bounded wait: the grid always drains), so a host wait with a shorter
+// deadline can be exercised without a hung peer
+__global__ void stall_kernel(long long cycles) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < cycles) __builtin_amdgcn_s_sleep(8);
+}
+
+void debug_stall(hipStream_t s, int stall_us) {
+  if (stall_us < 0 || stall_us > 10000000) fail(MX_ERR_ARG, "stall must be in [0, 10 s]");
+  int khz = 100000;                                   // wall_clock64 rate (100 MHz on gfx9)
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  stall_kernel<<<1, 64, 0, s>>>((long long)stall_us * khz / 1000);
+  HIPCHECK(hipGetLastError());
+}
+
 }  // namespace mx

@@ -102,6 +102,7 @@ SIGNATURES = {
     "mx_debug_set": (C.c_int, [C.c_int, C.c_int]),
     "mx_debug_stream_read": (C.c_int, [P, P, I64, C.c_int, P]),
     "mx_debug_comm_bench": (C.c_int, [P, P, C.c_int, C.c_int, DP]),
+    "mx_debug_comm_stall": (C.c_int, [P, C.c_int]),
     "mx_dev_alloc": (C.c_int, [C.c_int, C.c_size_t, C.POINTER(P)]),
     "mx_dev_free": (C.c_int, [P]),
 }
