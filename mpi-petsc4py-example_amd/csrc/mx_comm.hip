@@ -30,6 +30,7 @@
 #include <mutex>
 
 #include "mx_internal.hpp"
+#include "mx_shm_barrier.hpp"
 
 namespace mx {
 
@@ -295,18 +296,16 @@ struct LocalComm : Comm {
 // message directories) followed by one staging slot per rank.  Every
 // collective is a sequence of "write my slot -> barrier -> read peers' slots
 // -> barrier"; device data moves by synchronous copies on the rank's stream.
-constexpr int SHM_MAX = 64;
 constexpr int SHM_DIR = 2 * SHM_MAX;       // message directory entries per rank
 struct ShmDirEnt { int64_t peer, off, bytes; };
 struct ShmHeader {
-  std::atomic<int64_t> arrived, gen;
-  std::atomic<int> abort, opened;
+  ShmBarrierWords bar;                      // mx_shm_barrier.hpp
+  std::atomic<int> opened;
   int size, pad;
   int64_t slot_bytes;
   int64_t scratch[SHM_MAX][SHM_MAX];        // [rank][k]: small all-to-all / all-gather payloads
   int64_t ndir[SHM_MAX];
   ShmDirEnt dir[SHM_MAX][SHM_DIR];
-  int tags[2][SHM_MAX];                      // by generation parity (see LocalWorld)
 };
 
 struct ShmComm : Comm {
@@ -350,9 +349,7 @@ struct ShmComm : Comm {
     if (r == 0) {
       h->size = s;
       h->slot_bytes = slot;
-      h->arrived.store(0);
-      h->gen.store(0);
-      h->abort.store(0);
+      shm_barrier_init(&h->bar);
       h->opened.store(1, std::memory_order_release);
     } else {
       const auto t0 = std::chrono::steady_clock::now();
@@ -375,36 +372,14 @@ struct ShmComm : Comm {
   }
   char *slot(int q) { return base + (size_t)q * (size_t)h->slot_bytes; }
 
-  // sense-free generation barrier; tag checks that every rank is in the same
-  // collective.  Tags live in one row per generation parity (a rank released
-  // early may already write its next tag while a slower one checks these);
-  // unchecked barriers record tag 0.  The generation cannot move between the
-  // load below and this rank's arrival, which it needs.
+  // generation barrier with collective tags (mx_shm_barrier.hpp)
   void wait_barrier(int tag, int check) {
-    if (h->abort.load()) fail(MX_ERR_COMM, "shared-memory world: another rank failed");
-    const int64_t g = h->gen.load(std::memory_order_acquire);
-    int *tg = h->tags[g & 1];
-    tg[rank] = check ? tag : 0;
-    if (h->arrived.fetch_add(1, std::memory_order_acq_rel) == size - 1) {
-      h->arrived.store(0, std::memory_order_relaxed);
-      h->gen.fetch_add(1, std::memory_order_acq_rel);
-    } else {
-      const auto t0 = std::chrono::steady_clock::now();
-      int spins = 0;
-      while (h->gen.load(std::memory_order_acquire) == g) {
-        if (h->abort.load()) fail(MX_ERR_COMM, "shared-memory world: another rank failed");
-        if (++spins > 1000) {
-          sched_yield();
-          if ((spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600)) {
-            h->abort.store(1);
-            fail(MX_ERR_COMM, "shared-memory barrier timed out");
-          }
-        }
-      }
+    switch (shm_barrier_wait(&h->bar, rank, size, tag, check != 0, std::chrono::seconds(600))) {
+      case BarrierResult::ok: return;
+      case BarrierResult::peer_failed: fail(MX_ERR_COMM, "shared-memory world: another rank failed");
+      case BarrierResult::timeout: fail(MX_ERR_COMM, "shared-memory barrier timed out");
+      case BarrierResult::mismatch: fail(MX_ERR_COMM, "shared-memory world: ranks entered different collectives");
     }
-    if (check)
-      for (int q = 0; q < size; ++q)
-        if (tg[q] != tag) { h->abort.store(1); fail(MX_ERR_COMM, "shared-memory world: ranks entered different collectives"); }
   }
 
   void allreduce_sum(double *dev, int n) override {
@@ -445,7 +420,7 @@ struct ShmComm : Comm {
       bool ok = false;
       for (int64_t e = 0; e < h->ndir[r.peer]; ++e)
         if (h->dir[r.peer][e].peer == rank) { ok = h->dir[r.peer][e].bytes == (int64_t)r.bytes; break; }
-      if (!ok) { h->abort.store(1); fail(MX_ERR_COMM, "shared-memory exchange: unmatched message"); }
+      if (!ok) { h->bar.abort.store(1); fail(MX_ERR_COMM, "shared-memory exchange: unmatched message"); }
     }
     for (int64_t rd = 0; rd < rounds; ++rd) {
       const int64_t lo = rd * cap, hi = lo + cap;
@@ -492,7 +467,7 @@ struct ShmComm : Comm {
     HIPCHECK(hipStreamSynchronize(stream));
     wait_barrier(5, 1);
   }
-  void abort_world() { if (h) h->abort.store(1); }
+  void abort_world() { if (h) h->bar.abort.store(1); }
 };
 
 Comm *make_shm_comm(int rank, int size, int device, const char *name, int64_t slot_kib) {

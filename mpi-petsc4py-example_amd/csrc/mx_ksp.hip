@@ -122,16 +122,21 @@ __global__ void __launch_bounds__(256) diag_range_kernel(int64_t n, const double
 // ------------------------------------------------------------------ CG kernels
 // partials of [z.z, z.r, r.r] (z = d.*r) and, when b != null, the same of b
 // for the nonzero-guess rnorm0 (KSPConvergedDefault n == 0).
-template <int NV>
+// START (zero initial guess): one pass reads b and writes r = b and x = 0
+// (VecSet + VecCopy + the norms: 3 passes and 4 vectors' traffic in one)
+template <int NV, bool START = false>
 __global__ void __launch_bounds__(256) cg_norms_kernel(int64_t n, const double *__restrict__ r,
                                                       const double *__restrict__ b, const Jac jac,
-                                                      double *__restrict__ partials) {
+                                                      double *__restrict__ partials,
+                                                      double *__restrict__ r_out = nullptr,
+                                                      double *__restrict__ x_out = nullptr) {
   double v[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = 0.0;
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const double ri = r[i];
+    const double ri = START ? b[i] : r[i];
+    if constexpr (START) { r_out[i] = ri; x_out[i] = 0.0; }
     const double zi = papply(jac, ri, i);
     v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
     if (NV == 6) {
@@ -1046,15 +1051,12 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   if (p.guess_nonzero) {
     mat_mult(A, x, r.p);
     vec_aypx(st, n, -1.0, b, r.p);
-  } else {
-    vec_set(st, n, 0.0, x);
-    HIPCHECK(hipMemcpyAsync(r.p, b, sizeof(double) * n, hipMemcpyDeviceToDevice, st));
   }
   KspState *s = sd.p;
   double *red = s->red;
   const int nv0 = p.guess_nonzero ? 6 : 3;
   if (nv0 == 6) cg_norms_kernel<6><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
-  else cg_norms_kernel<3><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
+  else cg_norms_kernel<3, true><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p, r.p, x);   // x = 0, r = b
   HIPCHECK(hipGetLastError());
   if (!fused) { finish_reduce(part.p, RED_BLOCKS, nv0, red, st); c->allreduce_sum(red, nv0); }
   if (nv0 == 6) cg_init_kernel<6><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);

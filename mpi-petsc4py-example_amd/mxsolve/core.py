@@ -329,8 +329,12 @@ class DMat:
             call("mx_ksp_destroy", self.h)
 
     def destroy(self):
+        """MatDestroy.  A matrix must go before its communicator: once the
+        communicator is destroyed the device memory is left to process exit
+        (the library's matrix refers to the communicator's stream)."""
         if self.h:
-            call("mx_mat_destroy", self.h)
+            if self.comm.h:
+                call("mx_mat_destroy", self.h)
             self.h = None
 
     def __del__(self):

@@ -30,16 +30,19 @@ def test_rccl_wait_deadline_aborts_communicator():
         torch.cuda.synchronize()                 # the bounded stall has drained
         # the aborted communicator refuses further collectives
         old8 = L.mx_debug_set(8, 1)              # force the collective path on one rank
+        mats = []
         try:
             with pytest.raises(_lib.MxError) as ej:
-                A = DMat.stencil(rc, "poisson3d", 8)
-                m = A.info()["m"]
+                mats.append(DMat.stencil(rc, "poisson3d", 8))
+                m = mats[0].info()["m"]
                 b, x = rc.empty(m), rc.zeros(m)
                 rhs_hash(rc, 0, b)
-                A.solve(b, x, ksp="cg", pc="jacobi")
+                mats[0].solve(b, x, ksp="cg", pc="jacobi")
             assert ej.value.code == _lib.MX_ERR_COMM
         finally:
             L.mx_debug_set(8, old8)
+            for A in mats:                        # before the communicator goes
+                A.destroy()
     finally:
         torch.cuda.synchronize()
         rc.destroy()
