@@ -39,12 +39,20 @@ def main():
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
-    # per-launch durations from the trace: the median is the working launch
-    # (launches after a solve has stopped are ~5 us no-ops and skew the mean)
-    durs = {}
+    # per-launch durations from the trace.  Launches shorter than NOOP_US are
+    # dropped: a launch enqueued after the solve has stopped exits on the done
+    # flag in a few us (the library now launches only the max_it remainder,
+    # but a solve that converges inside a batch still has some), and would
+    # drag the mean and median of the working launches down
+    NOOP_US = 10.0
+    durs, dropped = {}, {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
-        durs.setdefault(short(r["Kernel_Name"]), []).append(
-            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        k = short(r["Kernel_Name"])
+        t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        if t < NOOP_US and k.startswith(("spmv_sell", "cg_", "mdot", "maxpy")):
+            dropped[k] = dropped.get(k, 0) + 1
+            continue
+        durs.setdefault(k, []).append(t)
     fetch = pmc(os.path.join(src, "fetch", "run_counter_collection.csv"))
     write = pmc(os.path.join(src, "write", "run_counter_collection.csv"))
     calib = pmc(os.path.join(src, "calib", "run_counter_collection.csv"))
@@ -65,15 +73,20 @@ def main():
     alg = spmv_alg + 32 * m          # SPMV_CG: + r read, x read/write, p_i write
     out = {}
     lines = [f"# {tag}: rocprofv3 summary (3D 7-pt Poisson {grid}^3, N={ngpu}, bench.py --steps 50)", "",
-             "| kernel | calls | avg us | median us (trace) | % time | FETCH_SIZE KB (raw, median) | WRITE_SIZE KB (median) |",
-             "|---|---|---|---|---|---|---|"]
+             "| kernel | calls | working launches | mean us (working) | median us (working) | % time | FETCH_SIZE KB (raw, median) | WRITE_SIZE KB (median) |",
+             "|---|---|---|---|---|---|---|---|"]
     for r in stats[:14]:
         k = short(r["Name"])
         fk = statistics.median(fetch[k]) if k in fetch else None
         wk = statistics.median(write[k]) if k in write else None
-        med = statistics.median(durs[k]) if k in durs else float("nan")
-        lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | {med:.1f} | {float(r['Percentage']):.1f} | "
+        w = durs.get(k, [])
+        med = statistics.median(w) if w else float("nan")
+        mean = statistics.mean(w) if w else float("nan")
+        lines.append(f"| {k} | {r['Calls']} | {len(w)} | {mean:.1f} | {med:.1f} | {float(r['Percentage']):.1f} | "
                      f"{'' if fk is None else f'{fk:.0f}'} | {'' if wk is None else f'{wk:.0f}'} |")
+    if dropped:
+        lines += ["", "No-op launches (< 10 us, after a stop) dropped from mean/median: " +
+                  ", ".join(f"{k} {n}" for k, n in sorted(dropped.items()))]
     # the CG-fused MatMult (mode 3) of the solve; mode 2 when fusion is off
     sp = next((k for k in fetch if k.startswith("spmv_sell_kernel<3,")), None) or \
         next((k for k in fetch if k.startswith("spmv_sell_kernel<2,")), None)
