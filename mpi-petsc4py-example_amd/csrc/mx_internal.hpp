@@ -219,6 +219,7 @@ struct Mat {
   // pinned convergence-flag slots the host polls and the solve's timing
   // events (a pinned allocation per solve costs more than a short solve)
   int *poll_pinned = nullptr;
+  void *state_pinned = nullptr;     // KspState staging for the host <-> device state copies
   hipEvent_t poll_ev[2] = {nullptr, nullptr};
   hipEvent_t solve_ev[2] = {nullptr, nullptr};
   void release_ksp();               // KSPReset: work space, state, graph, Jacobi setup

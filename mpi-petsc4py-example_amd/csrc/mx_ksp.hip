@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256) diag_range_kernel(int64_t n, const double
 // for the nonzero-guess rnorm0 (KSPConvergedDefault n == 0).
 // START (zero initial guess): one pass reads b and writes r = b and x = 0
 // (VecSet + VecCopy + the norms: 3 passes and 4 vectors' traffic in one)
-template <int NV, bool START = false>
+template <int NV, bool START = false, bool XZERO = true>
 __global__ void __launch_bounds__(256) cg_norms_kernel(int64_t n, const double *__restrict__ r,
                                                       const double *__restrict__ b, const Jac jac,
                                                       double *__restrict__ partials,
@@ -136,7 +136,10 @@ __global__ void __launch_bounds__(256) cg_norms_kernel(int64_t n, const double *
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const double ri = START ? b[i] : r[i];
-    if constexpr (START) { r_out[i] = ri; x_out[i] = 0.0; }
+    if constexpr (START) {
+      r_out[i] = ri;
+      if constexpr (XZERO) x_out[i] = 0.0;
+    }
     const double zi = papply(jac, ri, i);
     v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
     if (NV == 6) {
@@ -339,6 +342,10 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
     double al[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) al[q] = top.xal[q];
+    // the first batch ([0, B)) of a zero-guess solve is x's first write: x
+    // is the +0.0 the solve started from, so it is not read (nor zeroed at
+    // the start); fma(a, p, +0.0) is what the read would have given
+    const bool xz = top.xlo == 0 && s->guess_zero;
     double *__restrict__ pout = p0;
     const double *__restrict__ pprev = B == 4 ? p3 : p1;
     auto batch = [&](auto ntc) __attribute__((always_inline)) {   // non-temporal reads: see walk below
@@ -349,7 +356,7 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
       };
       for (; k < n; k += stride) {
         const double po = ldv(pprev + k);
-        double xx = fma(al[0], ldv(pout + k), ldv(x + k));   // x += a_{i-B} p_{i-B}, oldest first
+        double xx = fma(al[0], ldv(pout + k), xz ? 0.0 : ldv(x + k));   // x += a_{i-B} p_{i-B}, oldest first
         if constexpr (B == 4) {
           xx = fma(al[1], ldv(p1 + k), xx);
           xx = fma(al[2], ldv(p2 + k), xx);
@@ -568,14 +575,32 @@ __global__ void cg_finish_x_kernel(int64_t n, const KspState *__restrict__ s, co
 }
 
 // the batched x steps still pending when the solve stopped, oldest first
+// (a zero-guess solve that stopped before its first batch has never written
+// x: the pending steps start from +0.0, or x is set to 0 when there are none)
 __global__ void cg_finish_xb_kernel(int64_t n, const KspState *__restrict__ s, const PBufs pb, int B,
                                     double *__restrict__ x) {
   const int j0 = s->top.xlo, np = s->top.xhi - s->top.xlo;
-  if (np <= 0) return;
+  const bool xz = j0 == 0 && s->guess_zero;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (np <= 0) {
+    if (xz)
+      for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = 0.0;
+    return;
+  }
+  // at most B - 1 + 1 pending steps; their buffers and scalars picked once
+  const double *p[4];
+  double a[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = (j0 + (q < np ? q : 0)) % B;
+    p[q] = j == 0 ? pb.b[0] : j == 1 ? pb.b[1] : j == 2 ? pb.b[2] : pb.b[3];
+    a[q] = s->top.xal[j];
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    double xx = x[i];
-    for (int q = 0; q < np; ++q) xx = fma(s->top.xal[(j0 + q) % B], pb.b[(j0 + q) % B][i], xx);
+    double xx = xz ? 0.0 : x[i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < np) xx = fma(a[q], p[q][i], xx);
     x[i] = xx;
   }
 }
@@ -831,6 +856,7 @@ static void solve_resources(Mat *A) {
   if (A->poll_pinned) return;
   HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&A->poll_pinned), 2 * sizeof(int), hipHostMallocDefault));
   A->poll_pinned[0] = A->poll_pinned[1] = 0;
+  HIPCHECK(hipHostMalloc(&A->state_pinned, sizeof(KspState), hipHostMallocDefault));
   for (auto &e : A->poll_ev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : A->solve_ev) HIPCHECK(hipEventCreate(&e));
 }
@@ -900,9 +926,18 @@ void init_state(KspState &h, const mx_ksp_params &p, int normtype) {
   h.guess_zero = !p.guess_nonzero; h.max_k = p.restart; h.ksp_rnorm = -1.0;
 }
 
-void read_state(Comm *c, hipStream_t st, const KspState *d, KspState &h) {
-  HIPCHECK(hipMemcpyAsync(&h, d, sizeof(KspState), hipMemcpyDeviceToHost, st));
-  c->wait_stream(st);
+// device state -> host through the operator's pinned staging buffer (a
+// pageable copy is staged and synchronous in the runtime)
+void read_state(Mat *A, hipStream_t st, const KspState *d, KspState &h) {
+  solve_resources(A);
+  HIPCHECK(hipMemcpyAsync(A->state_pinned, d, sizeof(KspState), hipMemcpyDeviceToHost, st));
+  A->comm->wait_stream(st);
+  std::memcpy(&h, A->state_pinned, sizeof(KspState));
+}
+void write_state(Mat *A, hipStream_t st, KspState *d, const KspState &h) {
+  solve_resources(A);
+  std::memcpy(A->state_pinned, &h, sizeof(KspState));
+  HIPCHECK(hipMemcpyAsync(d, A->state_pinned, sizeof(KspState), hipMemcpyHostToDevice, st));
 }
 
 }  // namespace
@@ -918,6 +953,8 @@ void Mat::release_ksp() {
   jac_mode = -1;
   if (poll_pinned) (void)hipHostFree(poll_pinned);
   poll_pinned = nullptr;
+  if (state_pinned) (void)hipHostFree(state_pinned);
+  state_pinned = nullptr;
   for (auto &e : poll_ev) { if (e) (void)hipEventDestroy(e); e = nullptr; }
   for (auto &e : solve_ev) { if (e) (void)hipEventDestroy(e); e = nullptr; }
 }
@@ -1042,7 +1079,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   struct { KspState *p; } sd{state_buf(A)};
   KspState hs;
   init_state(hs, p, normtype);
-  HIPCHECK(hipMemcpyAsync(sd.p, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  write_state(A, st, sd.p, hs);
   Events ev(A);
   SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
   HIPCHECK(hipEventRecord(ev.a, st));
@@ -1056,7 +1093,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   double *red = s->red;
   const int nv0 = p.guess_nonzero ? 6 : 3;
   if (nv0 == 6) cg_norms_kernel<6><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
-  else cg_norms_kernel<3, true><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p, r.p, x);   // x = 0, r = b
+  // x = 0 and r = b; with batched x steps x is not written here at all (the
+  // first batch, or the finish pass, is its first write)
+  else if (xb > 1) cg_norms_kernel<3, true, false><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p, r.p, nullptr);
+  else cg_norms_kernel<3, true><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p, r.p, x);
   HIPCHECK(hipGetLastError());
   if (!fused) { finish_reduce(part.p, RED_BLOCKS, nv0, red, st); c->allreduce_sum(red, nv0); }
   if (nv0 == 6) cg_init_kernel<6><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
@@ -1204,7 +1244,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     HIPCHECK(hipGetLastError());
   }
   HIPCHECK(hipEventRecord(ev.b, st));
-  read_state(c, st, s, hs);
+  read_state(A, st, s, hs);
   float ms = 0.f;
   HIPCHECK(hipEventElapsedTime(&ms, ev.a, ev.b));
   res.its = hs.its;
@@ -1273,7 +1313,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   if (p.norm_type != MX_NORM_DEFAULT && p.norm_type != MX_NORM_PRECONDITIONED)
     fail(MX_ERR_UNSUPPORTED, "GMRES with left preconditioning supports the preconditioned norm only");
   hs.max_k = max_k;
-  HIPCHECK(hipMemcpyAsync(sd.p, &hs, sizeof(hs), hipMemcpyHostToDevice, st));
+  write_state(A, st, sd.p, hs);
   KspState *s = sd.p;
   double *sred = reinterpret_cast<double *>(s);
   const bool fused = c->size == 1;
@@ -1331,7 +1371,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
     gm_update_x_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, ldv, vsc.p, grs.p, x);
     gm_cycle_end_kernel<<<1, 64, 0, st>>>(s);
     HIPCHECK(hipGetLastError());
-    read_state(c, st, s, hs);
+    read_state(A, st, s, hs);
     if (hs.top.done) break;
   }
   HIPCHECK(hipEventRecord(ev.b, st));

@@ -340,6 +340,62 @@ __global__ void __launch_bounds__(256) pov_kernel(const double *__restrict__ x, 
   }
 }
 
+// codes without the LDS table: two distinct values selected per slot from
+// kernel-argument scalars (the constant-coefficient stencils have exactly
+// two), so no LDS read shares lgkmcnt with the scalar block-id loads;
+// META 0: block id from the unit index, 1: scalar loads two steps ahead
+template <int META>
+__global__ void __launch_bounds__(256) psel_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                   const uint8_t *__restrict__ dict, const int32_t *__restrict__ pblk,
+                                                   double v0, double v1, double *__restrict__ part) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t chunk = (nunits + 7) >> 3;
+  const int64_t s0 = xcd * chunk + (int64_t)j * 4 + wid, step = (int64_t)per * 4;
+  const int64_t send = min(nunits, (xcd + 1) * chunk);
+  double dot = 0.0;
+  struct T { UnitL l; u32x4 cw; };
+  auto ld = [&](int64_t u, int blk, T &t) {
+    unit_load(x, u, lane, t.l);
+    t.cw = *reinterpret_cast<const u32x4 *>(dict + ((int64_t)blk * 64 + lane) * 16);
+  };
+  auto fin = [&](int64_t u, const T &t) {
+    const int64_t r0 = u * 128 + 2 * lane;
+    auto code = [&](int i) -> int { return (t.cw[(i >> 2) & 3] >> (8 * (i & 3))) & 0xff; };
+    const double lo = wave_shift<true>(t.l.c.y, t.l.elo), hi = wave_shift<false>(t.l.c.x, t.l.ehi);
+    const double a0[7] = {t.l.zm.x, t.l.ym.x, lo, t.l.c.x, t.l.c.y, t.l.yp.x, t.l.zp.x};
+    const double a1[7] = {t.l.zm.y, t.l.ym.y, t.l.c.x, t.l.c.y, hi, t.l.yp.y, t.l.zp.y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int c0 = code(k), c1 = code(7 + k);
+      const double q0 = s0 + (c0 == 0 ? v0 : v1) * a0[k], q1 = s1 + (c1 == 0 ? v0 : v1) * a1[k];
+      s0 = c0 != ABSENT ? q0 : s0;
+      s1 = c1 != ABSENT ? q1 : s1;
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    dot += t.l.c.x * s0; dot += t.l.c.y * s1;
+  };
+  auto mb = [&](int64_t u) -> int { return u < send ? (META ? pblk[u] : (int)(u & 1)) : 0; };
+  int64_t u = s0;
+  int ca = mb(u), cb = mb(u + step), na = mb(u + 2 * step), nb = mb(u + 3 * step);
+  for (; u + step < send; u += 2 * step) {
+    const int fa = mb(u + 4 * step), fb = mb(u + 5 * step);
+    T ta, tb;
+    ld(u, ca, ta);
+    ld(u + step, cb, tb);
+    __builtin_amdgcn_sched_barrier(0);
+    fin(u, ta);
+    fin(u + step, tb);
+    ca = na; cb = nb; na = fa; nb = fb;
+  }
+  for (; u < send; u += step) { T t; ld(u, mb(u), t); fin(u, t); }
+  for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+  if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+}
+
 // 2.5D z-march: workgroup = (tile of TY lines in y) x (z range of ZR planes),
 // 256 threads = one line's columns, PER = TY values per thread per plane plus
 // the two y-halo values.  Planes live in a 4-slot register ring (static slot
@@ -514,6 +570,10 @@ int main(int argc, char **argv) {
     timeit(nm, [&] { pov_kernel<true, 0><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pov+meta1+dot %d/CU", wpc);
     timeit(nm, [&] { pov_kernel<true, 1><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "psel+meta0 %d/CU", wpc);
+    timeit(nm, [&] { psel_kernel<0><<<g, 256>>>(x, y, M / 128, dict, pblk, 6.0, -1.0, part); }, false);
+    snprintf(nm, sizeof nm, "psel+meta1 %d/CU", wpc);
+    timeit(nm, [&] { psel_kernel<1><<<g, 256>>>(x, y, M / 128, dict, pblk, 6.0, -1.0, part); }, false);
     snprintf(nm, sizeof nm, "pbuf<2> %d/CU", wpc);
     timeit(nm, [&] { pbuf_kernel<2, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pcodes<2>+meta+dot %d/CU", wpc);
