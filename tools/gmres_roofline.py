@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""GMRES(30) per-kernel algorithmic HBM fractions from a rocprofv3 kernel
+trace of tools/bench_general.py c4 (BASELINE C4, conv-diff 256^3).
+
+Algorithmic bytes per inner step j (0-based within a restart cycle, the new
+direction w = A v_j; SURVEY.md §8d's GMRES model, this build's fusions):
+  MatMult (SPMV_JACOBI_S, vector Jacobi): x 8m + dinv 8m + w 8m + codes
+  MDot  : w and v_0..v_j            8m (j + 2)
+  MAXPY + norm (fused)             : w read + write, v_0..v_j   8m (j + 3)
+The trace's kernels of each kind are summed over the whole solve and divided
+into the summed bytes of the same steps.
+    python tools/gmres_roofline.py TRACE_DIR its [m] [restart]"""
+import csv
+import glob
+import json
+import re
+import sys
+
+d = {}
+for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = re.sub(r"^void\s+", "", r["Kernel_Name"]).split("(")[0].replace("mx::", "").replace(" ", "")
+        d.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+its = int(sys.argv[2])
+m = int(sys.argv[3]) if len(sys.argv) > 3 else 256 ** 3
+restart = int(sys.argv[4]) if len(sys.argv) > 4 else 30
+# every GMRES step the bench leg runs: a 20-iteration warm-up, the converged
+# solve (its) and a 60-iteration profiled solve (its standalone products use
+# the plain SpMV kernel, not counted here)
+steps = [j % restart for n in (20, its, 60) for j in range(n)]
+mdot_b = sum(8 * m * (j + 2) for j in steps)
+maxpy_b = sum(8 * m * (j + 3) for j in steps)
+spmv_b = len(steps) * 24 * m
+
+
+def total(prefix, lo=20.0):      # working launches (the no-ops after a stop are shorter)
+    return sum(t for k, v in d.items() if k.startswith(prefix) for t in v if t >= lo)
+
+
+share = 1.0
+out = {}
+for name, prefix, b in (("MDot (mdot_kernel<NV>)", "mdot_kernel", mdot_b),
+                        ("MAXPY+norm (maxpy_norm_kernel)", "maxpy_norm_kernel", maxpy_b),
+                        ("MatMult (spmv_sell_kernel<5,...>, Jacobi)", "spmv_sell_kernel<5,", spmv_b)):
+    t_us = total(prefix) * share
+    out[name] = {"alg_bytes": b, "time_us": round(t_us, 1), "TBps": round(b / t_us / 1e6, 3),
+                 "frac_of_8TBps": round(b / t_us / 1e6 / 8.0, 3)}
+print(json.dumps(out, indent=1))

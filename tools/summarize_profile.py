@@ -45,14 +45,15 @@ def main():
     # but a solve that converges inside a batch still has some), and would
     # drag the mean and median of the working launches down
     NOOP_US = 10.0
-    durs, dropped = {}, {}
+    alld, durs, dropped = {}, {}, {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))):
-        k = short(r["Kernel_Name"])
-        t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if t < NOOP_US and k.startswith(("spmv_sell", "cg_", "mdot", "maxpy")):
-            dropped[k] = dropped.get(k, 0) + 1
-            continue
-        durs.setdefault(k, []).append(t)
+        alld.setdefault(short(r["Kernel_Name"]), []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for k, ts in alld.items():
+        work = len(ts) >= 10 and statistics.median(ts) >= 2 * NOOP_US   # an iteration kernel with some no-op launches
+        keep = [t for t in ts if not (work and t < NOOP_US)]
+        if len(keep) < len(ts):
+            dropped[k] = len(ts) - len(keep)
+        durs[k] = keep
     fetch = pmc(os.path.join(src, "fetch", "run_counter_collection.csv"))
     write = pmc(os.path.join(src, "write", "run_counter_collection.csv"))
     calib = pmc(os.path.join(src, "calib", "run_counter_collection.csv"))
@@ -87,9 +88,10 @@ def main():
     if dropped:
         lines += ["", "No-op launches (< 10 us, after a stop) dropped from mean/median: " +
                   ", ".join(f"{k} {n}" for k, n in sorted(dropped.items()))]
-    # the CG-fused MatMult (mode 3) of the solve; mode 2 when fusion is off
-    sp = next((k for k in fetch if k.startswith("spmv_sell_kernel<3,")), None) or \
-        next((k for k in fetch if k.startswith("spmv_sell_kernel<2,")), None)
+    # the solve's MatMult: the SpMV kernel with the most device time (the
+    # CG-fused SPMV_CG <3,...> at <= 3M rows/rank, SPMV_DOT <2,...> above)
+    cands = [k for k in fetch if k.startswith(("spmv_sell_kernel<3,", "spmv_sell_kernel<2,"))]
+    sp = max(cands, key=lambda k: sum(durs.get(k, [0.0]))) if cands else None
     if sp and not sp.startswith("spmv_sell_kernel<3,"):
         alg = spmv_alg
     # the profiled bench's own figure (bench.py spmv_format_bytes: code-block
