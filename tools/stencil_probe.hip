@@ -396,6 +396,62 @@ __global__ void __launch_bounds__(256) psel_kernel(const double *__restrict__ x,
   if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
 }
 
+// narrow codes: 2 bits per slot (0, 1 = table entries, 3 = absent), the 14
+// slots of a lane in ONE 4-byte word: the code-block load is 256 B per wave
+// instead of 1 KB (TA/L1 work is the bound); values still from the LDS table
+template <bool META>
+__global__ void __launch_bounds__(256) pnarrow_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                      const uint32_t *__restrict__ dict2, const int32_t *__restrict__ pblk,
+                                                      const double *__restrict__ vtab_g, double *__restrict__ part) {
+  __shared__ double vtab[256];
+  for (int i = threadIdx.x; i < 256; i += 256) vtab[i] = vtab_g[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t chunk = (nunits + 7) >> 3;
+  const int64_t s0 = xcd * chunk + (int64_t)j * 4 + wid, step = (int64_t)per * 4;
+  const int64_t send = min(nunits, (xcd + 1) * chunk);
+  double dot = 0.0;
+  struct T { UnitL l; uint32_t cw; };
+  auto ld = [&](int64_t u, int blk, T &t) {
+    unit_load(x, u, lane, t.l);
+    t.cw = dict2[(int64_t)blk * 64 + lane];
+  };
+  auto fin = [&](int64_t u, const T &t) {
+    const int64_t r0 = u * 128 + 2 * lane;
+    const double lo = wave_shift<true>(t.l.c.y, t.l.elo), hi = wave_shift<false>(t.l.c.x, t.l.ehi);
+    const double a0[7] = {t.l.zm.x, t.l.ym.x, lo, t.l.c.x, t.l.c.y, t.l.yp.x, t.l.zp.x};
+    const double a1[7] = {t.l.zm.y, t.l.ym.y, t.l.c.x, t.l.c.y, hi, t.l.yp.y, t.l.zp.y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int c0 = (t.cw >> (2 * k)) & 3, c1 = (t.cw >> (2 * (7 + k))) & 3;
+      const double q0 = s0 + vtab[c0] * a0[k], q1 = s1 + vtab[c1] * a1[k];
+      s0 = c0 != 3 ? q0 : s0;
+      s1 = c1 != 3 ? q1 : s1;
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    dot += t.l.c.x * s0; dot += t.l.c.y * s1;
+  };
+  auto mb = [&](int64_t u) -> int { return u < send ? (META ? pblk[u] : (int)(u & 1)) : 0; };
+  int64_t u = s0;
+  int ca = mb(u), cb = mb(u + step), na = mb(u + 2 * step), nb = mb(u + 3 * step);
+  for (; u + step < send; u += 2 * step) {
+    const int fa = mb(u + 4 * step), fb = mb(u + 5 * step);
+    T ta, tb;
+    ld(u, ca, ta);
+    ld(u + step, cb, tb);
+    __builtin_amdgcn_sched_barrier(0);
+    fin(u, ta);
+    fin(u + step, tb);
+    ca = na; cb = nb; na = fa; nb = fb;
+  }
+  for (; u < send; u += step) { T t; ld(u, mb(u), t); fin(u, t); }
+  for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+  if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+}
+
 // 2.5D z-march: workgroup = (tile of TY lines in y) x (z range of ZR planes),
 // 256 threads = one line's columns, PER = TY values per thread per plane plus
 // the two y-halo values.  Planes live in a 4-slot register ring (static slot
@@ -534,6 +590,19 @@ int main(int argc, char **argv) {
   std::vector<double> hv(256, 0.0); hv[0] = 6.0; hv[1] = -1.0;
   CK(hipMalloc(&vt, 256 * 8)); CK(hipMemcpy(vt, hv.data(), 256 * 8, hipMemcpyHostToDevice));
   CK(hipMalloc(&part, 1 << 20));
+  // the same dictionary in 2-bit codes (code 255 -> 3)
+  std::vector<uint32_t> hd2(2 * 64, 0);
+  for (int b = 0; b < 2; ++b)
+    for (int l = 0; l < 64; ++l) {
+      uint32_t w = 0;
+      for (int q = 0; q < 14; ++q) {
+        const uint8_t c = hd[(b * 64 + l) * 16 + q];
+        w |= (uint32_t)(c == ABSENT ? 3 : c) << (2 * q);
+      }
+      hd2[b * 64 + l] = w;
+    }
+  uint32_t *dict2;
+  CK(hipMalloc(&dict2, hd2.size() * 4)); CK(hipMemcpy(dict2, hd2.data(), hd2.size() * 4, hipMemcpyHostToDevice));
   for (int wpc : {2, 3, 4, 5}) {
     const int g = cus * wpc - 8;
     char nm[64];
@@ -574,6 +643,10 @@ int main(int argc, char **argv) {
     timeit(nm, [&] { psel_kernel<0><<<g, 256>>>(x, y, M / 128, dict, pblk, 6.0, -1.0, part); }, false);
     snprintf(nm, sizeof nm, "psel+meta1 %d/CU", wpc);
     timeit(nm, [&] { psel_kernel<1><<<g, 256>>>(x, y, M / 128, dict, pblk, 6.0, -1.0, part); }, false);
+    snprintf(nm, sizeof nm, "pnarrow+meta0 %d/CU", wpc);
+    timeit(nm, [&] { pnarrow_kernel<false><<<g, 256>>>(x, y, M / 128, dict2, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "pnarrow+meta1 %d/CU", wpc);
+    timeit(nm, [&] { pnarrow_kernel<true><<<g, 256>>>(x, y, M / 128, dict2, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pbuf<2> %d/CU", wpc);
     timeit(nm, [&] { pbuf_kernel<2, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pcodes<2>+meta+dot %d/CU", wpc);
