@@ -269,6 +269,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 33: deadline in ms of a host wait on an RCCL communicator's work; past
  *         it (or on an RCCL asynchronous error) the communicator is aborted
  *         and the call fails with MX_ERR_COMM (default 120000)
+ * key 34: grid of the CG initial-norms pass (0 = default 1024 workgroups)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

@@ -511,6 +511,7 @@ int mx_debug_set(int key, int value) {
     case 31: old = g_knobs.spmv_rev; g_knobs.spmv_rev = value; break;
     case 32: old = g_knobs.cg_ntl; g_knobs.cg_ntl = value; break;
     case 33: old = g_knobs.comm_timeout_ms; if (value > 0) g_knobs.comm_timeout_ms = value; break;
+    case 34: old = g_knobs.norm_grid; g_knobs.norm_grid = std::min(std::max(value, 0), 16384); break;
     default: break;
   }
   return old;

@@ -57,6 +57,7 @@ struct KspState {
   int its, reason, inner_stop, it;
   int itcount, max_k, nv, xi;
   int guess_zero;
+  long long t_start;        // wall_clock64() when the solve's first kernel ran (CG)
   int it_k;                 // current CG iteration, written by the iteration's first kernel
                             // (top.it_u: the next one, written by the update pass)
   double pb;

@@ -36,6 +36,18 @@ namespace mx {
 
 Comm::~Comm() {}
 
+void Comm::wait_until(const std::function<bool()> &ready, hipStream_t s) {
+  hipStream_t q = s ? s : stream;
+  for (int spins = 0; !ready(); ++spins) {
+    if ((spins & 63) == 63) {
+      const hipError_t e = hipStreamQuery(q);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) HIPCHECK(e);
+      if (spins > 4096) sched_yield();
+    }
+  }
+}
+
 static hipStream_t new_stream(int device) {
   HIPCHECK(hipSetDevice(device));
   hipStream_t s;
@@ -164,6 +176,11 @@ struct RcclComm : Comm {
   void wait_event(hipEvent_t ev) override {
     if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     watch([&] { return hipEventQuery(ev); }, "event wait");
+  }
+  void wait_until(const std::function<bool()> &ready, hipStream_t s) override {
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
+    hipStream_t q = s ? s : stream;
+    watch([&] { return ready() ? hipSuccess : hipStreamQuery(q); }, "progress wait");
   }
 };
 

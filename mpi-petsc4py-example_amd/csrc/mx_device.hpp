@@ -85,8 +85,9 @@ struct Fold {
   int ncount = 0;            // workgroups of this launch (all arrive)
 };
 
+// true in the workgroup that folded (every thread of it)
 template <int NV>
-__device__ __forceinline__ void block_fold(double (&v)[NV], double *partials, const Fold &f) {
+__device__ __forceinline__ bool block_fold(double (&v)[NV], double *partials, const Fold &f) {
   __shared__ double sh[NV][4];
   __shared__ int last;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -117,7 +118,7 @@ __device__ __forceinline__ void block_fold(double (&v)[NV], double *partials, co
     }
   }
   __syncthreads();
-  if (!last) return;
+  if (!last) return false;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const double t = block_sum_array<16, true>(partials + (size_t)k * f.ntotal, f.ntotal);
@@ -125,6 +126,7 @@ __device__ __forceinline__ void block_fold(double (&v)[NV], double *partials, co
   }
   if (threadIdx.x < 9)
     __hip_atomic_store(f.cnt + threadIdx.x * FOLD_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
 }
 
 // partials of this launch's workgroups: plain block partials, or an in-launch fold

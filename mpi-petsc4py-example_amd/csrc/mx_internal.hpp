@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -79,6 +80,10 @@ struct Comm {
   // (MX_ERR_COMM) instead of hanging on a peer that never arrives.
   virtual void wait_stream(hipStream_t s) { HIPCHECK(hipStreamSynchronize(s ? s : stream)); }
   virtual void wait_event(hipEvent_t e) { HIPCHECK(hipEventSynchronize(e)); }
+  // Host spins until ready() (a word the device writes into pinned host
+  // memory) or until stream s has drained (then the caller re-reads the word);
+  // a device error on s raises.
+  virtual void wait_until(const std::function<bool()> &ready, hipStream_t s);
 };
 
 Comm *make_self_comm(int device);
@@ -163,7 +168,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
-                int comm_timeout_ms = 120000; };
+                int comm_timeout_ms = 120000; int norm_grid = 0; };
 extern Knobs g_knobs;
 
 struct Halo {

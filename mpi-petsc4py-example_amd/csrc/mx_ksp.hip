@@ -66,6 +66,35 @@ __device__ __forceinline__ void stop(KspState *s, int reason) {
   s->inner_stop = 1;
 }
 
+// Words of pinned host memory the CG kernels write with system-scope stores
+// (Mat::poll_pinned): the done flag and the iteration count the host's poller
+// spins on, and the result the tail pass publishes (no device-to-host copy).
+enum { HW_DONE = 0, HW_PROGRESS = 1, HW_ITS = 2, HW_REASON = 3, HW_DP = 4 /* double: words 4-5 */, HW_TICKS = 6 /* int64: 6-7 */,
+       HW_WORDS = 8 };
+
+// The solver parameters a solve starts from (KspState's parameter fields).
+struct KspInit {
+  double rtol, atol, dtol, haptol, breakdowntol;
+  int max_it, normtype, guess_zero, max_k;
+};
+// KspState for a new solve, written on the device (no host-to-device copy):
+// zero everything -- which also clears the fold counters -- then the
+// parameters; stamps the solve's start on the device clock.
+__global__ void __launch_bounds__(256) ksp_state_init_kernel(KspState *__restrict__ s, const KspInit in) {
+  auto *w = reinterpret_cast<unsigned long long *>(s);
+  static_assert(sizeof(KspState) % 8 == 0, "KspState is cleared in 8-byte words");
+  for (size_t k = threadIdx.x; k < sizeof(KspState) / 8; k += blockDim.x) w[k] = 0ull;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s->t_start = wall_clock64();
+  s->rtol = in.rtol; s->top.atol = in.atol; s->top.dtol = in.dtol; s->haptol = in.haptol;
+  s->breakdowntol = in.breakdowntol; s->top.max_it = in.max_it; s->top.normtype = in.normtype;
+  s->guess_zero = in.guess_zero; s->max_k = in.max_k; s->ksp_rnorm = -1.0;
+}
+__device__ __forceinline__ void host_store(int *w, int v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Either one thread after an all-reduce (P > 1), or a fused single block that
 // first folds the per-block partials itself (P == 1, no collective between).
 template <int NV>
@@ -120,42 +149,79 @@ __global__ void __launch_bounds__(256) diag_range_kernel(int64_t n, const double
 }
 
 // ------------------------------------------------------------------ CG kernels
-// partials of [z.z, z.r, r.r] (z = d.*r) and, when b != null, the same of b
+// after the initial norms (red[0..NV)): dp, rnorm0/ttol, beta, checks for
+// iteration 0; one thread
+template <int NV>
+__device__ void cg_init_body(KspState *s, double *hist);
+
+// partials of [z.z, z.r, r.r] (z = d.*r) and, when NV == 6, the same of b
 // for the nonzero-guess rnorm0 (KSPConvergedDefault n == 0).
-// START (zero initial guess): one pass reads b and writes r = b and x = 0
-// (VecSet + VecCopy + the norms: 3 passes and 4 vectors' traffic in one)
+// START (zero initial guess, unbatched x steps): one pass reads b and writes
+// r = b and x = 0 (VecSet + VecCopy + the norms: 3 passes in one); batched x
+// steps read b as r_0 and write nothing here.  Eight (NV 6: four) rows'
+// loads per thread are issued together (the per-thread sum order is the plain strided loop's).
+// fin.cnt != null (one rank): the last workgroup folds the partials in-launch
+// into s->red and runs cg_init (no separate init launch).
 template <int NV, bool START = false, bool XZERO = true>
 __global__ void __launch_bounds__(256) cg_norms_kernel(int64_t n, const double *__restrict__ r,
                                                       const double *__restrict__ b, const Jac jac,
                                                       double *__restrict__ partials,
-                                                      double *__restrict__ r_out = nullptr,
-                                                      double *__restrict__ x_out = nullptr) {
+                                                      double *__restrict__ r_out, double *__restrict__ x_out,
+                                                      const Fold fin, KspState *__restrict__ s,
+                                                      double *__restrict__ hist) {
   double v[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = 0.0;
+  auto row = [&](double ri, double bi, int64_t i) {
+    const double zi = papply(jac, ri, i);
+    v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
+    if (NV == 6) {
+      const double zb = papply(jac, bi, i);
+      v[3 % NV] += zb * zb; v[4 % NV] += bi * zb; v[5 % NV] += bi * bi;
+    }
+  };
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  constexpr int U = NV == 6 ? 4 : 8;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    double rr[U], bb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      rr[u] = START ? b[i + u * stride] : r[i + u * stride];
+      bb[u] = NV == 6 ? b[i + u * stride] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (START) {
+        r_out[i + u * stride] = rr[u];
+        if constexpr (XZERO) x_out[i + u * stride] = 0.0;
+      }
+      row(rr[u], bb[u], i + u * stride);
+    }
+  }
+  for (; i < n; i += stride) {
     const double ri = START ? b[i] : r[i];
     if constexpr (START) {
       r_out[i] = ri;
       if constexpr (XZERO) x_out[i] = 0.0;
     }
-    const double zi = papply(jac, ri, i);
-    v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
-    if (NV == 6) {
-      const double bi = b[i];
-      const double zb = papply(jac, bi, i);
-      v[3 % NV] += zb * zb; v[4 % NV] += bi * zb; v[5 % NV] += bi * bi;
-    }
+    row(ri, NV == 6 ? b[i] : 0.0, i);
   }
-  block_sum_to_partials<NV>(v, partials, gridDim.x);
+  if (!fin.cnt) {
+    block_sum_to_partials<NV>(v, partials, gridDim.x);
+    return;
+  }
+  if (block_fold<NV>(v, partials, fin) && threadIdx.x == 0) cg_init_body<NV>(s, hist);
 }
 
-// after the initial norms: dp, rnorm0/ttol, beta, checks for iteration 0
 template <int NV>
 __global__ void __launch_bounds__(256) cg_init_kernel(KspState *s, const double *partials, int nblocks,
                                                       int fused, double *hist) {
-  if (!gather_red<NV>(s, partials, nblocks, fused)) return;
+  if (gather_red<NV>(s, partials, nblocks, fused)) cg_init_body<NV>(s, hist);
+}
+
+template <int NV>
+__device__ void cg_init_body(KspState *s, double *hist) {
   const double zz = s->red[0], zr = s->red[1], rr = s->red[2];
   double dp;
   switch (s->top.normtype) {
@@ -317,7 +383,8 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
                                                     const double *__restrict__ dv, const double dc,
                                                     double *__restrict__ p0, double *__restrict__ p1,
                                                     double *__restrict__ p2, double *__restrict__ p3,
-                                                    double *__restrict__ x, double *__restrict__ hist, const int unr) {
+                                                    double *__restrict__ x, double *__restrict__ hist, const int unr,
+                                                    const double *__restrict__ r0) {
   const CgTopIn top = s->top;
   if (top.done) return;
   const CgTop t = cg_top(top);
@@ -377,7 +444,10 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
   double *__restrict__ pout = pick(i % B);
   // unr bit 1 (knob 32): r and p_{i-1} read non-temporally, so the memory-side
   // cache keeps more of the p_i just written for the MatMult that reads it next
-  auto walk = [&](auto ntc) __attribute__((always_inline)) {
+  // (rs: r, or b at iteration 0 of a zero-guess solve -- r_0 = b is not
+  // copied into r at the start; iteration 0's update pass writes r_1.  Passed
+  // as an argument so the common call keeps r's own aliasing facts)
+  auto walk = [&](auto ntc, const double *__restrict__ rs) __attribute__((always_inline)) {
     constexpr bool NTL = decltype(ntc)::value;
     auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
       if constexpr (NTL) return __builtin_nontemporal_load(q);
@@ -389,17 +459,20 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           po[u] = ldv(pprev + k + u * stride);
-          rr[u] = ldv(r + k + u * stride);
+          rr[u] = ldv(rs + k + u * stride);
           dd[u] = JM == 1 ? dv[k + u * stride] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) pout[k + u * stride] = row(rr[u], dd[u], po[u]);
       }
     }
-    for (; k < n; k += stride) pout[k] = row(ldv(r + k), JM == 1 ? dv[k] : 0.0, ldv(pprev + k));
+    for (; k < n; k += stride) pout[k] = row(ldv(rs + k), JM == 1 ? dv[k] : 0.0, ldv(pprev + k));
   };
-  if (unr & 2) walk(std::true_type{});
-  else walk(std::false_type{});
+  if (r0 && i == 0) {
+    if (unr & 2) walk(std::true_type{}, r0);
+    else walk(std::false_type{}, r0);
+  } else if (unr & 2) walk(std::true_type{}, r);
+  else walk(std::false_type{}, r);
 }
 
 // dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
@@ -434,8 +507,14 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
                                                         const double *__restrict__ dv, const double dc,
                                                         double *__restrict__ partials, const Fold fold,
                                                         const int nts, const double *__restrict__ dot_part,
-                                                        const int ndot, const int unr, const int xb) {
-  if (s->top.done) return;
+                                                        const int ndot, const int unr, const int xb,
+                                                        const double *__restrict__ r0, int *__restrict__ hw) {
+  // the host's words (Poller): done, stored by every pass that finds the
+  // solve stopped and by the pass that stops it; else the iterations begun
+  if (s->top.done) {
+    if (hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(hw + HW_DONE, 1);
+    return;
+  }
   // p.w: folded and all-reduced before this launch, or (one rank) folded here
   // by every workgroup from the MatMult's partials, in fold_kernel's order
   const double pw = ndot > 0 ? block_sum_array<16>(dot_part, ndot) : s->red1;
@@ -449,7 +528,9 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
     if (xb > 1 && al.i % xb == 0) s->top.xlo = al.i;
     if (al.reason) {
       stop(s, al.reason);
+      if (hw) host_store(hw + HW_DONE, 1);
     } else {
+      if (hw) host_store(hw + HW_PROGRESS, al.i + 1);
       s->dpis[al.i & 1] = al.dpi;
       s->alpha = al.alpha;
       if (!XU) { s->top.xa = al.alpha; s->top.xpend = 1.0; s->xi = al.i; }
@@ -469,79 +550,83 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
     v[0] += zi * zi; v[1] += zi * ri; v[2] += ri * ri;
     return ri;
   };
-  if constexpr (!VEC) {          // row walk: one row per thread per step
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    // unr bit 1 (knob 32): w and r read non-temporally, so the memory-side
-    // cache keeps the r written here for the direction update that reads it
-    auto walk = [&](auto ntc) __attribute__((always_inline)) {
-      constexpr bool NTL = decltype(ntc)::value;
-      auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
-        if constexpr (NTL) return __builtin_nontemporal_load(q);
-        else return *q;
-      };
-      if (unr & 1) {             // knob 21: four steps' loads issued together, same sum order
-        for (; i + 3 * stride < n; i += 4 * stride) {
-          double pp[4], xx[4], ww[4], rr[4], dd[4];
+  // rin: r_i -- r, or b at iteration 0 of a zero-guess solve (see cg_pb_kernel)
+  auto body = [&](const double *__restrict__ rin) __attribute__((always_inline)) {
+    if constexpr (!VEC) {          // row walk: one row per thread per step
+      const int64_t stride = (int64_t)gridDim.x * 256;
+      int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+      // unr bit 1 (knob 32): w and r read non-temporally, so the memory-side
+      // cache keeps the r written here for the direction update that reads it
+      auto walk = [&](auto ntc) __attribute__((always_inline)) {
+        constexpr bool NTL = decltype(ntc)::value;
+        auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
+          if constexpr (NTL) return __builtin_nontemporal_load(q);
+          else return *q;
+        };
+        if (unr & 1) {             // knob 21: four steps' loads issued together, same sum order
+          for (; i + 3 * stride < n; i += 4 * stride) {
+            double pp[4], xx[4], ww[4], rr[4], dd[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            ww[u] = ldv(w + i + u * stride);
-            rr[u] = ldv(r + i + u * stride);
-            pp[u] = XU ? p[i + u * stride] : 0.0;
-            xx[u] = XU ? x[i + u * stride] : 0.0;
-            dd[u] = JM == 1 ? dv[i + u * stride] : 0.0;
-          }
+            for (int u = 0; u < 4; ++u) {
+              ww[u] = ldv(w + i + u * stride);
+              rr[u] = ldv(rin + i + u * stride);
+              pp[u] = XU ? p[i + u * stride] : 0.0;
+              xx[u] = XU ? x[i + u * stride] : 0.0;
+              dd[u] = JM == 1 ? dv[i + u * stride] : 0.0;
+            }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (XU) st1(x + i + u * stride, fma(a, pp[u], xx[u]), nts);
-            st1(r + i + u * stride, rnew(ww[u], rr[u], dd[u]), nts);
+            for (int u = 0; u < 4; ++u) {
+              if (XU) st1(x + i + u * stride, fma(a, pp[u], xx[u]), nts);
+              st1(r + i + u * stride, rnew(ww[u], rr[u], dd[u]), nts);
+            }
           }
         }
+        for (; i < n; i += stride) {
+          if (XU) st1(x + i, fma(a, p[i], x[i]), nts);
+          st1(r + i, rnew(ldv(w + i), ldv(rin + i), JM == 1 ? dv[i] : 0.0), nts);
+        }
+      };
+      if (unr & 2) walk(std::true_type{});
+      else walk(std::false_type{});
+      return;
+    }
+    const int64_t np = n >> 1, stride = (int64_t)gridDim.x * 256;
+    int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; k < np; k += 2 * stride) {
+      const int64_t k2 = k + stride;
+      const bool two = k2 < np;
+      const dbl2 w0 = ld2<VEC>(w, k);
+      const dbl2 r0v = ld2<VEC>(rin, k);
+      const dbl2 p0 = XU ? ld2<VEC>(p, k) : dbl2{0.0, 0.0};
+      const dbl2 x0 = XU ? ld2<VEC>(x, k) : dbl2{0.0, 0.0};
+      const dbl2 d0 = JM == 1 ? ld2<VEC>(dv, k) : dbl2{0.0, 0.0};
+      dbl2 w1 = {0.0, 0.0}, r1 = {0.0, 0.0}, p1 = {0.0, 0.0}, x1 = {0.0, 0.0}, d1 = {0.0, 0.0};
+      if (two) {
+        w1 = ld2<VEC>(w, k2); r1 = ld2<VEC>(rin, k2);
+        if (XU) { p1 = ld2<VEC>(p, k2); x1 = ld2<VEC>(x, k2); }
+        if (JM == 1) d1 = ld2<VEC>(dv, k2);
       }
-      for (; i < n; i += stride) {
-        if (XU) st1(x + i, fma(a, p[i], x[i]), nts);
-        st1(r + i, rnew(ldv(w + i), ldv(r + i), JM == 1 ? dv[i] : 0.0), nts);
+      if (XU) st2<VEC>(x, k, dbl2{fma(a, p0.x, x0.x), fma(a, p0.y, x0.y)});
+      {
+        const double ra = rnew(w0.x, r0v.x, d0.x);
+        const double rb = rnew(w0.y, r0v.y, d0.y);
+        st2<VEC>(r, k, dbl2{ra, rb});
       }
-    };
-    if (unr & 2) walk(std::true_type{});
-    else walk(std::false_type{});
-    block_partials<3>(v, partials, gridDim.x, fold);
-    return;
-  }
-  const int64_t np = n >> 1, stride = (int64_t)gridDim.x * 256;
-  int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; k < np; k += 2 * stride) {
-    const int64_t k2 = k + stride;
-    const bool two = k2 < np;
-    const dbl2 w0 = ld2<VEC>(w, k);
-    const dbl2 r0 = ld2<VEC>(r, k);
-    const dbl2 p0 = XU ? ld2<VEC>(p, k) : dbl2{0.0, 0.0};
-    const dbl2 x0 = XU ? ld2<VEC>(x, k) : dbl2{0.0, 0.0};
-    const dbl2 d0 = JM == 1 ? ld2<VEC>(dv, k) : dbl2{0.0, 0.0};
-    dbl2 w1 = {0.0, 0.0}, r1 = {0.0, 0.0}, p1 = {0.0, 0.0}, x1 = {0.0, 0.0}, d1 = {0.0, 0.0};
-    if (two) {
-      w1 = ld2<VEC>(w, k2); r1 = ld2<VEC>(r, k2);
-      if (XU) { p1 = ld2<VEC>(p, k2); x1 = ld2<VEC>(x, k2); }
-      if (JM == 1) d1 = ld2<VEC>(dv, k2);
+      if (two) {
+        if (XU) st2<VEC>(x, k2, dbl2{fma(a, p1.x, x1.x), fma(a, p1.y, x1.y)});
+        const double ra = rnew(w1.x, r1.x, d1.x);
+        const double rb = rnew(w1.y, r1.y, d1.y);
+        st2<VEC>(r, k2, dbl2{ra, rb});
+      }
     }
-    if (XU) st2<VEC>(x, k, dbl2{fma(a, p0.x, x0.x), fma(a, p0.y, x0.y)});
-    {
-      const double ra = rnew(w0.x, r0.x, d0.x);
-      const double rb = rnew(w0.y, r0.y, d0.y);
-      st2<VEC>(r, k, dbl2{ra, rb});
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {     // odd last row
+      const int64_t i = n - 1;
+      if (XU) x[i] = fma(a, p[i], x[i]);
+      r[i] = rnew(w[i], rin[i], JM == 1 ? dv[i] : 0.0);
     }
-    if (two) {
-      if (XU) st2<VEC>(x, k2, dbl2{fma(a, p1.x, x1.x), fma(a, p1.y, x1.y)});
-      const double ra = rnew(w1.x, r1.x, d1.x);
-      const double rb = rnew(w1.y, r1.y, d1.y);
-      st2<VEC>(r, k2, dbl2{ra, rb});
-    }
-  }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {     // odd last row
-    const int64_t i = n - 1;
-    if (XU) x[i] = fma(a, p[i], x[i]);
-    r[i] = rnew(w[i], r[i], JM == 1 ? dv[i] : 0.0);
-  }
+  };
+  if (r0 && al.i == 0) body(r0);
+  else body(r);
   block_partials<3>(v, partials, gridDim.x, fold);
 }
 
@@ -559,9 +644,18 @@ __global__ void __launch_bounds__(256) fold_kernel(const double *__restrict__ pa
 }
 
 // the scalar top after the last launched iteration (max_it reached without a stop)
-__global__ void cg_tail_kernel(KspState *s, double *hist) {
-  if (threadIdx.x != 0 || s->top.done) return;
-  cg_commit_top(s, cg_top(s->top), hist);
+__global__ void cg_tail_kernel(KspState *s, double *hist, int *hw) {
+  if (threadIdx.x != 0) return;
+  const long long t_end = wall_clock64();   // the solve's last kernel: its device time ends here
+  if (!s->top.done) cg_commit_top(s, cg_top(s->top), hist);
+  // the result, straight into the host's words
+  host_store(hw + HW_ITS, s->its);
+  host_store(hw + HW_REASON, s->reason);
+  const unsigned long long dp = __builtin_bit_cast(unsigned long long, s->dp);
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(hw + HW_DP), dp, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(reinterpret_cast<long long *>(hw + HW_TICKS), t_end - s->t_start, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the x step still pending when the solve stopped (fused CG)
@@ -851,41 +945,53 @@ __global__ void gm_cycle_end_kernel(KspState *s) {
 // ------------------------------------------------------------------ host drivers
 namespace {
 
+// wall_clock64() ticks per ms on this device (100 MHz on gfx9)
+static double wall_clock_khz(int dev) {
+  static int khz[64] = {};
+  const int d = dev >= 0 && dev < 64 ? dev : 0;
+  if (!khz[d] && (hipDeviceGetAttribute(&khz[d], hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz[d] <= 0))
+    khz[d] = 100000;
+  return (double)khz[d];
+}
+
 // the operator's pinned flag slots and events (Mat::poll_*), made once
 static void solve_resources(Mat *A) {
   if (A->poll_pinned) return;
-  HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&A->poll_pinned), 2 * sizeof(int), hipHostMallocDefault));
-  A->poll_pinned[0] = A->poll_pinned[1] = 0;
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&A->poll_pinned), HW_WORDS * sizeof(int),
+                         hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(A->poll_pinned, 0, HW_WORDS * sizeof(int));
   HIPCHECK(hipHostMalloc(&A->state_pinned, sizeof(KspState), hipHostMallocDefault));
   for (auto &e : A->poll_ev) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (auto &e : A->solve_ev) HIPCHECK(hipEventCreate(&e));
 }
 
+// Done-flag polling, one batch behind, without device-side markers: the
+// update pass stores the count of iterations begun and, once the solve has
+// stopped, a done flag into pinned host words (HW_*); after enqueuing batch k
+// the host spins until batch k-1's last iteration has begun (or done), so at
+// most about two batches are in flight and a stopped solve is seen one batch
+// late.  (An event record + device-to-host flag copy per batch left the GPU
+// idle ~14 us per batch.)
 struct Poller {
   hipStream_t st;
   Comm *c;
-  int *pinned;
-  hipEvent_t *ev;
-  int pending = 0;  // batches enqueued
+  int *hw;
+  int pending = 0;    // batches enqueued
+  int prev_end = 0;   // iteration count at the end of the previous batch
   Poller(Mat *A, hipStream_t s) : st(s), c(A->comm) {
     solve_resources(A);
-    pinned = A->poll_pinned;
-    ev = A->poll_ev;
-    pinned[0] = pinned[1] = 0;
+    hw = A->poll_pinned;
+    for (int k = 0; k < HW_WORDS; ++k) reinterpret_cast<volatile int *>(hw)[k] = 0;
   }
   ~Poller() { (void)hipStreamSynchronize(st); }
-  // enqueue the flag copy for this batch; return true if the PREVIOUS batch saw done
-  bool batch(const int *dev_done) {
-    const int slot = pending & 1;
-    HIPCHECK(hipMemcpyAsync(&pinned[slot], dev_done, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipEventRecord(ev[slot], st));
-    ++pending;
-    if (pending >= 2) {
-      const int prev = (pending - 2) & 1;
-      c->wait_event(ev[prev]);
-      if (pinned[prev]) return true;
-    }
-    return false;
+  int word(int k) const { return reinterpret_cast<const volatile int *>(hw)[k]; }
+  // the batch ending at iteration `end` is enqueued; true once done was seen
+  bool batch(int end) {
+    const int target = prev_end;
+    prev_end = end;
+    if (++pending < 2) return false;
+    c->wait_until([&] { return word(HW_DONE) != 0 || word(HW_PROGRESS) >= target; }, st);
+    return word(HW_DONE) != 0;
   }
 };
 
@@ -1019,11 +1125,11 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
 }
 
 static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r, const Jac &j, const PBufs &pb,
-                         int B, double *x, double *hist) {
+                         int B, double *x, double *hist, const double *r0) {
   const unsigned g = cg_vec_grid(n, false, 8192);
   const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 1) ? 2 : 0);
 #define CGPB(JM, BB) cg_pb_kernel<JM, BB><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], pb.b[3], \
-                                                           x, hist, unr)
+                                                           x, hist, unr, r0)
 #define CGPB_J(JM) do { if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
   switch (j.mode) { case 1: CGPB_J(1); break; case 2: CGPB_J(2); break; default: CGPB_J(0); }
 #undef CGPB_J
@@ -1034,7 +1140,7 @@ static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r
 // update pass; returns its grid (= partials per value)
 static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double *p, const double *w, double *x,
                             double *r, const Jac &j, double *partials, const Fold &fold_in,
-                            const double *dot_part, int ndot, int xb) {
+                            const double *dot_part, int ndot, int xb, const double *r0, int *hw) {
   const bool vec = g_knobs.cg_vec && aligned16({p, w, x, r, j.d});
   const unsigned g = g_knobs.cg_upd_grid > 0 ? grid_for(n, 256, g_knobs.cg_upd_grid)
                                              : cg_vec_grid(n, vec, vec ? CG_VEC_BLOCKS : RED_BLOCKS);
@@ -1043,7 +1149,8 @@ static int cg_update_launch(hipStream_t st, int64_t n, KspState *s, const double
   const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 2) ? 2 : 0);
   f.base = 0;
 #define CGU(JM, XU, V) cg_update_kernel<JM, XU, V><<<g, 256, 0, st>>>(n, s, p, w, x, r, j.d, j.c, partials, f, \
-                                                                        g_knobs.cg_nts, dot_part, ndot, unr, xb)
+                                                                        g_knobs.cg_nts, dot_part, ndot, unr, xb, r0, \
+                                                                        hw)
 #define CGU_J(JM) do { if (x) { if (vec) CGU(JM, true, true); else CGU(JM, true, false); } \
                        else { if (vec) CGU(JM, false, true); else CGU(JM, false, false); } } while (0)
   switch (j.mode) { case 1: CGU_J(1); break; case 2: CGU_J(2); break; default: CGU_J(0); }
@@ -1062,7 +1169,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   int normtype = p.norm_type == MX_NORM_DEFAULT ? MX_NORM_PRECONDITIONED : p.norm_type;
   const size_t nv = (size_t)std::max<int64_t>(n, 1);
   // MatMult partials (+ boundary launch), then the update pass's 3 per workgroup
-  const size_t npart = (size_t)std::max(spmv_blocks(A) + 64, RED_BLOCKS) * 6 + 3 * (size_t)CG_MAX_VEC_GRID + 128;
+  const size_t npart = (size_t)std::max({spmv_blocks(A) + 64, RED_BLOCKS, g_knobs.norm_grid}) * 6 +
+                       3 * (size_t)CG_MAX_VEC_GRID + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   // mode 2 batches B x steps (knob 29; 2 or 4 p buffers) when the batch of
   // launched iterations (poll) is a multiple of B; 1 = the x step every iteration
@@ -1077,12 +1185,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   double *pv4 = xb == 4 ? cv.take(nv) : pv2;
   const PBufs pbs{{pv.p, pv2, pv3, pv4}};
   struct { KspState *p; } sd{state_buf(A)};
-  KspState hs;
-  init_state(hs, p, normtype);
-  write_state(A, st, sd.p, hs);
-  Events ev(A);
+  const KspInit kin{p.rtol, p.atol, p.dtol, p.haptol, p.breakdowntol, p.max_it, normtype, !p.guess_nonzero, p.restart};
+  ksp_state_init_kernel<<<1, 256, 0, st>>>(sd.p, kin);
+  HIPCHECK(hipGetLastError());
   SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
-  HIPCHECK(hipEventRecord(ev.a, st));
 
   // r = b - A x  (or b)
   if (p.guess_nonzero) {
@@ -1092,22 +1198,35 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   KspState *s = sd.p;
   double *red = s->red;
   const int nv0 = p.guess_nonzero ? 6 : 3;
-  if (nv0 == 6) cg_norms_kernel<6><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p);
-  // x = 0 and r = b; with batched x steps x is not written here at all (the
-  // first batch, or the finish pass, is its first write)
-  else if (xb > 1) cg_norms_kernel<3, true, false><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p, r.p, nullptr);
-  else cg_norms_kernel<3, true><<<RED_BLOCKS, 256, 0, st>>>(n, r.p, b, dinv, part.p, r.p, x);
+  double *hist0 = hist_host ? hist.p : nullptr;
+  // one rank: the norms pass folds its partials and runs cg_init in-launch
+  // (knob 34: its grid; partials per value = the grid)
+  const int ngrid = g_knobs.norm_grid > 0 ? g_knobs.norm_grid : RED_BLOCKS;
+  Fold fin;
+  if (fused) { fin.cnt = s->fold_upd; fin.out = red; fin.ntotal = fin.ncount = ngrid; }
+#define CGN(...) cg_norms_kernel<__VA_ARGS__><<<ngrid, 256, 0, st>>>
+  if (nv0 == 6) CGN(6)(n, r.p, b, dinv, part.p, nullptr, nullptr, fin, s, hist0);
+  // x = 0 and r = b; with batched x steps neither is written here: iteration 0
+  // reads b as r_0 and the first batch (or the finish pass) writes x first
+  else if (xb > 1) CGN(3)(n, b, b, dinv, part.p, nullptr, nullptr, fin, s, hist0);
+  else CGN(3, true)(n, r.p, b, dinv, part.p, r.p, x, fin, s, hist0);
+#undef CGN
   HIPCHECK(hipGetLastError());
-  if (!fused) { finish_reduce(part.p, RED_BLOCKS, nv0, red, st); c->allreduce_sum(red, nv0); }
-  if (nv0 == 6) cg_init_kernel<6><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
-  else cg_init_kernel<3><<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, hist_host ? hist.p : nullptr);
-  HIPCHECK(hipGetLastError());
+  if (!fused) {
+    finish_reduce(part.p, ngrid, nv0, red, st);
+    c->allreduce_sum(red, nv0);
+    if (nv0 == 6) cg_init_kernel<6><<<1, 256, 0, st>>>(s, part.p, ngrid, 0, hist0);
+    else cg_init_kernel<3><<<1, 256, 0, st>>>(s, part.p, ngrid, 0, hist0);
+    HIPCHECK(hipGetLastError());
+  }
 
   Poller poller(A, st);
   int i = 0;
   const unsigned egrid = grid_for(n, 256, 8192);
   int *done = &s->top.done;
   double *hist_d = hist_host ? hist.p : nullptr;
+  // zero-guess batched solves read b as r_0 (nothing copies b into r)
+  const double *r0 = (xb > 1 && !p.guess_nonzero) ? b : nullptr;
   // fused: the direction update and the previous x step ride in the MatMult
   // (SPMV_CG); p ping-pongs between two buffers since neighbours read p_{i-1}
   // 1: direction update + x step inside the MatMult (SPMV_CG)
@@ -1146,7 +1265,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg, fdot_p);
       timer.end();
     } else if (xb > 1) {
-      cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d);
+      cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0);
       timer.begin();
       nb_spmv = matmult_overlap(A, pbs.b[it % xb], w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
@@ -1164,7 +1283,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     // the update's own partials go after the MatMult's when it folds those
     double *upart = fold_in_update ? part.p + ((nb_spmv + 63) / 64) * 64 : part.p;
     const int nb_upd = cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, upart, fupd,
-                                        fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb);
+                                        fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb,
+                                        xb > 1 ? r0 : nullptr, poller.hw);
     if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(upart, nb_upd, s->top.red3, done);
     if (!fused) c->allreduce_sum(s->top.red3, 3);
     HIPCHECK(hipGetLastError());
@@ -1180,12 +1300,12 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   if (graph) {
     // the whole knob block is part of the key: every knob a captured kernel
     // could have baked in (template choice, launch geometry, argument) counts
-    key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
+    key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)r0, (uintptr_t)poller.hw, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
            (uintptr_t)poll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p, (uintptr_t)w.p, (uintptr_t)pv2,
            (uintptr_t)part.p, (uintptr_t)xb, (uintptr_t)pv3, (uintptr_t)pv4};
     const int *kw = reinterpret_cast<const int *>(&g_knobs);
     for (size_t q = 0; q < sizeof(Knobs) / sizeof(int); ++q) key.push_back((uintptr_t)(uint32_t)kw[q]);
-    std::memcpy(&key[5], &dinv.c, sizeof(double));
+    std::memcpy(&key[7], &dinv.c, sizeof(double));
   }
   bool use_graph = graph && A->cg_graph && A->cg_key == key;
   // A capture records a batch of `poll` iterations without running them. A
@@ -1231,11 +1351,11 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     } else {
       for (int k = 0; k < poll && i < p.max_it; ++k, ++i) iteration(i);
     }
-    if (poller.batch(done)) break;
+    if (poller.batch(i)) break;
     if (graph && !use_graph && i < p.max_it) capture();
   }
-  cg_tail_kernel<<<1, 64, 0, st>>>(s, hist_d);   // max_it launched without a stop
-  HIPCHECK(hipGetLastError());
+  // the pending x steps (neither pass changes what the other reads), then
+  // the tail: max_it launched without a stop, the result into the host words
   if (xb > 1) {
     cg_finish_xb_kernel<<<egrid, 256, 0, st>>>(n, s, pbs, xb, x);
     HIPCHECK(hipGetLastError());
@@ -1243,17 +1363,20 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     cg_finish_x_kernel<<<egrid, 256, 0, st>>>(n, s, pv.p, fuse_cg ? pv2 : pv.p, x);
     HIPCHECK(hipGetLastError());
   }
-  HIPCHECK(hipEventRecord(ev.b, st));
-  read_state(A, st, s, hs);
-  float ms = 0.f;
-  HIPCHECK(hipEventElapsedTime(&ms, ev.a, ev.b));
-  res.its = hs.its;
-  res.reason = hs.reason;
-  res.rnorm = hs.dp;
-  res.solve_ms = ms;
+  cg_tail_kernel<<<1, 64, 0, st>>>(s, hist_d, poller.hw);
+  HIPCHECK(hipGetLastError());
+  c->wait_stream(st);
+  res.its = poller.word(HW_ITS);
+  res.reason = poller.word(HW_REASON);
+  std::memcpy(&res.rnorm, (const void *)(poller.hw + HW_DP), sizeof(double));
+  // device time: the state-init kernel to the tail kernel, on the device clock
+  long long ticks = 0;
+  std::memcpy(&ticks, (const void *)(poller.hw + HW_TICKS), sizeof(ticks));
+  res.solve_ms = (double)ticks / wall_clock_khz(c->device);
   res.launched_its = i;
   timer.collect(res.spmv_ms, res.spmv_count);
-  if (hist_host) HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)hs.its + 1), hipMemcpyDeviceToHost));
+  if (hist_host)
+    HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)res.its + 1), hipMemcpyDeviceToHost));
 }
 
 template <int NV>
