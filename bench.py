@@ -43,12 +43,15 @@ def spmv_format_bytes(info: dict, m: int, nnz: int, nghost: int) -> int:
     y written once, 16 B of slice metadata per 64 rows, A_o as 12 B/nnz;
     row-pair units whose code blocks come from the block dictionary stream a
     4-byte block index per 128 rows and the dictionary once instead of their
-    codes; without codes, SURVEY.md §8d's CSR bytes."""
+    codes (uniform-slot dictionaries: 256 B of slot values and lane masks per
+    block); without codes, SURVEY.md §8d's CSR bytes."""
     if not info.get("value_codes"):
         return spmv_bytes(m, nnz, nghost)
     codes = info["code_bytes"]
     if info.get("pair_blocks"):
-        codes += (4 - info["pair_block_bytes"]) * info["pair_units"] + info["pair_blocks"] * info["pair_block_bytes"]
+        # uniform-slot blocks are read as 256-byte slot-value/lane-mask records
+        blk = 256 if info.get("pair_uniform") else info["pair_block_bytes"]
+        codes += (4 - info["pair_block_bytes"]) * info["pair_units"] + info["pair_blocks"] * blk
     return (codes + 8 * (m + nghost) + 8 * m + 16 * ((m + 63) // 64)
             + 12 * info["nnz_o"] + 4 * (m + 1) * (info["nnz_o"] > 0))
 
@@ -341,7 +344,8 @@ def main():
                          "bytes_per_launch": bytes_launch, "avg_launch_ms": round(spmv_avg_ms, 5),
                          "format": ("value codes (" + str(info.get("value_codes")) + " distinct), " +
                                     ("row pairs" if info.get("pair_shape") else "one row per lane") +
-                                    (f", {info['pair_blocks']} distinct code blocks" if info.get("pair_blocks") else ""))
+                                    (f", {info['pair_blocks']} distinct code blocks" if info.get("pair_blocks") else "") +
+                                    (" (uniform slots: values + lane masks)" if info.get("pair_uniform") else ""))
                                    if info.get("value_codes") else "fp64 SELL-64",
                          # how much faster than a CSR SpMV (SURVEY §8d bytes) streaming at HBM peak
                          "csr_bytes_per_launch": bytes_csr,

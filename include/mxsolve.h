@@ -94,6 +94,9 @@ typedef struct {
   int64_t pair_blocks;                /* distinct unit code blocks streamed from the
                                          dictionary (0: one block per unit)           */
   int64_t pair_block_bytes;           /* bytes of one unit's code block               */
+  int64_t pair_uniform;               /* 1: every dictionary block is uniform per slot
+                                         (5/7-point): SpMV reads each block's slot values
+                                         and lane masks, not code bytes (key 35)       */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */
@@ -270,6 +273,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         it (or on an RCCL asynchronous error) the communicator is aborted
  *         and the call fails with MX_ERR_COMM (default 120000)
  * key 34: grid of the CG initial-norms pass (0 = default 1024 workgroups)
+ * key 35: row-pair SpMV reads uniform-slot dictionary blocks as slot values +
+ *         lane masks when the matrix has them (0/1, default 1)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

@@ -241,6 +241,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_units = info->pair_shape ? A->sd.pair_used : 0;
     info->pair_blocks = info->pair_shape ? A->sd.pair_blocks : 0;
     info->pair_block_bytes = info->pair_shape ? 64 * (int64_t)((2 * A->sd.dia_k + 15) / 16 * 16) : 0;
+    info->pair_uniform = info->pair_shape && info->pair_blocks > 0 && A->sd.puni.p ? 1 : 0;
   });
 }
 
@@ -512,6 +513,7 @@ int mx_debug_set(int key, int value) {
     case 32: old = g_knobs.cg_ntl; g_knobs.cg_ntl = value; break;
     case 33: old = g_knobs.comm_timeout_ms; if (value > 0) g_knobs.comm_timeout_ms = value; break;
     case 34: old = g_knobs.norm_grid; g_knobs.norm_grid = std::min(std::max(value, 0), 16384); break;
+    case 35: old = g_knobs.pair_uni; g_knobs.pair_uni = value; break;
     default: break;
   }
   return old;

@@ -1088,6 +1088,39 @@ static void dedupe_pair_blocks(Sell &S, hipStream_t st) {
   S.pair_blocks = nb;
 }
 
+// Uniform-slot form of the code-block dictionary (Sell::puni), 5/7-point
+// shapes: kept only when, in every block, each slot-row's present codes are
+// one code (constant-coefficient stencils: a few dozen boundary classes).
+static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream_t st) {
+  S.puni.reset();
+  const int K = S.dia_k;
+  if (S.pair_blocks <= 0 || (S.pair_shape != 5 && S.pair_shape != 7) || K != S.pair_shape || 2 * K > 16) return;
+  const int pb = pair_bytes(K);
+  const int64_t nb = S.pair_blocks;
+  std::vector<uint8_t> d((size_t)nb * 64 * pb);
+  HIPCHECK(hipMemcpyAsync(d.data(), S.pcode.p, d.size(), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  std::vector<PairUni> u((size_t)nb);
+  for (int64_t b = 0; b < nb; ++b) {
+    PairUni &B = u[(size_t)b];
+    for (int q = 0; q < 16; ++q) { B.v[q] = 0.0; B.pm[q] = 0ull; }
+    for (int q = 0; q < 2 * K; ++q) {
+      int code = -1;
+      for (int lane = 0; lane < 64; ++lane) {
+        const int c = d[((size_t)b * 64 + lane) * pb + q];
+        if (c == VCODE_ABSENT) continue;
+        if (code >= 0 && c != code) return;       // two values in one slot-row: not uniform
+        code = c;
+        B.pm[q] |= 1ull << lane;
+      }
+      if (code >= 0) B.v[q] = vt[(size_t)code];
+    }
+  }
+  S.puni.alloc((size_t)nb);
+  HIPCHECK(hipMemcpyAsync(S.puni.p, u.data(), sizeof(PairUni) * u.size(), hipMemcpyHostToDevice, st));
+  HIPCHECK(hipStreamSynchronize(st));
+}
+
 static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st) {
   S.ntab = 0;
   if (S.slots == 0 || !g_knobs.vcodes) return;
@@ -1150,6 +1183,7 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
       S.pair_used = (int64_t)hc;
     }
     dedupe_pair_blocks(S, st);
+    build_pair_uniform(S, vt, st);
     S.pair_ghosts = false;
     if (wid_o && S.nunits) {
       DBuf<int> any(1);

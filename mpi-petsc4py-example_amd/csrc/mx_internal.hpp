@@ -116,6 +116,13 @@ constexpr int DIA_MAX = 32;
 constexpr int32_t DPAT_INB = 1 << 30;
 constexpr int32_t DPAT_PAIR = 1 << 29;   // on slice 2u: unit u is stored as row pairs
 constexpr int32_t DPAT_ID = DPAT_PAIR - 1;
+// one uniform-slot dictionary block (Sell::puni): slot-row q = slot q of
+// row 0 (q < K) or slot q - K of row 1
+struct PairUni {
+  double v[16];                 // the slot-row's value
+  unsigned long long pm[16];    // lanes whose row stores it
+};
+
 struct Sell {
   int64_t nslices = 0, slots = 0, dia_slices = 0;
   int dia_k = 0;         // most common aligned-offset width (kernel specialisation)
@@ -151,6 +158,11 @@ struct Sell {
   int64_t pair_used = 0;   // units stored as row pairs
   bool pair_ghosts = false;  // some pair unit has A_o entries (SpMV then always splits)
   bool pair_all = false;     // every full unit is a pair unit
+  // uniform-slot dictionary (5/7-point row pairs): every present code of a
+  // block's slot-row is one value, so block b is puni[b] -- the 2K values and
+  // the 2K lane masks of present slots -- read by scalar loads (no code bytes,
+  // no LDS table lookups); empty when some block is not uniform
+  DBuf<PairUni> puni;
 };
 constexpr uint32_t PBLK_GHOST_LO = 1u << 30;
 constexpr uint32_t PBLK_GHOST_HI = 1u << 31;
@@ -168,7 +180,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
-                int comm_timeout_ms = 120000; int norm_grid = 0; };
+                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

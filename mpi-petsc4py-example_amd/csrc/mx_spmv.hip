@@ -409,7 +409,11 @@ __device__ __forceinline__ double wave_shift(double v, double edge) {
 // order, so the +-1 / +-n / +-n^2 re-reads of x stay in that XCD's 4 MB L2.
 // Placement only affects speed, never results.  KD > 0 specialises the
 // aligned-offset body for the matrix's dominant slice width.
-template <int MODE, bool NT, int KD, bool SPLIT, int JM = 0, bool VC = false, int PS = 0>
+// UNI (5/7-point row pairs with a uniform-slot dictionary, Sell::puni): a
+// unit's values and presence are its block's wave-uniform slot-row values and
+// lane masks (scalar loads; the mask is the select condition itself), not
+// code bytes looked up in the LDS table -- the same products and sums.
+template <int MODE, bool NT, int KD, bool SPLIT, int JM = 0, bool VC = false, int PS = 0, bool UNI = false>
 __global__ void __launch_bounds__(256) spmv_sell_kernel(
     int64_t m, int64_t ncols, int64_t nslices, const int64_t *__restrict__ sptr_d,
     const int32_t *__restrict__ wid_d, const int32_t *__restrict__ col_d,
@@ -421,8 +425,9 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
     const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
     const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star,
-    const int32_t *__restrict__ pblk, int pdict, int rev) {
+    const int32_t *__restrict__ pblk, int pdict, int rev, const PairUni *__restrict__ puni) {
   static_assert(PS == 0 || VC, "row pairs: coded values");
+  static_assert(!UNI || PS == 5 || PS == 7, "uniform-slot blocks: 5/7-point row pairs");
   CgTopIn top;
   if constexpr (MODE == SPMV_CG) top = cg.st->top;   // one batch of scalar loads, done included
   else if (done && *done) return;  // wave-uniform: solver finished, the launch is a no-op
@@ -561,7 +566,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     // (dictionary ids and/or ghost flags), 4 = every full unit is a pair unit
     const bool use_pblk = (pdict & 3) != 0;
     // one unit's loads: its code block, every x pair and the edge values
-    struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e[NR]; uint32_t fl; };
+    struct Unit { u32x4 cw[PB / 16]; dbl2 L[NR]; double e[NR]; uint32_t fl; int32_t bid; };
     auto unit_load = [&](int u, int32_t blkw, Unit &t) __attribute__((always_inline)) {
       const int ubase = u * 128, r0 = ubase + 2 * lane;
       const uint32_t bw = (uint32_t)blkw;
@@ -579,6 +584,8 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       // block shared with every unit of the same boundary/value class (cached:
       // the dictionary stays in L2)
       const int64_t blk = use_pblk ? (int64_t)(bw & PBLK_ID) : (int64_t)u;
+      t.bid = (int32_t)blk;
+      if constexpr (UNI) return;                  // values and presence: puni[blk] at the finish
       const u32x4 *__restrict__ cp = reinterpret_cast<const u32x4 *>(pcode + (blk * 64 + lane) * PB);
       if (pdict & 1) {                            // kernel-uniform
 #pragma unroll
@@ -608,10 +615,17 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
         else if (p < 0) { a0 = lo_m1; a1 = t.L[r].x; }
         else if (p == 0) { a0 = t.L[r].x; a1 = t.L[r].y; }
         else { a0 = t.L[r].y; a1 = hi_p1; }
-        const int c0 = code(j), c1 = code(K + j);
-        const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
-        sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
-        sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
+        if constexpr (UNI) {
+          const PairUni &B = puni[t.bid];        // wave-uniform: scalar loads
+          const double t0 = sum0 + B.v[j] * a0, t1 = sum1 + B.v[K + j] * a1;
+          sum0 = __builtin_amdgcn_inverse_ballot_w64(B.pm[j]) ? t0 : sum0;
+          sum1 = __builtin_amdgcn_inverse_ballot_w64(B.pm[K + j]) ? t1 : sum1;
+        } else {
+          const int c0 = code(j), c1 = code(K + j);
+          const double t0 = sum0 + vtab[c0] * a0, t1 = sum1 + vtab[c1] * a1;
+          sum0 = c0 != VCODE_ABSENT ? t0 : sum0;
+          sum1 = c1 != VCODE_ABSENT ? t1 : sum1;
+        }
       }
       // SPLIT: rows of a slice with A_o entries store the diagonal-block sum;
       // the boundary kernel continues it (and applies the epilogue)
@@ -868,7 +882,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
       partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt, \
-      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, pair_flags(A), g_knobs.spmv_rev
+      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, pair_flags(A), g_knobs.spmv_rev, A->sd.puni.p
   using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
   KFn kf = nullptr;
 #define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>
@@ -883,18 +897,24 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   } while (0)
 #define SPMV_CGKD(JM, SP)                                                                    \
   do {                                                                                       \
-    if (ps == 5) kf = &spmv_sell_kernel<SPMV_CG, true, 5, SP, JM, true, 5>;                  \
-    else if (ps == 7) kf = &spmv_sell_kernel<SPMV_CG, true, 7, SP, JM, true, 7>;             \
+    if (ps == 5) { if (uni) kf = &spmv_sell_kernel<SPMV_CG, true, 5, SP, JM, true, 5, true>;   \
+                   else kf = &spmv_sell_kernel<SPMV_CG, true, 5, SP, JM, true, 5>; }          \
+    else if (ps == 7) { if (uni) kf = &spmv_sell_kernel<SPMV_CG, true, 7, SP, JM, true, 7, true>; \
+                        else kf = &spmv_sell_kernel<SPMV_CG, true, 7, SP, JM, true, 7>; }     \
     else if (ps == 27) kf = &spmv_sell_kernel<SPMV_CG, true, 27, SP, JM, true, 27>;          \
     else if (vcode) SPMV_KD(SPMV_CG, true, SP, JM, true);                                    \
     else SPMV_KD(SPMV_CG, true, SP, JM, false);                                              \
   } while (0)
   // code blocks are always read non-temporally; row pairs when the matrix has them
   const int ps = vcode && g_knobs.spmv_pairs ? A->sd.pair_shape : 0;
+  // uniform-slot dictionary (knob 35 = 0: the LDS table path)
+  const bool uni = ps && A->sd.puni.p && g_knobs.pair_uni && (pair_flags(A) & 1);
 #define SPMV_PS(MODE, SP)                                                                         \
   do {                                                                                            \
-    if (ps == 5) kf = &spmv_sell_kernel<MODE, true, 5, SP, 0, true, 5>;                           \
-    else if (ps == 7) kf = &spmv_sell_kernel<MODE, true, 7, SP, 0, true, 7>;                      \
+    if (ps == 5) { if (uni) kf = &spmv_sell_kernel<MODE, true, 5, SP, 0, true, 5, true>;           \
+                   else kf = &spmv_sell_kernel<MODE, true, 5, SP, 0, true, 5>; }                  \
+    else if (ps == 7) { if (uni) kf = &spmv_sell_kernel<MODE, true, 7, SP, 0, true, 7, true>;      \
+                        else kf = &spmv_sell_kernel<MODE, true, 7, SP, 0, true, 7>; }             \
     else kf = &spmv_sell_kernel<MODE, true, 27, SP, 0, true, 27>;                                 \
   } while (0)
 #define SPMV_GO(MODE)                                                         \

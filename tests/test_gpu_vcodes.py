@@ -232,3 +232,49 @@ def test_pair_code_dictionary_cg(selfcomm):
     assert on[3] > 0 and off[3] == 0
     assert on[:2] == off[:2]
     assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
+
+
+@pytest.mark.parametrize("kind,n,shape,uni", [("poisson2d", 256, 5, 1), ("poisson3d", 64, 7, 1),
+                                              ("poisson3d", 32, 7, 1), ("convdiff3d", 64, 7, 0)])
+def test_pair_uniform_blocks(selfcomm, oracle_mod, kind, n, shape, uni):
+    """Uniform-slot dictionary blocks (knob 35 = 1, the default: each block's
+    slot values and lane masks read by scalar loads, no code bytes): MatMult
+    bit-exact against the oracle and against the LDS-table path (knob 35 = 0).
+    The convection-diffusion operator's face coefficients vary along x, so
+    its blocks are not uniform; nor is a dictionary whose slot-row holds two
+    values."""
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    L = lib()
+    info1, got1, exp = mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=17)
+    info0, got0, _ = _with_knob(L, 35, 0, lambda: mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=17))
+    assert info1["pair_shape"] == shape and info1["pair_blocks"] > 0 and info1["pair_uniform"] == uni
+    assert np.array_equal(got1, exp) and np.array_equal(got0, exp)
+    # two values in the diagonal slot-row of the interior units: not uniform
+    v2 = v.copy()
+    rows = np.repeat(np.arange(M), np.diff(ip))
+    diag = (c == rows) & (rows % 3 == 0)
+    v2[diag] *= 2.0
+    info2, got2, exp2 = mult_bits(selfcomm, oracle_mod, M, ip, c, v2, seed=17)
+    assert info2["pair_uniform"] == 0 and np.array_equal(got2, exp2)
+
+
+def test_pair_uniform_cg(selfcomm):
+    """CG (MatMult + p.w in one pass) on 3D 7-point 64^3 with the uniform-slot
+    blocks and with the LDS table: same iterations, same solution bits."""
+    from mxsolve.core import DMat, rhs_hash
+    L = lib()
+
+    def run():
+        A = DMat.stencil(selfcomm, "poisson3d", 64)
+        m = A.info()["m"]
+        b = selfcomm.empty(m)
+        rhs_hash(selfcomm, 0, b)
+        x = selfcomm.zeros(m)
+        r = A.solve(b, x, ksp="cg", pc="jacobi")
+        return r["its"], r["reason"], x.cpu().numpy().copy()
+
+    on = run()
+    off = _with_knob(L, 35, 0, run)
+    assert on[:2] == off[:2]
+    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))

@@ -5,7 +5,7 @@
 //               each XCD sweeping one contiguous eighth (the product's order)
 //   zmarch    : 2.5D: a workgroup owns a y-tile of lines and marches z,
 //               keeping planes in LDS (x read once from HBM per tile)
-// hipcc --offload-arch=gfx950 -O3 -o /tmp/stencil_probe tools/stencil_probe.hip
+// hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/stencil_probe tools/stencil_probe.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -135,7 +135,9 @@ __global__ void __launch_bounds__(256) pcodes_kernel(const double *__restrict__ 
 // pcodes with buffer loads (out-of-range reads return 0: no bounds logic) and
 // the dictionary block ids of the wave's next 64 steps in one vector load,
 // read per step by readlane (no dependent scalar load per unit)
-template <int U, bool DOT, int META = 1, bool BUF = true>
+// DREG: the dictionary's two blocks held in VGPRs (loaded once per wave),
+// the unit's block selected by its id -- no dependent code load per unit
+template <int U, bool DOT, int META = 1, bool BUF = true, bool DREG = false>
 __global__ void __launch_bounds__(256) pbuf_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
                                                    const uint8_t *__restrict__ dict, const int32_t *__restrict__ pblk,
                                                    const double *__restrict__ vtab_g, double *__restrict__ part) {
@@ -152,6 +154,11 @@ __global__ void __launch_bounds__(256) pbuf_kernel(const double *__restrict__ x,
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, (int)(M * 8), 0x00020000);
   double dot = 0.0;
   struct T { dbl2 zm, ym, c, yp, zp; double elo, ehi; u32x4 cw; };
+  u32x4 dreg0 = {0, 0, 0, 0}, dreg1 = {0, 0, 0, 0};
+  if (DREG) {
+    dreg0 = *reinterpret_cast<const u32x4 *>(dict + (int64_t)lane * 16);
+    dreg1 = *reinterpret_cast<const u32x4 *>(dict + (int64_t)(64 + lane) * 16);
+  }
   auto ldp = [&](int64_t i) -> dbl2 {
     if (!BUF) return xpair(x, i);
     return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(i * 8), 0, 0));
@@ -164,7 +171,8 @@ __global__ void __launch_bounds__(256) pbuf_kernel(const double *__restrict__ x,
     const int64_t ub = u * 128, r0 = ub + 2 * lane;
     t.zm = ldp(r0 - NN); t.ym = ldp(r0 - N); t.c = ldp(r0); t.yp = ldp(r0 + N); t.zp = ldp(r0 + NN);
     t.elo = lds(ub - 1); t.ehi = lds(ub + 128);
-    t.cw = *reinterpret_cast<const u32x4 *>(dict + ((int64_t)blk * 64 + lane) * 16);
+    if (DREG) t.cw = blk ? dreg1 : dreg0;
+    else t.cw = *reinterpret_cast<const u32x4 *>(dict + ((int64_t)blk * 64 + lane) * 16);
   };
   auto fin = [&](int64_t u, const T &t) {
     const int64_t r0 = u * 128 + 2 * lane;
@@ -516,6 +524,76 @@ __global__ void ref_kernel(const double *__restrict__ x, double *__restrict__ y)
   y[i] = s;
 }
 
+// Uniform-slot dictionary: every present code of a slot-row of a block is
+// the same value, so a block is 14 wave-uniform values and 14 lane masks
+// (SGPRs by scalar loads); presence is the mask itself as the exec/select
+// condition (inverse ballot) -- no code bytes, no LDS table, no compares
+struct BMeta { double v[16]; unsigned long long pm[16]; };
+template <int U, bool DOT>
+__global__ void __launch_bounds__(256) puni_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                   const BMeta *__restrict__ bm, const int32_t *__restrict__ pblk,
+                                                   double *__restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int64_t chunk = (nunits + 7) >> 3;
+  const int64_t s0 = xcd * chunk + (int64_t)j * 4 + wid, step = (int64_t)per * 4;
+  const int64_t send = min(nunits, (xcd + 1) * chunk);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, (int)(M * 8), 0x00020000);
+  double dot = 0.0;
+  struct T { dbl2 zm, ym, c, yp, zp; double elo, ehi; };
+  auto ldp = [&](int64_t i) -> dbl2 {
+    return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(i * 8), 0, 0));
+  };
+  auto lds = [&](int64_t i) -> double {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (int)(i * 8), 0, 0));
+  };
+  auto ld = [&](int64_t u, T &t) {
+    const int64_t ub = u * 128, r0 = ub + 2 * lane;
+    t.zm = ldp(r0 - NN); t.ym = ldp(r0 - N); t.c = ldp(r0); t.yp = ldp(r0 + N); t.zp = ldp(r0 + NN);
+    t.elo = lds(ub - 1); t.ehi = lds(ub + 128);
+  };
+  auto fin = [&](int64_t u, int blk, const T &t) {
+    const int64_t r0 = u * 128 + 2 * lane;
+    const BMeta &B = bm[blk];
+    const double lo = wave_shift<true>(t.c.y, t.elo), hi = wave_shift<false>(t.c.x, t.ehi);
+    const double a0[7] = {t.zm.x, t.ym.x, lo, t.c.x, t.c.y, t.yp.x, t.zp.x};
+    const double a1[7] = {t.zm.y, t.ym.y, t.c.x, t.c.y, hi, t.yp.y, t.zp.y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const double q0 = s0 + B.v[k] * a0[k], q1 = s1 + B.v[7 + k] * a1[k];
+      s0 = __builtin_amdgcn_inverse_ballot_w64(B.pm[k]) ? q0 : s0;
+      s1 = __builtin_amdgcn_inverse_ballot_w64(B.pm[7 + k]) ? q1 : s1;
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    if (DOT) { dot += t.c.x * s0; dot += t.c.y * s1; }
+  };
+  int64_t u = s0;
+  int kstep = 64;
+  int bv = 0;
+  for (; u + (U - 1) * step < send; u += U * step) {
+    if (kstep + U > 64) {
+      const int64_t uu = u + lane * step;
+      bv = uu < send ? pblk[uu] : 0;
+      kstep = 0;
+    }
+    T t[U];
+    int bk[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) { ld(u + k * step, t[k]); bk[k] = __builtin_amdgcn_readlane(bv, kstep + k); }
+    kstep += U;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) fin(u + k * step, bk[k], t[k]);
+  }
+  for (; u < send; u += step) { T t; ld(u, t); fin(u, pblk[u], t); }
+  if (DOT) {
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+    if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+  }
+}
+
 int main(int argc, char **argv) {
   double *x, *y, *yr, *flush;
   CK(hipMalloc(&x, M * 8)); CK(hipMalloc(&y, M * 8)); CK(hipMalloc(&yr, M * 8)); CK(hipMalloc(&flush, 512ull << 20));
@@ -601,6 +679,18 @@ int main(int argc, char **argv) {
       }
       hd2[b * 64 + l] = w;
     }
+  // uniform-slot metadata of the same two blocks
+  std::vector<BMeta> hbm(2);
+  for (int bb = 0; bb < 2; ++bb)
+    for (int q = 0; q < 16; ++q) {
+      hbm[bb].v[q] = 0.0; hbm[bb].pm[q] = 0;
+      for (int l = 0; l < 64; ++l) {
+        const uint8_t c = hd[(bb * 64 + l) * 16 + q];
+        if (c != ABSENT) { hbm[bb].v[q] = hv[c]; hbm[bb].pm[q] |= 1ull << l; }
+      }
+    }
+  BMeta *dbm;
+  CK(hipMalloc(&dbm, 2 * sizeof(BMeta))); CK(hipMemcpy(dbm, hbm.data(), 2 * sizeof(BMeta), hipMemcpyHostToDevice));
   uint32_t *dict2;
   CK(hipMalloc(&dict2, hd2.size() * 4)); CK(hipMemcpy(dict2, hd2.data(), hd2.size() * 4, hipMemcpyHostToDevice));
   for (int wpc : {2, 3, 4, 5}) {
@@ -624,6 +714,18 @@ int main(int argc, char **argv) {
     timeit(nm, [&] { pbuf_kernel<2, true, 1, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "buf+nometa+dot %d/CU", wpc);
     timeit(nm, [&] { pbuf_kernel<2, true, 0, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "puni<1>+dot %d/CU", wpc);
+    timeit(nm, [&] { puni_kernel<1, true><<<g, 256>>>(x, y, M / 128, dbm, pblk, part); }, false);
+    snprintf(nm, sizeof nm, "puni<2>+dot %d/CU", wpc);
+    timeit(nm, [&] { puni_kernel<2, true><<<g, 256>>>(x, y, M / 128, dbm, pblk, part); }, false);
+    snprintf(nm, sizeof nm, "dreg+batchmeta+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<2, true, 1, true, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "dreg<1>+batchmeta+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<1, true, 1, true, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "dreg<3>+batchmeta+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<3, true, 1, true, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+    snprintf(nm, sizeof nm, "buf+batchmeta+dot %d/CU", wpc);
+    timeit(nm, [&] { pbuf_kernel<2, true, 1, true, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "glob+nometa+dot %d/CU", wpc);
     timeit(nm, [&] { pbuf_kernel<2, true, 0, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     for (int U2 : {1, 2, 4}) {
