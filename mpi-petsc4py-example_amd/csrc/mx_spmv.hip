@@ -318,22 +318,31 @@ __device__ __forceinline__ double dia_slice_any(const VS &vs, const int32_t *__r
   return sum;
 }
 
-// general SELL slice (paired layout), continuing `sum`: batches of 8 entries
+// general SELL slice (paired layout), continuing `sum`: batches of 8 entries;
+// the unpaired last entry of an odd width rides in the batch that holds pair
+// np (a 7-wide slice -- a diagonal plus six off-diagonal entries -- is one
+// batch: all column, value and x loads in flight together, instead of a
+// dependent second round trip for the last entry)
 template <bool NT, class VS, class XS>
 __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, const VS &vs,
                                              int w, double sum, const XS &x, int lane) {
   const int np = w >> 1;
+  const bool odd = (w & 1) != 0;
+  const int nb = np + (odd ? 1 : 0);          // pairs, the tail counted as one
   const int2v *__restrict__ cp = reinterpret_cast<const int2v *>(cbase) + lane;
-  for (int p0 = 0; p0 < np; p0 += 4) {
+  for (int p0 = 0; p0 < nb; p0 += 4) {
     int c[8];
     double v[8], xv[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int p = p0 + q;
-      const int2v cc = p < np ? ld<NT>(cp + (int64_t)p * SLICE) : int2v{-1, -1};
+      int2v cc = int2v{-1, -1};
+      if (p < np) cc = ld<NT>(cp + (int64_t)p * SLICE);
+      else if (odd && p == np) cc.x = ld<NT>(cbase + (int64_t)np * 2 * SLICE + lane);
       c[2 * q] = cc.x; c[2 * q + 1] = cc.y;
     }
     vs.eight(p0, np, lane, v);
+    if (odd && np >= p0 && np < p0 + 4) v[2 * (np - p0)] = vs.last(np, lane);
 #pragma unroll
     for (int q = 0; q < 8; ++q) xv[q] = x(c[q] >= 0 ? c[q] : 0);
 #pragma unroll
@@ -341,14 +350,6 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
       const double t = sum + v[q] * xv[q];
       sum = c[q] >= 0 ? t : sum;
     }
-  }
-  if (w & 1) {
-    const int64_t t = (int64_t)np * 2 * SLICE + lane;
-    const int c = ld<NT>(cbase + t);
-    const double v = vs.last(np, lane);
-    const double xv = x(c >= 0 ? c : 0);
-    const double tt = sum + v * xv;
-    sum = c >= 0 ? tt : sum;
   }
   return sum;
 }

@@ -32,6 +32,8 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-petsc4py-example_amd"))
 import torch  # noqa: E402
 
 from mxsolve.core import DeviceComm, DMat, rhs_hash  # noqa: E402
+sys.path.insert(0, ROOT)
+from bench import spmv_format_bytes  # noqa: E402
 
 PEAK = 8000.0
 
@@ -90,15 +92,29 @@ def random_csr(N: int, k: int = 6, seed: int = 11):
 
 
 def streamed_bytes(info) -> int:
-    """Bytes the SpMV streams for this layout: A_d slots (aligned-offset slices:
-    8 B value + the row's mask byte; general slices 12 B per slot incl.
-    padding), x read once, y written once, 16 B of slice metadata per slice."""
+    """Bytes the SpMV streams for this layout: value-coded layouts as bench.py
+    counts them (codes or dictionary block ids, x once, y once, slice
+    metadata); fp64 layouts: A_d slots (aligned-offset slices: 8 B value + the
+    row's mask byte; general slices 12 B per slot incl. padding), x read once,
+    y written once, 16 B of slice metadata per slice."""
     m, slots = info["m"], info["sell_slots_d"]
+    if info.get("value_codes"):
+        return spmv_format_bytes(info, m, info["nnz_d"] + info["nnz_o"], info["nghost"])
     if info["dia_slices"] * 64 >= m:          # every slice aligned-offset
         mat = 8 * slots + m
     else:
         mat = 12 * slots
     return mat + 16 * m + 16 * ((m + 63) // 64)
+
+
+def gather_bytes(info) -> int:
+    """Column-index layouts: each x gather of a random column fetches a whole
+    64-byte sector from memory (measured: FETCH_SIZE of the random leg is
+    ~64 B per off-diagonal entry, tools/random_spmv.py under rocprofv3), so
+    the memory traffic is the slot stream + y + the own-row x (coalesced) +
+    64 B per off-diagonal nonzero."""
+    m = info["m"]
+    return 12 * info["sell_slots_d"] + 16 * m + 16 * ((m + 63) // 64) + 64 * (info["nnz_d"] - m)
 
 
 def leg(comm, name, A, ksp, rtol=1e-5, max_it=10000, asm_s=None):
@@ -131,6 +147,10 @@ def leg(comm, name, A, ksp, rtol=1e-5, max_it=10000, asm_s=None):
                         "frac": round(sb / spmv_ms / 1e6 / PEAK, 4),
                         "csr_bytes": csr, "csr_achieved": round(csr / spmv_ms / 1e6, 1),
                         "csr_frac": round(csr / spmv_ms / 1e6 / PEAK, 4)}}
+    if not info["dia_slices"]:                 # column-index SELL: the gather-aware traffic model
+        gb = gather_bytes(info)
+        rec["roofline"].update({"gather_model_bytes": gb, "gather_model_achieved": round(gb / spmv_ms / 1e6, 1),
+                                "gather_model_frac": round(gb / spmv_ms / 1e6 / PEAK, 4)})
     print(json.dumps(rec), flush=True)
     del b, x, y
     return rec
