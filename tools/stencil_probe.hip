@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
@@ -524,12 +525,33 @@ __global__ void ref_kernel(const double *__restrict__ x, double *__restrict__ y)
   y[i] = s;
 }
 
+// CG-like vector passes around the MatMult (state experiments): the direction
+// update p = c r + b pp (r, pp read non-temporally) and the residual update
+// r = r - a w (w, r read non-temporally); NTS: non-temporal stores
+template <bool NTS>
+__global__ void pb_like(const double *__restrict__ r, const double *__restrict__ pp, double *__restrict__ p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = 0.25 * __builtin_nontemporal_load(r + i) + 0.5 * __builtin_nontemporal_load(pp + i);
+    if (NTS) __builtin_nontemporal_store(v, p + i); else p[i] = v;
+  }
+}
+template <bool NTS>
+__global__ void upd_like(const double *__restrict__ w, double *__restrict__ r, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = __builtin_nontemporal_load(r + i) - 1e-3 * __builtin_nontemporal_load(w + i);
+    if (NTS) __builtin_nontemporal_store(v, r + i); else r[i] = v;
+  }
+}
+
 // Uniform-slot dictionary: every present code of a slot-row of a block is
 // the same value, so a block is 14 wave-uniform values and 14 lane masks
 // (SGPRs by scalar loads); presence is the mask itself as the exec/select
 // condition (inverse ballot) -- no code bytes, no LDS table, no compares
 struct BMeta { double v[16]; unsigned long long pm[16]; };
-template <int U, bool DOT>
+// OPT bit 1: a slot-row whose mask is all lanes skips the select (uniform
+// branch); bit 2: a slot-row valued exactly -1 or +1 adds/subtracts the
+// operand (fl(-1 * a) = -a exactly, so the sum has the same bits)
+template <int U, bool DOT, int OPT = 0>
 __global__ void __launch_bounds__(256) puni_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
                                                    const BMeta *__restrict__ bm, const int32_t *__restrict__ pblk,
                                                    double *__restrict__ part) {
@@ -562,9 +584,16 @@ __global__ void __launch_bounds__(256) puni_kernel(const double *__restrict__ x,
     double s0 = 0.0, s1 = 0.0;
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      const double q0 = s0 + B.v[k] * a0[k], q1 = s1 + B.v[7 + k] * a1[k];
-      s0 = __builtin_amdgcn_inverse_ballot_w64(B.pm[k]) ? q0 : s0;
-      s1 = __builtin_amdgcn_inverse_ballot_w64(B.pm[7 + k]) ? q1 : s1;
+      auto term = [&](double s, double v, double a, unsigned long long pm) {
+        double q;
+        if ((OPT & 2) && v == -1.0) q = s - a;
+        else if ((OPT & 2) && v == 1.0) q = s + a;
+        else q = s + v * a;
+        if ((OPT & 1) && pm == ~0ull) return q;
+        return __builtin_amdgcn_inverse_ballot_w64(pm) ? q : s;
+      };
+      s0 = term(s0, B.v[k], a0[k], B.pm[k]);
+      s1 = term(s1, B.v[7 + k], a1[k], B.pm[7 + k]);
     }
     *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
     if (DOT) { dot += t.c.x * s0; dot += t.c.y * s1; }
@@ -718,6 +747,12 @@ int main(int argc, char **argv) {
     timeit(nm, [&] { puni_kernel<1, true><<<g, 256>>>(x, y, M / 128, dbm, pblk, part); }, false);
     snprintf(nm, sizeof nm, "puni<2>+dot %d/CU", wpc);
     timeit(nm, [&] { puni_kernel<2, true><<<g, 256>>>(x, y, M / 128, dbm, pblk, part); }, false);
+    snprintf(nm, sizeof nm, "puni<2>+dot opt1 %d/CU", wpc);
+    timeit(nm, [&] { puni_kernel<2, true, 1><<<g, 256>>>(x, y, M / 128, dbm, pblk, part); }, false);
+    snprintf(nm, sizeof nm, "puni<2>+dot opt2 %d/CU", wpc);
+    timeit(nm, [&] { puni_kernel<2, true, 2><<<g, 256>>>(x, y, M / 128, dbm, pblk, part); }, false);
+    snprintf(nm, sizeof nm, "puni<2>+dot opt3 %d/CU", wpc);
+    timeit(nm, [&] { puni_kernel<2, true, 3><<<g, 256>>>(x, y, M / 128, dbm, pblk, part); }, false);
     snprintf(nm, sizeof nm, "dreg+batchmeta+dot %d/CU", wpc);
     timeit(nm, [&] { pbuf_kernel<2, true, 1, true, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "dreg<1>+batchmeta+dot %d/CU", wpc);
@@ -753,6 +788,54 @@ int main(int argc, char **argv) {
     timeit(nm, [&] { pbuf_kernel<2, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pcodes<2>+meta+dot %d/CU", wpc);
     timeit(nm, [&] { pcodes_kernel<2, true, true><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
+  }
+  // operand state: the same SpMV (uniform-slot, 4/CU) timed alone by events
+  // around each launch, when (a) x was the previous launch's operand too, (b)
+  // launches alternate between two operands, (c) a copy kernel has just
+  // written x (as CG's direction update writes p_i before the MatMult)
+  {
+    double *x2, *x3;
+    CK(hipMalloc(&x2, M * 8)); CK(hipMalloc(&x3, M * 8));
+    CK(hipMemcpy(x2, x, M * 8, hipMemcpyDeviceToDevice)); CK(hipMemcpy(x3, x, M * 8, hipMemcpyDeviceToDevice));
+    const int g = cus * 4 - 8;
+    auto spmv = [&](const double *xx) { puni_kernel<2, true><<<g, 256>>>(xx, y, M / 128, dbm, pblk, part); };
+    auto ev_time = [&](const char *name, auto before, auto op) {
+      if (!only.empty() && only.find(std::string(";") + name + ";") == std::string::npos) return;
+      std::vector<float> t;
+      for (int k = 0; k < 40; ++k) {
+        before(k);
+        CK(hipEventRecord(a)); op(k); CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+        float ms; CK(hipEventElapsedTime(&ms, a, b)); if (k >= 4) t.push_back(ms * 1e3f);
+      }
+      std::sort(t.begin(), t.end());
+      printf("%-28s median %7.1f us  min %7.1f us\n", name, t[t.size() / 2], t[0]);
+    };
+    ev_time("state same-x", [&](int) {}, [&](int) { spmv(x); });
+    ev_time("state alternate-x", [&](int) {}, [&](int k) { spmv((k & 1) ? x2 : x); });
+    ev_time("state x-just-copied", [&](int) { copy_kernel<<<8192, 256>>>((const dbl2 *)x3, (dbl2 *)x2, M / 2); },
+            [&](int) { spmv(x2); });
+    ev_time("state x-just-copied-nt", [&](int) { copy_kernel<<<8192, 256>>>((const dbl2 *)x3, (dbl2 *)x2, M / 2); CK(hipDeviceSynchronize()); },
+            [&](int) { spmv(x2); });
+    // the CG iteration's order: pb (r, p_{i-1} -> p_i), MatMult (p_i -> w), update (w, r -> r)
+    {
+      double *pv[2] = {x2, x3}, *rr, *ww;
+      CK(hipMalloc(&rr, M * 8)); CK(hipMalloc(&ww, M * 8));
+      CK(hipMemcpy(rr, x, M * 8, hipMemcpyDeviceToDevice));
+      auto cg_like = [&](const char *name, bool pnts, bool rnts) {
+        ev_time(name, [&](int k) {
+                  if (k) { if (rnts) upd_like<true><<<1024, 256>>>(ww, rr, M); else upd_like<false><<<1024, 256>>>(ww, rr, M); }
+                  if (pnts) pb_like<true><<<8192, 256>>>(rr, pv[(k + 1) & 1], pv[k & 1], M);
+                  else pb_like<false><<<8192, 256>>>(rr, pv[(k + 1) & 1], pv[k & 1], M);
+                },
+                [&](int k) { puni_kernel<2, true><<<g, 256>>>(pv[k & 1], ww, M / 128, dbm, pblk, part); });
+      };
+      cg_like("state cg-like", false, false);
+      cg_like("state cg-like p-nts", true, false);
+      cg_like("state cg-like r-nts", false, true);
+      cg_like("state cg-like both-nts", true, true);
+    }
+    ev_time("state copy-other", [&](int) { copy_kernel<<<8192, 256>>>((const dbl2 *)x3, (dbl2 *)yr, M / 2); },
+            [&](int) { spmv(x); });
   }
   timeit("zmarch TY4 ZR16", [&] { zmarch_kernel<4, 16><<<(N / 4) * (N / 16), 256>>>(x, y); }, true);
   timeit("zmarch TY4 ZR32", [&] { zmarch_kernel<4, 32><<<(N / 4) * (N / 32), 256>>>(x, y); }, true);
