@@ -180,7 +180,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
-                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; };
+                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; };
 extern Knobs g_knobs;
 
 struct Halo {

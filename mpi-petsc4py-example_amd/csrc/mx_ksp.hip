@@ -1379,24 +1379,30 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)res.its + 1), hipMemcpyDeviceToHost));
 }
 
+// Grid of every MDot launch of a solve (one partial row stride for the
+// finish): knob 36, default RED_BLOCKS.  mdot_kernel<32> holds 139 VGPRs (3
+// waves per SIMD, 768 resident workgroups), yet its resident grid measured
+// 1.1% slower per GMRES(30) step than 1024 and 512 0.8% (tools/gmres_ab.py)
+static int mdot_grid() { return g_knobs.mdot_grid > 0 ? g_knobs.mdot_grid : RED_BLOCKS; }
+
 template <int NV>
 static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int j0, int k,
-                        const double *vscale, double *partials, const int *stop_flag) {
-  mdot_kernel<NV><<<RED_BLOCKS, 256, 0, st>>>(n, w, V, ldv, j0, k, vscale, partials, stop_flag);
+                        const double *vscale, double *partials, const int *stop_flag, int grid) {
+  mdot_kernel<NV><<<grid, 256, 0, st>>>(n, w, V, ldv, j0, k, vscale, partials, stop_flag);
 }
 
 // partials rows [j0, j0 + NV) are written (rows >= nv with zeros): the
 // buffer holds max_k + 2 rows rounded up to 32; groups are gw wide (knob 16)
 static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
-                 const double *vscale, double *partials, const int *stop_flag) {
+                 const double *vscale, double *partials, const int *stop_flag, int grid) {
   const int gw = g_knobs.mdot_group == 16 || g_knobs.mdot_group == 32 || g_knobs.mdot_group == 4 ? g_knobs.mdot_group : 8;
   for (int j0 = 0; j0 < nv; j0 += gw) {
     const int k = std::min(gw, nv - j0);
-    if (k <= 2) launch_mdot<2>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
-    else if (k <= 4) launch_mdot<4>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
-    else if (k <= 8) launch_mdot<8>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
-    else if (k <= 16) launch_mdot<16>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
-    else launch_mdot<32>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag);
+    if (k <= 2) launch_mdot<2>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
+    else if (k <= 4) launch_mdot<4>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
+    else if (k <= 8) launch_mdot<8>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
+    else if (k <= 16) launch_mdot<16>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
+    else launch_mdot<32>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
     HIPCHECK(hipGetLastError());
   }
 }
@@ -1421,6 +1427,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   const size_t nV = (size_t)ldv * (max_k + 1), nh = (size_t)ld * (max_k + 1);
   const size_t prow = std::max<size_t>((size_t)max_k + 2, ((size_t)max_k + 1 + 31) / 32 * 32);   // MDot groups of 32
   const size_t npart = (size_t)RED_BLOCKS * prow + (size_t)spmv_blocks(A) + 128;
+  const int mgrid = mdot_grid();   // <= RED_BLOCKS
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   const size_t k1 = (size_t)max_k + 1, k2 = (size_t)max_k + 2;
   Carve cv(workspace(A, carve_size({nV, (size_t)ldv, nh, k2, k1, k1, k2, k2, npart, nhist})));
@@ -1480,8 +1487,8 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       matmult_overlap(A, vk, vk1, dinv.mode ? SPMV_JACOBI_S : SPMV_PLAIN_S, dinv, nullptr, istop, nullptr,
                       nullptr, vsc.p + k);
       timer.end();
-      mdot(st, n, vk1, V.p, ldv, k + 1, vsc.p, part.p, istop);
-      finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, RED_BLOCKS, red.p, istop);
+      mdot(st, n, vk1, V.p, ldv, k + 1, vsc.p, part.p, istop, mgrid);
+      finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, mgrid, red.p, istop);
       c->allreduce_sum(red.p, k + 1);
       // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
       maxpy_norm_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
