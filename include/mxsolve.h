@@ -272,7 +272,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 33: deadline in ms of a host wait on an RCCL communicator's work; past
  *         it (or on an RCCL asynchronous error) the communicator is aborted
  *         and the call fails with MX_ERR_COMM (default 120000)
- * key 34: grid of the CG initial-norms pass (0 = default 1024 workgroups)
+ * key 34: grid of the CG initial-norms pass (0 = default: the direction update's grid,
+ *         whose fused iteration-0 norms it must match bit for bit)
  * key 35: row-pair SpMV reads uniform-slot dictionary blocks as slot values +
  *         lane masks when the matrix has them (0/1, default 1)
  * key 36: grid of the GMRES MDot pass (0 = default 1024 workgroups)

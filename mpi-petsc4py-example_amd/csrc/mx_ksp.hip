@@ -384,7 +384,8 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
                                                     double *__restrict__ p0, double *__restrict__ p1,
                                                     double *__restrict__ p2, double *__restrict__ p3,
                                                     double *__restrict__ x, double *__restrict__ hist, const int unr,
-                                                    const double *__restrict__ r0) {
+                                                    const double *__restrict__ r0, double *__restrict__ npart,
+                                                    const Fold fin) {
   const CgTopIn top = s->top;
   if (top.done) return;
   const CgTop t = cg_top(top);
@@ -447,11 +448,23 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
   // (rs: r, or b at iteration 0 of a zero-guess solve -- r_0 = b is not
   // copied into r at the start; iteration 0's update pass writes r_1.  Passed
   // as an argument so the common call keeps r's own aliasing facts)
-  auto walk = [&](auto ntc, const double *__restrict__ rs) __attribute__((always_inline)) {
+  // NRM (iteration 0 of a zero-guess solve on one rank, fin.cnt set): the
+  // initial norms [z.z, z.r, r.r] of r_0 = b ride in this pass -- the same
+  // rows per thread in the same order as cg_norms_kernel on this grid, so the
+  // same bits -- folded in-launch, the last workgroup running cg_init
+  double nv[3] = {0.0, 0.0, 0.0};
+  auto walk = [&](auto ntc, const double *__restrict__ rs, auto nrmc) __attribute__((always_inline)) {
     constexpr bool NTL = decltype(ntc)::value;
+    constexpr bool NRM = decltype(nrmc)::value;
     auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
       if constexpr (NTL) return __builtin_nontemporal_load(q);
       else return *q;
+    };
+    auto norms = [&](double rr, double dd) __attribute__((always_inline)) {
+      if constexpr (NRM) {
+        const double z = jac1<JM>(rr, dd, dc);
+        nv[0] += z * z; nv[1] += z * rr; nv[2] += rr * rr;
+      }
     };
     if (unr & 1) {                               // four steps' loads issued together
       for (; k + 3 * stride < n; k += 4 * stride) {
@@ -463,16 +476,27 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
           dd[u] = JM == 1 ? dv[k + u * stride] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) pout[k + u * stride] = row(rr[u], dd[u], po[u]);
+        for (int u = 0; u < 4; ++u) {
+          pout[k + u * stride] = row(rr[u], dd[u], po[u]);
+          norms(rr[u], dd[u]);
+        }
       }
     }
-    for (; k < n; k += stride) pout[k] = row(ldv(rs + k), JM == 1 ? dv[k] : 0.0, ldv(pprev + k));
+    for (; k < n; k += stride) {
+      const double rr = ldv(rs + k), dd = JM == 1 ? dv[k] : 0.0;
+      pout[k] = row(rr, dd, ldv(pprev + k));
+      norms(rr, dd);
+    }
   };
   if (r0 && i == 0) {
-    if (unr & 2) walk(std::true_type{}, r0);
-    else walk(std::false_type{}, r0);
-  } else if (unr & 2) walk(std::true_type{}, r);
-  else walk(std::false_type{}, r);
+    if (fin.cnt) {
+      if (unr & 2) walk(std::true_type{}, r0, std::true_type{});
+      else walk(std::false_type{}, r0, std::true_type{});
+      if (block_fold<3>(nv, npart, fin) && threadIdx.x == 0) cg_init_body<3>(s, hist);
+    } else if (unr & 2) walk(std::true_type{}, r0, std::false_type{});
+    else walk(std::false_type{}, r0, std::false_type{});
+  } else if (unr & 2) walk(std::true_type{}, r, std::false_type{});
+  else walk(std::false_type{}, r, std::false_type{});
 }
 
 // dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
@@ -1124,12 +1148,18 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
   HIPCHECK(hipGetLastError());
 }
 
+// the direction-update grid (row walk); the zero-guess norms pass runs on
+// the same grid so that its partial sums equal the fused iteration-0 ones
+static unsigned cg_pb_grid(int64_t n) { return cg_vec_grid(n, false, 8192); }
+
 static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r, const Jac &j, const PBufs &pb,
-                         int B, double *x, double *hist, const double *r0) {
-  const unsigned g = cg_vec_grid(n, false, 8192);
+                         int B, double *x, double *hist, const double *r0, double *npart, const Fold &fin_in) {
+  const unsigned g = cg_pb_grid(n);
+  Fold fin = fin_in;
+  fin.ntotal = fin.ncount = (int)g;
   const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 1) ? 2 : 0);
 #define CGPB(JM, BB) cg_pb_kernel<JM, BB><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], pb.b[3], \
-                                                           x, hist, unr, r0)
+                                                           x, hist, unr, r0, npart, fin)
 #define CGPB_J(JM) do { if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
   switch (j.mode) { case 1: CGPB_J(1); break; case 2: CGPB_J(2); break; default: CGPB_J(0); }
 #undef CGPB_J
@@ -1169,7 +1199,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   int normtype = p.norm_type == MX_NORM_DEFAULT ? MX_NORM_PRECONDITIONED : p.norm_type;
   const size_t nv = (size_t)std::max<int64_t>(n, 1);
   // MatMult partials (+ boundary launch), then the update pass's 3 per workgroup
-  const size_t npart = (size_t)std::max({spmv_blocks(A) + 64, RED_BLOCKS, g_knobs.norm_grid}) * 6 +
+  const size_t npart = (size_t)std::max({spmv_blocks(A) + 64, RED_BLOCKS, g_knobs.norm_grid, (int)cg_pb_grid(n)}) * 6 +
                        3 * (size_t)CG_MAX_VEC_GRID + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   // mode 2 batches B x steps (knob 29; 2 or 4 p buffers) when the batch of
@@ -1199,16 +1229,21 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   double *red = s->red;
   const int nv0 = p.guess_nonzero ? 6 : 3;
   double *hist0 = hist_host ? hist.p : nullptr;
-  // one rank: the norms pass folds its partials and runs cg_init in-launch
-  // (knob 34: its grid; partials per value = the grid)
-  const int ngrid = g_knobs.norm_grid > 0 ? g_knobs.norm_grid : RED_BLOCKS;
+  // Zero guess, batched x steps, one rank: iteration 0's direction update
+  // reads b as r_0 and also forms the initial norms, folds them and runs
+  // cg_init (cg_pb_kernel NRM) -- no separate pass over b.  Otherwise the
+  // norms pass runs on the direction update's grid (knob 34 overrides), so
+  // both give the same bits, then folds in-launch and runs cg_init (one rank)
+  // or leaves partials for the all-reduce.
+  const bool norms_in_pb = fused && xb > 1 && !p.guess_nonzero;
+  const int ngrid = g_knobs.norm_grid > 0 ? g_knobs.norm_grid : (int)cg_pb_grid(n);
   Fold fin;
   if (fused) { fin.cnt = s->fold_upd; fin.out = red; fin.ntotal = fin.ncount = ngrid; }
 #define CGN(...) cg_norms_kernel<__VA_ARGS__><<<ngrid, 256, 0, st>>>
   if (nv0 == 6) CGN(6)(n, r.p, b, dinv, part.p, nullptr, nullptr, fin, s, hist0);
   // x = 0 and r = b; with batched x steps neither is written here: iteration 0
   // reads b as r_0 and the first batch (or the finish pass) writes x first
-  else if (xb > 1) CGN(3)(n, b, b, dinv, part.p, nullptr, nullptr, fin, s, hist0);
+  else if (xb > 1) { if (!norms_in_pb) CGN(3)(n, b, b, dinv, part.p, nullptr, nullptr, fin, s, hist0); }
   else CGN(3, true)(n, r.p, b, dinv, part.p, r.p, x, fin, s, hist0);
 #undef CGN
   HIPCHECK(hipGetLastError());
@@ -1219,6 +1254,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     else cg_init_kernel<3><<<1, 256, 0, st>>>(s, part.p, ngrid, 0, hist0);
     HIPCHECK(hipGetLastError());
   }
+  Fold fpb;                                   // iteration 0's fused norms (norms_in_pb)
+  if (norms_in_pb) { fpb.cnt = s->fold_upd; fpb.out = red; }
 
   Poller poller(A, st);
   int i = 0;
@@ -1265,7 +1302,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg, fdot_p);
       timer.end();
     } else if (xb > 1) {
-      cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0);
+      cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb);
       timer.begin();
       nb_spmv = matmult_overlap(A, pbs.b[it % xb], w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
