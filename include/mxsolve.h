@@ -251,7 +251,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         vector is aligned (0/1, default 0: one row per thread per step)
  * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
  * key 15: grid cap of the halo-boundary SpMV launch (0 = default 2048)
- * key 16: GMRES VecMDot vectors per pass over w (4, 8, 16 or 32; default 32)
+ * key 16: GMRES VecMDot vectors per pass over w (4, 8, 16 or 32; default 8: one
+ *         pass over w per 8 basis vectors measured 1.4% faster per GMRES(30) step
+ *         than 32 at 256^3 -- the 32-wide kernel holds 139 VGPRs)
  * key 18: library buffers >= 64 MiB physically contiguous when the driver can
  *         provide them (hipDeviceMallocContiguous, else hipMalloc; 0/1, default 1)
  * key 19: one-byte row masks for aligned-offset slices when every slice has

@@ -176,7 +176,7 @@ struct VCodes { const uint8_t *code; const int64_t *cptr; const double *tab; int
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
 struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
-                int bnd_grid = 0; int mdot_group = 32;
+                int bnd_grid = 0; int mdot_group = 8;
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
