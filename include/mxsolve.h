@@ -279,6 +279,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 35: row-pair SpMV reads uniform-slot dictionary blocks as slot values +
  *         lane masks when the matrix has them (0/1, default 1)
  * key 36: grid of the GMRES MDot pass (0 = default 1024 workgroups)
+ * key 37: the Jacobi-fused row-pair MatMult (GMRES) takes dinv from a table
+ *         indexed by the rows' diagonal code instead of reading the dinv
+ *         vector (0/1, default 1; the same bits)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

@@ -515,6 +515,7 @@ int mx_debug_set(int key, int value) {
     case 34: old = g_knobs.norm_grid; g_knobs.norm_grid = std::min(std::max(value, 0), 16384); break;
     case 35: old = g_knobs.pair_uni; g_knobs.pair_uni = value; break;
     case 36: old = g_knobs.mdot_grid; g_knobs.mdot_grid = std::min(std::max(value, 0), RED_BLOCKS); break;
+    case 37: old = g_knobs.pair_dtab; g_knobs.pair_dtab = value; break;
     default: break;
   }
   return old;

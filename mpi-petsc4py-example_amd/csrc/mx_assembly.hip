@@ -1158,6 +1158,14 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
   DBuf<uint8_t> sc(VDICT_SLOTS);
   HIPCHECK(hipMemcpyAsync(sc.p, slot_code.data(), VDICT_SLOTS, hipMemcpyHostToDevice, st));
   HIPCHECK(hipMemcpyAsync(S.vtab.p, vt.data(), sizeof(double) * vt.size(), hipMemcpyHostToDevice, st));
+  {
+    // jacobi_setup_kernel's dinv = d == 0 ? 1 : 1 / d, per code (IEEE division,
+    // the same correctly rounded quotient on the host); absent -> 1
+    std::vector<double> dt(VCODE_MAX, 1.0);
+    for (size_t i = 0; i < keys.size(); ++i) dt[i] = vt[i] == 0.0 ? 1.0 : 1.0 / vt[i];
+    S.dtab.alloc(VCODE_MAX);
+    HIPCHECK(hipMemcpyAsync(S.dtab.p, dt.data(), sizeof(double) * dt.size(), hipMemcpyHostToDevice, st));
+  }
   code_fill_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(ns, S.sptr.p, S.width.p, S.col.p, S.val.p, S.cptr.p, tab.p, sc.p,
                                                           S.mask.p, S.mask8.p, S.code.p);
   HIPCHECK(hipGetLastError());

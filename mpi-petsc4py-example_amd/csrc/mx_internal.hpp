@@ -163,6 +163,11 @@ struct Sell {
   // the 2K lane masks of present slots -- read by scalar loads (no code bytes,
   // no LDS table lookups); empty when some block is not uniform
   DBuf<PairUni> puni;
+  // 1 / value per code (1 for a zero value and for absent slots): PCJacobi's
+  // dinv of a row is dtab[its diagonal slot's code] -- the division the
+  // Jacobi setup does, so the Jacobi-fused row-pair MatMult reads no dinv
+  // vector (the same bits)
+  DBuf<double> dtab;
 };
 constexpr uint32_t PBLK_GHOST_LO = 1u << 30;
 constexpr uint32_t PBLK_GHOST_HI = 1u << 31;
@@ -180,7 +185,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
-                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; };
+                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

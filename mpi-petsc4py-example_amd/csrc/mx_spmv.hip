@@ -426,7 +426,8 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
     const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
     const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star,
-    const int32_t *__restrict__ pblk, int pdict, int rev, const PairUni *__restrict__ puni) {
+    const int32_t *__restrict__ pblk, int pdict, int rev, const PairUni *__restrict__ puni,
+    const double *__restrict__ dtab_g) {
   static_assert(PS == 0 || VC, "row pairs: coded values");
   static_assert(!UNI || PS == 5 || PS == 7, "uniform-slot blocks: 5/7-point row pairs");
   CgTopIn top;
@@ -469,8 +470,16 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     X = XPlainT<SC>{x, xs};
   }
   __shared__ double vtab[VC ? VCODE_MAX : 1];
+  // row pairs, Jacobi-fused modes (dtab_g set: the operator's own vector
+  // Jacobi): dinv per diagonal code, so no dinv vector is read
+  constexpr bool DT = spmv_jac(MODE) && PS != 0 && !UNI;
+  __shared__ double dtab[DT ? VCODE_MAX : 1];
   if constexpr (VC) {   // every early return above is workgroup-uniform
     for (int i = threadIdx.x; i < VCODE_MAX; i += 256) vtab[i] = vtab_g[i];   // [ntab, 256) zero
+    if constexpr (DT) {
+      if (dtab_g)
+        for (int i = threadIdx.x; i < VCODE_MAX; i += 256) dtab[i] = dtab_g[i];
+    }
     __syncthreads();
   }
   double dot = 0.0;
@@ -633,7 +642,19 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
       const bool gh = SPLIT && (t.fl & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
       double o0 = sum0, o1 = sum1;
       if constexpr (spmv_jac(MODE)) {
-        if (!gh) { o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1); }
+        if (!gh) {
+          if constexpr (DT) {
+            if (dtab_g) {                        // the rows' diagonal slot: offset 0 of the centre run
+              constexpr int JC = SH::first(SH::CENTER_RUN) + 1;
+              o0 = sum0 * dtab[code(JC)];
+              o1 = sum1 * dtab[code(K + JC)];
+            } else {
+              o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1);
+            }
+          } else {
+            o0 = papply(jac, sum0, r0); o1 = papply(jac, sum1, r0 + 1);
+          }
+        }
       }
       if (ynt) __builtin_nontemporal_store(dbl2{o0, o1}, reinterpret_cast<dbl2 *>(y + r0));
       else *reinterpret_cast<dbl2 *>(y + r0) = dbl2{o0, o1};
@@ -883,7 +904,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
       partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt, \
-      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, pair_flags(A), g_knobs.spmv_rev, A->sd.puni.p
+      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, pair_flags(A), g_knobs.spmv_rev, A->sd.puni.p, dtab
   using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
   KFn kf = nullptr;
 #define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>
@@ -910,6 +931,9 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   const int ps = vcode && g_knobs.spmv_pairs ? A->sd.pair_shape : 0;
   // uniform-slot dictionary (knob 35 = 0: the LDS table path)
   const bool uni = ps && A->sd.puni.p && g_knobs.pair_uni && (pair_flags(A) & 1);
+  // Jacobi by diagonal code (knob 37): the operator's own vector Jacobi only
+  const double *dtab = ps && !uni && spmv_jac(mode) && jac.mode == 1 && jac.d == A->jac_dinv.p && A->sd.dtab.p &&
+                               g_knobs.pair_dtab ? A->sd.dtab.p : nullptr;
 #define SPMV_PS(MODE, SP)                                                                         \
   do {                                                                                            \
     if (ps == 5) { if (uni) kf = &spmv_sell_kernel<MODE, true, 5, SP, 0, true, 5, true>;           \

@@ -278,3 +278,35 @@ def test_pair_uniform_cg(selfcomm):
     off = _with_knob(L, 35, 0, run)
     assert on[:2] == off[:2]
     assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
+
+
+@pytest.mark.parametrize("kind,n,ksp", [("convdiff3d", 24, "gmres"), ("poisson3d27", 16, "gmres")])
+def test_pair_jacobi_by_code(selfcomm, oracle_mod, kind, n, ksp):
+    """GMRES(30) + vector Jacobi on the row-pair path: dinv from the table
+    indexed by the rows' diagonal code (knob 37 = 1, default) and from the
+    dinv vector (knob 37 = 0) give the same iterations, history and solution
+    bits; both against the oracle."""
+    from mxsolve.core import DMat
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    L = lib()
+    b = np.random.default_rng(9).random(M)
+
+    def run():
+        A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+        assert A.info()["pair_shape"] > 0
+        bt = torch.from_numpy(b).cuda()
+        x = torch.zeros(M, dtype=torch.float64, device="cuda")
+        r = A.solve(bt, x, ksp=ksp, rtol=1e-8, history=True)
+        A.destroy()
+        return r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy()
+
+    on = run()
+    off = _with_knob(L, 37, 0, run)
+    assert on[:2] == off[:2]
+    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
+    assert np.array_equal(on[3].view(np.uint64), off[3].view(np.uint64))
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    o = O.solve(b, ksp=ksp, rtol=1e-8)
+    assert on[1] == o["reason"] and abs(on[0] - o["its"]) <= 1
+    assert np.linalg.norm(on[3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
