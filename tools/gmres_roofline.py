@@ -4,7 +4,9 @@ trace of tools/bench_general.py c4 (BASELINE C4, conv-diff 256^3).
 
 Algorithmic bytes per inner step j (0-based within a restart cycle, the new
 direction w = A v_j; SURVEY.md §8d's GMRES model, this build's fusions):
-  MatMult (SPMV_JACOBI_S, vector Jacobi): x 8m + dinv 8m + w 8m + codes
+  MatMult (SPMV_JACOBI_S, vector Jacobi): x 8m + w 8m (+ the dictionary's
+           block ids, 4 B per 128 rows); dinv comes from the per-code table
+           (knob 37; 24m with the dinv vector read, knob 37 = 0)
   MDot  : w and v_0..v_j            8m (j + 2)
   MAXPY + norm (fused)             : w read + write, v_0..v_j   8m (j + 3)
 The trace's kernels of each kind are summed over the whole solve and divided
@@ -30,7 +32,7 @@ restart = int(sys.argv[4]) if len(sys.argv) > 4 else 30
 steps = [j % restart for n in (20, its, 60) for j in range(n)]
 mdot_b = sum(8 * m * (j + 2) for j in steps)
 maxpy_b = sum(8 * m * (j + 3) for j in steps)
-spmv_b = len(steps) * 24 * m
+spmv_b = len(steps) * (16 * m + 4 * (m // 128))
 
 
 def total(prefix, lo=20.0):      # working launches (the no-ops after a stop are shorter)
