@@ -97,6 +97,10 @@ typedef struct {
   int64_t pair_uniform;               /* 1: every dictionary block is uniform per slot
                                          (5/7-point): SpMV reads each block's slot values
                                          and lane masks, not code bytes (key 35)       */
+  int64_t pair_lean;                  /* MatMult kernel of the uniform-slot layout:
+                                         0 general SELL kernel, 1 lean row-pair kernel
+                                         with presence selects, 2 lean select-free
+                                         ("clean": absent operands read as 0.0; key 38) */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */

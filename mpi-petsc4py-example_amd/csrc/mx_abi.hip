@@ -242,6 +242,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_blocks = info->pair_shape ? A->sd.pair_blocks : 0;
     info->pair_block_bytes = info->pair_shape ? 64 * (int64_t)((2 * A->sd.dia_k + 15) / 16 * 16) : 0;
     info->pair_uniform = info->pair_shape && info->pair_blocks > 0 && A->sd.puni.p ? 1 : 0;
+    info->pair_lean = pair_lean_kind(A);
   });
 }
 
@@ -516,6 +517,7 @@ int mx_debug_set(int key, int value) {
     case 35: old = g_knobs.pair_uni; g_knobs.pair_uni = value; break;
     case 36: old = g_knobs.mdot_grid; g_knobs.mdot_grid = std::min(std::max(value, 0), RED_BLOCKS); break;
     case 37: old = g_knobs.pair_dtab; g_knobs.pair_dtab = value; break;
+    case 38: old = g_knobs.pair_lean; g_knobs.pair_lean = value; break;
     default: break;
   }
   return old;

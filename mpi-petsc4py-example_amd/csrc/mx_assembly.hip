@@ -1088,11 +1088,20 @@ static void dedupe_pair_blocks(Sell &S, hipStream_t st) {
   S.pair_blocks = nb;
 }
 
+// select-free flags of each pair unit's dictionary block (build_pair_uniform)
+__global__ void pair_clean_flags_kernel(int64_t nunits, const int32_t *__restrict__ dpat, const int32_t *__restrict__ bfl,
+                                        int32_t *__restrict__ pblk) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nunits || !(dpat[2 * u] & DPAT_PAIR)) return;
+  pblk[u] = (int32_t)((uint32_t)pblk[u] | (uint32_t)bfl[(uint32_t)pblk[u] & PBLK_ID]);
+}
+
 // Uniform-slot form of the code-block dictionary (Sell::puni), 5/7-point
 // shapes: kept only when, in every block, each slot-row's present codes are
 // one code (constant-coefficient stencils: a few dozen boundary classes).
 static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream_t st) {
   S.puni.reset();
+  S.pair_clean = false;
   const int K = S.dia_k;
   if (S.pair_blocks <= 0 || (S.pair_shape != 5 && S.pair_shape != 7) || K != S.pair_shape || 2 * K > 16) return;
   const int pb = pair_bytes(K);
@@ -1118,6 +1127,44 @@ static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream
   }
   S.puni.alloc((size_t)nb);
   HIPCHECK(hipMemcpyAsync(S.puni.p, u.data(), sizeof(PairUni) * u.size(), hipMemcpyHostToDevice, st));
+  // select-free form (mx_spmv_pair.hip): every absent slot's operand can be
+  // made exactly 0.0 by an out-of-range read -- a run whose slot-rows are
+  // empty for both rows, or the tri run's edge value when only lane 0 row 0
+  // lacks -1 / lane 63 row 1 lacks +1 -- so no presence select is needed
+  std::vector<int32_t> fl((size_t)nb, 0);
+  bool clean = true;
+  for (int64_t b = 0; b < nb && clean; ++b) {
+    const PairUni &B = u[(size_t)b];
+    const unsigned long long F = ~0ull;
+    uint32_t f = 0;
+    const int NR = S.pair_shape == 5 ? 3 : 5;
+    for (int r = 0; r < NR && clean; ++r) {
+      const bool tri = S.pair_shape == 5 ? r == 1 : r == 2;
+      const int j = S.pair_shape == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
+      if (!tri) {
+        const unsigned long long a = B.pm[j], c = B.pm[K + j];
+        if (a == 0 && c == 0) f |= PBLK_RUN0 << r;
+        else if (a != F || c != F) clean = false;
+        continue;
+      }
+      const unsigned long long m0 = B.pm[j], m1 = B.pm[j + 1], m2 = B.pm[j + 2];
+      const unsigned long long n0 = B.pm[K + j], n1 = B.pm[K + j + 1], n2 = B.pm[K + j + 2];
+      if ((m0 | m1 | m2 | n0 | n1 | n2) == 0) { f |= (PBLK_RUN0 << r) | PBLK_ELO | PBLK_EHI; continue; }
+      if (m1 != F || m2 != F || n0 != F || n1 != F) clean = false;
+      else if (m0 != F && m0 != (F & ~1ull)) clean = false;
+      else if (n2 != F && n2 != (F >> 1)) clean = false;
+      if (m0 != F) f |= PBLK_ELO;
+      if (n2 != F) f |= PBLK_EHI;
+    }
+    fl[(size_t)b] = (int32_t)f;
+  }
+  S.pair_clean = clean && S.nunits > 0;
+  if (S.pair_clean) {
+    DBuf<int32_t> fd((size_t)nb);
+    HIPCHECK(hipMemcpyAsync(fd.p, fl.data(), sizeof(int32_t) * fl.size(), hipMemcpyHostToDevice, st));
+    pair_clean_flags_kernel<<<(unsigned)cdiv(S.nunits, 256), 256, 0, st>>>(S.nunits, S.dpat.p, fd.p, S.pblk.p);
+    HIPCHECK(hipGetLastError());
+  }
   HIPCHECK(hipStreamSynchronize(st));
 }
 

@@ -163,6 +163,7 @@ struct Sell {
   // the 2K lane masks of present slots -- read by scalar loads (no code bytes,
   // no LDS table lookups); empty when some block is not uniform
   DBuf<PairUni> puni;
+  bool pair_clean = false;  // every puni block is select-free (PBLK_RUN0/ELO/EHI flags in pblk)
   // 1 / value per code (1 for a zero value and for absent slots): PCJacobi's
   // dinv of a row is dtab[its diagonal slot's code] -- the division the
   // Jacobi setup does, so the Jacobi-fused row-pair MatMult reads no dinv
@@ -171,7 +172,13 @@ struct Sell {
 };
 constexpr uint32_t PBLK_GHOST_LO = 1u << 30;
 constexpr uint32_t PBLK_GHOST_HI = 1u << 31;
-constexpr uint32_t PBLK_ID = PBLK_GHOST_LO - 1;
+// select-free ("clean") uniform-slot units: run r's slot-rows are empty for
+// both rows (PBLK_RUN0 << r), lane 0 row 0 lacks the tri run's -1 entry
+// (PBLK_ELO), lane 63 row 1 lacks its +1 entry (PBLK_EHI); mx_spmv_pair.hip
+constexpr uint32_t PBLK_RUN0 = 1u << 22;
+constexpr uint32_t PBLK_ELO = 1u << 27;
+constexpr uint32_t PBLK_EHI = 1u << 28;
+constexpr uint32_t PBLK_ID = PBLK_RUN0 - 1;   // block ids < 2^22 (units < 2^21, dictionaries <= 2048 blocks)
 constexpr int64_t PAIR_MAX_ROWS = int64_t(1) << 28;   // operand byte offsets (unsigned 32-bit voffset, bound n * 8 < 2^31)
 constexpr int VCODE_MAX = 256;      // table entries; code 255 marks an absent slot
 constexpr int VCODE_ABSENT = VCODE_MAX - 1;
@@ -185,7 +192,8 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
-                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1; };
+                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
+                int pair_lean = 1; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -311,6 +319,11 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
                     int *done_flag, const CgFuse *cg = nullptr, const Fold *fold = nullptr,
                     const double *xscale = nullptr);
 int spmv_blocks(const Mat *A, int mode = SPMV_PLAIN);
+// lean row-pair MatMult (mx_spmv_pair.hip): the kernel for this product, or null
+const void *pair_lean_select(const Mat *A, int mode, bool split);
+int pair_lean_kind(const Mat *A);   // 0 general kernel, 1 lean, 2 lean select-free (mx_mat_info.pair_lean)
+void pair_lean_run(const Mat *A, const void *kf, int grid, const double *x, double *y, double *partials,
+                   const int *done, const Fold &fold, hipStream_t st);
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);

@@ -30,6 +30,7 @@
 #include "mx_cg.hpp"
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
+#include "mx_pair.hpp"
 
 namespace mx {
 
@@ -39,7 +40,6 @@ constexpr int SPMV_WAVES = 4;  // 256-thread workgroups, one slice per wave at a
 #endif
 Knobs g_knobs;
 
-typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef int int2v __attribute__((ext_vector_type(2)));
 
 template <bool NT, class T> __device__ __forceinline__ T ld(const T *p) {
@@ -99,21 +99,8 @@ struct XCg {
   }
 };
 
-// Buffer-load forms of the operand sources for the row-pair body: 32-bit
-// element indices, and a read outside the vector (an absent slot of a
-// boundary unit: its offset points before row 0 or past the last row)
-// returns 0 by the hardware range check instead of faulting, so no unit
-// needs an in-range test.  Bound: n * 8 < 2^31 (PAIR_MAX_ROWS); a negative
-// index wraps to an offset >= 2^31, outside every vector.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double *p, int64_t n) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), 0, (int)(n * 8), 0x00020000);
-}
-__device__ __forceinline__ dbl2 bload2(__amdgpu_buffer_rsrc_t r, int i) {
-  return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)((unsigned)i * 8u), 0, 0));
-}
-__device__ __forceinline__ double bload1(__amdgpu_buffer_rsrc_t r, int i) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)((unsigned)i * 8u), 0, 0));
-}
+// Buffer-load forms of the operand sources for the row-pair body
+// (vec_rsrc / bload1 / bload2: mx_pair.hpp).
 template <class XS> struct XBuf;
 template <bool S> struct XBuf<XPlainT<S>> {
   __amdgpu_buffer_rsrc_t x;
@@ -364,45 +351,7 @@ __device__ __forceinline__ double sell_slice(const int32_t *__restrict__ cbase, 
 // one 16-byte store, against two code loads, 2 K gathers and two stores for
 // two single-row slices.  Every row still sums its entries in ascending
 // column order, one rounding per multiply and add.
-template <int PS> struct PairShape;
-template <> struct PairShape<5> {     // a, -1, 0, 1, b
-  static constexpr int K = 5, NR = 3, CENTER_RUN = 1;
-  static constexpr int run(int j) { return j == 0 ? 0 : j == 4 ? 2 : 1; }
-  static constexpr int pos(int j) { return j >= 1 && j <= 3 ? j - 2 : 0; }
-  static constexpr bool tri(int r) { return r == 1; }
-  static constexpr int first(int r) { return r == 0 ? 0 : r == 1 ? 1 : 4; }
-};
-template <> struct PairShape<7> {     // a, b, -1, 0, 1, c, d
-  static constexpr int K = 7, NR = 5, CENTER_RUN = 2;
-  static constexpr int run(int j) { return j < 2 ? j : j <= 4 ? 2 : j - 2; }
-  static constexpr int pos(int j) { return j >= 2 && j <= 4 ? j - 3 : 0; }
-  static constexpr bool tri(int r) { return r == 2; }
-  static constexpr int first(int r) { return r < 2 ? r : r == 2 ? 2 : r + 2; }
-};
-template <> struct PairShape<27> {    // nine runs c-1, c, c+1
-  static constexpr int K = 27, NR = 9, CENTER_RUN = 4;
-  static constexpr int run(int j) { return j / 3; }
-  static constexpr int pos(int j) { return j % 3 - 1; }
-  static constexpr bool tri(int) { return true; }
-  static constexpr int first(int r) { return 3 * r; }
-};
-template <> struct PairShape<0> {
-  static constexpr int K = 1, NR = 1, CENTER_RUN = 0;
-  static constexpr int run(int) { return 0; }
-  static constexpr int pos(int) { return 0; }
-  static constexpr bool tri(int) { return false; }
-  static constexpr int first(int) { return 0; }
-};
-
-// lane i takes lane i - 1's value (UP) or lane i + 1's (!UP); the edge lane takes `edge`
-template <bool UP>
-__device__ __forceinline__ double wave_shift(double v, double edge) {
-  const long long b = __double_as_longlong(v), e = __double_as_longlong(edge);
-  constexpr int ctrl = UP ? 0x138 : 0x130;   // wave_shr:1 / wave_shl:1
-  const int lo = __builtin_amdgcn_update_dpp((int)e, (int)b, ctrl, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp((int)(e >> 32), (int)(b >> 32), ctrl, 0xf, 0xf, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
+// PairShape / wave_shift: mx_pair.hpp
 
 // One wave sweeps slices; lane = row.  Grid-stride over a fixed grid whose
 // blocks are grouped by XCD (block b runs on XCD b % 8 under the observed
@@ -965,10 +914,14 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
       break;
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
-  const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf), ps != 0);
+  // constant-coefficient 5/7-point blocks: the lean row-pair kernel
+  // (mx_spmv_pair.hip; the same bits)
+  const void *lean = pair_lean_select(A, mode, split);
+  const int grid = main_grid(A, mode, lean ? lean : reinterpret_cast<const void *>(kf), ps != 0);
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
-  kf<<<grid, 256, 0, st>>>(SPMV_ARGS);
+  if (lean) pair_lean_run(A, lean, grid, x, y, partials, done_flag, fold, st);
+  else kf<<<grid, 256, 0, st>>>(SPMV_ARGS);
 #undef SPMV_GO
 #undef SPMV_PS
 #undef SPMV_CGKD

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "mpi-petsc4py-example_amd", "lib", "libmxsolve.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
-HOT = re.compile(r"spmv_sell_kernel|cg_|mdot|maxpy|fold_kernel")
+HOT = re.compile(r"spmv_sell_kernel|spmv_pair_lean|cg_|mdot|maxpy|fold_kernel")
 
 
 def code_objects(fatbin: bytes):

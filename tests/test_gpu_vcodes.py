@@ -310,3 +310,70 @@ def test_pair_jacobi_by_code(selfcomm, oracle_mod, kind, n, ksp):
     o = O.solve(b, ksp=ksp, rtol=1e-8)
     assert on[1] == o["reason"] and abs(on[0] - o["its"]) <= 1
     assert np.linalg.norm(on[3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
+
+
+@pytest.mark.parametrize("kind,n,lean", [("poisson3d", 128, 2), ("poisson2d", 256, 2), ("poisson2d", 384, 2),
+                                         ("poisson3d", 64, 1), ("poisson2d", 96, 1), ("poisson3d", 48, 1)])
+def test_pair_lean_kernel(selfcomm, oracle_mod, kind, n, lean):
+    """Lean row-pair MatMult (mx_spmv_pair.hip, knob 38 = 1, the default) for
+    uniform-slot layouts: bit-exact against the oracle and against the general
+    SELL kernel (knob 38 = 0).  lean = 2: every block select-free (absent
+    operands read as 0.0 -- y/z-boundary runs and the x-line edges, x-lines a
+    multiple of 128 rows); lean = 1: a block whose -1/+1 slot-row misses a lane
+    other than the unit's edge lane (x-lines of 64 / 96 / 48 rows inside a
+    128-row unit) keeps the presence selects.
+    Operand values include infinities and NaN: an absent slot must not let them
+    into a row that PETSc's product keeps finite."""
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    L = lib()
+    from mxsolve.core import DMat
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    rng = np.random.default_rng(23)
+    for special in (False, True):
+        x = rng.standard_normal(M)
+        if special:
+            x[rng.integers(0, M, 40)] = np.inf
+            x[rng.integers(0, M, 40)] = -np.inf
+            x[rng.integers(0, M, 40)] = np.nan
+        exp = O.mult(x).view(np.uint64)
+        outs = []
+        for knob in (1, 0):
+            def run():
+                A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+                y = torch.zeros(M, dtype=torch.float64, device="cuda")
+                A.mult(torch.from_numpy(x).cuda(), y)
+                info = A.info()
+                A.destroy()
+                return info, y.cpu().numpy().view(np.uint64)
+            outs.append(_with_knob(L, 38, knob, run))
+        (i1, g1), (i0, g0) = outs
+        assert i1["pair_uniform"] == 1 and i1["pair_lean"] == lean and i0["pair_lean"] == 0
+        assert np.array_equal(g1, exp) and np.array_equal(g0, exp)
+
+
+@pytest.mark.parametrize("n", [128, 96])
+def test_pair_lean_cg(selfcomm, n):
+    """CG with the lean MatMult (+ p.w partials) and with the general kernel:
+    same iterations, same history, same solution bits (same grid and sweep,
+    so the same dot grouping)."""
+    from mxsolve.core import DMat, rhs_hash
+    L = lib()
+
+    def run():
+        A = DMat.stencil(selfcomm, "poisson3d" if n == 128 else "poisson2d", n)
+        m = A.info()["m"]
+        b = selfcomm.empty(m)
+        rhs_hash(selfcomm, 0, b)
+        x = selfcomm.zeros(m)
+        r = A.solve(b, x, ksp="cg", pc="jacobi", history=True)
+        kind = A.info()["pair_lean"]
+        A.destroy()
+        return r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy(), kind
+
+    on = run()
+    off = _with_knob(L, 38, 0, run)
+    assert on[4] > 0 and off[4] == 0
+    assert on[:2] == off[:2]
+    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
+    assert np.array_equal(on[3].view(np.uint64), off[3].view(np.uint64))

@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <algorithm>
 #include <vector>
@@ -623,6 +624,79 @@ __global__ void __launch_bounds__(256) puni_kernel(const double *__restrict__ x,
   }
 }
 
+// Select-free uniform-slot body ("clean" dictionaries): every absent slot's
+// operand is made exactly 0.0 by an out-of-range buffer read -- whole runs
+// whose slot-rows are empty for both rows (y/z boundaries), and the run's
+// edge value where lane 0 row 0 lacks -1 / lane 63 row 1 lacks +1 -- so
+// sum + v * 0 = sum (a running sum from +0.0 is never -0.0) and no select is
+// needed.  Flags per unit in the block-id word: bit 22 + r = run r empty,
+// bit 27 = low edge absent, bit 28 = high edge absent.
+constexpr int CL_RUN = 22, CL_ELO = 27, CL_EHI = 28, CL_ID = (1 << 22) - 1;
+constexpr int OOR = 1 << 28;   // element offset added to an absent read: bytes >= 2^30 > M * 8
+template <int U, bool DOT>
+__global__ void __launch_bounds__(256) pclean_kernel(const double *__restrict__ x, double *__restrict__ y, int64_t nunits,
+                                                     const BMeta *__restrict__ bm, const int32_t *__restrict__ pblk,
+                                                     double *__restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int chunk = (int)((nunits + 7) >> 3);
+  const int s0 = xcd * chunk + j * 4 + wid, step = per * 4;
+  const int send = (int)min(nunits, (int64_t)(xcd + 1) * chunk);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, (int)(M * 8), 0x00020000);
+  const int anchor[5] = {-(int)NN, -N, 0, N, (int)NN};
+  const int eoff = lane == 0 ? -1 : 128;            // lane 0: x[ub - 1], others x[ub + 128]
+  double dot = 0.0;
+  struct T { dbl2 L[5]; double e; int bw; };
+  auto ldp = [&](int i) -> dbl2 { return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)((unsigned)i * 8u), 0, 0)); };
+  auto lds = [&](int i) -> double { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (int)((unsigned)i * 8u), 0, 0)); };
+  auto ld = [&](int u, int bw, T &t) {
+    const int ub = u * 128, r0 = ub + 2 * lane;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) t.L[r] = ldp(r0 + anchor[r] + (((bw >> (CL_RUN + r)) & 1) ? OOR : 0));
+    const int elo = ((bw >> CL_ELO) & 1) ? OOR : 0, ehi = ((bw >> CL_EHI) & 1) ? OOR : 0;
+    t.e = lds(ub + eoff + (lane == 0 ? elo : ehi));
+    t.bw = bw;
+  };
+  auto fin = [&](int u, const T &t) {
+    const int r0 = u * 128 + 2 * lane;
+    const BMeta &B = bm[t.bw & CL_ID];
+    const double lo = wave_shift<true>(t.L[2].y, t.e), hi = wave_shift<false>(t.L[2].x, t.e);
+    const double a0[7] = {t.L[0].x, t.L[1].x, lo, t.L[2].x, t.L[2].y, t.L[3].x, t.L[4].x};
+    const double a1[7] = {t.L[0].y, t.L[1].y, t.L[2].x, t.L[2].y, hi, t.L[3].y, t.L[4].y};
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      s0 = s0 + B.v[k] * a0[k];
+      s1 = s1 + B.v[7 + k] * a1[k];
+    }
+    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+    if (DOT) { dot += t.L[2].x * s0; dot += t.L[2].y * s1; }
+  };
+  int u = s0;
+  int kstep = 64;
+  int bv = 0;
+  for (; u + (U - 1) * step < send; u += U * step) {
+    if (kstep + U > 64) {
+      const int uu = u + lane * step;
+      bv = uu < send ? pblk[uu] : 0;
+      kstep = 0;
+    }
+    T t[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) ld(u + k * step, __builtin_amdgcn_readlane(bv, kstep + k), t[k]);
+    kstep += U;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < U; ++k) fin(u + k * step, t[k]);
+  }
+  for (; u < send; u += step) { T t; ld(u, pblk[u], t); fin(u, t); }
+  if (DOT) {
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+    if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+  }
+}
+
 int main(int argc, char **argv) {
   double *x, *y, *yr, *flush;
   CK(hipMalloc(&x, M * 8)); CK(hipMalloc(&y, M * 8)); CK(hipMalloc(&yr, M * 8)); CK(hipMalloc(&flush, 512ull << 20));
@@ -722,9 +796,32 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&dbm, 2 * sizeof(BMeta))); CK(hipMemcpy(dbm, hbm.data(), 2 * sizeof(BMeta), hipMemcpyHostToDevice));
   uint32_t *dict2;
   CK(hipMalloc(&dict2, hd2.size() * 4)); CK(hipMemcpy(dict2, hd2.data(), hd2.size() * 4, hipMemcpyHostToDevice));
+  // the same two blocks for the select-free body: block ids with edge flags
+  std::vector<int32_t> hbc(M / 128);
+  for (size_t u = 0; u < hbc.size(); ++u) hbc[u] = (int)(u & 1) | ((u & 1) ? 1 << CL_EHI : 1 << CL_ELO);
+  int32_t *pblkc;
+  CK(hipMalloc(&pblkc, hbc.size() * 4)); CK(hipMemcpy(pblkc, hbc.data(), hbc.size() * 4, hipMemcpyHostToDevice));
+  {
+    const int g = cus * 4 - 8;
+    puni_kernel<2, true><<<g, 256>>>(x, yr, M / 128, dbm, pblk, part);
+    pclean_kernel<2, true><<<g, 256>>>(x, y, M / 128, dbm, pblkc, part);
+    CK(hipDeviceSynchronize());
+    std::vector<double> g1(M), g2(M);
+    CK(hipMemcpy(g1.data(), yr, M * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(g2.data(), y, M * 8, hipMemcpyDeviceToHost));
+    int64_t nd = 0;
+    for (int64_t i = 0; i < M; ++i) nd += memcmp(&g1[i], &g2[i], 8) != 0;
+    printf("pclean vs puni: %lld rows differ bitwise\n", (long long)nd);
+  }
   for (int wpc : {2, 3, 4, 5}) {
     const int g = cus * wpc - 8;
     char nm[64];
+    for (int U3 : {1, 2, 3}) {
+      snprintf(nm, sizeof nm, "pclean<%d>+dot %d/CU", U3, wpc);
+      if (U3 == 1) timeit(nm, [&] { pclean_kernel<1, true><<<g, 256>>>(x, y, M / 128, dbm, pblkc, part); }, false);
+      if (U3 == 2) timeit(nm, [&] { pclean_kernel<2, true><<<g, 256>>>(x, y, M / 128, dbm, pblkc, part); }, false);
+      if (U3 == 3) timeit(nm, [&] { pclean_kernel<3, true><<<g, 256>>>(x, y, M / 128, dbm, pblkc, part); }, false);
+    }
     snprintf(nm, sizeof nm, "pcodes<1> %d/CU", wpc);
     timeit(nm, [&] { pcodes_kernel<1, false, false><<<g, 256>>>(x, y, M / 128, dict, pblk, vt, part); }, false);
     snprintf(nm, sizeof nm, "pcodes<2> %d/CU", wpc);
