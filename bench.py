@@ -264,9 +264,11 @@ def main():
     assert r["its"] == args.steps, r
     value = args.steps / dt
 
-    # roofline pass: the same CG iterations with a HIP event pair around every
-    # SpMV launch (on the library stream the kernel runs on).  Kept out of the
-    # K timed steps because the event records themselves cost ~10% per step.
+    # roofline pass: the same CG iterations with a HIP event pair on every
+    # SpMV launch (on the library stream the kernel runs on; one rank: the
+    # events are attached to the kernel's own dispatch by hipExtLaunchKernel,
+    # so they time the kernel alone, as the profiler's trace does).  Kept out
+    # of the K timed steps: the profiled solve runs eagerly (no graph).
     x.zero_()
     rp = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=min(args.steps, 100), profile=True)
     spmv_avg_ms = rp["spmv_ms"] / max(rp["spmv_count"], 1)
@@ -340,7 +342,11 @@ def main():
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_detail": traffic,
                          "kernel": ("spmv_sell_kernel<SPMV_CG> (CG-fused MatMult" if mode == 1 else
-                                    "spmv_sell_kernel<SPMV_DOT> (CG MatMult") + ", HIP events, rank 0)",
+                                    ("spmv_pair_zm_kernel<SPMV_DOT> (CG MatMult, lean row-pair z-march" if info.get("pair_zmarch") else
+                                     "spmv_pair_lean_kernel<SPMV_DOT> (CG MatMult, lean row-pair" if info.get("pair_lean") else
+                                     "spmv_sell_kernel<SPMV_DOT> (CG MatMult")) +
+                                   (", HIP events attached to the kernel's dispatch (hipExtLaunchKernel)" if world == 1 else
+                                    ", HIP events around the MatMult") + ", rank 0)",
                          "bytes_per_launch": bytes_launch, "avg_launch_ms": round(spmv_avg_ms, 5),
                          "format": ("value codes (" + str(info.get("value_codes")) + " distinct), " +
                                     ("row pairs" if info.get("pair_shape") else "one row per lane") +

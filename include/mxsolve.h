@@ -101,6 +101,9 @@ typedef struct {
                                          0 general SELL kernel, 1 lean row-pair kernel
                                          with presence selects, 2 lean select-free
                                          ("clean": absent operands read as 0.0; key 38) */
+  int64_t pair_zmarch;                /* 1: the lean kernel marches columns of units one
+                                         plane (3D) / line (2D) apart, carrying two
+                                         operand pairs in registers (key 39)          */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */

@@ -243,6 +243,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_block_bytes = info->pair_shape ? 64 * (int64_t)((2 * A->sd.dia_k + 15) / 16 * 16) : 0;
     info->pair_uniform = info->pair_shape && info->pair_blocks > 0 && A->sd.puni.p ? 1 : 0;
     info->pair_lean = pair_lean_kind(A);
+    info->pair_zmarch = info->pair_lean && pair_zm_applies(A) ? 1 : 0;
   });
 }
 
@@ -518,6 +519,10 @@ int mx_debug_set(int key, int value) {
     case 36: old = g_knobs.mdot_grid; g_knobs.mdot_grid = std::min(std::max(value, 0), RED_BLOCKS); break;
     case 37: old = g_knobs.pair_dtab; g_knobs.pair_dtab = value; break;
     case 38: old = g_knobs.pair_lean; g_knobs.pair_lean = value; break;
+    case 39: old = g_knobs.pair_zm; g_knobs.pair_zm = value; break;
+    case 40: old = g_knobs.pair_zm_bpc; g_knobs.pair_zm_bpc = std::min(std::max(value, 1), 8); break;
+    case 41: old = g_knobs.pair_zm_len; g_knobs.pair_zm_len = std::min(std::max(value, 1), 1024); break;
+    case 42: old = g_knobs.pair_zm_units; g_knobs.pair_zm_units = value == 2 ? 2 : 1; break;
     default: break;
   }
   return old;

@@ -193,7 +193,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
-                int pair_lean = 1; };
+                int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -319,11 +319,20 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
                     int *done_flag, const CgFuse *cg = nullptr, const Fold *fold = nullptr,
                     const double *xscale = nullptr);
 int spmv_blocks(const Mat *A, int mode = SPMV_PLAIN);
-// lean row-pair MatMult (mx_spmv_pair.hip): the kernel for this product, or null
-const void *pair_lean_select(const Mat *A, int mode, bool split);
+// MatMult kernel timing from the dispatch's own timestamps (hipExtLaunchKernel
+// start/stop events: no event packets between the kernels, so the measured
+// span is the kernel's, as a profiler's trace sees it).  The KSP's SpMV timer
+// arms it on one-rank solves; the next main SpMV launch of this host thread
+// consumes it (mx_spmv.hip launch_timed).
+struct ExtTiming { hipEvent_t a = nullptr, b = nullptr; bool armed = false, used = false; };
+extern thread_local ExtTiming g_ext_timing;
+int device_cu_count();
+int main_grid(const Mat *A, int mode, const void *kf, bool pairs);   // the SpMV's resident grid
+// lean row-pair MatMult (mx_spmv_pair.hip): launched when it applies (returns its grid, else 0)
+int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials, const int *done,
+                     const Fold &fold, hipStream_t st);
 int pair_lean_kind(const Mat *A);   // 0 general kernel, 1 lean, 2 lean select-free (mx_mat_info.pair_lean)
-void pair_lean_run(const Mat *A, const void *kf, int grid, const double *x, double *y, double *partials,
-                   const int *done, const Fold &fold, hipStream_t st);
+bool pair_zm_applies(const Mat *A);  // the lean kernel's z-march form (mx_mat_info.pair_zmarch)
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);

@@ -1030,8 +1030,25 @@ struct SpmvTimer {
     for (auto &e : ev) HIPCHECK(hipEventCreate(&e));
   }
   ~SpmvTimer() { for (auto &e : ev) (void)hipEventDestroy(e); }
-  void begin() { if (on && used + 2 <= ev.size()) HIPCHECK(hipEventRecord(ev[used], st)); }
-  void end() { if (on && used + 2 <= ev.size()) { HIPCHECK(hipEventRecord(ev[used + 1], st)); used += 2; } }
+  // ext: one-rank solves time the main SpMV kernel by its own dispatch
+  // timestamps (g_ext_timing); otherwise events bracket the whole MatMult
+  // (halo, interior and boundary launches)
+  bool ext = false;
+  void begin() {
+    if (!on || used + 2 > ev.size()) return;
+    if (ext) g_ext_timing = ExtTiming{ev[used], ev[used + 1], true, false};
+    else HIPCHECK(hipEventRecord(ev[used], st));
+  }
+  void end() {
+    if (!on || used + 2 > ev.size()) return;
+    if (ext) {
+      if (g_ext_timing.used) used += 2;   // a launch took the events
+      g_ext_timing = ExtTiming{};
+      return;
+    }
+    HIPCHECK(hipEventRecord(ev[used + 1], st));
+    used += 2;
+  }
   void collect(double &ms, int &count) {
     ms = 0.0; count = 0;
     if (!on) return;
@@ -1219,6 +1236,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   ksp_state_init_kernel<<<1, 256, 0, st>>>(sd.p, kin);
   HIPCHECK(hipGetLastError());
   SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
+  timer.ext = c->size == 1;
 
   // r = b - A x  (or b)
   if (p.guess_nonzero) {
@@ -1487,6 +1505,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   double *hist_d = hist_host ? hist.p : nullptr;
   Events ev(A);
   SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
+  timer.ext = c->size == 1;
   HIPCHECK(hipEventRecord(ev.a, st));
   const unsigned egrid = grid_for(n, 256, 8192);
   if (!p.guess_nonzero) vec_set(st, n, 0.0, x);

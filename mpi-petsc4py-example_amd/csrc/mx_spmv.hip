@@ -31,6 +31,7 @@
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 #include "mx_pair.hpp"
+#include "mx_launch.hpp"
 
 namespace mx {
 
@@ -39,6 +40,7 @@ constexpr int SPMV_WAVES = 4;  // 256-thread workgroups, one slice per wave at a
 #define SPMV_PAIR_TWO 1   // 5/7-point row pairs: two units' loads in flight per wave
 #endif
 Knobs g_knobs;
+thread_local ExtTiming g_ext_timing;
 
 typedef int int2v __attribute__((ext_vector_type(2)));
 
@@ -691,7 +693,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
 // launch-geometry caches, shared by the host threads of in-process ranks
 static std::mutex g_geom_mu;
 
-static int device_cus() {
+int device_cu_count() {
   static int cus[64] = {0};
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
@@ -704,7 +706,7 @@ static int device_cus() {
 // Upper bound of the main launch's grid (partial-sum buffers are sized by it)
 int spmv_blocks(const Mat *A, int) {
   const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
-  const int64_t cap = g_knobs.spmv_grid > 0 ? g_knobs.spmv_grid : 8 * (int64_t)device_cus();
+  const int64_t cap = g_knobs.spmv_grid > 0 ? g_knobs.spmv_grid : 8 * (int64_t)device_cu_count();
   return (int)std::max<int64_t>(1, std::min<int64_t>(need, std::max<int64_t>(cap, 8192)));
 }
 
@@ -720,7 +722,7 @@ int spmv_blocks(const Mat *A, int) {
 // 82 us at 4, 87 at 5, 93 at 6).  SPMV_CG
 // evaluates the iteration's scalar top once per workgroup, so it keeps >= 4
 // slices per wave.  Knob 3 > 0 overrides the grid.
-static int main_grid(const Mat *A, int mode, const void *kf, bool pairs) {
+int main_grid(const Mat *A, int mode, const void *kf, bool pairs) {
   const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
   int64_t g;
   if (g_knobs.spmv_grid > 0) {
@@ -739,7 +741,7 @@ static int main_grid(const Mat *A, int mode, const void *kf, bool pairs) {
       bpc = it->second;
     }
     const int cap = pairs ? g_knobs.spmv_pair_bpc : g_knobs.spmv_bpc;
-    g = (int64_t)std::min(bpc, std::max(1, cap)) * device_cus();
+    g = (int64_t)std::min(bpc, std::max(1, cap)) * device_cu_count();
     // one workgroup fewer per XCD: a per-XCD wave count that is a multiple of
     // 256 (grids of 1024 / 1536) puts the concurrent x streams on aliasing
     // strides -- measured +35..+80% MatMult time (tools/op_ab.py)
@@ -843,6 +845,12 @@ static int pair_flags(const Mat *A) {
 static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold_in,
                        const double *xscale) {
+  // constant-coefficient 5/7-point blocks: the lean row-pair kernels
+  // (mx_spmv_pair.hip; each row's sum has the same bits)
+  if (!cgp && !xscale) {
+    const int lg = pair_lean_launch(A, mode, split, x, y, partials, done_flag, fold_in, st);
+    if (lg) return lg;
+  }
   const double *lvec = (A->nghost && !split) ? A->halo.lvec.p : nullptr;
   const int kd = A->sd.dia_k;
   const CgFuse cg = cgp ? *cgp : CgFuse{};
@@ -914,14 +922,10 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
       break;
     default: fail(MX_ERR_INTERNAL, "bad spmv mode");
   }
-  // constant-coefficient 5/7-point blocks: the lean row-pair kernel
-  // (mx_spmv_pair.hip; the same bits)
-  const void *lean = pair_lean_select(A, mode, split);
-  const int grid = main_grid(A, mode, lean ? lean : reinterpret_cast<const void *>(kf), ps != 0);
+  const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf), ps != 0);
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
-  if (lean) pair_lean_run(A, lean, grid, x, y, partials, done_flag, fold, st);
-  else kf<<<grid, 256, 0, st>>>(SPMV_ARGS);
+  launch_timed(kf, grid, st, SPMV_ARGS);
 #undef SPMV_GO
 #undef SPMV_PS
 #undef SPMV_CGKD

@@ -20,13 +20,21 @@
 //     and its slot-row value is the uniform value (0 for empty rows).  A row
 //     sum that starts at +0.0 is never -0.0, so sum + v * 0.0 == sum bit for
 //     bit: the same result as skipping the slot, with no presence select;
-//   * !CLEAN: the lane masks as select conditions (the general UNI body).
+//   * !CLEAN: the lane masks as select conditions (the general UNI body);
+//   * z-march (spmv_pair_zm_kernel, the default where the pattern's outermost
+//     runs are +-D with D a multiple of 128 rows -- the 3D planes, the 2D
+//     lines): a wave owns a column of units one plane (D rows) apart and
+//     marches it, carrying the -D and centre pairs in registers, so a unit
+//     loads 3 operand pairs and its edge instead of 5 and its edge; the
+//     ceiling probe's matrix-free form of it runs at the copy rate
+//     (tools/stencil_probe.hip pzm_kernel).
 // Each row still sums its entries in ascending column order, one rounding per
 // multiply and add (PETSc's MatMult_SeqAIJ), so the product is bitwise equal
 // to the general kernel's and to the oracle's (tests/test_gpu_vcodes.py).
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 #include "mx_pair.hpp"
+#include "mx_launch.hpp"
 
 namespace mx {
 
@@ -39,14 +47,60 @@ constexpr int LEAN_WAVES = 4;
 struct PairLeanArgs {
   int m, n, nunits;            // rows, operand length, 128-row units (m = 128 nunits)
   int anchor[5];               // per run: the singleton offset, or the tri run's centre
+  int P, NZ, L, S;             // z-march: units per plane, planes, planes per segment, segments
   double *partials;            // SPMV_DOT: one p.y partial per workgroup
   const int *done;             // solver stop flag (the launch is then a no-op)
   Fold fold;
 };
 
+// One unit's products: L[r] = run r's operand pair, e = the tri run's edge
+// value (lane 0: x[r0 + c - 1], lane 63: x[r0 + 127 + c + 1]), bw = the unit's
+// block word.  Each row sums its slots in ascending column order.
+template <int MODE, int PS, bool SPLIT, bool CLEAN>
+__device__ __forceinline__ void pair_unit(const dbl2 (&L)[PairShape<PS>::NR], double e, uint32_t bw,
+                                          const PairUni *__restrict__ puni, double *__restrict__ y, int r0,
+                                          int lane, double &dot) {
+  using SH = PairShape<PS>;
+  constexpr int K = SH::K, C = SH::CENTER_RUN;
+  const PairUni &B = puni[bw & PBLK_ID];                  // wave-uniform: scalar loads
+  double s0v = 0.0, s1v = 0.0, lo = 0.0, hi = 0.0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int r = SH::run(j), p = SH::pos(j);
+    if (SH::tri(r) && p < 0) {
+      lo = wave_shift<true>(L[r].y, e);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
+      hi = wave_shift<false>(L[r].x, e);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
+    }
+    double a0, a1;
+    if (!SH::tri(r)) { a0 = L[r].x; a1 = L[r].y; }
+    else if (p < 0) { a0 = lo; a1 = L[r].x; }
+    else if (p == 0) { a0 = L[r].x; a1 = L[r].y; }
+    else { a0 = L[r].y; a1 = hi; }
+    const double q0 = s0v + B.v[j] * a0, q1 = s1v + B.v[K + j] * a1;
+    if constexpr (CLEAN) {
+      s0v = q0;
+      s1v = q1;
+    } else {
+      s0v = __builtin_amdgcn_inverse_ballot_w64(B.pm[j]) ? q0 : s0v;
+      s1v = __builtin_amdgcn_inverse_ballot_w64(B.pm[K + j]) ? q1 : s1v;
+    }
+  }
+  *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
+  if constexpr (MODE == SPMV_DOT) {
+    // SPLIT: rows with A_o entries stored their diagonal-block sum; the
+    // boundary kernel continues them and adds their p.y terms
+    const bool gh = SPLIT && (bw & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+    if (!gh) {
+      dot += L[C].x * s0v;
+      dot += L[C].y * s1v;
+    }
+  }
+}
+
 // The vectors and tables are __restrict__ kernel arguments: the block's slot
 // values then compile to scalar loads (a pointer inside the by-value struct
 // is not known unclobbered, and the values went through vector loads).
+// Sweep form: the general kernel's XCD-grouped order, two units per step.
 template <int MODE, int PS, bool SPLIT, bool CLEAN>
 __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs a, const double *__restrict__ x,
                                                              double *__restrict__ y,
@@ -54,12 +108,11 @@ __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs 
                                                              const PairUni *__restrict__ puni) {
   if (a.done && *a.done) return;   // wave-uniform: solver finished
   using SH = PairShape<PS>;
-  constexpr int K = SH::K, NR = SH::NR, C = SH::CENTER_RUN;
+  constexpr int NR = SH::NR;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // the general kernel's XCD-grouped sweep: each XCD walks one contiguous
-  // eighth of the units, its waves interleaved (the +-n / +-n^2 re-reads of x
-  // stay in that XCD's L2)
+  // each XCD walks one contiguous eighth of the units, its waves interleaved
+  // (the +-n / +-n^2 re-reads of x stay in that XCD's L2)
   int s0, sstep, send;
   if ((gridDim.x & 7) == 0) {
     const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
@@ -90,42 +143,6 @@ __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs 
     t.e = bload1(xr, ub + eo);
     t.bw = bw;
   };
-  auto finish = [&](int u, const Unit &t) __attribute__((always_inline)) {
-    const int r0 = u * 128 + 2 * lane;
-    const PairUni &B = puni[t.bw & PBLK_ID];              // wave-uniform: scalar loads
-    double s0v = 0.0, s1v = 0.0, lo = 0.0, hi = 0.0;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const int r = SH::run(j), p = SH::pos(j);
-      if (SH::tri(r) && p < 0) {
-        lo = wave_shift<true>(t.L[r].y, t.e);    // x[r0 + c - 1] = lane - 1's x[r0' + c + 1]
-        hi = wave_shift<false>(t.L[r].x, t.e);   // x[r0 + c + 2] = lane + 1's x[r0' + c]
-      }
-      double a0, a1;
-      if (!SH::tri(r)) { a0 = t.L[r].x; a1 = t.L[r].y; }
-      else if (p < 0) { a0 = lo; a1 = t.L[r].x; }
-      else if (p == 0) { a0 = t.L[r].x; a1 = t.L[r].y; }
-      else { a0 = t.L[r].y; a1 = hi; }
-      const double q0 = s0v + B.v[j] * a0, q1 = s1v + B.v[K + j] * a1;
-      if constexpr (CLEAN) {
-        s0v = q0;
-        s1v = q1;
-      } else {
-        s0v = __builtin_amdgcn_inverse_ballot_w64(B.pm[j]) ? q0 : s0v;
-        s1v = __builtin_amdgcn_inverse_ballot_w64(B.pm[K + j]) ? q1 : s1v;
-      }
-    }
-    *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
-    if constexpr (MODE == SPMV_DOT) {
-      // SPLIT: rows with A_o entries stored their diagonal-block sum; the
-      // boundary kernel continues them and adds their p.y terms
-      const bool gh = SPLIT && (t.bw & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
-      if (!gh) {
-        dot += t.L[C].x * s0v;
-        dot += t.L[C].y * s1v;
-      }
-    }
-  };
   // two units per wave step, both units' loads in flight before the first
   // product; block words of the next 64 units in one vector load
   int u = s0, k = 64;
@@ -141,13 +158,108 @@ __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs 
     load(u + sstep, (uint32_t)__builtin_amdgcn_readlane(bv, k + 1), tb);
     k += 2;
     __builtin_amdgcn_sched_barrier(0);
-    finish(u, ta);
-    finish(u + sstep, tb);
+    pair_unit<MODE, PS, SPLIT, CLEAN>(ta.L, ta.e, ta.bw, puni, y, u * 128 + 2 * lane, lane, dot);
+    pair_unit<MODE, PS, SPLIT, CLEAN>(tb.L, tb.e, tb.bw, puni, y, (u + sstep) * 128 + 2 * lane, lane, dot);
   }
-  if (u < send) {
+  for (; u < send; u += sstep) {
     Unit t;
     load(u, (uint32_t)pblk[u], t);
-    finish(u, t);
+    pair_unit<MODE, PS, SPLIT, CLEAN>(t.L, t.e, t.bw, puni, y, u * 128 + 2 * lane, lane, dot);
+  }
+  if constexpr (MODE == SPMV_DOT) {
+    double v[1] = {dot};
+    block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  }
+}
+
+// Z-march form.  The pattern's first and last runs are -D and +D (D = P
+// units: a 3D plane, a 2D line); unit u and unit u + P are one plane apart.
+// A task is (segment of L planes, column of units); XCD x takes segments
+// [S x / 8, S (x + 1) / 8) -- a contiguous slab of planes -- and its waves take
+// the slab's tasks segment-major, so the waves running together sit in the
+// same planes and the +-n pairs and edges they load hit L2.  Along a column
+// the -D pair of a unit is the previous unit's centre pair and its centre the
+// previous +D pair: carried in registers, so a unit loads the +D pair (the
+// one line x is read from HBM for), its inner runs and its edge.  CLEAN: a
+// carried operand whose run is empty for this unit is zeroed at use (it is
+// real x, read for the neighbouring unit); inner runs and the edge take the
+// out-of-range read as in the sweep form.
+template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU>
+__global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a, const double *__restrict__ x,
+                                                           double *__restrict__ y, const int32_t *__restrict__ pblk,
+                                                           const PairUni *__restrict__ puni) {
+  if (a.done && *a.done) return;   // wave-uniform: solver finished
+  using SH = PairShape<PS>;
+  constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[LAST];
+  const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
+  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
+  double dot = 0.0;
+  const int ntask = (se - sb) * a.P;
+  for (int t = w; t < ntask; t += W) {
+    const int seg = sb + t / a.P, col = t % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;       // the lane's rows within a plane
+    dbl2 zm = bload2(xr, z0 * D + cb - D), c = bload2(xr, z0 * D + cb);
+    uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
+    // NQ units (planes z .. z + NQ - 1) with all their loads in flight
+    auto step = [&](int z, auto nq) __attribute__((always_inline)) {
+      constexpr int NQ = decltype(nq)::value;
+      dbl2 L[NQ][NR], zp[NQ];
+      double e[NQ];
+      uint32_t bw[NQ];
+      bw[0] = bwn;
+#pragma unroll
+      for (int q = 1; q < NQ; ++q) bw[q] = (uint32_t)pblk[(z + q) * a.P + col];
+      if (z + NQ < z1) bwn = (uint32_t)pblk[(z + NQ) * a.P + col];   // next step's, ahead
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
+        zp[q] = bload2(xr, r0 + D);
+#pragma unroll
+        for (int r = 1; r < LAST; ++r)
+          if (r != TR) L[q][r] = bload2(xr, r0 + a.anchor[r] + (CLEAN && (bw[q] & (PBLK_RUN0 << r)) ? PAIR_OOR : 0));
+        int eo = ecst;
+        if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
+        e[q] = bload1(xr, ub + eo);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        L[q][0] = q == 0 ? zm : q == 1 ? c : zp[q - 2];
+        L[q][TR] = q == 0 ? c : zp[q - 1];
+        L[q][LAST] = zp[q];
+        if constexpr (CLEAN) {
+          if (bw[q] & CARRY) {                     // wave-uniform, rare: an empty carried run
+            if (bw[q] & PBLK_RUN0) L[q][0] = dbl2{0.0, 0.0};
+            if (bw[q] & (PBLK_RUN0 << TR)) L[q][TR] = dbl2{0.0, 0.0};
+            if (bw[q] & (PBLK_RUN0 << LAST)) L[q][LAST] = dbl2{0.0, 0.0};
+          }
+        }
+        pair_unit<MODE, PS, SPLIT, CLEAN>(L[q], e[q], bw[q], puni, y, (z + q) * D + cb, lane, dot);
+      }
+      zm = NQ == 1 ? c : zp[NQ - 2];
+      c = zp[NQ - 1];
+    };
+    int z = z0;
+    for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
+    for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
   }
   if constexpr (MODE == SPMV_DOT) {
     double v[1] = {dot};
@@ -157,7 +269,6 @@ __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs 
 
 using LeanFn = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const PairUni *);
 
-// the lean kernel for this product, or null (the general kernel then runs)
 // the layout side of the choice (mode and split aside): 0 none, 1 lean, 2 lean select-free
 int pair_lean_kind(const Mat *A) {
   const Sell &S = A->sd;
@@ -170,44 +281,83 @@ int pair_lean_kind(const Mat *A) {
   return S.pair_clean && A->m <= PAIR_CLEAN_MAX_ROWS && A->n <= PAIR_CLEAN_MAX_ROWS ? 2 : 1;
 }
 
-const void *pair_lean_select(const Mat *A, int mode, bool split) {
-  const Sell &S = A->sd;
-  if (mode != SPMV_PLAIN && mode != SPMV_DOT) return nullptr;
-  const int kind = pair_lean_kind(A);
-  if (!kind) return nullptr;
-  if (!split && (A->nghost > 0 || S.pair_ghosts)) return nullptr;   // A_o continues in the general kernel
-  const bool clean = kind == 2;
-  LeanFn f = nullptr;
-#define LEAN_PICK(MODE, PS)                                                              \
-  do {                                                                                   \
-    if (split) f = clean ? &spmv_pair_lean_kernel<MODE, PS, true, true> : &spmv_pair_lean_kernel<MODE, PS, true, false>; \
-    else f = clean ? &spmv_pair_lean_kernel<MODE, PS, false, true> : &spmv_pair_lean_kernel<MODE, PS, false, false>;      \
-  } while (0)
-  if (mode == SPMV_PLAIN) { if (S.pair_shape == 5) LEAN_PICK(SPMV_PLAIN, 5); else LEAN_PICK(SPMV_PLAIN, 7); }
-  else { if (S.pair_shape == 5) LEAN_PICK(SPMV_DOT, 5); else LEAN_PICK(SPMV_DOT, 7); }
-#undef LEAN_PICK
-  return reinterpret_cast<const void *>(f);
+// run r's anchor: the singleton's offset, or the tri run's centre slot
+static void pair_anchors(const Sell &S, int anchor[5]) {
+  const int ps = S.pair_shape;
+  for (int r = 0; r < 5; ++r) {
+    const bool tri = ps == 5 ? r == 1 : r == 2;
+    const int first = ps == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
+    anchor[r] = (ps == 5 && r >= 3) ? 0 : S.pat_star_off[(size_t)(first + (tri ? 1 : 0))];
+  }
 }
 
-void pair_lean_run(const Mat *A, const void *kf, int grid, const double *x, double *y, double *partials,
-                   const int *done, const Fold &fold, hipStream_t st) {
+// z-march: the outermost runs are -D, +D with D a multiple of 128 rows, m a multiple of D
+bool pair_zm_applies(const Mat *A) {
   const Sell &S = A->sd;
+  if (!g_knobs.pair_zm || (S.pair_shape != 5 && S.pair_shape != 7)) return false;
+  int anchor[5];
+  pair_anchors(S, anchor);
+  const int D = anchor[S.pair_shape == 5 ? 2 : 4];
+  return D > 0 && anchor[0] == -D && D % 128 == 0 && A->m % D == 0;
+}
+
+// Launch the lean MatMult for this product; returns its grid, or 0 when it
+// does not apply (the general kernel then runs).  A fold (fold.cnt set)
+// counts this launch's workgroups.
+int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials, const int *done,
+                     const Fold &fold_in, hipStream_t st) {
+  const Sell &S = A->sd;
+  if (mode != SPMV_PLAIN && mode != SPMV_DOT) return 0;
+  const int kind = pair_lean_kind(A);
+  if (!kind) return 0;
+  if (!split && (A->nghost > 0 || S.pair_ghosts)) return 0;   // A_o continues in the general kernel
+  const bool clean = kind == 2;
   PairLeanArgs a{};
   a.m = (int)A->m;
   a.n = (int)A->n;
   a.nunits = (int)S.nunits;
-  const int ps = S.pair_shape;
-  for (int r = 0; r < 5; ++r) {
-    // run r's anchor: the singleton's offset, or the tri run's centre slot
-    const bool tri = ps == 5 ? r == 1 : r == 2;
-    const int first = ps == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
-    a.anchor[r] = (ps == 5 && r >= 3) ? 0 : S.pat_star_off[(size_t)(first + (tri ? 1 : 0))];
-  }
+  pair_anchors(S, a.anchor);
   a.partials = partials;
   a.done = done;
+  const int NR = S.pair_shape == 5 ? 3 : 5, D = a.anchor[NR - 1];
+  const bool zm = pair_zm_applies(A);
+  LeanFn f = nullptr;
+  int grid;
+  if (zm) {
+    a.P = D / 128;
+    a.NZ = (int)(A->m / D);
+    grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
+    grid &= ~7;
+    const int W = grid / 8 * LEAN_WAVES;               // waves per XCD
+    const int slab = (a.NZ + 7) / 8;                    // planes per XCD
+    // segments of up to 32 planes, shorter when one slab's columns do not
+    // give every wave a task
+    int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
+    while (L > 1 && (int64_t)a.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
+    a.L = L;
+    a.S = (a.NZ + L - 1) / L;
+#define ZM_PICK(MODE, PS, SP, CL) \
+    f = g_knobs.pair_zm_units == 2 ? &spmv_pair_zm_kernel<MODE, PS, SP, CL, 2> : &spmv_pair_zm_kernel<MODE, PS, SP, CL, 1>
+#define ZM_C(MODE, PS) do { if (split) { if (clean) ZM_PICK(MODE, PS, true, true); else ZM_PICK(MODE, PS, true, false); } \
+                            else { if (clean) ZM_PICK(MODE, PS, false, true); else ZM_PICK(MODE, PS, false, false); } } while (0)
+    if (mode == SPMV_PLAIN) { if (S.pair_shape == 5) ZM_C(SPMV_PLAIN, 5); else ZM_C(SPMV_PLAIN, 7); }
+    else { if (S.pair_shape == 5) ZM_C(SPMV_DOT, 5); else ZM_C(SPMV_DOT, 7); }
+#undef ZM_C
+#undef ZM_PICK
+  } else {
+#define LEAN_C(MODE, PS) do { if (split) f = clean ? &spmv_pair_lean_kernel<MODE, PS, true, true> : &spmv_pair_lean_kernel<MODE, PS, true, false>; \
+                              else f = clean ? &spmv_pair_lean_kernel<MODE, PS, false, true> : &spmv_pair_lean_kernel<MODE, PS, false, false>; } while (0)
+    if (mode == SPMV_PLAIN) { if (S.pair_shape == 5) LEAN_C(SPMV_PLAIN, 5); else LEAN_C(SPMV_PLAIN, 7); }
+    else { if (S.pair_shape == 5) LEAN_C(SPMV_DOT, 5); else LEAN_C(SPMV_DOT, 7); }
+#undef LEAN_C
+    grid = main_grid(A, mode, reinterpret_cast<const void *>(f), true);
+  }
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   a.fold = fold;
-  reinterpret_cast<LeanFn>(const_cast<void *>(kf))<<<grid, 256, 0, st>>>(a, x, y, S.pblk.p, S.puni.p);
+  launch_timed(f, grid, st, a, x, y, S.pblk.p, S.puni.p);
   HIPCHECK(hipGetLastError());
+  return grid;
 }
 
 }  // namespace mx

@@ -227,7 +227,7 @@ def test_pair_code_dictionary_cg(selfcomm):
         r = A.solve(b, x, ksp="cg", pc="jacobi")
         return r["its"], r["reason"], x.cpu().numpy().copy(), A.info()["pair_blocks"]
 
-    on = run()
+    on = _with_knob(L, 39, 0, run)          # the sweep form: the general kernel's p.w grouping
     off = _with_knob(L, 30, 0, run)
     assert on[3] > 0 and off[3] == 0
     assert on[:2] == off[:2]
@@ -274,7 +274,8 @@ def test_pair_uniform_cg(selfcomm):
         r = A.solve(b, x, ksp="cg", pc="jacobi")
         return r["its"], r["reason"], x.cpu().numpy().copy()
 
-    on = run()
+    # the lean kernel's sweep form keeps the general kernel's p.w grouping
+    on = _with_knob(L, 39, 0, run)
     off = _with_knob(L, 35, 0, run)
     assert on[:2] == off[:2]
     assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
@@ -312,9 +313,26 @@ def test_pair_jacobi_by_code(selfcomm, oracle_mod, kind, n, ksp):
     assert np.linalg.norm(on[3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
 
 
+def _with_knobs(L, kv, fn):
+    """fn() under the knob settings kv ({key: value}), restored after."""
+    old = {k: L.mx_debug_set(k, v) for k, v in kv.items()}
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            L.mx_debug_set(k, v)
+
+
+# lean-kernel forms: default (z-march, two planes per step, 4 workgroups per
+# CU, segments of up to 32 planes), the sweep form (39 = 0), one plane per
+# step (42 = 1), short / odd segments with tails (41), other grids (40)
+LEAN_FORMS = [{}, {39: 0}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}, {40: 2}]
+
+
+@pytest.mark.parametrize("form", range(len(LEAN_FORMS)))
 @pytest.mark.parametrize("kind,n,lean", [("poisson3d", 128, 2), ("poisson2d", 256, 2), ("poisson2d", 384, 2),
                                          ("poisson3d", 64, 1), ("poisson2d", 96, 1), ("poisson3d", 48, 1)])
-def test_pair_lean_kernel(selfcomm, oracle_mod, kind, n, lean):
+def test_pair_lean_kernel(selfcomm, oracle_mod, kind, n, lean, form):
     """Lean row-pair MatMult (mx_spmv_pair.hip, knob 38 = 1, the default) for
     uniform-slot layouts: bit-exact against the oracle and against the general
     SELL kernel (knob 38 = 0).  lean = 2: every block select-free (absent
@@ -346,17 +364,19 @@ def test_pair_lean_kernel(selfcomm, oracle_mod, kind, n, lean):
                 info = A.info()
                 A.destroy()
                 return info, y.cpu().numpy().view(np.uint64)
-            outs.append(_with_knob(L, 38, knob, run))
+            outs.append(_with_knobs(L, {38: knob, **LEAN_FORMS[form]}, run))
         (i1, g1), (i0, g0) = outs
         assert i1["pair_uniform"] == 1 and i1["pair_lean"] == lean and i0["pair_lean"] == 0
         assert np.array_equal(g1, exp) and np.array_equal(g0, exp)
 
 
 @pytest.mark.parametrize("n", [128, 96])
-def test_pair_lean_cg(selfcomm, n):
-    """CG with the lean MatMult (+ p.w partials) and with the general kernel:
-    same iterations, same history, same solution bits (same grid and sweep,
-    so the same dot grouping)."""
+def test_pair_lean_cg(selfcomm, oracle_mod, n):
+    """CG with the lean MatMult (+ p.w partials) and with the general kernel.
+    The sweep form (knob 39 = 0) walks the general kernel's grid and order:
+    same iterations, history and solution bits.  The z-march form groups each
+    lane's p.w terms by column, not by sweep step: same iterations and reason,
+    iterates equal to rounding; both against the oracle."""
     from mxsolve.core import DMat, rhs_hash
     L = lib()
 
@@ -371,9 +391,13 @@ def test_pair_lean_cg(selfcomm, n):
         A.destroy()
         return r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy(), kind
 
-    on = run()
+    zm = run()
+    sweep = _with_knob(L, 39, 0, run)
     off = _with_knob(L, 38, 0, run)
-    assert on[4] > 0 and off[4] == 0
-    assert on[:2] == off[:2]
-    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
-    assert np.array_equal(on[3].view(np.uint64), off[3].view(np.uint64))
+    assert zm[4] > 0 and sweep[4] > 0 and off[4] == 0
+    assert sweep[:2] == off[:2]
+    assert np.array_equal(sweep[2].view(np.uint64), off[2].view(np.uint64))
+    assert np.array_equal(sweep[3].view(np.uint64), off[3].view(np.uint64))
+    assert zm[:2] == off[:2]
+    assert np.allclose(zm[2], off[2], rtol=1e-9, atol=0)
+    assert np.linalg.norm(zm[3] - off[3]) <= 1e-10 * np.linalg.norm(off[3])

@@ -697,6 +697,59 @@ __global__ void __launch_bounds__(256) pclean_kernel(const double *__restrict__ 
   }
 }
 
+// Row-pair z-march: a wave owns a column of 128-row units (one half x-line)
+// and marches L planes in z, carrying the centre and -n^2 pairs in registers:
+// per unit 4 loads (the +n^2 pair -- the only HBM-first line --, the -n and
+// +n pairs, the edge) instead of 6.  XCD k takes the z-slab [32k, 32k + 32);
+// its waves take (segment, column) tasks segment-major, so the waves running
+// together sit in the same planes and the +-n pairs hit L2.  Z steps per
+// iteration: ZU (their loads in flight together).
+template <int L, int ZU>
+__global__ void __launch_bounds__(256) pzm_kernel(const double *__restrict__ x, double *__restrict__ y,
+                                                  double *__restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int W = per * 4, w = j * 4 + wid;
+  constexpr int COLS = (int)(NN / 128), SLAB = N / 8, SEGS = SLAB / L;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, (int)(M * 8), 0x00020000);
+  auto ldp = [&](int i) -> dbl2 { return __builtin_bit_cast(dbl2, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)((unsigned)i * 8u), 0, 0)); };
+  auto lds = [&](int i) -> double { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, (int)((unsigned)i * 8u), 0, 0)); };
+  const int eoff = lane == 0 ? -1 : 128;
+  double dot = 0.0;
+  for (int t = w; t < COLS * SEGS; t += W) {
+    const int seg = t / COLS, col = t % COLS;
+    const int zs = xcd * SLAB + seg * L;
+    const int cb = col * 128 + 2 * lane;          // row of lane's pair within a plane
+    dbl2 zm = ldp((zs - 1) * (int)NN + cb), c = ldp(zs * (int)NN + cb);
+    for (int z = zs; z < zs + L; z += ZU) {
+      dbl2 zp[ZU], ym[ZU], yp[ZU];
+      double e[ZU];
+#pragma unroll
+      for (int q = 0; q < ZU; ++q) {
+        const int r0 = (z + q) * (int)NN + cb, ub = (z + q) * (int)NN + col * 128;
+        zp[q] = ldp(r0 + (int)NN);
+        ym[q] = ldp(r0 - N);
+        yp[q] = ldp(r0 + N);
+        e[q] = lds(ub + eoff);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < ZU; ++q) {
+        const int r0 = (z + q) * (int)NN + cb;
+        const double lo = wave_shift<true>(c.y, e[q]), hi = wave_shift<false>(c.x, e[q]);
+        const double s0 = 6.0 * c.x - zm.x - ym[q].x - lo - c.y - yp[q].x - zp[q].x;
+        const double s1 = 6.0 * c.y - zm.y - ym[q].y - c.x - hi - yp[q].y - zp[q].y;
+        *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0, s1};
+        dot += c.x * s0; dot += c.y * s1;
+        zm = c; c = zp[q];
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+  if (lane == 0) part[blockIdx.x * 4 + wid] = dot;
+}
+
 int main(int argc, char **argv) {
   double *x, *y, *yr, *flush;
   CK(hipMalloc(&x, M * 8)); CK(hipMalloc(&y, M * 8)); CK(hipMalloc(&yr, M * 8)); CK(hipMalloc(&flush, 512ull << 20));
@@ -708,7 +761,13 @@ int main(int argc, char **argv) {
   const double bytes = 2.0 * M * 8;
   const std::string only = argc > 1 ? std::string(";") + argv[1] + ";" : std::string();
   auto timeit = [&](const char *name, auto launch, bool check) {
-    if (!only.empty() && only.find(std::string(";") + name + ";") == std::string::npos) return;
+    if (!only.empty() && only.find(std::string(";") + name + ";") == std::string::npos) {
+      // "prefix*" tokens select every name with that prefix
+      bool hit = false;
+      for (size_t a = 1, b; a < only.size() && (b = only.find(';', a)) != std::string::npos; a = b + 1)
+        if (b > a && only[b - 1] == '*' && std::string(name).rfind(only.substr(a, b - a - 1), 0) == 0) hit = true;
+      if (!hit) return;
+    }
     for (int w = 0; w < 3; ++w) launch();
     CK(hipDeviceSynchronize());
     const int it = 50;
@@ -812,6 +871,17 @@ int main(int argc, char **argv) {
     int64_t nd = 0;
     for (int64_t i = 0; i < M; ++i) nd += memcmp(&g1[i], &g2[i], 8) != 0;
     printf("pclean vs puni: %lld rows differ bitwise\n", (long long)nd);
+  }
+  for (int wpc : {2, 3, 4, 5, 6, 8}) {
+    for (int gsub : {0, 8}) {
+      const int g = cus * wpc - gsub;
+      char nm[64];
+#define PZM(LL, ZZ)                                                                                          \
+      snprintf(nm, sizeof nm, "pzm L%d ZU%d %d/CU-%d", LL, ZZ, wpc, gsub);                                  \
+      timeit(nm, [&] { pzm_kernel<LL, ZZ><<<g, 256>>>(x, y, part); }, false);
+      PZM(32, 1) PZM(32, 2) PZM(16, 1) PZM(16, 2) PZM(8, 2) PZM(32, 4) PZM(16, 4)
+#undef PZM
+    }
   }
   for (int wpc : {2, 3, 4, 5}) {
     const int g = cus * wpc - 8;
