@@ -89,8 +89,10 @@ def main():
         lines += ["", "No-op launches (< 10 us, after a stop) dropped from mean/median: " +
                   ", ".join(f"{k} {n}" for k, n in sorted(dropped.items()))]
     # the solve's MatMult: the SpMV kernel with the most device time (the
-    # CG-fused SPMV_CG <3,...> at <= 3M rows/rank, SPMV_DOT <2,...> above)
-    cands = [k for k in fetch if k.startswith(("spmv_sell_kernel<3,", "spmv_sell_kernel<2,"))]
+    # CG-fused SPMV_CG <3,...> at <= 3M rows/rank, SPMV_DOT <2,...> above:
+    # the general kernel or the lean row-pair / z-march kernels)
+    cands = [k for k in fetch if k.startswith(("spmv_sell_kernel<3,", "spmv_sell_kernel<2,",
+                                               "spmv_pair_zm_kernel<2,", "spmv_pair_lean_kernel<2,"))]
     sp = max(cands, key=lambda k: sum(durs.get(k, [0.0]))) if cands else None
     if sp and not sp.startswith("spmv_sell_kernel<3,"):
         alg = spmv_alg
