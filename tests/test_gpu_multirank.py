@@ -382,12 +382,15 @@ def test_random_ksp(oracle_mod, seed):
 
 
 @pytest.mark.parametrize("P,kind,n,fuse", [(2, "poisson3d", 32, 1), (4, "poisson3d", 32, 2), (2, "poisson3d27", 24, 1),
-                                           (4, "poisson2d", 128, 2), (3, "poisson3d", 32, 2)])
+                                           (4, "poisson2d", 128, 2), (3, "poisson3d", 32, 2), (2, "poisson3d", 128, 2),
+                                           (4, "poisson2d", 256, 2), (3, "poisson3d", 128, 2)])
 def test_distributed_row_pairs(oracle_mod, P, kind, n, fuse):
     """The row-pair MatMult on every rank (interior units), with the overlapped
     halo (ghost slices take the single-row body and the boundary launch), CG
-    fusion mode 1 (SPMV_CG on pairs) and mode 2 (SPMV_DOT + batched x steps):
-    MatMult bit-exact, iteration count equal, x within 1e-10 of the oracle."""
+    fusion mode 1 (SPMV_CG on pairs) and mode 2 (SPMV_DOT + batched x steps;
+    with constant coefficients the lean z-march kernel, ghost units flagged,
+    select-free where the x-lines are multiples of 128 rows): MatMult
+    bit-exact, iteration count equal, x within 1e-10 of the oracle."""
     from mxsolve import _lib
     from mxsolve.core import DMat, rhs_hash
     ip, c, v = oracle_mod.stencil(kind, n)
@@ -408,7 +411,7 @@ def test_distributed_row_pairs(oracle_mod, P, kind, n, fuse):
         rhs_hash(comm, info["rstart"], b)
         x = comm.zeros(info["m"])
         r = A.solve(b, x, ksp="cg")
-        out = (r["its"], r["reason"], x.cpu().numpy(), yl.cpu().numpy(), info["pair_shape"])
+        out = (r["its"], r["reason"], x.cpu().numpy(), yl.cpu().numpy(), info["pair_shape"], info["pair_zmarch"])
         A.destroy()
         return out
 
@@ -419,6 +422,8 @@ def test_distributed_row_pairs(oracle_mod, P, kind, n, fuse):
     finally:
         L.mx_debug_set(9, old)
     assert all(r[4] > 0 for r in res)
+    if (kind, n, P) in (("poisson3d", 128, 2), ("poisson2d", 256, 4)):
+        assert all(r[5] == 1 for r in res)          # whole planes per rank: the z-march form
     assert np.array_equal(np.concatenate([r[3] for r in res]).view(np.uint64), y_ref.view(np.uint64))
     assert all(r[0] == o["its"] and r[1] == o["reason"] for r in res), ([r[:2] for r in res], o["its"])
     xs = np.concatenate([r[2] for r in res])
