@@ -95,8 +95,8 @@ typedef struct {
                                          dictionary (0: one block per unit)           */
   int64_t pair_block_bytes;           /* bytes of one unit's code block               */
   int64_t pair_uniform;               /* 1: every dictionary block is uniform per slot
-                                         (5/7-point): SpMV reads each block's slot values
-                                         and lane masks, not code bytes (key 35)       */
+                                         (5/7/27-point): SpMV reads each block's slot
+                                         values and lane masks, not code bytes (key 35) */
   int64_t pair_lean;                  /* MatMult kernel of the uniform-slot layout:
                                          0 general SELL kernel, 1 lean row-pair kernel
                                          with presence selects, 2 lean select-free
@@ -245,7 +245,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        RCCL communicator (testing, default 0)
  * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
- *        1 for <= 3M local rows, else 2)
+ *        1 for <= 3M local rows, else 2); 4 mode 2 with the direction update and
+ *        the batched x steps inside the z-march MatMult (one rank, lean z-march
+ *        layout, no or uniform Jacobi; else 2; mode 2's bits)
  * key 10: where CG folds its per-workgroup partials: 0 one-block fold kernels;
  *        1 the update pass folds its own inside the launch, and the MatMult's
  *        halo-boundary launch when the product is split (default); 2 the
@@ -289,6 +291,14 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 37: the Jacobi-fused row-pair MatMult (GMRES) takes dinv from a table
  *         indexed by the rows' diagonal code instead of reading the dinv
  *         vector (0/1, default 1; the same bits)
+ * key 38: the lean row-pair MatMult (mx_spmv_pair.hip) for uniform-slot 5/7-point
+ *         layouts (0/1, default 1; the same bits)
+ * key 39: its z-march form (a wave marches a column of units one plane apart,
+ *         two operand pairs carried in registers; 0 = the sweep form; default 1)
+ * key 40: z-march resident workgroups per CU (1..8, default 4)
+ * key 41: z-march segment length in planes (default 32, shortened when a slab
+ *         has too few columns for every wave)
+ * key 42: z-march planes per step (1 or 2, default 2)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

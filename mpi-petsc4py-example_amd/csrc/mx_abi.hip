@@ -241,7 +241,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_units = info->pair_shape ? A->sd.pair_used : 0;
     info->pair_blocks = info->pair_shape ? A->sd.pair_blocks : 0;
     info->pair_block_bytes = info->pair_shape ? 64 * (int64_t)((2 * A->sd.dia_k + 15) / 16 * 16) : 0;
-    info->pair_uniform = info->pair_shape && info->pair_blocks > 0 && A->sd.puni.p ? 1 : 0;
+    info->pair_uniform = info->pair_shape && info->pair_blocks > 0 && (A->sd.puni.p || A->sd.puni27.p) ? 1 : 0;
     info->pair_lean = pair_lean_kind(A);
     info->pair_zmarch = info->pair_lean && pair_zm_applies(A) ? 1 : 0;
   });

@@ -1168,6 +1168,65 @@ static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream
   HIPCHECK(hipStreamSynchronize(st));
 }
 
+// 27-point uniform-slot dictionary (Sell::puni27): kept when every block's
+// 54 slot-rows are uniform; each block also gets its select-free flags (runs
+// empty for both rows, and the x-line edges, which the nine runs of a
+// regular grid share).
+static void build_pair_uniform27(Sell &S, const std::vector<double> &vt, hipStream_t st) {
+  S.puni27.reset();
+  S.pair_clean27 = false;
+  const int K = 27;
+  if (S.pair_blocks <= 0 || S.pair_shape != 27 || S.dia_k != 27) return;
+  const int pb = pair_bytes(K);
+  const int64_t nb = S.pair_blocks;
+  std::vector<uint8_t> d((size_t)nb * 64 * pb);
+  HIPCHECK(hipMemcpyAsync(d.data(), S.pcode.p, d.size(), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  std::vector<PairUni27> u((size_t)nb);
+  const unsigned long long F = ~0ull;
+  bool all_clean = true;
+  for (int64_t b = 0; b < nb; ++b) {
+    PairUni27 &B = u[(size_t)b];
+    std::memset(&B, 0, sizeof(B));
+    for (int q = 0; q < 2 * K; ++q) {
+      int code = -1;
+      for (int lane = 0; lane < 64; ++lane) {
+        const int c = d[((size_t)b * 64 + lane) * pb + q];
+        if (c == VCODE_ABSENT) continue;
+        if (code >= 0 && c != code) return;         // two values in one slot-row: not uniform
+        code = c;
+        B.pm[q] |= 1ull << lane;
+      }
+      if (code >= 0) B.v[q] = vt[(size_t)code];
+    }
+    uint32_t f = 0;
+    int elo = -1, ehi = -1;                         // every non-empty run must agree
+    bool clean = true;
+    for (int r = 0; r < 9 && clean; ++r) {
+      const int j = 3 * r;
+      const unsigned long long m0 = B.pm[j], m1 = B.pm[j + 1], m2 = B.pm[j + 2];
+      const unsigned long long n0 = B.pm[K + j], n1 = B.pm[K + j + 1], n2 = B.pm[K + j + 2];
+      if ((m0 | m1 | m2 | n0 | n1 | n2) == 0) { f |= 1u << r; continue; }
+      if (m1 != F || m2 != F || n0 != F || n1 != F) { clean = false; break; }
+      if (m0 != F && m0 != (F & ~1ull)) { clean = false; break; }
+      if (n2 != F && n2 != (F >> 1)) { clean = false; break; }
+      const int lo = m0 != F, hi = n2 != F;
+      if ((elo >= 0 && elo != lo) || (ehi >= 0 && ehi != hi)) { clean = false; break; }
+      elo = lo;
+      ehi = hi;
+    }
+    if (elo == 1) f |= U27_ELO;
+    if (ehi == 1) f |= U27_EHI;
+    B.flags = f;
+    B.clean = clean ? 1u : 0u;
+    all_clean = all_clean && clean;
+  }
+  S.puni27.alloc((size_t)nb);
+  HIPCHECK(hipMemcpyAsync(S.puni27.p, u.data(), sizeof(PairUni27) * u.size(), hipMemcpyHostToDevice, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  S.pair_clean27 = all_clean;
+}
+
 static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st) {
   S.ntab = 0;
   if (S.slots == 0 || !g_knobs.vcodes) return;
@@ -1239,6 +1298,7 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
     }
     dedupe_pair_blocks(S, st);
     build_pair_uniform(S, vt, st);
+    build_pair_uniform27(S, vt, st);
     S.pair_ghosts = false;
     if (wid_o && S.nunits) {
       DBuf<int> any(1);

@@ -122,6 +122,16 @@ struct PairUni {
   double v[16];                 // the slot-row's value
   unsigned long long pm[16];    // lanes whose row stores it
 };
+// the same for 27-point row pairs (54 slot-rows), with the block's select-free
+// flags: bit r = run r empty for both rows, U27_ELO / U27_EHI = lane 0 row 0
+// lacks every non-empty run's -1 entry / lane 63 row 1 its +1 entry
+struct PairUni27 {
+  double v[54];
+  unsigned long long pm[54];
+  uint32_t flags, clean;        // clean: the block needs no presence select
+};
+constexpr uint32_t U27_ELO = 1u << 9;
+constexpr uint32_t U27_EHI = 1u << 10;
 
 struct Sell {
   int64_t nslices = 0, slots = 0, dia_slices = 0;
@@ -164,6 +174,8 @@ struct Sell {
   // no LDS table lookups); empty when some block is not uniform
   DBuf<PairUni> puni;
   bool pair_clean = false;  // every puni block is select-free (PBLK_RUN0/ELO/EHI flags in pblk)
+  DBuf<PairUni27> puni27;   // 27-point uniform-slot dictionary (mx_spmv_pair.hip z-march)
+  bool pair_clean27 = false;  // every puni27 block is select-free
   // 1 / value per code (1 for a zero value and for absent slots): PCJacobi's
   // dinv of a row is dtab[its diagonal slot's code] -- the division the
   // Jacobi setup does, so the Jacobi-fused row-pair MatMult reads no dinv
@@ -333,6 +345,10 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
                      const Fold &fold, hipStream_t st);
 int pair_lean_kind(const Mat *A);   // 0 general kernel, 1 lean, 2 lean select-free (mx_mat_info.pair_lean)
 bool pair_zm_applies(const Mat *A);  // the lean kernel's z-march form (mx_mat_info.pair_zmarch)
+// CG mode 4: the direction update inside the z-march MatMult (mx_spmv_pair.hip)
+bool pair_zmcg_applies(const Mat *A, int jac_mode);
+int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac_c, const double *r, double *pb0,
+                     double *pb1, double *x, double *w, double *partials, const Fold *fold, hipStream_t st);
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);

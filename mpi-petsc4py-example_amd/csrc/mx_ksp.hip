@@ -1222,8 +1222,14 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // mode 2 batches B x steps (knob 29; 2 or 4 p buffers) when the batch of
   // launched iterations (poll) is a multiple of B; 1 = the x step every iteration
   const int poll = p.poll_every > 0 ? p.poll_every : 16;
-  const int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
-  const int xb = (fmode == 2 && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 4) && poll % g_knobs.cg_xbatch == 0)
+  // mode 4 (knob 9 = 4): mode 2 whose direction update rides in the z-march
+  // MatMult (mx_spmv_pair.hip spmv_pair_zmcg_kernel) -- one rank, a lean
+  // z-march layout, no or uniform Jacobi, x steps batched by 2; otherwise 2
+  int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
+  if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && g_knobs.cg_xbatch == 2 && poll % 2 == 0 && !p.guess_nonzero))
+    fmode = 2;
+  const int xb = ((fmode == 2 || fmode == 4) && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 4) &&
+                  poll % g_knobs.cg_xbatch == 0)
                      ? g_knobs.cg_xbatch : 1;
   Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist, xb == 4 ? nv : 0, xb == 4 ? nv : 0})));
   struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
@@ -1319,6 +1325,11 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       timer.begin();
       nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg, fdot_p);
       timer.end();
+    } else if (fmode == 4 && it > 0) {
+      timer.begin();
+      nb_spmv = pair_zmcg_launch(A, s, hist_d, dinv.mode, dinv.c, r.p, pbs.b[0], pbs.b[1], x, w.p, part.p, fdot_p, st);
+      timer.end();
+      if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG mode 4 without its MatMult");
     } else if (xb > 1) {
       cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb);
       timer.begin();
@@ -1398,7 +1409,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       graph = false;
     }
   };
-  if (graph && !use_graph && c->size == 1 && p.max_it > 0) capture();
+  // mode 4: iteration 0 (its direction update also forms the initial norms)
+  // runs as mode 2, eagerly; the captured batches start at iteration 1
+  if (fmode == 4 && p.max_it > 0) iteration(i++);
+  if (graph && !use_graph && c->size == 1 && i < p.max_it) capture();
   for (; i < p.max_it;) {
     if (use_graph && p.max_it - i >= poll) {
       HIPCHECK(hipGraphLaunch(A->cg_graph, st));

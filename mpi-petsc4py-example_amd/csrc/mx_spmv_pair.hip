@@ -31,6 +31,7 @@
 // Each row still sums its entries in ascending column order, one rounding per
 // multiply and add (PETSc's MatMult_SeqAIJ), so the product is bitwise equal
 // to the general kernel's and to the oracle's (tests/test_gpu_vcodes.py).
+#include "mx_cg.hpp"
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 #include "mx_pair.hpp"
@@ -267,6 +268,309 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
   }
 }
 
+
+// 27-point z-march (Sell::puni27).  The nine runs are (dz, dy) in {-1,0,1}^2
+// at anchors -D-n, -D, -D+n, -n, 0, +n, D-n, D, D+n (each a tri run c-1, c,
+// c+1); marching a column in z, the runs of planes z-1 and z (six pairs and
+// their edge values) are carried and a unit loads only plane z+1's three runs
+// and edges: 3 pair loads + 3 edge loads instead of 9 + 9.  CLEAN: the
+// block's flags (PairUni27::flags) zero lane 0's / lane 63's edge values where
+// the x-line starts / ends -- at use, so the carried values stay the real x
+// for the next unit; units with an empty run take the select body.
+template <int MODE, bool SPLIT, bool CLEAN>
+__device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e)[9], uint32_t bw,
+                                            const PairUni27 *__restrict__ puni, double *__restrict__ y, int r0,
+                                            int lane, double &dot) {
+  constexpr int K = 27;
+  const PairUni27 &B = puni[bw & PBLK_ID];                // wave-uniform: scalar loads
+  double s0v = 0.0, s1v = 0.0;
+  // SEL: presence by the lane masks (every unit of a !CLEAN layout; a clean
+  // layout's units with an empty run -- the y/z-boundary classes, whose
+  // empty runs read real x of the neighbouring line or plane).  !SEL: no
+  // selects; lane 0's / lane 63's edge value is zeroed where the x-line
+  // starts / ends (U27_ELO / U27_EHI), so sum + v * 0.0 = sum
+  auto body = [&](auto selc, bool zlo, bool zhi) __attribute__((always_inline)) {
+    constexpr bool SEL = decltype(selc)::value;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      double er = e[r];
+      if constexpr (!SEL) er = (lane == 0 ? zlo : zhi) ? 0.0 : er;
+      const double lo = wave_shift<true>(L[r].y, er);     // x[r0 + c - 1]
+      const double hi = wave_shift<false>(L[r].x, er);    // x[r0 + c + 2]
+      const double a0[3] = {lo, L[r].x, L[r].y}, a1[3] = {L[r].x, L[r].y, hi};
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int j = 3 * r + p;
+        const double q0 = s0v + B.v[j] * a0[p], q1 = s1v + B.v[K + j] * a1[p];
+        if constexpr (SEL) {
+          s0v = __builtin_amdgcn_inverse_ballot_w64(B.pm[j]) ? q0 : s0v;
+          s1v = __builtin_amdgcn_inverse_ballot_w64(B.pm[K + j]) ? q1 : s1v;
+        } else {
+          s0v = q0;
+          s1v = q1;
+        }
+      }
+    }
+  };
+  if constexpr (CLEAN) {
+    const uint32_t fl = B.flags;
+    if (fl & 0x1ffu) body(std::true_type{}, false, false);   // wave-uniform
+    else body(std::false_type{}, (fl & U27_ELO) != 0, (fl & U27_EHI) != 0);
+  } else {
+    body(std::true_type{}, false, false);
+  }
+  *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
+  if constexpr (MODE == SPMV_DOT) {
+    const bool gh = SPLIT && (bw & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+    if (!gh) {
+      dot += L[4].x * s0v;
+      dot += L[4].y * s1v;
+    }
+  }
+}
+
+struct PairLean27Args {
+  int n, P, NZ, L, S;
+  int anchor[9];
+  double *partials;
+  const int *done;
+  Fold fold;
+};
+
+template <int MODE, bool SPLIT, bool CLEAN, int ZU>
+__global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
+                                                             double *__restrict__ y, const int32_t *__restrict__ pblk,
+                                                             const PairUni27 *__restrict__ puni) {
+  if (a.done && *a.done) return;   // wave-uniform: solver finished
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[7];
+  const int eb = lane == 0 ? -1 : 128;                   // edge: lane 0 x[ub + c - 1], others x[ub + 128 + c]
+  double dot = 0.0;
+  const int ntask = (se - sb) * a.P;
+  for (int t = w; t < ntask; t += W) {
+    const int seg = sb + t / a.P, col = t % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;
+    dbl2 C[6];                                           // runs 0..5 of the current unit (planes z-1, z)
+    double Ce[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      C[r] = bload2(xr, z0 * D + cb + a.anchor[r]);
+      Ce[r] = bload1(xr, z0 * D + col * 128 + eb + a.anchor[r]);
+    }
+    uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
+    auto step = [&](int z, auto nq) __attribute__((always_inline)) {
+      constexpr int NQ = decltype(nq)::value;
+      dbl2 Nw[NQ][3];
+      double Ne[NQ][3];
+      uint32_t bw[NQ];
+      bw[0] = bwn;
+#pragma unroll
+      for (int q = 1; q < NQ; ++q) bw[q] = (uint32_t)pblk[(z + q) * a.P + col];
+      if (z + NQ < z1) bwn = (uint32_t)pblk[(z + NQ) * a.P + col];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          Nw[q][k] = bload2(xr, r0 + a.anchor[6 + k]);
+          Ne[q][k] = bload1(xr, ub + eb + a.anchor[6 + k]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        dbl2 L[9];
+        double e[9];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) { L[r] = C[r]; e[r] = Ce[r]; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { L[6 + k] = Nw[q][k]; e[6 + k] = Ne[q][k]; }
+        pair_unit27<MODE, SPLIT, CLEAN>(L, e, bw[q], puni, y, (z + q) * D + cb, lane, dot);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          C[k] = C[3 + k]; Ce[k] = Ce[3 + k];
+          C[3 + k] = Nw[q][k]; Ce[3 + k] = Ne[q][k];
+        }
+      }
+    };
+    int z = z0;
+    for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
+    for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
+  }
+  if constexpr (MODE == SPMV_DOT) {
+    double v[1] = {dot};
+    block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  }
+}
+
+
+// CG mode 4 (knob 9 = 4): the direction update rides in the z-march MatMult.
+// Every operand value is formed where it is read, p_i(j) = z(j) + b p_{i-1}(j)
+// with z = r (JM 0) or c r (JM 2, uniform Jacobi) -- cg_pb_kernel's row(),
+// the same expression, so the same bits -- from r and p_{i-1}, which no
+// kernel of this launch writes.  Along a column the formed -D and centre
+// pairs are carried, so the +D plane (r and p_{i-1}: the lines read from HBM
+// for the first time) is formed once per unit; the +-n pairs and the edge
+// values are formed from L2-resident r / p_{i-1} lines.  At its own rows a
+// unit stores p_i (the centre pair) into buffer i % 2 and, every second
+// iteration, applies the two pending x steps (x = fma(a_{i-1}, p_{i-1},
+// fma(a_{i-2}, p_{i-2}, x)), reading p_{i-2} from that buffer before p_i
+// overwrites it -- cg_pb_kernel's batch).  The grid, the task order and the
+// per-lane p.w order are the plain z-march MatMult's, so mode 4 gives mode
+// 2's bits (tests/test_gpu_cgfuse.py).  One rank; iteration 0 runs as mode 2
+// (its direction update also forms the initial norms).
+struct PairCgArgs {
+  KspState *s;
+  double *hist;
+  double c;                    // JM 2: the uniform Jacobi scalar 1 / d
+};
+
+template <int PS, bool CLEAN, int ZU, int JM>
+__global__ void __launch_bounds__(256) spmv_pair_zmcg_kernel(const PairLeanArgs a, const PairCgArgs cga,
+                                                             const double *__restrict__ r, double *__restrict__ pb0,
+                                                             double *__restrict__ pb1, double *__restrict__ xv,
+                                                             double *__restrict__ y, const int32_t *__restrict__ pblk,
+                                                             const PairUni *__restrict__ puni) {
+  const CgTopIn top = cga.s->top;
+  if (top.done) return;                            // wave-uniform: solver finished
+  const CgTop t = cg_top(top);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(cga.s, t, cga.hist);
+  if (t.reason) return;
+  const int it = t.i;
+  const double bb = t.b, jc = cga.c;
+  // p_{i-1} in buffer (i - 1) % 2, p_i into buffer i % 2 (wave-uniform selects)
+  const double *__restrict__ pprev = (it & 1) ? pb0 : pb1;
+  double *__restrict__ pout = (it & 1) ? pb1 : pb0;
+  const bool xbatch = (it & 1) == 0 && top.xhi == it && top.xlo == it - 2;
+  const double al0 = top.xal[0], al1 = top.xal[1];
+  const bool xz = top.xlo == 0 && cga.s->guess_zero;   // x's first write: not read (+0.0)
+  auto form = [&](double rr, double po) __attribute__((always_inline)) -> double {
+    const double z = JM == 2 ? rr * jc : rr;
+    return (bb == 0.0) ? z : z + bb * po;             // VecAYPX_Seq (b == 0 copies)
+  };
+  auto form2 = [&](dbl2 rv, dbl2 pv) __attribute__((always_inline)) -> dbl2 {
+    return dbl2{form(rv.x, pv.x), form(rv.y, pv.y)};
+  };
+  using SH = PairShape<PS>;
+  constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t rr_ = vec_rsrc(r, a.n), pr_ = vec_rsrc(pprev, a.n);
+  const int D = a.anchor[LAST];
+  const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
+  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
+  double dot = 0.0;
+  const int ntask = (se - sb) * a.P;
+  for (int tk = w; tk < ntask; tk += W) {
+    const int seg = sb + tk / a.P, col = tk % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;
+    // carried: the formed -D and centre pairs, and p_{i-1} at the centre
+    dbl2 pcr = bload2(pr_, z0 * D + cb);
+    dbl2 zm = form2(bload2(rr_, z0 * D + cb - D), bload2(pr_, z0 * D + cb - D)), c = form2(bload2(rr_, z0 * D + cb), pcr);
+    uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
+    auto step = [&](int z, auto nq) __attribute__((always_inline)) {
+      constexpr int NQ = decltype(nq)::value;
+      dbl2 Rr[NQ][NR], Pp[NQ][NR];             // raw r / p_{i-1} of the loaded runs
+      double er[NQ], ep[NQ];
+      dbl2 xo[NQ], po2[NQ];
+      uint32_t bw[NQ];
+      bw[0] = bwn;
+#pragma unroll
+      for (int q = 1; q < NQ; ++q) bw[q] = (uint32_t)pblk[(z + q) * a.P + col];
+      if (z + NQ < z1) bwn = (uint32_t)pblk[(z + NQ) * a.P + col];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
+        Rr[q][LAST] = bload2(rr_, r0 + D);
+        Pp[q][LAST] = bload2(pr_, r0 + D);
+#pragma unroll
+        for (int rn = 1; rn < LAST; ++rn)
+          if (rn != TR) {
+            const int o = r0 + a.anchor[rn] + (CLEAN && (bw[q] & (PBLK_RUN0 << rn)) ? PAIR_OOR : 0);
+            Rr[q][rn] = bload2(rr_, o);
+            Pp[q][rn] = bload2(pr_, o);
+          }
+        int eo = ecst;
+        if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
+        er[q] = bload1(rr_, ub + eo);
+        ep[q] = bload1(pr_, ub + eo);
+        if (xbatch) {                            // p_{i-2} and x at the own rows (own lanes only)
+          po2[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(pout + r0));
+          xo[q] = xz ? dbl2{0.0, 0.0} : __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(xv + r0));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r0 = (z + q) * D + cb;
+        dbl2 L[NR];
+        const dbl2 pnext = form2(Rr[q][LAST], Pp[q][LAST]);
+#pragma unroll
+        for (int rn = 1; rn < LAST; ++rn)
+          if (rn != TR) L[rn] = form2(Rr[q][rn], Pp[q][rn]);
+        L[0] = zm;
+        L[TR] = c;
+        L[LAST] = pnext;
+        const double e = form(er[q], ep[q]);
+        // own rows: p_i (the centre pair), then the batched x steps from
+        // p_{i-2} (read above, before this store) and p_{i-1}
+        if (xbatch) {
+          const dbl2 xx = dbl2{fma(al0, po2[q].x, xo[q].x), fma(al0, po2[q].y, xo[q].y)};
+          const dbl2 xn = dbl2{fma(al1, pcr.x, xx.x), fma(al1, pcr.y, xx.y)};
+          __builtin_nontemporal_store(xn, reinterpret_cast<dbl2 *>(xv + r0));
+        }
+        *reinterpret_cast<dbl2 *>(pout + r0) = c;
+        if constexpr (CLEAN) {
+          if (bw[q] & CARRY) {                     // wave-uniform, rare: an empty carried run
+            if (bw[q] & PBLK_RUN0) L[0] = dbl2{0.0, 0.0};
+            if (bw[q] & (PBLK_RUN0 << TR)) L[TR] = dbl2{0.0, 0.0};
+            if (bw[q] & (PBLK_RUN0 << LAST)) L[LAST] = dbl2{0.0, 0.0};
+          }
+        }
+        pair_unit<SPMV_DOT, PS, false, CLEAN>(L, e, bw[q], puni, y, r0, lane, dot);
+        zm = c;
+        c = pnext;
+        pcr = Pp[q][LAST];
+      }
+    };
+    int z = z0;
+    for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
+    for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
+  }
+  double v[1] = {dot};
+  block_partials<1>(v, a.partials, gridDim.x, a.fold);
+}
+
 using LeanFn = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const PairUni *);
 
 // the layout side of the choice (mode and split aside): 0 none, 1 lean, 2 lean select-free
@@ -275,6 +579,17 @@ int pair_lean_kind(const Mat *A) {
   if (!g_knobs.pair_lean || !g_knobs.vcodes || !g_knobs.spmv_pairs || !g_knobs.pair_uni || g_knobs.spmv_ynt ||
       g_knobs.spmv_rev)
     return 0;
+  if (S.pair_shape == 27) {    // the 27-point form exists as a z-march only
+    if (S.ntab <= 0 || !S.puni27.p || S.pair_blocks <= 0 || !S.pair_all || !g_knobs.pair_zm) return 0;
+    if (A->m % 128 != 0 || A->m >= PAIR_MAX_ROWS || A->n >= PAIR_MAX_ROWS || S.nunits * 128 != A->m) return 0;
+    int an[9];
+    for (int r = 0; r < 9; ++r) an[r] = S.pat_star_off[(size_t)(3 * r + 1)];
+    const int D = an[7];
+    if (D <= 0 || D % 128 != 0 || A->m % D != 0) return 0;
+    for (int r = 0; r < 6; ++r)
+      if (an[r + 3] - an[r] != D) return 0;
+    return S.pair_clean27 ? 2 : 1;
+  }
   if (S.ntab <= 0 || (S.pair_shape != 5 && S.pair_shape != 7) || !S.puni.p || S.pair_blocks <= 0 || !S.pair_all)
     return 0;
   if (A->m % 128 != 0 || A->m >= PAIR_MAX_ROWS || A->n >= PAIR_MAX_ROWS || S.nunits * 128 != A->m) return 0;
@@ -294,6 +609,7 @@ static void pair_anchors(const Sell &S, int anchor[5]) {
 // z-march: the outermost runs are -D, +D with D a multiple of 128 rows, m a multiple of D
 bool pair_zm_applies(const Mat *A) {
   const Sell &S = A->sd;
+  if (S.pair_shape == 27) return pair_lean_kind(A) > 0;   // its only form
   if (!g_knobs.pair_zm || (S.pair_shape != 5 && S.pair_shape != 7)) return false;
   int anchor[5];
   pair_anchors(S, anchor);
@@ -312,6 +628,38 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   if (!kind) return 0;
   if (!split && (A->nghost > 0 || S.pair_ghosts)) return 0;   // A_o continues in the general kernel
   const bool clean = kind == 2;
+  if (S.pair_shape == 27) {
+    PairLean27Args b{};
+    b.n = (int)A->n;
+    for (int r = 0; r < 9; ++r) b.anchor[r] = S.pat_star_off[(size_t)(3 * r + 1)];
+    const int D = b.anchor[7];
+    b.P = D / 128;
+    b.NZ = (int)(A->m / D);
+    int grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
+    grid &= ~7;
+    const int W = grid / 8 * LEAN_WAVES;
+    const int slab = (b.NZ + 7) / 8;
+    int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
+    while (L > 1 && (int64_t)b.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
+    b.L = L;
+    b.S = (b.NZ + L - 1) / L;
+    b.partials = partials;
+    b.done = done;
+    Fold fold = fold_in;
+    if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+    b.fold = fold;
+    using F27 = void (*)(PairLean27Args, const double *, double *, const int32_t *, const PairUni27 *);
+    F27 f = nullptr;
+    const bool z2 = g_knobs.pair_zm_units == 2;
+#define Z27(MODE, SP) do { if (clean) f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, true, 2> : &spmv_pair_zm27_kernel<MODE, SP, true, 1>; \
+                           else f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, false, 2> : &spmv_pair_zm27_kernel<MODE, SP, false, 1>; } while (0)
+    if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
+    else { if (split) Z27(SPMV_DOT, true); else Z27(SPMV_DOT, false); }
+#undef Z27
+    launch_timed(f, grid, st, b, x, y, S.pblk.p, S.puni27.p);
+    HIPCHECK(hipGetLastError());
+    return grid;
+  }
   PairLeanArgs a{};
   a.m = (int)A->m;
   a.n = (int)A->n;
@@ -356,6 +704,53 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   a.fold = fold;
   launch_timed(f, grid, st, a, x, y, S.pblk.p, S.puni.p);
+  HIPCHECK(hipGetLastError());
+  return grid;
+}
+
+// CG mode 4 (spmv_pair_zmcg_kernel): applies on one rank to a lean z-march
+// layout with no or uniform Jacobi; returns the grid, 0 when it does not apply
+bool pair_zmcg_applies(const Mat *A, int jac_mode) {
+  return A->comm->size == 1 && A->sd.pair_shape != 27 && (jac_mode == 0 || jac_mode == 2) && pair_lean_kind(A) > 0 &&
+         pair_zm_applies(A) &&
+         A->nghost == 0 && !A->sd.pair_ghosts;
+}
+
+int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac_c, const double *r, double *pb0,
+                     double *pb1, double *x, double *w, double *partials, const Fold *fold_in, hipStream_t st) {
+  if (!pair_zmcg_applies(A, jac_mode)) return 0;
+  const Sell &S = A->sd;
+  PairLeanArgs a{};
+  a.m = (int)A->m;
+  a.n = (int)A->n;
+  a.nunits = (int)S.nunits;
+  pair_anchors(S, a.anchor);
+  a.partials = partials;
+  const int D = a.anchor[S.pair_shape == 5 ? 2 : 4];
+  a.P = D / 128;
+  a.NZ = (int)(A->m / D);
+  int grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
+  grid &= ~7;
+  const int W = grid / 8 * LEAN_WAVES;
+  const int slab = (a.NZ + 7) / 8;
+  int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
+  while (L > 1 && (int64_t)a.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
+  a.L = L;
+  a.S = (a.NZ + L - 1) / L;
+  Fold fold = fold_in ? *fold_in : Fold{};
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  a.fold = fold;
+  const PairCgArgs c{s, hist, jac_c};
+  const bool clean = pair_lean_kind(A) == 2;
+  using F = void (*)(PairLeanArgs, PairCgArgs, const double *, double *, double *, double *, double *,
+                     const int32_t *, const PairUni *);
+  F f = nullptr;
+#define ZMCG(PS, CL) do { if (jac_mode == 2) f = g_knobs.pair_zm_units == 2 ? &spmv_pair_zmcg_kernel<PS, CL, 2, 2> : &spmv_pair_zmcg_kernel<PS, CL, 1, 2>; \
+                          else f = g_knobs.pair_zm_units == 2 ? &spmv_pair_zmcg_kernel<PS, CL, 2, 0> : &spmv_pair_zmcg_kernel<PS, CL, 1, 0>; } while (0)
+  if (S.pair_shape == 5) { if (clean) ZMCG(5, true); else ZMCG(5, false); }
+  else { if (clean) ZMCG(7, true); else ZMCG(7, false); }
+#undef ZMCG
+  launch_timed(f, grid, st, a, c, r, pb0, pb1, x, w, S.pblk.p, S.puni.p);
   HIPCHECK(hipGetLastError());
   return grid;
 }
