@@ -299,6 +299,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 41: z-march segment length in planes (default 32, shortened when a slab
  *         has too few columns for every wave)
  * key 42: z-march planes per step (1 or 2, default 2)
+ * key 43: grid of the SpMV for fp64-valued (uncoded) layouts (default 8192
+ *         workgroups; 0 = the resident grid of key 26)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

@@ -523,6 +523,7 @@ int mx_debug_set(int key, int value) {
     case 40: old = g_knobs.pair_zm_bpc; g_knobs.pair_zm_bpc = std::min(std::max(value, 1), 8); break;
     case 41: old = g_knobs.pair_zm_len; g_knobs.pair_zm_len = std::min(std::max(value, 1), 1024); break;
     case 42: old = g_knobs.pair_zm_units; g_knobs.pair_zm_units = value == 2 ? 2 : 1; break;
+    case 43: old = g_knobs.spmv_fp64_grid; g_knobs.spmv_fp64_grid = std::min(std::max(value, 0), 65536); break;
     default: break;
   }
   return old;

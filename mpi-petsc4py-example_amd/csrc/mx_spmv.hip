@@ -707,11 +707,11 @@ int device_cu_count() {
 int spmv_blocks(const Mat *A, int) {
   const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
   const int64_t cap = g_knobs.spmv_grid > 0 ? g_knobs.spmv_grid : 8 * (int64_t)device_cu_count();
-  return (int)std::max<int64_t>(1, std::min<int64_t>(need, std::max<int64_t>(cap, 8192)));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(need, std::max<int64_t>({cap, (int64_t)8192, (int64_t)g_knobs.spmv_fp64_grid})));
 }
 
-// Grid of the main SpMV launch: exactly the workgroups that are resident at
-// once (one generation).  Each XCD then walks its slices in one sweep with a
+// Grid of the main SpMV launch (value-coded layouts): exactly the workgroups
+// that are resident at once (one generation).  Each XCD then walks its slices in one sweep with a
 // window of ~ the resident waves, so the x lines of the +-n^2 neighbours are
 // re-read from L2 (tools/pmc_spmv.sh: FETCH_SIZE = the compulsory bytes at
 // this grid, ~2x at a 4.6-generation grid) and no second generation leaves a
@@ -725,8 +725,15 @@ int spmv_blocks(const Mat *A, int) {
 int main_grid(const Mat *A, int mode, const void *kf, bool pairs) {
   const int64_t need = cdiv(A->sd.nslices, SPMV_WAVES);
   int64_t g;
+  const bool coded = A->sd.ntab > 0 && g_knobs.vcodes;
   if (g_knobs.spmv_grid > 0) {
     g = g_knobs.spmv_grid;
+  } else if (!pairs && !coded && g_knobs.spmv_fp64_grid > 0) {
+    // fp64 values streamed (more than 255 distinct values): the matrix stream
+    // dominates, and several workgroup generations keep more of it in flight
+    // than one resident generation (variable-coefficient 7-point 256^3:
+    // 214 -> 203 us standalone, CG -4% per iteration at 8192; knob 43)
+    g = g_knobs.spmv_fp64_grid;
   } else {
     static std::unordered_map<const void *, int> bpc_of;
     int bpc;

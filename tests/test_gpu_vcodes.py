@@ -123,6 +123,7 @@ def test_cg_with_and_without_codes(selfcomm):
     L = lib()
     res = []
     old27 = L.mx_debug_set(27, 0)          # single-row layout in both (same dot grouping)
+    old43 = L.mx_debug_set(43, 0)          # and the same (resident) grid for the fp64 values
     for knob in (0, 1):
         old = L.mx_debug_set(23, knob)
         try:
@@ -136,6 +137,7 @@ def test_cg_with_and_without_codes(selfcomm):
         finally:
             L.mx_debug_set(23, old)
     L.mx_debug_set(27, old27)
+    L.mx_debug_set(43, old43)
     assert res[0][3] == 0 and res[1][3] > 0
     assert res[0][:2] == res[1][:2]
     assert np.array_equal(res[0][2].view(np.uint64), res[1][2].view(np.uint64))
