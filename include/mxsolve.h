@@ -104,6 +104,10 @@ typedef struct {
   int64_t pair_zmarch;                /* 1: the lean kernel marches columns of units one
                                          plane (3D) / line (2D) apart, carrying two
                                          operand pairs in registers (key 39)          */
+  int64_t pair_f64;                   /* 5 / 7: the fp64-valued (uncoded) layout also has
+                                         row pairs -- each unit's values streamed as
+                                         16-byte pairs -- and the z-march MatMult runs on
+                                         them (one rank, select-free units; key 44)    */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */
@@ -301,6 +305,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 42: z-march planes per step (1 or 2, default 2)
  * key 43: grid of the SpMV for fp64-valued (uncoded) layouts (default 8192
  *         workgroups; 0 = the resident grid of key 26)
+ * key 44: fp64 row-pair layout + z-march MatMult for uncoded 5/7-point blocks
+ *         (read at assembly; 0/1, default 1; the same bits)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

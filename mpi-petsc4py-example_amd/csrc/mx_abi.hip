@@ -244,6 +244,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_uniform = info->pair_shape && info->pair_blocks > 0 && (A->sd.puni.p || A->sd.puni27.p) ? 1 : 0;
     info->pair_lean = pair_lean_kind(A);
     info->pair_zmarch = info->pair_lean && pair_zm_applies(A) ? 1 : 0;
+    info->pair_f64 = pair_f64_kind(A);
   });
 }
 
@@ -524,6 +525,7 @@ int mx_debug_set(int key, int value) {
     case 41: old = g_knobs.pair_zm_len; g_knobs.pair_zm_len = std::min(std::max(value, 1), 1024); break;
     case 42: old = g_knobs.pair_zm_units; g_knobs.pair_zm_units = value == 2 ? 2 : 1; break;
     case 43: old = g_knobs.spmv_fp64_grid; g_knobs.spmv_fp64_grid = std::min(std::max(value, 0), 65536); break;
+    case 44: old = g_knobs.pair_f64; g_knobs.pair_f64 = value; break;
     default: break;
   }
   return old;

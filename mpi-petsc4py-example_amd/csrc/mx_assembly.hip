@@ -954,6 +954,110 @@ __global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star,
   if (lane == 0) dpat[s0] |= DPAT_PAIR;
 }
 
+// fp64 row pairs (Sell::pval / pflag): one wave per unit, the pair_fill_kernel
+// slot mapping with values instead of codes; the unit's presence ballots give
+// its select-free flags (build_pair_uniform's rule), and a unit that is not
+// select-free (or not a pair unit) clears *clean
+__global__ void pair_fill_f64_kernel(int64_t m, int64_t nunits, int k, int ps, int32_t star,
+                                     const int64_t *__restrict__ sptr, const int32_t *__restrict__ width,
+                                     const int32_t *__restrict__ dpat, const int32_t *__restrict__ doff,
+                                     const double *__restrict__ sval, const uint32_t *__restrict__ mask,
+                                     const uint8_t *__restrict__ mask8, double *__restrict__ pval,
+                                     int32_t *__restrict__ pflag, int *__restrict__ clean) {
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= nunits) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t *__restrict__ so = doff + (int64_t)star * DIA_MAX;
+  auto slot_of = [&](int64_t sl, int j) -> int {
+    const int32_t *__restrict__ po = doff + (int64_t)(dpat[sl] & DPAT_ID) * DIA_MAX;
+    for (int q = 0; q < -width[sl]; ++q)
+      if (po[q] == so[j]) return q;
+    return -1;
+  };
+  auto ok = [&](int64_t sl) {
+    if (width[sl] >= 0) return false;
+    const int32_t *__restrict__ po = doff + (int64_t)(dpat[sl] & DPAT_ID) * DIA_MAX;
+    for (int q = 0; q < -width[sl]; ++q) {
+      bool in = false;
+      for (int j = 0; j < k; ++j) in = in || po[q] == so[j];
+      if (!in) return false;
+    }
+    return true;
+  };
+  if (u * 128 + 127 >= m || !ok(2 * u) || !ok(2 * u + 1)) {   // wave-uniform
+    if (lane == 0) *clean = 0;
+    return;
+  }
+  unsigned long long pm[2][8];
+  for (int j = 0; j < k; ++j) {
+    double v[2];
+    bool pr[2];
+    for (int h = 0; h < 2; ++h) {
+      const int64_t row = u * 128 + 2 * lane + h;
+      const int64_t sl = row >> 6;
+      const int li = (int)(row & 63);
+      const uint32_t mk = mask8 ? (uint32_t)mask8[row] : mask[row];
+      const int q = slot_of(sl, j);
+      pr[h] = q >= 0 && ((mk >> q) & 1u);
+      v[h] = pr[h] ? sval[sell_slot(sptr[sl], q, -width[sl], li, true)] : 0.0;
+    }
+    reinterpret_cast<double2 *>(pval)[(u * k + j) * 64 + lane] = make_double2(v[0], v[1]);
+    pm[0][j] = __ballot(pr[0]);
+    pm[1][j] = __ballot(pr[1]);
+  }
+  if (lane != 0) return;
+  const unsigned long long F = ~0ull;
+  const int NR = ps == 5 ? 3 : 5;
+  uint32_t f = 0;
+  bool cl = true;
+  for (int r = 0; r < NR && cl; ++r) {
+    const bool tri = ps == 5 ? r == 1 : r == 2;
+    const int j = ps == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
+    if (!tri) {
+      if (pm[0][j] == 0 && pm[1][j] == 0) f |= PBLK_RUN0 << r;
+      else if (pm[0][j] != F || pm[1][j] != F) cl = false;
+      continue;
+    }
+    const unsigned long long m0 = pm[0][j], m1 = pm[0][j + 1], m2 = pm[0][j + 2];
+    const unsigned long long n0 = pm[1][j], n1 = pm[1][j + 1], n2 = pm[1][j + 2];
+    if ((m0 | m1 | m2 | n0 | n1 | n2) == 0) { f |= (PBLK_RUN0 << r) | PBLK_ELO | PBLK_EHI; continue; }
+    if (m1 != F || m2 != F || n0 != F || n1 != F) cl = false;
+    else if (m0 != F && m0 != (F & ~1ull)) cl = false;
+    else if (n2 != F && n2 != (F >> 1)) cl = false;
+    if (m0 != F) f |= PBLK_ELO;
+    if (n2 != F) f |= PBLK_EHI;
+  }
+  pflag[u] = (int32_t)f;
+  if (!cl) *clean = 0;
+}
+
+// fp64 row-pair layout for uncoded 5/7-point diagonal blocks of one rank
+static void build_pair_f64(Sell &S, int64_t m, int64_t ncols, bool one_rank, hipStream_t st) {
+  S.pval.reset();
+  S.pflag.reset();
+  S.pair_f64 = 0;
+  if (!g_knobs.pair_f64 || !one_rank || S.ntab > 0 || S.pat_star < 0 || m % 128 != 0 || m > (int64_t(1) << 27) ||
+      ncols > (int64_t(1) << 27) || S.nslices * 64 != m)
+    return;
+  const int ps = pair_shape_of(S.pat_star_off);
+  if ((ps != 5 && ps != 7) || S.dia_k != ps) return;
+  const int64_t nu = m / 128;
+  S.pval.alloc((size_t)nu * ps * 128);
+  S.pflag.alloc((size_t)nu);
+  DBuf<int> clean(1);
+  const int one = 1;
+  HIPCHECK(hipMemcpyAsync(clean.p, &one, sizeof(int), hipMemcpyHostToDevice, st));
+  pair_fill_f64_kernel<<<(unsigned)cdiv(nu, 4), 256, 0, st>>>(m, nu, ps, ps, S.pat_star, S.sptr.p, S.width.p, S.dpat.p,
+                                                              S.doff.p, S.val.p, S.mask.p, S.mask8.p, S.pval.p,
+                                                              S.pflag.p, clean.p);
+  HIPCHECK(hipGetLastError());
+  int hc = 0;
+  HIPCHECK(hipMemcpyAsync(&hc, clean.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  if (!hc) { S.pval.reset(); S.pflag.reset(); return; }
+  S.pair_f64 = ps;
+}
+
 __global__ void pair_count_kernel(int64_t nunits, const int32_t *__restrict__ dpat, unsigned long long *__restrict__ cnt) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool p = u < nunits && (dpat[2 * u] & DPAT_PAIR);
@@ -1590,6 +1694,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
   build_sell(A->so, m, A->nghost, A->optr.p, A->ocol.p, A->oval.p, st, false);
   build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, A->n, st);
+  build_pair_f64(A->sd, m, A->n, !multi, st);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
 

@@ -175,6 +175,14 @@ struct Sell {
   DBuf<PairUni> puni;
   bool pair_clean = false;  // every puni block is select-free (PBLK_RUN0/ELO/EHI flags in pblk)
   DBuf<PairUni27> puni27;   // 27-point uniform-slot dictionary (mx_spmv_pair.hip z-march)
+  // fp64 row pairs (uncoded 5/7-point layouts, one rank): per unit u, slot j,
+  // lane l the values of rows 128u + 2l and + 1 (0.0 where absent) as one
+  // 16-byte pair at pval[(u * K + j) * 64 + l]; pflag[u] = the unit's
+  // select-free flags (PBLK_RUN0 << r, PBLK_ELO / EHI).  Built only when every
+  // unit is select-free (mx_spmv_pair.hip spmv_pair_zmf64_kernel)
+  DBuf<double> pval;
+  DBuf<int32_t> pflag;
+  int pair_f64 = 0;         // 5 / 7: the fp64 row-pair layout's shape, 0 none
   bool pair_clean27 = false;  // every puni27 block is select-free
   // 1 / value per code (1 for a zero value and for absent slots): PCJacobi's
   // dinv of a row is dtab[its diagonal slot's code] -- the division the
@@ -206,7 +214,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
-                int spmv_fp64_grid = 8192; };
+                int spmv_fp64_grid = 8192; int pair_f64 = 1; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -346,6 +354,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
                      const Fold &fold, hipStream_t st);
 int pair_lean_kind(const Mat *A);   // 0 general kernel, 1 lean, 2 lean select-free (mx_mat_info.pair_lean)
 bool pair_zm_applies(const Mat *A);  // the lean kernel's z-march form (mx_mat_info.pair_zmarch)
+int pair_f64_kind(const Mat *A);     // 5 / 7: the fp64 row-pair z-march applies (mx_mat_info.pair_f64)
 // CG mode 4: the direction update inside the z-march MatMult (mx_spmv_pair.hip)
 bool pair_zmcg_applies(const Mat *A, int jac_mode);
 int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac_c, const double *r, double *pb0,

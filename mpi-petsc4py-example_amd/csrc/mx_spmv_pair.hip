@@ -420,6 +420,116 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Arg
 }
 
 
+// fp64 row pairs (Sell::pval, uncoded 5/7-point layouts whose every unit is
+// select-free): the z-march with the unit's values streamed (K 16-byte pairs
+// per lane, non-temporal) instead of a dictionary block's uniform values.
+// Absent slots hold 0.0 and read a 0.0 operand (the flags in Sell::pflag:
+// inner runs and edges by out-of-range reads, carried runs zeroed at use), so
+// sum + 0.0 * 0.0 = sum.  One rank (no A_o).
+template <int MODE, int PS, int ZU>
+__global__ void __launch_bounds__(256) spmv_pair_zmf64_kernel(const PairLeanArgs a, const double *__restrict__ x,
+                                                              double *__restrict__ y, const int32_t *__restrict__ pflag,
+                                                              const double *__restrict__ pval) {
+  if (a.done && *a.done) return;   // wave-uniform: solver finished
+  using SH = PairShape<PS>;
+  constexpr int K = SH::K, NR = SH::NR, C = SH::CENTER_RUN, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[LAST];
+  const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
+  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
+  const dbl2 *__restrict__ pv = reinterpret_cast<const dbl2 *>(pval) + lane;
+  double dot = 0.0;
+  const int ntask = (se - sb) * a.P;
+  for (int t = w; t < ntask; t += W) {
+    const int seg = sb + t / a.P, col = t % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;
+    dbl2 zm = bload2(xr, z0 * D + cb - D), c = bload2(xr, z0 * D + cb);
+    uint32_t fn = (uint32_t)pflag[z0 * a.P + col];
+    auto step = [&](int z, auto nq) __attribute__((always_inline)) {
+      constexpr int NQ = decltype(nq)::value;
+      dbl2 L[NQ][NR], zp[NQ], V[NQ][K];
+      double e[NQ];
+      uint32_t fl[NQ];
+      fl[0] = fn;
+#pragma unroll
+      for (int q = 1; q < NQ; ++q) fl[q] = (uint32_t)pflag[(z + q) * a.P + col];
+      if (z + NQ < z1) fn = (uint32_t)pflag[(z + NQ) * a.P + col];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int u = (z + q) * a.P + col;
+        const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
+        zp[q] = bload2(xr, r0 + D);
+#pragma unroll
+        for (int r = 1; r < LAST; ++r)
+          if (r != TR) L[q][r] = bload2(xr, r0 + a.anchor[r] + ((fl[q] & (PBLK_RUN0 << r)) ? PAIR_OOR : 0));
+        const int eo = ecst + (lane == 0 ? ((fl[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((fl[q] & PBLK_EHI) ? PAIR_OOR : 0));
+        e[q] = bload1(xr, ub + eo);
+#pragma unroll
+        for (int j = 0; j < K; ++j) V[q][j] = __builtin_nontemporal_load(pv + ((int64_t)u * K + j) * 64);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        L[q][0] = q == 0 ? zm : q == 1 ? c : zp[q - 2];
+        L[q][TR] = q == 0 ? c : zp[q - 1];
+        L[q][LAST] = zp[q];
+        if (fl[q] & CARRY) {                       // wave-uniform, rare: an empty carried run
+          if (fl[q] & PBLK_RUN0) L[q][0] = dbl2{0.0, 0.0};
+          if (fl[q] & (PBLK_RUN0 << TR)) L[q][TR] = dbl2{0.0, 0.0};
+          if (fl[q] & (PBLK_RUN0 << LAST)) L[q][LAST] = dbl2{0.0, 0.0};
+        }
+        const int r0 = (z + q) * D + cb;
+        double s0v = 0.0, s1v = 0.0, lo = 0.0, hi = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int r = SH::run(j), p = SH::pos(j);
+          if (SH::tri(r) && p < 0) {
+            lo = wave_shift<true>(L[q][r].y, e[q]);
+            hi = wave_shift<false>(L[q][r].x, e[q]);
+          }
+          double a0, a1;
+          if (!SH::tri(r)) { a0 = L[q][r].x; a1 = L[q][r].y; }
+          else if (p < 0) { a0 = lo; a1 = L[q][r].x; }
+          else if (p == 0) { a0 = L[q][r].x; a1 = L[q][r].y; }
+          else { a0 = L[q][r].y; a1 = hi; }
+          s0v = s0v + V[q][j].x * a0;
+          s1v = s1v + V[q][j].y * a1;
+        }
+        *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
+        if constexpr (MODE == SPMV_DOT) {
+          dot += L[q][C].x * s0v;
+          dot += L[q][C].y * s1v;
+        }
+      }
+      zm = NQ == 1 ? c : zp[NQ - 2];
+      c = zp[NQ - 1];
+    };
+    int z = z0;
+    for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
+    for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
+  }
+  if constexpr (MODE == SPMV_DOT) {
+    double v[1] = {dot};
+    block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  }
+}
+
 // CG mode 4 (knob 9 = 4): the direction update rides in the z-march MatMult.
 // Every operand value is formed where it is read, p_i(j) = z(j) + b p_{i-1}(j)
 // with z = r (JM 0) or c r (JM 2, uniform Jacobi) -- cg_pb_kernel's row(),
@@ -617,6 +727,75 @@ bool pair_zm_applies(const Mat *A) {
   return D > 0 && anchor[0] == -D && D % 128 == 0 && A->m % D == 0;
 }
 
+// the z-march geometry of a 5/7-point pattern given its run anchors (0: none)
+static int zm_plane(const Mat *A, int ps, const int anchor[5]) {
+  const int D = anchor[ps == 5 ? 2 : 4];
+  return D > 0 && anchor[0] == -D && D % 128 == 0 && A->m % D == 0 ? D : 0;
+}
+
+// grid, segment length and segments of a z-march over NZ planes of P columns
+static int zm_tasks(int P, int NZ, int &L, int &S) {
+  int grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
+  grid &= ~7;
+  const int W = grid / 8 * LEAN_WAVES;               // waves per XCD
+  const int slab = (NZ + 7) / 8;                      // planes per XCD
+  L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
+  while (L > 1 && (int64_t)P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
+  S = (NZ + L - 1) / L;
+  return grid;
+}
+
+// fp64 row-pair z-march (Sell::pval): applies to one-rank uncoded 5/7-point layouts
+int pair_f64_kind(const Mat *A) {
+  const Sell &S = A->sd;
+  if (!S.pair_f64 || !S.pval.p || !g_knobs.pair_lean || !g_knobs.pair_zm || A->nghost > 0) return 0;
+  int anchor[5] = {0, 0, 0, 0, 0};
+  const int ps = S.pair_f64;
+  for (int r = 0; r < (ps == 5 ? 3 : 5); ++r) {
+    const bool tri = ps == 5 ? r == 1 : r == 2;
+    const int first = ps == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
+    anchor[r] = S.pat_star_off[(size_t)(first + (tri ? 1 : 0))];
+  }
+  return zm_plane(A, ps, anchor) ? ps : 0;
+}
+
+static int pair_f64_launch(Mat *A, int mode, const double *x, double *y, double *partials, const int *done,
+                           const Fold &fold_in, hipStream_t st) {
+  const Sell &S = A->sd;
+  const int ps = S.pair_f64;
+  PairLeanArgs a{};
+  a.m = (int)A->m;
+  a.n = (int)A->n;
+  a.nunits = (int)(A->m / 128);
+  for (int r = 0; r < 5; ++r) {
+    const bool tri = ps == 5 ? r == 1 : r == 2;
+    const int first = ps == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
+    a.anchor[r] = (ps == 5 && r >= 3) ? 0 : S.pat_star_off[(size_t)(first + (tri ? 1 : 0))];
+  }
+  const int D = zm_plane(A, ps, a.anchor);
+  a.P = D / 128;
+  a.NZ = (int)(A->m / D);
+  const int grid = zm_tasks(a.P, a.NZ, a.L, a.S);
+  a.partials = partials;
+  a.done = done;
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  a.fold = fold;
+  using F = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const double *);
+  F f;
+  const bool z2 = g_knobs.pair_zm_units == 2;
+  if (mode == SPMV_PLAIN) {
+    if (ps == 5) f = z2 ? &spmv_pair_zmf64_kernel<SPMV_PLAIN, 5, 2> : &spmv_pair_zmf64_kernel<SPMV_PLAIN, 5, 1>;
+    else f = z2 ? &spmv_pair_zmf64_kernel<SPMV_PLAIN, 7, 2> : &spmv_pair_zmf64_kernel<SPMV_PLAIN, 7, 1>;
+  } else {
+    if (ps == 5) f = z2 ? &spmv_pair_zmf64_kernel<SPMV_DOT, 5, 2> : &spmv_pair_zmf64_kernel<SPMV_DOT, 5, 1>;
+    else f = z2 ? &spmv_pair_zmf64_kernel<SPMV_DOT, 7, 2> : &spmv_pair_zmf64_kernel<SPMV_DOT, 7, 1>;
+  }
+  launch_timed(f, grid, st, a, x, y, S.pflag.p, S.pval.p);
+  HIPCHECK(hipGetLastError());
+  return grid;
+}
+
 // Launch the lean MatMult for this product; returns its grid, or 0 when it
 // does not apply (the general kernel then runs).  A fold (fold.cnt set)
 // counts this launch's workgroups.
@@ -624,6 +803,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
                      const Fold &fold_in, hipStream_t st) {
   const Sell &S = A->sd;
   if (mode != SPMV_PLAIN && mode != SPMV_DOT) return 0;
+  if (!split && pair_f64_kind(A)) return pair_f64_launch(A, mode, x, y, partials, done, fold_in, st);
   const int kind = pair_lean_kind(A);
   if (!kind) return 0;
   if (!split && (A->nghost > 0 || S.pair_ghosts)) return 0;   // A_o continues in the general kernel

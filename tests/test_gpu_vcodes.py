@@ -408,3 +408,51 @@ def test_pair_lean_cg(selfcomm, oracle_mod, n):
     assert zm[:2] == off[:2]
     assert np.allclose(zm[2], off[2], rtol=1e-9, atol=0)
     assert np.linalg.norm(zm[3] - off[3]) <= 1e-10 * np.linalg.norm(off[3])
+
+
+@pytest.mark.parametrize("kind,n,f64", [("poisson3d", 128, 7), ("poisson2d", 256, 5), ("poisson3d", 64, 0)])
+def test_pair_f64_zmarch(selfcomm, oracle_mod, kind, n, f64):
+    """fp64-valued (uncoded: every entry a different value) 5/7-point blocks
+    get an fp64 row-pair layout and the z-march MatMult (knob 44 = 1, the
+    default) when every unit is select-free (x-lines a multiple of 128 rows;
+    64-row lines keep the aligned-offset SELL kernel): MatMult bit-exact
+    against the oracle and against knob 44 = 0, operands with infinities and
+    NaN included; CG on the symmetrically scaled operator D A D against the
+    oracle."""
+    from mxsolve.core import DMat
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    rng = np.random.default_rng(29)
+    f = 1.0 + 0.5 * rng.random(M)
+    rows = np.repeat(np.arange(M), np.diff(ip))
+    v = v * f[rows] * f[c]                         # D A D: SPD, ~all values distinct
+    L = lib()
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    for special in (False, True):
+        x = rng.standard_normal(M)
+        if special:
+            x[rng.integers(0, M, 40)] = np.inf
+            x[rng.integers(0, M, 40)] = -np.inf
+            x[rng.integers(0, M, 40)] = np.nan
+        exp = O.mult(x).view(np.uint64)
+        outs = []
+        for knob in (1, 0):
+            def run():
+                A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+                y = torch.zeros(M, dtype=torch.float64, device="cuda")
+                A.mult(torch.from_numpy(x).cuda(), y)
+                info = A.info()
+                A.destroy()
+                return info, y.cpu().numpy().view(np.uint64)
+            outs.append(_with_knob(L, 44, knob, run))
+        (i1, g1), (i0, g0) = outs
+        assert i1["value_codes"] == 0 and i1["pair_f64"] == f64 and i0["pair_f64"] == 0
+        assert np.array_equal(g1, exp) and np.array_equal(g0, exp)
+    A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+    b = rng.random(M)
+    xs = torch.zeros(M, dtype=torch.float64, device="cuda")
+    r = A.solve(torch.from_numpy(b).cuda(), xs, ksp="cg", rtol=1e-8)
+    A.destroy()
+    o = O.solve(b, ksp="cg", rtol=1e-8)
+    assert r["reason"] == o["reason"] and abs(r["its"] - o["its"]) <= 1
+    assert np.linalg.norm(xs.cpu().numpy() - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])

@@ -94,10 +94,13 @@ def random_csr(N: int, k: int = 6, seed: int = 11):
 def streamed_bytes(info) -> int:
     """Bytes the SpMV streams for this layout: value-coded layouts as bench.py
     counts them (codes or dictionary block ids, x once, y once, slice
-    metadata); fp64 layouts: A_d slots (aligned-offset slices: 8 B value + the
+    metadata); fp64 row pairs (mx_mat_info.pair_f64): K values per row and a
+    flag word per 128 rows, x once, y once; other fp64 layouts: A_d slots (aligned-offset slices: 8 B value + the
     row's mask byte; general slices 12 B per slot incl. padding), x read once,
     y written once, 16 B of slice metadata per slice."""
     m, slots = info["m"], info["sell_slots_d"]
+    if info.get("pair_f64"):                  # fp64 row pairs: K values per row (0.0 where absent) + a flag word per 128 rows
+        return 8 * info["pair_f64"] * m + 4 * (m // 128) + 16 * m
     if info.get("value_codes"):
         return spmv_format_bytes(info, m, info["nnz_d"] + info["nnz_o"], info["nghost"])
     if info["dia_slices"] * 64 >= m:          # every slice aligned-offset
