@@ -307,6 +307,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         workgroups; 0 = the resident grid of key 26)
  * key 44: fp64 row-pair layout + z-march MatMult for uncoded 5/7-point blocks
  *         (read at assembly; 0/1, default 1; the same bits)
+ * key 45: 27-point z-march resident workgroups per CU (default 3; 0 = key 40)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Calibration stream for PMC byte counters: reads n doubles once with

@@ -526,6 +526,7 @@ int mx_debug_set(int key, int value) {
     case 42: old = g_knobs.pair_zm_units; g_knobs.pair_zm_units = value == 2 ? 2 : 1; break;
     case 43: old = g_knobs.spmv_fp64_grid; g_knobs.spmv_fp64_grid = std::min(std::max(value, 0), 65536); break;
     case 44: old = g_knobs.pair_f64; g_knobs.pair_f64 = value; break;
+    case 45: old = g_knobs.pair_zm27_bpc; g_knobs.pair_zm27_bpc = std::min(std::max(value, 0), 8); break;
     default: break;
   }
   return old;

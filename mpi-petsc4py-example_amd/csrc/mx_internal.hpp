@@ -214,7 +214,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
-                int spmv_fp64_grid = 8192; int pair_f64 = 1; };
+                int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 3; };
 extern Knobs g_knobs;
 
 struct Halo {

@@ -815,7 +815,9 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
     const int D = b.anchor[7];
     b.P = D / 128;
     b.NZ = (int)(A->m / D);
-    int grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
+    // 3 workgroups per CU (knob 45): the VALU-bound 27-point body measured
+    // 245 us per CG iteration at C5's share against 249 at 4 and 272 at 2
+    int grid = std::max(8, (g_knobs.pair_zm27_bpc > 0 ? g_knobs.pair_zm27_bpc : g_knobs.pair_zm_bpc) * device_cu_count());
     grid &= ~7;
     const int W = grid / 8 * LEAN_WAVES;
     const int slab = (b.NZ + 7) / 8;
