@@ -255,7 +255,8 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
         }
         pair_unit<MODE, PS, SPLIT, CLEAN>(L[q], e[q], bw[q], puni, y, (z + q) * D + cb, lane, dot);
       }
-      zm = NQ == 1 ? c : zp[NQ - 2];
+      if constexpr (NQ == 1) zm = c;
+      else zm = zp[NQ - 2];
       c = zp[NQ - 1];
     };
     int z = z0;
@@ -517,7 +518,8 @@ __global__ void __launch_bounds__(256) spmv_pair_zmf64_kernel(const PairLeanArgs
           dot += L[q][C].y * s1v;
         }
       }
-      zm = NQ == 1 ? c : zp[NQ - 2];
+      if constexpr (NQ == 1) zm = c;
+      else zm = zp[NQ - 2];
       c = zp[NQ - 1];
     };
     int z = z0;

@@ -13,6 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mpi-petsc4py-example_amd")
 
 
+def _free_port() -> int:
+    """A port the kernel reports free on 127.0.0.1 (a pid-derived port could
+    still be in TIME_WAIT from an earlier run and make the rendezvous fail)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
 def test_options_parsing():
     from mxsolve import PETSc
     PETSc.init(["prog", "-ksp_type", "cg", "-ksp_rtol", "1e-8", "-ksp_monitor", "-pc_type", "jacobi",
@@ -115,7 +124,7 @@ def test_mpi_shim_gloo(tmp_path, P):
     script = tmp_path / "rank.py"
     script.write_text(RANK_SCRIPT.format(pkg=PKG, oracle=os.path.join(ROOT, "oracle"),
                                          golden=os.path.join(ROOT, "tests", "golden", "reference_systems.npz")))
-    port = str(29500 + P + (os.getpid() % 1000))
+    port = str(_free_port())
     procs = []
     for r in range(P):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
@@ -197,7 +206,7 @@ def test_vec_stash_gloo(tmp_path, P):
     """VecSetValues on off-process entries reach their owner at assemblyEnd."""
     script = tmp_path / "vec.py"
     script.write_text(VEC_STASH_SCRIPT.format(pkg=PKG))
-    port = str(29700 + P + (os.getpid() % 1000))
+    port = str(_free_port())
     procs = []
     for r in range(P):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
