@@ -144,13 +144,16 @@ class EPS:
             its += 1
             for j in range(k, ncv):
                 h.mult(V[j], w)
-                # classical Gram-Schmidt against V[0..j], applied twice (refinement)
+                # classical Gram-Schmidt against V[0..j], applied twice
+                # (refinement; SLEPc's default BV orthogonalisation is CGS with
+                # refinement): all j + 1 dots in one VecMDot pass over w, then
+                # one VecMAXPY -- two host round trips per pass instead of two
+                # per basis vector
                 hcol = np.zeros(j + 1)
                 for _ in range(2):
-                    for i in range(j + 1):
-                        c = core.vdot(dc, w, V[i])
-                        hcol[i] += c
-                        core.vaxpy(dc, -c, V[i], w)
+                    c = core.vmdot(dc, w, V[: j + 1])
+                    hcol += c
+                    core.vmaxpy(dc, w, -c, V[: j + 1])
                 T[: j + 1, j] = hcol
                 T[j, : j + 1] = hcol
                 beta = core.vnorm(dc, w)
@@ -177,8 +180,7 @@ class EPS:
             k = max(nev, ncv // 2)
             Y = [dc.zeros(m) for _ in range(k)]
             for q in range(k):
-                for i in range(ncv):
-                    core.vaxpy(dc, S[i, q], V[i], Y[q])
+                core.vmaxpy(dc, Y[q], S[:ncv, q], V[:ncv])
             for q in range(k):
                 V[q].copy_(Y[q])
             V[k].copy_(V[ncv])
