@@ -383,7 +383,8 @@ def test_random_ksp(oracle_mod, seed):
 
 @pytest.mark.parametrize("P,kind,n,fuse", [(2, "poisson3d", 32, 1), (4, "poisson3d", 32, 2), (2, "poisson3d27", 24, 1),
                                            (4, "poisson2d", 128, 2), (3, "poisson3d", 32, 2), (2, "poisson3d", 128, 2),
-                                           (4, "poisson2d", 256, 2), (3, "poisson3d", 128, 2)])
+                                           (4, "poisson2d", 256, 2), (3, "poisson3d", 128, 2),
+                                           (2, "poisson3d27", 128, 2)])
 def test_distributed_row_pairs(oracle_mod, P, kind, n, fuse):
     """The row-pair MatMult on every rank (interior units), with the overlapped
     halo (ghost slices take the single-row body and the boundary launch), CG
@@ -422,7 +423,7 @@ def test_distributed_row_pairs(oracle_mod, P, kind, n, fuse):
     finally:
         L.mx_debug_set(9, old)
     assert all(r[4] > 0 for r in res)
-    if (kind, n, P) in (("poisson3d", 128, 2), ("poisson2d", 256, 4)):
+    if (kind, n, P) in (("poisson3d", 128, 2), ("poisson2d", 256, 4), ("poisson3d27", 128, 2)):
         assert all(r[5] == 1 for r in res)          # whole planes per rank: the z-march form
     assert np.array_equal(np.concatenate([r[3] for r in res]).view(np.uint64), y_ref.view(np.uint64))
     assert all(r[0] == o["its"] and r[1] == o["reason"] for r in res), ([r[:2] for r in res], o["its"])
