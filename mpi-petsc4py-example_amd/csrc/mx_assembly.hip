@@ -1031,12 +1031,24 @@ __global__ void pair_fill_f64_kernel(int64_t m, int64_t nunits, int k, int ps, i
   if (!cl) *clean = 0;
 }
 
-// fp64 row-pair layout for uncoded 5/7-point diagonal blocks of one rank
-static void build_pair_f64(Sell &S, int64_t m, int64_t ncols, bool one_rank, hipStream_t st) {
+__global__ void pair_f64_ghost_kernel(int64_t nunits, int64_t nslices, const int32_t *__restrict__ wid_o,
+                                      int32_t *__restrict__ pflag) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nunits) return;
+  uint32_t f = 0;
+  if (wid_o[2 * u]) f |= PBLK_GHOST_LO;
+  if (2 * u + 1 < nslices && wid_o[2 * u + 1]) f |= PBLK_GHOST_HI;
+  if (f) pflag[u] = (int32_t)((uint32_t)pflag[u] | f);
+}
+
+// fp64 row-pair layout for uncoded 5/7-point diagonal blocks (wid_o: the A_o
+// widths per slice on a multi-rank matrix -- units with ghost entries are
+// flagged, the SpMV then splits and the boundary kernel finishes them)
+static void build_pair_f64(Sell &S, int64_t m, int64_t ncols, const int32_t *wid_o, hipStream_t st) {
   S.pval.reset();
   S.pflag.reset();
   S.pair_f64 = 0;
-  if (!g_knobs.pair_f64 || !one_rank || S.ntab > 0 || S.pat_star < 0 || m % 128 != 0 || m > (int64_t(1) << 27) ||
+  if (!g_knobs.pair_f64 || S.ntab > 0 || S.pat_star < 0 || m % 128 != 0 || m > (int64_t(1) << 27) ||
       ncols > (int64_t(1) << 27) || S.nslices * 64 != m)
     return;
   const int ps = pair_shape_of(S.pat_star_off);
@@ -1055,6 +1067,10 @@ static void build_pair_f64(Sell &S, int64_t m, int64_t ncols, bool one_rank, hip
   HIPCHECK(hipMemcpyAsync(&hc, clean.p, sizeof(int), hipMemcpyDeviceToHost, st));
   HIPCHECK(hipStreamSynchronize(st));
   if (!hc) { S.pval.reset(); S.pflag.reset(); return; }
+  if (wid_o) {      // the ghost flags go into the flag word as into pblk (pair units only here)
+    pair_f64_ghost_kernel<<<(unsigned)cdiv(nu, 256), 256, 0, st>>>(nu, S.nslices, wid_o, S.pflag.p);
+    HIPCHECK(hipGetLastError());
+  }
   S.pair_f64 = ps;
 }
 
@@ -1694,7 +1710,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
   build_sell(A->so, m, A->nghost, A->optr.p, A->ocol.p, A->oval.p, st, false);
   build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, A->n, st);
-  build_pair_f64(A->sd, m, A->n, !multi, st);
+  build_pair_f64(A->sd, m, A->n, A->so.nslices ? A->so.width.p : nullptr, st);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
 

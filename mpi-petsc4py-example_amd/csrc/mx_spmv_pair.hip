@@ -426,8 +426,9 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Arg
 // per lane, non-temporal) instead of a dictionary block's uniform values.
 // Absent slots hold 0.0 and read a 0.0 operand (the flags in Sell::pflag:
 // inner runs and edges by out-of-range reads, carried runs zeroed at use), so
-// sum + 0.0 * 0.0 = sum.  One rank (no A_o).
-template <int MODE, int PS, int ZU>
+// sum + 0.0 * 0.0 = sum.  SPLIT: units with A_o entries (PBLK_GHOST_* in
+// the flag word) keep their rows' p.y terms for the boundary kernel.
+template <int MODE, int PS, int ZU, bool SPLIT>
 __global__ void __launch_bounds__(256) spmv_pair_zmf64_kernel(const PairLeanArgs a, const double *__restrict__ x,
                                                               double *__restrict__ y, const int32_t *__restrict__ pflag,
                                                               const double *__restrict__ pval) {
@@ -514,8 +515,13 @@ __global__ void __launch_bounds__(256) spmv_pair_zmf64_kernel(const PairLeanArgs
         }
         *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
         if constexpr (MODE == SPMV_DOT) {
-          dot += L[q][C].x * s0v;
-          dot += L[q][C].y * s1v;
+          // SPLIT: rows with A_o entries stored their diagonal-block sum; the
+          // boundary kernel continues them and adds their p.y terms
+          const bool gh = SPLIT && (fl[q] & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+          if (!gh) {
+            dot += L[q][C].x * s0v;
+            dot += L[q][C].y * s1v;
+          }
         }
       }
       if constexpr (NQ == 1) zm = c;
@@ -747,10 +753,10 @@ static int zm_tasks(int P, int NZ, int &L, int &S) {
   return grid;
 }
 
-// fp64 row-pair z-march (Sell::pval): applies to one-rank uncoded 5/7-point layouts
+// fp64 row-pair z-march (Sell::pval): uncoded 5/7-point layouts
 int pair_f64_kind(const Mat *A) {
   const Sell &S = A->sd;
-  if (!S.pair_f64 || !S.pval.p || !g_knobs.pair_lean || !g_knobs.pair_zm || A->nghost > 0) return 0;
+  if (!S.pair_f64 || !S.pval.p || !g_knobs.pair_lean || !g_knobs.pair_zm) return 0;
   int anchor[5] = {0, 0, 0, 0, 0};
   const int ps = S.pair_f64;
   for (int r = 0; r < (ps == 5 ? 3 : 5); ++r) {
@@ -761,8 +767,8 @@ int pair_f64_kind(const Mat *A) {
   return zm_plane(A, ps, anchor) ? ps : 0;
 }
 
-static int pair_f64_launch(Mat *A, int mode, const double *x, double *y, double *partials, const int *done,
-                           const Fold &fold_in, hipStream_t st) {
+static int pair_f64_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials,
+                           const int *done, const Fold &fold_in, hipStream_t st) {
   const Sell &S = A->sd;
   const int ps = S.pair_f64;
   PairLeanArgs a{};
@@ -786,13 +792,11 @@ static int pair_f64_launch(Mat *A, int mode, const double *x, double *y, double 
   using F = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const double *);
   F f;
   const bool z2 = g_knobs.pair_zm_units == 2;
-  if (mode == SPMV_PLAIN) {
-    if (ps == 5) f = z2 ? &spmv_pair_zmf64_kernel<SPMV_PLAIN, 5, 2> : &spmv_pair_zmf64_kernel<SPMV_PLAIN, 5, 1>;
-    else f = z2 ? &spmv_pair_zmf64_kernel<SPMV_PLAIN, 7, 2> : &spmv_pair_zmf64_kernel<SPMV_PLAIN, 7, 1>;
-  } else {
-    if (ps == 5) f = z2 ? &spmv_pair_zmf64_kernel<SPMV_DOT, 5, 2> : &spmv_pair_zmf64_kernel<SPMV_DOT, 5, 1>;
-    else f = z2 ? &spmv_pair_zmf64_kernel<SPMV_DOT, 7, 2> : &spmv_pair_zmf64_kernel<SPMV_DOT, 7, 1>;
-  }
+#define F64K(MODE, PS) do { if (split) f = z2 ? &spmv_pair_zmf64_kernel<MODE, PS, 2, true> : &spmv_pair_zmf64_kernel<MODE, PS, 1, true>; \
+                            else f = z2 ? &spmv_pair_zmf64_kernel<MODE, PS, 2, false> : &spmv_pair_zmf64_kernel<MODE, PS, 1, false>; } while (0)
+  if (mode == SPMV_PLAIN) { if (ps == 5) F64K(SPMV_PLAIN, 5); else F64K(SPMV_PLAIN, 7); }
+  else { if (ps == 5) F64K(SPMV_DOT, 5); else F64K(SPMV_DOT, 7); }
+#undef F64K
   launch_timed(f, grid, st, a, x, y, S.pflag.p, S.pval.p);
   HIPCHECK(hipGetLastError());
   return grid;
@@ -805,7 +809,8 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
                      const Fold &fold_in, hipStream_t st) {
   const Sell &S = A->sd;
   if (mode != SPMV_PLAIN && mode != SPMV_DOT) return 0;
-  if (!split && pair_f64_kind(A)) return pair_f64_launch(A, mode, x, y, partials, done, fold_in, st);
+  if (pair_f64_kind(A) && (split || A->nghost == 0))   // without a split, A_o continues in the general kernel
+    return pair_f64_launch(A, mode, split, x, y, partials, done, fold_in, st);
   const int kind = pair_lean_kind(A);
   if (!kind) return 0;
   if (!split && (A->nghost > 0 || S.pair_ghosts)) return 0;   // A_o continues in the general kernel

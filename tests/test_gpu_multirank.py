@@ -457,3 +457,53 @@ def test_local_barrier_then_collectives_skewed():
     finally:
         W.destroy()
     assert out == [300 * 4000.0] * 4
+
+
+@pytest.mark.parametrize("P,kind,n", [(2, "poisson3d", 128), (4, "poisson2d", 512)])
+def test_distributed_fp64_row_pairs(oracle_mod, P, kind, n):
+    """Uncoded (every value distinct: the D A D scaled operator) 5/7-point
+    blocks on P ranks: the fp64 row-pair z-march on every rank (the units of
+    the planes next to another rank flagged as ghost units, the product split,
+    the boundary kernel finishing them): MatMult bit-exact, CG (mode 2) against
+    the oracle."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    rng = np.random.default_rng(31)
+    f = 1.0 + 0.5 * rng.random(M)
+    rows = np.repeat(np.arange(M), np.diff(ip))
+    v = v * f[rows] * f[c]
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+    ranges = oracle_mod.split_ownership(M, P)
+    x = rng.standard_normal(M)
+    y_ref = O.mult(x)
+    bvec = rng.random(M)
+    o = O.solve(bvec, ksp="cg", rtol=1e-8)
+
+    def body(comm):
+        r = comm.rank
+        lip, lc, lv = local_csr(ip, c, v, ranges[r], ranges[r + 1])
+        A = DMat.from_csr(comm, M, M, lip, lc, lv)
+        info = A.info()
+        xl = torch.from_numpy(x[ranges[r]:ranges[r + 1]].copy()).cuda()
+        yl = torch.zeros(ranges[r + 1] - ranges[r], dtype=torch.float64, device="cuda")
+        A.mult(xl, yl)
+        bl = torch.from_numpy(bvec[ranges[r]:ranges[r + 1]].copy()).cuda()
+        xs = torch.zeros_like(bl)
+        rs = A.solve(bl, xs, ksp="cg", rtol=1e-8)
+        out = (info["pair_f64"], yl.cpu().numpy(), rs["its"], rs["reason"], xs.cpu().numpy())
+        A.destroy()
+        return out
+
+    L = _lib.load()
+    old = L.mx_debug_set(9, 2)
+    try:
+        res = run_ranks(P, body)
+    finally:
+        L.mx_debug_set(9, old)
+    assert all(r[0] in (5, 7) for r in res)
+    assert np.array_equal(np.concatenate([r[1] for r in res]).view(np.uint64), y_ref.view(np.uint64))
+    assert all(r[2] == o["its"] and r[3] == o["reason"] for r in res), ([r[2:4] for r in res], o["its"])
+    xs = np.concatenate([r[4] for r in res])
+    assert np.linalg.norm(xs - o["x"]) <= REL_TOL * np.linalg.norm(o["x"])
