@@ -251,7 +251,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
  *        1 for <= 3M local rows, else 2); 4 mode 2 with the direction update and
  *        the batched x steps inside the z-march MatMult (one rank, lean z-march
- *        layout, no or uniform Jacobi; else 2; mode 2's bits)
+ *        layout, no or uniform Jacobi; else 2; mode 2's bits); 5 mode 2 whose
+ *        MatMult stores no product: a p.Ap pass, and the update pass
+ *        recomputes A p where it forms r - alpha A p (one rank, lean 5/7-point
+ *        z-march layout, no or uniform Jacobi; else 2)
  * key 10: where CG folds its per-workgroup partials: 0 one-block fold kernels;
  *        1 the update pass folds its own inside the launch, and the MatMult's
  *        halo-boundary launch when the product is split (default); 2 the
@@ -284,9 +287,11 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 28: resident workgroups per CU for the row-pair SpMV grid (default 4)
  * key 29: CG mode 2 applies the deferred x steps every B iterations from B
  *         rotating direction buffers (1, 2 or 4; default 2)
- * key 33: deadline in ms of a host wait on an RCCL communicator's work; past
- *         it (or on an RCCL asynchronous error) the communicator is aborted
- *         and the call fails with MX_ERR_COMM (default 120000)
+ * key 33: no-progress deadline in ms of the KSP poller's wait on an RCCL
+ *         communicator (re-armed whenever the device's count of iterations
+ *         begun moves); past it the communicator is aborted and the call fails
+ *         with MX_ERR_COMM (default 120000).  An RCCL asynchronous error aborts
+ *         at once in every wait
  * key 34: grid of the CG initial-norms pass (0 = default: the direction update's grid,
  *         whose fused iteration-0 norms it must match bit for bit)
  * key 35: row-pair SpMV reads uniform-slot dictionary blocks as slot values +
@@ -308,8 +313,22 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 44: fp64 row-pair layout + z-march MatMult for uncoded 5/7-point blocks
  *         (read at assembly; 0/1, default 1; the same bits)
  * key 45: 27-point z-march resident workgroups per CU (default 3; 0 = key 40)
+ * key 46: CG mode 5: the residual-update pass folds the p.Ap pass's partials
+ *         itself (1, default) or a one-block fold kernel runs between (0)
+ * key 47: deadline in ms of the RCCL waits that observe no progress (stream /
+ *         event waits, setup collectives, barrier); 0 = none (default: a slow
+ *         peer is not an error, as with MPI)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
+/* Test hook: host-side counts of the MatMult-family kernel launches
+ * enqueued (or captured into a graph) since the last reset, by kind --
+ * 0 general SELL, 1 SELL CG-fused (mode 1), 2 row-pair sweep, 3 / 4 7/5-point
+ * z-march (split: ghost units), 5 / 6 27-point z-march, 7 / 8 fp64 row-pair
+ * z-march, 9 CG mode 4, 10 halo-boundary kernel, 11 / 12 CG mode 5's p.Ap and
+ * residual-update z-march passes.  Writes min(n, 16) counts; reset != 0
+ * zeroes them.  Not a PETSc call: it lets the parity tests show which
+ * kernel ran (replayed graph launches are not counted).                     */
+int mx_debug_dispatch_counts(int64_t *out, int n, int reset);
 /* Calibration stream for PMC byte counters: reads n doubles once with
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,
  * and writes one partial sum per workgroup to out_dev.                      */
@@ -326,7 +345,7 @@ int mx_dev_free(void *ptr);
 int mx_debug_comm_bench(mx_comm c, mx_mat A, int what, int iters, double *us_per);
 /* Failure-detection test hook: enqueues ~stall_us of device time on the
  * communicator's stream (a bounded spin) and waits for it through the
- * communicator's watched wait (key 33 deadline, RCCL async-error polling).  */
+ * communicator's watched wait (key 47 deadline, RCCL async-error polling).  */
 int mx_debug_comm_stall(mx_comm c, int stall_us);
 
 #ifdef __cplusplus

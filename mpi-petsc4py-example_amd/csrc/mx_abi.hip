@@ -527,9 +527,19 @@ int mx_debug_set(int key, int value) {
     case 43: old = g_knobs.spmv_fp64_grid; g_knobs.spmv_fp64_grid = std::min(std::max(value, 0), 65536); break;
     case 44: old = g_knobs.pair_f64; g_knobs.pair_f64 = value; break;
     case 45: old = g_knobs.pair_zm27_bpc; g_knobs.pair_zm27_bpc = std::min(std::max(value, 0), 8); break;
+    case 46: old = g_knobs.cg5_fold; g_knobs.cg5_fold = value; break;
+    case 47: old = g_knobs.comm_wait_ms; g_knobs.comm_wait_ms = std::max(value, 0); break;
     default: break;
   }
   return old;
+}
+
+int mx_debug_dispatch_counts(int64_t *out, int n, int reset) {
+  for (int k = 0; k < DSP_COUNT; ++k) {
+    const long long v = reset ? g_dispatch[k].exchange(0) : g_dispatch[k].load();
+    if (out && k < n) out[k] = v;
+  }
+  return 0;
 }
 
 int mx_debug_stream_read(mx_comm c, const double *x, int64_t n, int width, double *out) {

@@ -1232,7 +1232,7 @@ static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream
   std::vector<PairUni> u((size_t)nb);
   for (int64_t b = 0; b < nb; ++b) {
     PairUni &B = u[(size_t)b];
-    for (int q = 0; q < 16; ++q) { B.v[q] = 0.0; B.pm[q] = 0ull; }
+    std::memset(&B, 0, sizeof(B));
     for (int q = 0; q < 2 * K; ++q) {
       int code = -1;
       for (int lane = 0; lane < 64; ++lane) {
@@ -1243,6 +1243,11 @@ static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream
         B.pm[q] |= 1ull << lane;
       }
       if (code >= 0) B.v[q] = vt[(size_t)code];
+    }
+    for (int lane = 0; lane < 64; ++lane) {
+      uint32_t w = 0;
+      for (int q = 0; q < 2 * K; ++q) w |= (uint32_t)((B.pm[q] >> lane) & 1ull) << q;
+      B.lane[lane] = w;
     }
   }
   S.puni.alloc((size_t)nb);
@@ -1318,6 +1323,19 @@ static void build_pair_uniform27(Sell &S, const std::vector<double> &vt, hipStre
         B.pm[q] |= 1ull << lane;
       }
       if (code >= 0) B.v[q] = vt[(size_t)code];
+    }
+    // one value per slot for both rows (the lean kernel reads 27, not 54):
+    // the rows of a regular-grid block share their stencil values; a block
+    // whose rows differ keeps the general kernel
+    for (int j = 0; j < K; ++j) {
+      if (B.pm[j] && B.pm[K + j] && std::memcmp(&B.v[j], &B.v[K + j], sizeof(double)) != 0) return;
+      if (!B.pm[j]) B.v[j] = B.v[K + j];
+      B.v[K + j] = B.v[j];
+    }
+    for (int lane = 0; lane < 64; ++lane) {
+      unsigned long long w = 0;
+      for (int j = 0; j < 2 * K; ++j) w |= ((B.pm[j] >> lane) & 1ull) << j;
+      B.lane[lane] = w;
     }
     uint32_t f = 0;
     int elo = -1, ehi = -1;                         // every non-empty run must agree

@@ -144,4 +144,69 @@ __device__ __forceinline__ void cg_commit_top(KspState *s, const CgTop &t, doubl
   s->pb = t.b;
 }
 
+// The CG update pass's helpers, shared by cg_update_kernel (mx_ksp.hip) and
+// CG mode 5's residual-update MatMult (mx_spmv_pair.hip).
+__device__ __forceinline__ void stop(KspState *s, int reason) {
+  s->reason = reason;
+  s->top.done = 1;
+  s->inner_stop = 1;
+}
+
+// Words of pinned host memory the CG kernels write with system-scope stores
+// (Mat::poll_pinned): the done flag and the iteration count the host's poller
+// spins on, and the result the tail pass publishes (no device-to-host copy).
+enum { HW_DONE = 0, HW_PROGRESS = 1, HW_ITS = 2, HW_REASON = 3, HW_DP = 4 /* double: words 4-5 */, HW_TICKS = 6 /* int64: 6-7 */,
+       HW_WORDS = 8 };
+
+__device__ __forceinline__ void host_store(int *w, int v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
+// Read-only; cg_update_kernel's workgroup 0 commits it.
+struct CgAlpha { int i, reason; double dpi, alpha; };
+__device__ __forceinline__ CgAlpha cg_alpha(const KspState *s, double dpi) {
+  // every input loaded before the first branch
+  const int i = s->it_k;
+  const double d0 = s->dpis[0], d1 = s->dpis[1];
+  const double b0 = s->top.betas[0], b1 = s->top.betas[1];
+  CgAlpha a;
+  a.i = i;
+  a.reason = R_ITERATING;
+  a.dpi = dpi;
+  a.alpha = 0.0;
+  if (not_finite(dpi)) { a.reason = R_DIVERGED_NANORINF; return a; }
+  const double dpo = i > 0 ? ((i & 1) ? d0 : d1) : 0.0;     // dpi_{i-1}
+  const int sg = (dpi > 0) - (dpi < 0), sgo = (dpo > 0) - (dpo < 0);
+  if (dpi == 0.0 || (i > 0 && sg * sgo < 0)) { a.reason = R_DIVERGED_INDEFINITE_MAT; return a; }
+  a.alpha = ((i & 1) ? b1 : b0) / dpi;                        // beta_i / dpi
+  return a;
+}
+
+// workgroup 0, thread 0 of the update pass: commit alpha (or the stop), the
+// deferred / batched x step bookkeeping and the host words
+__device__ __forceinline__ void cg_commit_alpha(KspState *s, const CgAlpha &al, double pw, int xb, bool xu,
+                                                int *hw) {
+  s->dpi = al.dpi;
+  s->red1 = pw;
+  s->top.xpend = 0.0;            // a deferred step of i-1 was applied by this iteration's first kernel
+  // batched x steps: this iteration's cg_pb applied [i - B, i) when i % B == 0
+  // (also when this pass stops the solve, so the finish pass does not repeat them)
+  if (xb > 1 && al.i % xb == 0) s->top.xlo = al.i;
+  if (al.reason) {
+    stop(s, al.reason);
+    if (hw) host_store(hw + HW_DONE, 1);
+  } else {
+    if (hw) host_store(hw + HW_PROGRESS, al.i + 1);
+    s->dpis[al.i & 1] = al.dpi;
+    s->alpha = al.alpha;
+    if (!xu) { s->top.xa = al.alpha; s->top.xpend = 1.0; s->xi = al.i; }
+    if (xb > 1) {                // the step of direction i joins the pending batch
+      s->top.xal[al.i % xb] = al.alpha;
+      s->top.xhi = al.i + 1;
+    }
+    s->top.it_u = al.i + 1;
+  }
+}
+
 }  // namespace mx

@@ -36,7 +36,7 @@ namespace mx {
 
 Comm::~Comm() {}
 
-void Comm::wait_until(const std::function<bool()> &ready, hipStream_t s) {
+void Comm::wait_until(const std::function<bool()> &ready, hipStream_t s, const std::function<long long()> &) {
   hipStream_t q = s ? s : stream;
   for (int spins = 0; !ready(); ++spins) {
     if ((spins & 63) == 63) {
@@ -140,11 +140,19 @@ struct RcclComm : Comm {
     wait_stream(stream);
   }
   // Failure detection: poll the device work and RCCL's
-  // asynchronous error state; past the deadline (knob 33, default 120 s) or on
-  // an RCCL error, abort the communicator so this rank fails with MX_ERR_COMM
-  // rather than waiting forever on a peer that died or took another path.
-  template <class Q> void watch(Q query, const char *what) {
-    const auto t0 = std::chrono::steady_clock::now();
+  // asynchronous error state.  An RCCL error aborts the communicator at once
+  // (this rank fails with MX_ERR_COMM rather than waiting forever on a peer
+  // that died).  Deadlines: a wait that can observe progress (the KSP poller:
+  // the count of iterations begun, which the device advances) fails after
+  // knob 33 ms (default 120 s) WITHOUT progress -- the timer re-arms whenever
+  // the count moves, so a long healthy solve never trips it; a wait that
+  // cannot (stream/event waits, setup collectives, barrier) has no deadline
+  // unless knob 47 sets one (ms, default 0 = wait as MPI would: a slow peer,
+  // e.g. one still building its CSR on the host, is not an error).
+  template <class Q> void watch(Q query, const char *what, const std::function<long long()> &progress = {}) {
+    const int limit = progress ? g_knobs.comm_timeout_ms : g_knobs.comm_wait_ms;
+    auto t0 = std::chrono::steady_clock::now();
+    long long seen = progress ? progress() : 0;
     for (int spins = 0;; ++spins) {
       const hipError_t e = query();
       if (e == hipSuccess) return;
@@ -154,10 +162,17 @@ struct RcclComm : Comm {
         abort_comm();
         fail(MX_ERR_COMM, std::string(what) + ": RCCL asynchronous error: " + ncclGetErrorString(ar));
       }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(g_knobs.comm_timeout_ms)) {
-        abort_comm();
-        fail(MX_ERR_COMM, std::string(what) + ": no progress for " + std::to_string(g_knobs.comm_timeout_ms) +
-                              " ms; RCCL communicator aborted");
+      if (limit > 0) {
+        const auto now = std::chrono::steady_clock::now();
+        if (progress) {
+          const long long p = progress();
+          if (p != seen) { seen = p; t0 = now; }
+        }
+        if (now - t0 > std::chrono::milliseconds(limit)) {
+          abort_comm();
+          fail(MX_ERR_COMM, std::string(what) + ": no progress for " + std::to_string(limit) +
+                                " ms; RCCL communicator aborted");
+        }
       }
       if (spins > 200) usleep(50); else sched_yield();
     }
@@ -177,10 +192,11 @@ struct RcclComm : Comm {
     if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     watch([&] { return hipEventQuery(ev); }, "event wait");
   }
-  void wait_until(const std::function<bool()> &ready, hipStream_t s) override {
+  void wait_until(const std::function<bool()> &ready, hipStream_t s,
+                  const std::function<long long()> &progress) override {
     if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     hipStream_t q = s ? s : stream;
-    watch([&] { return ready() ? hipSuccess : hipStreamQuery(q); }, "progress wait");
+    watch([&] { return ready() ? hipSuccess : hipStreamQuery(q); }, "progress wait", progress);
   }
 };
 

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <functional>
 #include <memory>
@@ -82,8 +83,10 @@ struct Comm {
   virtual void wait_event(hipEvent_t e) { HIPCHECK(hipEventSynchronize(e)); }
   // Host spins until ready() (a word the device writes into pinned host
   // memory) or until stream s has drained (then the caller re-reads the word);
-  // a device error on s raises.
-  virtual void wait_until(const std::function<bool()> &ready, hipStream_t s);
+  // a device error on s raises.  progress (optional): a count the device
+  // advances -- RCCL communicators re-arm their no-progress deadline on it.
+  virtual void wait_until(const std::function<bool()> &ready, hipStream_t s,
+                          const std::function<long long()> &progress = {});
 };
 
 Comm *make_self_comm(int device);
@@ -121,14 +124,22 @@ constexpr int32_t DPAT_ID = DPAT_PAIR - 1;
 struct PairUni {
   double v[16];                 // the slot-row's value
   unsigned long long pm[16];    // lanes whose row stores it
+  // the masks transposed for the lean kernel's select body: lane l's bit q =
+  // pm[q] bit l (one vector load per unit instead of 2K wave-uniform masks)
+  uint32_t lane[64];
 };
 // the same for 27-point row pairs (54 slot-rows), with the block's select-free
 // flags: bit r = run r empty for both rows, U27_ELO / U27_EHI = lane 0 row 0
 // lacks every non-empty run's -1 entry / lane 63 row 1 its +1 entry
 struct PairUni27 {
-  double v[54];
+  double v[54];                 // v[j] == v[27 + j]: one value per slot (the build requires it)
   unsigned long long pm[54];
   uint32_t flags, clean;        // clean: the block needs no presence select
+  uint32_t pad[2];
+  // the masks transposed, for the select body: lane l's bit j = pm[j] bit l
+  // (row 0), bit 27 + j = pm[27 + j] bit l (row 1) -- one vector load per unit
+  // instead of 54 wave-uniform masks (which do not fit the SGPR file)
+  unsigned long long lane[64];
 };
 constexpr uint32_t U27_ELO = 1u << 9;
 constexpr uint32_t U27_EHI = 1u << 10;
@@ -214,7 +225,8 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
-                int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 3; };
+                int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 3; int cg5_fold = 1;
+                int comm_wait_ms = 0; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -310,7 +322,11 @@ __device__ __forceinline__ double papply(const Jac &J, double r, int64_t i) {
 enum SpmvMode { SPMV_PLAIN = 0, SPMV_JACOBI = 1, SPMV_DOT = 2, SPMV_CG = 3,
                 // the operand is s * x with s = *xscale: a GMRES basis vector kept
                 // unnormalised (VecScale applied at every read, the same bits)
-                SPMV_PLAIN_S = 4, SPMV_JACOBI_S = 5 };
+                SPMV_PLAIN_S = 4, SPMV_JACOBI_S = 5,
+                // CG mode 5 (z-march only, one rank): the p.Ap partials without
+                // storing the product, and the residual update that recomputes
+                // it (mx_spmv_pair.hip spmv_pair_zm_kernel)
+                SPMV_PW = 6, SPMV_RUPD = 7 };
 constexpr bool spmv_jac(int mode) { return mode == SPMV_JACOBI || mode == SPMV_JACOBI_S; }
 constexpr bool spmv_scaled(int mode) { return mode == SPMV_PLAIN_S || mode == SPMV_JACOBI_S; }
 // SPMV_CG: the CG direction update and the deferred solution update ride in
@@ -347,6 +363,27 @@ int spmv_blocks(const Mat *A, int mode = SPMV_PLAIN);
 // consumes it (mx_spmv.hip launch_timed).
 struct ExtTiming { hipEvent_t a = nullptr, b = nullptr; bool armed = false, used = false; };
 extern thread_local ExtTiming g_ext_timing;
+// Host-side counts of the MatMult-family launches enqueued (or captured) by
+// kind, for tests that must show which kernel a configuration ran
+// (mx_debug_dispatch_counts); a relaxed atomic add per launch.
+enum Dispatch {
+  DSP_SELL = 0,          // spmv_sell_kernel (general SELL), any mode but SPMV_CG
+  DSP_SELL_CG = 1,       // spmv_sell_kernel<SPMV_CG> (CG mode 1)
+  DSP_PAIR_LEAN = 2,     // spmv_pair_lean_kernel (sweep form)
+  DSP_PAIR_ZM = 3,       // spmv_pair_zm_kernel, one rank / no ghost units
+  DSP_PAIR_ZM_SPLIT = 4, // spmv_pair_zm_kernel<SPLIT> (ghost units, boundary kernel after)
+  DSP_PAIR_ZM27 = 5,
+  DSP_PAIR_ZM27_SPLIT = 6,
+  DSP_PAIR_ZMF64 = 7,
+  DSP_PAIR_ZMF64_SPLIT = 8,
+  DSP_PAIR_ZMCG = 9,     // CG mode 4
+  DSP_BOUNDARY = 10,     // spmv_boundary_kernel
+  DSP_ZM_PW = 11,        // CG mode 5: the z-march p.Ap pass (no product stored)
+  DSP_ZM_RUPD = 12,      // CG mode 5: the z-march residual update (product recomputed)
+  DSP_COUNT = 16
+};
+void note_dispatch(int kind);
+extern std::atomic<long long> g_dispatch[DSP_COUNT];
 int device_cu_count();
 int main_grid(const Mat *A, int mode, const void *kf, bool pairs);   // the SpMV's resident grid
 // lean row-pair MatMult (mx_spmv_pair.hip): launched when it applies (returns its grid, else 0)
@@ -359,6 +396,13 @@ int pair_f64_kind(const Mat *A);     // 5 / 7: the fp64 row-pair z-march applies
 bool pair_zmcg_applies(const Mat *A, int jac_mode);
 int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac_c, const double *r, double *pb0,
                      double *pb1, double *x, double *w, double *partials, const Fold *fold, hipStream_t st);
+// CG mode 5: w = A p is never stored -- the p.Ap pass (SPMV_PW) gives p.w,
+// the update pass recomputes A p where it forms r - alpha A p (SPMV_RUPD)
+bool pair_cg5_applies(const Mat *A, int jac_mode);
+int pair_cg5_pw_launch(Mat *A, const double *p, double *partials, const int *done, const Fold *fold, hipStream_t st);
+int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, double *r, const double *r0, int jac_mode,
+                         double jac_c, double *partials, const Fold &fold, const double *dot_part, int ndot, int xb,
+                         int *hw, hipStream_t st);
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);

@@ -60,18 +60,6 @@ __device__ int dev_converged(KspState *s, int n, double rnorm, bool guess_zero, 
   return R_ITERATING;
 }
 
-__device__ __forceinline__ void stop(KspState *s, int reason) {
-  s->reason = reason;
-  s->top.done = 1;
-  s->inner_stop = 1;
-}
-
-// Words of pinned host memory the CG kernels write with system-scope stores
-// (Mat::poll_pinned): the done flag and the iteration count the host's poller
-// spins on, and the result the tail pass publishes (no device-to-host copy).
-enum { HW_DONE = 0, HW_PROGRESS = 1, HW_ITS = 2, HW_REASON = 3, HW_DP = 4 /* double: words 4-5 */, HW_TICKS = 6 /* int64: 6-7 */,
-       HW_WORDS = 8 };
-
 // The solver parameters a solve starts from (KspState's parameter fields).
 struct KspInit {
   double rtol, atol, dtol, haptol, breakdowntol;
@@ -90,9 +78,6 @@ __global__ void __launch_bounds__(256) ksp_state_init_kernel(KspState *__restric
   s->rtol = in.rtol; s->top.atol = in.atol; s->top.dtol = in.dtol; s->haptol = in.haptol;
   s->breakdowntol = in.breakdowntol; s->top.max_it = in.max_it; s->top.normtype = in.normtype;
   s->guess_zero = in.guess_zero; s->max_k = in.max_k; s->ksp_rnorm = -1.0;
-}
-__device__ __forceinline__ void host_store(int *w, int v) {
-  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Either one thread after an all-reduce (P > 1), or a fused single block that
@@ -499,27 +484,6 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
   else walk(std::false_type{}, r, std::false_type{});
 }
 
-// dpi = p.w (red1), the indefinite-matrix test, alpha = beta_i / dpi.
-// Read-only; cg_update_kernel's workgroup 0 commits it.
-struct CgAlpha { int i, reason; double dpi, alpha; };
-__device__ __forceinline__ CgAlpha cg_alpha(const KspState *s, double dpi) {
-  // every input loaded before the first branch
-  const int i = s->it_k;
-  const double d0 = s->dpis[0], d1 = s->dpis[1];
-  const double b0 = s->top.betas[0], b1 = s->top.betas[1];
-  CgAlpha a;
-  a.i = i;
-  a.reason = R_ITERATING;
-  a.dpi = dpi;
-  a.alpha = 0.0;
-  if (not_finite(dpi)) { a.reason = R_DIVERGED_NANORINF; return a; }
-  const double dpo = i > 0 ? ((i & 1) ? d0 : d1) : 0.0;     // dpi_{i-1}
-  const int sg = (dpi > 0) - (dpi < 0), sgo = (dpo > 0) - (dpo < 0);
-  if (dpi == 0.0 || (i > 0 && sg * sgo < 0)) { a.reason = R_DIVERGED_INDEFINITE_MAT; return a; }
-  a.alpha = ((i & 1) ? b1 : b0) / dpi;                        // beta_i / dpi
-  return a;
-}
-
 // x += a p, r -= a w (BLAS daxpy = fma), z = d.*r, [z.z, z.r, r.r] folded
 // into red3 inside the launch.  XU false: the x step is deferred (modes 1/2:
 // applied by the next iteration's first kernel, or by cg_finish_x_kernel).
@@ -543,28 +507,7 @@ __global__ void __launch_bounds__(256) cg_update_kernel(int64_t n, KspState *__r
   // by every workgroup from the MatMult's partials, in fold_kernel's order
   const double pw = ndot > 0 ? block_sum_array<16>(dot_part, ndot) : s->red1;
   const CgAlpha al = cg_alpha(s, pw);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    s->dpi = al.dpi;
-    s->red1 = pw;
-    s->top.xpend = 0.0;            // a deferred step of i-1 was applied by this iteration's first kernel
-    // batched x steps: this iteration's cg_pb applied [i - B, i) when i % B == 0
-    // (also when this pass stops the solve, so the finish pass does not repeat them)
-    if (xb > 1 && al.i % xb == 0) s->top.xlo = al.i;
-    if (al.reason) {
-      stop(s, al.reason);
-      if (hw) host_store(hw + HW_DONE, 1);
-    } else {
-      if (hw) host_store(hw + HW_PROGRESS, al.i + 1);
-      s->dpis[al.i & 1] = al.dpi;
-      s->alpha = al.alpha;
-      if (!XU) { s->top.xa = al.alpha; s->top.xpend = 1.0; s->xi = al.i; }
-      if (xb > 1) {                // the step of direction i joins the pending batch
-        s->top.xal[al.i % xb] = al.alpha;
-        s->top.xhi = al.i + 1;
-      }
-      s->top.it_u = al.i + 1;
-    }
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, xb, XU, hw);
   if (al.reason) return;
   const double a = al.alpha;
   double v[3] = {0.0, 0.0, 0.0};
@@ -1014,7 +957,8 @@ struct Poller {
     const int target = prev_end;
     prev_end = end;
     if (++pending < 2) return false;
-    c->wait_until([&] { return word(HW_DONE) != 0 || word(HW_PROGRESS) >= target; }, st);
+    c->wait_until([&] { return word(HW_DONE) != 0 || word(HW_PROGRESS) >= target; }, st,
+                  [&] { return (long long)word(HW_PROGRESS); });
     return word(HW_DONE) != 0;
   }
 };
@@ -1228,7 +1172,12 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
   if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && g_knobs.cg_xbatch == 2 && poll % 2 == 0 && !p.guess_nonzero))
     fmode = 2;
-  const int xb = ((fmode == 2 || fmode == 4) && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 4) &&
+  // mode 5 (knob 9 = 5): mode 2 whose MatMult stores no product -- a p.Ap
+  // pass, then the update pass recomputes A p (mx_spmv_pair.hip SPMV_PW /
+  // SPMV_RUPD) -- one rank, a lean 5/7-point z-march layout, no or uniform
+  // Jacobi; otherwise 2
+  if (fmode == 5 && !(fused && pair_cg5_applies(A, dinv.mode))) fmode = 2;
+  const int xb = ((fmode == 2 || fmode == 4 || fmode == 5) && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 4) &&
                   poll % g_knobs.cg_xbatch == 0)
                      ? g_knobs.cg_xbatch : 1;
   Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist, xb == 4 ? nv : 0, xb == 4 ? nv : 0})));
@@ -1330,27 +1279,32 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       nb_spmv = pair_zmcg_launch(A, s, hist_d, dinv.mode, dinv.c, r.p, pbs.b[0], pbs.b[1], x, w.p, part.p, fdot_p, st);
       timer.end();
       if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG mode 4 without its MatMult");
-    } else if (xb > 1) {
-      cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb);
-      timer.begin();
-      nb_spmv = matmult_overlap(A, pbs.b[it % xb], w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
-      timer.end();
     } else {
-      cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
+      double *pi = xb > 1 ? pbs.b[it % xb] : pv.p;
+      if (xb > 1) cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb);
+      else cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
       timer.begin();
-      nb_spmv = matmult_overlap(A, pv.p, w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
+      nb_spmv = fmode == 5 ? pair_cg5_pw_launch(A, pi, part.p, done, fdot_p, st)
+                           : matmult_overlap(A, pi, w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
+      if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG without its MatMult");
     }
-    // one rank: the update pass folds the MatMult's partials itself (knob 10 = 3)
-    const bool fold_in_update = !fdot_p && fused && fold_at == 3;
+    // one rank: the update pass folds the MatMult's partials itself (knob 10
+    // = 3; mode 5's residual update by default, knob 46)
+    const bool fold_in_update = !fdot_p && fused && (fold_at == 3 || (fmode == 5 && g_knobs.cg5_fold));
     if (!fdot_p && !fold_in_update) fold_kernel<1><<<1, 256, 0, st>>>(part.p, nb_spmv, &s->red1, done);
     if (!fused) c->allreduce_sum(&s->red1, 1);
     const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : xb > 1 ? pbs.b[it % xb] : pv.p;
     // the update's own partials go after the MatMult's when it folds those
     double *upart = fold_in_update ? part.p + ((nb_spmv + 63) / 64) * 64 : part.p;
-    const int nb_upd = cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, upart, fupd,
-                                        fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb,
-                                        xb > 1 ? r0 : nullptr, poller.hw);
+    const int nb_upd =
+        fmode == 5 ? pair_cg5_rupd_launch(A, s, pcur, r.p, xb > 1 ? r0 : nullptr, dinv.mode, dinv.c, upart, fupd,
+                                          fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb,
+                                          poller.hw, st)
+                   : cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, upart, fupd,
+                                      fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb,
+                                      xb > 1 ? r0 : nullptr, poller.hw);
+    if (!nb_upd) fail(MX_ERR_INTERNAL, "CG without its update pass");
     if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(upart, nb_upd, s->top.red3, done);
     if (!fused) c->allreduce_sum(s->top.red3, 3);
     HIPCHECK(hipGetLastError());

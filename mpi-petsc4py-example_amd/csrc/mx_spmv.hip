@@ -27,6 +27,8 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <atomic>
+
 #include "mx_cg.hpp"
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
@@ -41,6 +43,8 @@ constexpr int SPMV_WAVES = 4;  // 256-thread workgroups, one slice per wave at a
 #endif
 Knobs g_knobs;
 thread_local ExtTiming g_ext_timing;
+std::atomic<long long> g_dispatch[DSP_COUNT];
+void note_dispatch(int kind) { g_dispatch[kind].fetch_add(1, std::memory_order_relaxed); }
 
 typedef int int2v __attribute__((ext_vector_type(2)));
 
@@ -932,6 +936,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   const int grid = main_grid(A, mode, reinterpret_cast<const void *>(kf), ps != 0);
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  note_dispatch(mode == SPMV_CG ? DSP_SELL_CG : DSP_SELL);
   launch_timed(kf, grid, st, SPMV_ARGS);
 #undef SPMV_GO
 #undef SPMV_PS
@@ -997,6 +1002,7 @@ int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, doubl
   const double *xb = mode == SPMV_CG ? cg->pnew : x;
 #define BND(MODE) spmv_boundary_kernel<MODE><<<nb, 256, 0, st>>>(A->m, H.bnd_slices.p, H.nbnd, A->so.sptr.p, \
       A->so.width.p, A->so.col.p, A->so.val.p, xb, H.lvec.p, y, jac, pb, done_flag, f, xscale)
+  note_dispatch(DSP_BOUNDARY);
   switch (mode) {
     case SPMV_PLAIN: BND(SPMV_PLAIN); break;
     case SPMV_JACOBI: BND(SPMV_JACOBI); break;

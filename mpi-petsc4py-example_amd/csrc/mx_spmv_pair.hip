@@ -57,13 +57,15 @@ struct PairLeanArgs {
 // One unit's products: L[r] = run r's operand pair, e = the tri run's edge
 // value (lane 0: x[r0 + c - 1], lane 63: x[r0 + 127 + c + 1]), bw = the unit's
 // block word.  Each row sums its slots in ascending column order.
-template <int MODE, int PS, bool SPLIT, bool CLEAN>
-__device__ __forceinline__ void pair_unit(const dbl2 (&L)[PairShape<PS>::NR], double e, uint32_t bw,
-                                          const PairUni *__restrict__ puni, double *__restrict__ y, int r0,
-                                          int lane, double &dot) {
+template <int PS, bool CLEAN>
+__device__ __forceinline__ dbl2 pair_sums(const dbl2 (&L)[PairShape<PS>::NR], double e, uint32_t bw,
+                                          const PairUni *__restrict__ puni, int lane) {
   using SH = PairShape<PS>;
-  constexpr int K = SH::K, C = SH::CENTER_RUN;
+  constexpr int K = SH::K;
   const PairUni &B = puni[bw & PBLK_ID];                  // wave-uniform: scalar loads
+  // !CLEAN: the lane's own presence bits (one vector load; 2K wave-uniform
+  // masks beside the 2K values spilled SGPRs)
+  const uint32_t pb = CLEAN ? 0u : B.lane[lane];
   double s0v = 0.0, s1v = 0.0, lo = 0.0, hi = 0.0;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
@@ -82,18 +84,28 @@ __device__ __forceinline__ void pair_unit(const dbl2 (&L)[PairShape<PS>::NR], do
       s0v = q0;
       s1v = q1;
     } else {
-      s0v = __builtin_amdgcn_inverse_ballot_w64(B.pm[j]) ? q0 : s0v;
-      s1v = __builtin_amdgcn_inverse_ballot_w64(B.pm[K + j]) ? q1 : s1v;
+      s0v = ((pb >> j) & 1u) ? q0 : s0v;
+      s1v = ((pb >> (K + j)) & 1u) ? q1 : s1v;
     }
   }
-  *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
-  if constexpr (MODE == SPMV_DOT) {
+  return dbl2{s0v, s1v};
+}
+
+// y = the sums (not stored for SPMV_PW); SPMV_DOT / SPMV_PW: + the p.y terms
+template <int MODE, int PS, bool SPLIT, bool CLEAN>
+__device__ __forceinline__ void pair_unit(const dbl2 (&L)[PairShape<PS>::NR], double e, uint32_t bw,
+                                          const PairUni *__restrict__ puni, double *__restrict__ y, int r0,
+                                          int lane, double &dot) {
+  constexpr int C = PairShape<PS>::CENTER_RUN;
+  const dbl2 sv = pair_sums<PS, CLEAN>(L, e, bw, puni, lane);
+  if constexpr (MODE != SPMV_PW) *reinterpret_cast<dbl2 *>(y + r0) = sv;
+  if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
     // SPLIT: rows with A_o entries stored their diagonal-block sum; the
     // boundary kernel continues them and adds their p.y terms
     const bool gh = SPLIT && (bw & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
     if (!gh) {
-      dot += L[C].x * s0v;
-      dot += L[C].y * s1v;
+      dot += L[C].x * sv.x;
+      dot += L[C].y * sv.y;
     }
   }
 }
@@ -185,11 +197,49 @@ __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs 
 // carried operand whose run is empty for this unit is zeroed at use (it is
 // real x, read for the neighbouring unit); inner runs and the edge take the
 // out-of-range read as in the sweep form.
-template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU>
+//
+// CG mode 5 (one rank; x = p_i, the direction): w = A p is never stored.
+//   SPMV_PW: only the p.w partials (the MatMult's 8 B/row of y written and
+//   the update pass's 8 B/row of w read disappear);
+//   SPMV_RUPD: the update pass -- every workgroup folds p.w from the PW pass's
+//   partials and evaluates alpha (cg_alpha, workgroup 0 commits it), then per
+//   unit recomputes A p (the same sums, the same bits as the PW pass's) and
+//   forms r = r - alpha A p (BLAS daxpy's fma), z = c r and the [z.z, z.r, r.r]
+//   partials, folded in-launch into red3.  p is re-read from the memory-side
+//   cache the PW pass left it in; r is read non-temporally (the direction
+//   update reads the r written here next).
+struct PairRuArgs {
+  KspState *s;
+  double *r;                   // r_i in, r_{i+1} out
+  const double *r0;            // iteration 0 of a zero-guess solve reads r_0 = b (not copied into r)
+  const double *dot_part;      // the PW pass's partials, folded here by every workgroup
+  int ndot, xb;
+  double c;                    // JM 2: the uniform Jacobi scalar 1 / d
+  int *hw;                     // the host's pinned words (Poller)
+};
+
+template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0>
 __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a, const double *__restrict__ x,
                                                            double *__restrict__ y, const int32_t *__restrict__ pblk,
-                                                           const PairUni *__restrict__ puni) {
-  if (a.done && *a.done) return;   // wave-uniform: solver finished
+                                                           const PairUni *__restrict__ puni, const PairRuArgs ru) {
+  constexpr bool RU = MODE == SPMV_RUPD;
+  double alpha = 0.0;
+  const double *rin = nullptr;
+  if constexpr (RU) {
+    KspState *s = ru.s;
+    if (s->top.done) {
+      if (ru.hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(ru.hw + HW_DONE, 1);
+      return;
+    }
+    const double pw = ru.ndot > 0 ? block_sum_array<16>(ru.dot_part, ru.ndot) : s->red1;
+    const CgAlpha al = cg_alpha(s, pw);
+    if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, ru.xb, false, ru.hw);
+    if (al.reason) return;
+    alpha = al.alpha;
+    rin = (ru.r0 && al.i == 0) ? ru.r0 : ru.r;
+  } else {
+    if (a.done && *a.done) return;   // wave-uniform: solver finished
+  }
   using SH = PairShape<PS>;
   constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
   const int lane = threadIdx.x & 63;
@@ -212,6 +262,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
   const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
   constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
   double dot = 0.0;
+  double nv[3] = {0.0, 0.0, 0.0};            // RU: [z.z, z.r, r.r]
   const int ntask = (se - sb) * a.P;
   for (int t = w; t < ntask; t += W) {
     const int seg = sb + t / a.P, col = t % a.P;
@@ -222,7 +273,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
     // NQ units (planes z .. z + NQ - 1) with all their loads in flight
     auto step = [&](int z, auto nq) __attribute__((always_inline)) {
       constexpr int NQ = decltype(nq)::value;
-      dbl2 L[NQ][NR], zp[NQ];
+      dbl2 L[NQ][NR], zp[NQ], rq[NQ];
       double e[NQ];
       uint32_t bw[NQ];
       bw[0] = bwn;
@@ -239,6 +290,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
         int eo = ecst;
         if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
         e[q] = bload1(xr, ub + eo);
+        if constexpr (RU) rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -253,7 +305,17 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
             if (bw[q] & (PBLK_RUN0 << LAST)) L[q][LAST] = dbl2{0.0, 0.0};
           }
         }
-        pair_unit<MODE, PS, SPLIT, CLEAN>(L[q], e[q], bw[q], puni, y, (z + q) * D + cb, lane, dot);
+        const int r0 = (z + q) * D + cb;
+        if constexpr (RU) {
+          const dbl2 w2 = pair_sums<PS, CLEAN>(L[q], e[q], bw[q], puni, lane);
+          const double ra = fma(-alpha, w2.x, rq[q].x), rb = fma(-alpha, w2.y, rq[q].y);
+          const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
+          nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
+          nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
+          *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+        } else {
+          pair_unit<MODE, PS, SPLIT, CLEAN>(L[q], e[q], bw[q], puni, y, r0, lane, dot);
+        }
       }
       if constexpr (NQ == 1) zm = c;
       else zm = zp[NQ - 2];
@@ -263,21 +325,30 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
     for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
     for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
   }
-  if constexpr (MODE == SPMV_DOT) {
+  if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
     double v[1] = {dot};
     block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  } else if constexpr (RU) {
+    block_partials<3>(nv, a.partials, gridDim.x, a.fold);
   }
 }
-
 
 // 27-point z-march (Sell::puni27).  The nine runs are (dz, dy) in {-1,0,1}^2
 // at anchors -D-n, -D, -D+n, -n, 0, +n, D-n, D, D+n (each a tri run c-1, c,
 // c+1); marching a column in z, the runs of planes z-1 and z (six pairs and
 // their edge values) are carried and a unit loads only plane z+1's three runs
-// and edges: 3 pair loads + 3 edge loads instead of 9 + 9.  CLEAN: the
-// block's flags (PairUni27::flags) zero lane 0's / lane 63's edge values where
-// the x-line starts / ends -- at use, so the carried values stay the real x
-// for the next unit; units with an empty run take the select body.
+// and edges: 3 pair loads + 3 edge loads instead of 9 + 9.
+//   CLEAN (every block select-free, Sell::pair_clean27): a block's absent
+//   entries are whole runs (the y/z-boundary classes) and the x-line's first /
+//   last entry (lane 0 row 0's -1, lane 63 row 1's +1 slots); an empty run is
+//   skipped by a wave-uniform branch (its operands are real x of the
+//   neighbouring line or plane, so it must add nothing, not v * x), and the
+//   x-edge value is zeroed at use (U27_ELO / U27_EHI: lane 0's / lane 63's
+//   edge), so sum + v * 0.0 = sum -- the carried values stay the real x for
+//   the next unit.  The two rows share each slot's value (clean requires
+//   v[j] == v[K + j]): 27 wave-uniform values, no lane masks.
+//   !CLEAN: presence selects from the lane's own 54 mask bits (PairUni27::lane,
+//   one vector load per unit) and the same 27 values.
 template <int MODE, bool SPLIT, bool CLEAN>
 __device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e)[9], uint32_t bw,
                                             const PairUni27 *__restrict__ puni, double *__restrict__ y, int r0,
@@ -285,40 +356,39 @@ __device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e
   constexpr int K = 27;
   const PairUni27 &B = puni[bw & PBLK_ID];                // wave-uniform: scalar loads
   double s0v = 0.0, s1v = 0.0;
-  // SEL: presence by the lane masks (every unit of a !CLEAN layout; a clean
-  // layout's units with an empty run -- the y/z-boundary classes, whose
-  // empty runs read real x of the neighbouring line or plane).  !SEL: no
-  // selects; lane 0's / lane 63's edge value is zeroed where the x-line
-  // starts / ends (U27_ELO / U27_EHI), so sum + v * 0.0 = sum
-  auto body = [&](auto selc, bool zlo, bool zhi) __attribute__((always_inline)) {
-    constexpr bool SEL = decltype(selc)::value;
+  if constexpr (CLEAN) {
+    const uint32_t fl = B.flags;
+    const bool zedge = lane == 0 ? (fl & U27_ELO) != 0 : (fl & U27_EHI) != 0;
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
-      double er = e[r];
-      if constexpr (!SEL) er = (lane == 0 ? zlo : zhi) ? 0.0 : er;
+      if (fl & (1u << r)) continue;                       // wave-uniform: an empty run
+      const double er = zedge ? 0.0 : e[r];
       const double lo = wave_shift<true>(L[r].y, er);     // x[r0 + c - 1]
       const double hi = wave_shift<false>(L[r].x, er);    // x[r0 + c + 2]
       const double a0[3] = {lo, L[r].x, L[r].y}, a1[3] = {L[r].x, L[r].y, hi};
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        const int j = 3 * r + p;
-        const double q0 = s0v + B.v[j] * a0[p], q1 = s1v + B.v[K + j] * a1[p];
-        if constexpr (SEL) {
-          s0v = __builtin_amdgcn_inverse_ballot_w64(B.pm[j]) ? q0 : s0v;
-          s1v = __builtin_amdgcn_inverse_ballot_w64(B.pm[K + j]) ? q1 : s1v;
-        } else {
-          s0v = q0;
-          s1v = q1;
-        }
+        const double v = B.v[3 * r + p];
+        s0v = s0v + v * a0[p];
+        s1v = s1v + v * a1[p];
       }
     }
-  };
-  if constexpr (CLEAN) {
-    const uint32_t fl = B.flags;
-    if (fl & 0x1ffu) body(std::true_type{}, false, false);   // wave-uniform
-    else body(std::false_type{}, (fl & U27_ELO) != 0, (fl & U27_EHI) != 0);
   } else {
-    body(std::true_type{}, false, false);
+    const unsigned long long pb = B.lane[lane];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const double lo = wave_shift<true>(L[r].y, e[r]);
+      const double hi = wave_shift<false>(L[r].x, e[r]);
+      const double a0[3] = {lo, L[r].x, L[r].y}, a1[3] = {L[r].x, L[r].y, hi};
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int j = 3 * r + p;
+        const double v = B.v[j];
+        const double q0 = s0v + v * a0[p], q1 = s1v + v * a1[p];
+        s0v = ((pb >> j) & 1ull) ? q0 : s0v;
+        s1v = ((pb >> (K + j)) & 1ull) ? q1 : s1v;
+      }
+    }
   }
   *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
   if constexpr (MODE == SPMV_DOT) {
@@ -690,6 +760,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zmcg_kernel(const PairLeanArgs 
 }
 
 using LeanFn = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const PairUni *);
+using ZmFn = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const PairUni *, PairRuArgs);
 
 // the layout side of the choice (mode and split aside): 0 none, 1 lean, 2 lean select-free
 int pair_lean_kind(const Mat *A) {
@@ -797,6 +868,7 @@ static int pair_f64_launch(Mat *A, int mode, bool split, const double *x, double
   if (mode == SPMV_PLAIN) { if (ps == 5) F64K(SPMV_PLAIN, 5); else F64K(SPMV_PLAIN, 7); }
   else { if (ps == 5) F64K(SPMV_DOT, 5); else F64K(SPMV_DOT, 7); }
 #undef F64K
+  note_dispatch(split ? DSP_PAIR_ZMF64_SPLIT : DSP_PAIR_ZMF64);
   launch_timed(f, grid, st, a, x, y, S.pflag.p, S.pval.p);
   HIPCHECK(hipGetLastError());
   return grid;
@@ -845,6 +917,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
     if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
     else { if (split) Z27(SPMV_DOT, true); else Z27(SPMV_DOT, false); }
 #undef Z27
+    note_dispatch(split ? DSP_PAIR_ZM27_SPLIT : DSP_PAIR_ZM27);
     launch_timed(f, grid, st, b, x, y, S.pblk.p, S.puni27.p);
     HIPCHECK(hipGetLastError());
     return grid;
@@ -859,6 +932,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   const int NR = S.pair_shape == 5 ? 3 : 5, D = a.anchor[NR - 1];
   const bool zm = pair_zm_applies(A);
   LeanFn f = nullptr;
+  ZmFn fz = nullptr;
   int grid;
   if (zm) {
     a.P = D / 128;
@@ -874,7 +948,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
     a.L = L;
     a.S = (a.NZ + L - 1) / L;
 #define ZM_PICK(MODE, PS, SP, CL) \
-    f = g_knobs.pair_zm_units == 2 ? &spmv_pair_zm_kernel<MODE, PS, SP, CL, 2> : &spmv_pair_zm_kernel<MODE, PS, SP, CL, 1>
+    fz = g_knobs.pair_zm_units == 2 ? &spmv_pair_zm_kernel<MODE, PS, SP, CL, 2> : &spmv_pair_zm_kernel<MODE, PS, SP, CL, 1>
 #define ZM_C(MODE, PS) do { if (split) { if (clean) ZM_PICK(MODE, PS, true, true); else ZM_PICK(MODE, PS, true, false); } \
                             else { if (clean) ZM_PICK(MODE, PS, false, true); else ZM_PICK(MODE, PS, false, false); } } while (0)
     if (mode == SPMV_PLAIN) { if (S.pair_shape == 5) ZM_C(SPMV_PLAIN, 5); else ZM_C(SPMV_PLAIN, 7); }
@@ -892,7 +966,9 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   a.fold = fold;
-  launch_timed(f, grid, st, a, x, y, S.pblk.p, S.puni.p);
+  note_dispatch(!zm ? DSP_PAIR_LEAN : split ? DSP_PAIR_ZM_SPLIT : DSP_PAIR_ZM);
+  if (zm) launch_timed(fz, grid, st, a, x, y, S.pblk.p, S.puni.p, PairRuArgs{});
+  else launch_timed(f, grid, st, a, x, y, S.pblk.p, S.puni.p);
   HIPCHECK(hipGetLastError());
   return grid;
 }
@@ -939,7 +1015,76 @@ int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac
   if (S.pair_shape == 5) { if (clean) ZMCG(5, true); else ZMCG(5, false); }
   else { if (clean) ZMCG(7, true); else ZMCG(7, false); }
 #undef ZMCG
+  note_dispatch(DSP_PAIR_ZMCG);
   launch_timed(f, grid, st, a, c, r, pb0, pb1, x, w, S.pblk.p, S.puni.p);
+  HIPCHECK(hipGetLastError());
+  return grid;
+}
+
+// CG mode 5 (knob 9 = 5): one rank, a lean 5/7-point z-march layout, no or
+// uniform Jacobi
+bool pair_cg5_applies(const Mat *A, int jac_mode) {
+  return A->comm->size == 1 && A->sd.pair_shape != 27 && (jac_mode == 0 || jac_mode == 2) && pair_lean_kind(A) > 0 &&
+         pair_zm_applies(A) && A->nghost == 0 && !A->sd.pair_ghosts;
+}
+
+static int cg5_args(const Mat *A, PairLeanArgs &a) {
+  const Sell &S = A->sd;
+  a = PairLeanArgs{};
+  a.m = (int)A->m;
+  a.n = (int)A->n;
+  a.nunits = (int)S.nunits;
+  pair_anchors(S, a.anchor);
+  const int D = a.anchor[S.pair_shape == 5 ? 2 : 4];
+  a.P = D / 128;
+  a.NZ = (int)(A->m / D);
+  return zm_tasks(a.P, a.NZ, a.L, a.S);
+}
+
+int pair_cg5_pw_launch(Mat *A, const double *p, double *partials, const int *done, const Fold *fold_in,
+                       hipStream_t st) {
+  if (!pair_cg5_applies(A, 0)) return 0;
+  PairLeanArgs a;
+  const int grid = cg5_args(A, a);
+  a.partials = partials;
+  a.done = done;
+  Fold fold = fold_in ? *fold_in : Fold{};
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  a.fold = fold;
+  const bool clean = pair_lean_kind(A) == 2, z2 = g_knobs.pair_zm_units == 2;
+  ZmFn f;
+#define PW(PS, CL) f = z2 ? &spmv_pair_zm_kernel<SPMV_PW, PS, false, CL, 2> : &spmv_pair_zm_kernel<SPMV_PW, PS, false, CL, 1>
+  if (A->sd.pair_shape == 5) { if (clean) PW(5, true); else PW(5, false); }
+  else { if (clean) PW(7, true); else PW(7, false); }
+#undef PW
+  note_dispatch(DSP_ZM_PW);
+  launch_timed(f, grid, st, a, p, nullptr, A->sd.pblk.p, A->sd.puni.p, PairRuArgs{});
+  HIPCHECK(hipGetLastError());
+  return grid;
+}
+
+int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, double *r, const double *r0, int jac_mode,
+                         double jac_c, double *partials, const Fold &fold_in, const double *dot_part, int ndot, int xb,
+                         int *hw, hipStream_t st) {
+  if (!pair_cg5_applies(A, jac_mode)) return 0;
+  PairLeanArgs a;
+  const int grid = cg5_args(A, a);
+  a.partials = partials;
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  a.fold = fold;
+  const PairRuArgs ru{s, r, r0, dot_part, ndot, xb, jac_c, hw};
+  const bool clean = pair_lean_kind(A) == 2, z2 = g_knobs.pair_zm_units == 2;
+  ZmFn f;
+#define RU(PS, CL, JM) f = z2 ? &spmv_pair_zm_kernel<SPMV_RUPD, PS, false, CL, 2, JM> \
+                              : &spmv_pair_zm_kernel<SPMV_RUPD, PS, false, CL, 1, JM>
+#define RU_J(PS, CL) do { if (jac_mode == 2) RU(PS, CL, 2); else RU(PS, CL, 0); } while (0)
+  if (A->sd.pair_shape == 5) { if (clean) RU_J(5, true); else RU_J(5, false); }
+  else { if (clean) RU_J(7, true); else RU_J(7, false); }
+#undef RU_J
+#undef RU
+  note_dispatch(DSP_ZM_RUPD);
+  launch_timed(f, grid, st, a, p, nullptr, A->sd.pblk.p, A->sd.puni.p, ru);
   HIPCHECK(hipGetLastError());
   return grid;
 }

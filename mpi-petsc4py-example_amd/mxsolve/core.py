@@ -392,5 +392,17 @@ def vmaxpy(comm: DeviceComm, y, alphas, xs):
     call("mx_vec_maxpy", comm.h, y.numel(), _ptr(y), len(xs), a.ctypes.data_as(C.POINTER(C.c_double)), arr)
 
 
+DISPATCH_KINDS = ("sell", "sell_cg", "pair_lean", "pair_zm", "pair_zm_split", "pair_zm27", "pair_zm27_split",
+                  "pair_zmf64", "pair_zmf64_split", "pair_zmcg", "boundary", "zm_pw", "zm_rupd")
+
+
+def dispatch_counts(reset: bool = False) -> dict:
+    """Host-side counts of the MatMult-family launches by kernel kind since the
+    last reset (mx_debug_dispatch_counts; replayed graph launches not counted)."""
+    out = (C.c_int64 * 16)()
+    call("mx_debug_dispatch_counts", out, 16, int(reset))
+    return {k: int(out[i]) for i, k in enumerate(DISPATCH_KINDS)}
+
+
 def rhs_hash(comm, i0: int, out: torch.Tensor):
     call("mx_vec_rhs_hash", comm.h, i0, out.numel(), _ptr(out))

@@ -268,3 +268,76 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
         o = O.solve(bh, ksp="cg", pc=pc, rtol=1e-8)
         assert m4[0][1] == o["reason"] and abs(m4[0][0] - o["its"]) <= 1
         assert np.linalg.norm(m4[0][3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
+
+
+@pytest.mark.parametrize("kind,n,pc,max_it,kw", [("poisson3d", 128, "jacobi", 10000, {}),
+                                                 ("poisson3d", 64, "jacobi", 10000, {}),
+                                                 ("poisson2d", 256, "none", 10000, {}),
+                                                 ("poisson3d", 128, "jacobi", 37, {}),
+                                                 ("poisson3d", 128, "jacobi", 1, {}),
+                                                 ("poisson3d", 128, "jacobi", 2, {}),
+                                                 ("poisson2d", 384, "jacobi", 10000, {}),
+                                                 ("poisson3d", 128, "jacobi", 10000, {"guess": True}),
+                                                 ("poisson3d", 128, "jacobi", 10000, {"norm": "natural"}),
+                                                 ("poisson3d", 128, "jacobi", 10000, {"norm": "unpreconditioned"})])
+def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
+    """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
+    gives p.w, and the update pass recomputes A p (the same sums, the same
+    bits) where it forms r - alpha A p and the norms.  Against the oracle: its
+    and reason equal, history within 1e-8, x within rel-L2 1e-10; against mode
+    2 (the stored-product iteration): the same its and reason, iterates equal
+    to rounding (the norms' partials are grouped per z-march column); the
+    graph-replayed second solve gives the first one's bits; the dispatch
+    counts show both mode-5 passes ran."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    L = _lib.load()
+    guess = kw.get("guess", False)
+    norm = kw.get("norm", "default")
+
+    def run(mode):
+        old = L.mx_debug_set(9, mode)
+        old27 = L.mx_debug_set(27, 1)           # the row-pair layout (this module's fixture turns it off)
+        try:
+            A = DMat.stencil(selfcomm, kind, n)
+            m = A.info()["m"]
+            b = selfcomm.empty(m)
+            rhs_hash(selfcomm, 0, b)
+            x0 = selfcomm.zeros(m)
+            if guess:
+                rhs_hash(selfcomm, 7, x0)
+                x0.mul_(0.25)
+            x = selfcomm.zeros(m)
+            outs = []
+            dispatch_counts(reset=True)
+            for k in range(2):                  # the second solve replays the cached graph
+                x.copy_(x0)
+                r = A.solve(b, x, ksp="cg", pc=pc, rtol=1e-8, max_it=max_it, history=True, norm=norm,
+                            guess_nonzero=guess)
+                outs.append((r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy()))
+                if k == 0:
+                    dc = dispatch_counts(reset=True)
+            A.destroy()
+            return outs, dc, b.cpu().numpy(), x0.cpu().numpy()
+        finally:
+            L.mx_debug_set(9, old)
+            L.mx_debug_set(27, old27)
+
+    m5, dc5, bh, x0 = run(5)
+    m2, dc2, _, _ = run(2)
+    # (a nonzero guess forms r = b - A x with the stored-product MatMult first)
+    assert dc5["zm_pw"] > 0 and dc5["zm_rupd"] > 0 and dc5["pair_zm"] == (1 if guess else 0), dc5
+    assert dc2["zm_pw"] == 0 and dc2["pair_zm"] > 0, dc2
+    for a, c in zip(m5, m2):
+        assert a[:2] == c[:2], (a[:2], c[:2])
+        assert np.allclose(a[2], c[2], rtol=1e-10, atol=0)
+        assert np.linalg.norm(a[3] - c[3]) <= 1e-12 * max(np.linalg.norm(c[3]), 1e-300)
+    assert m5[0][:2] == m5[1][:2]
+    assert np.array_equal(m5[0][2].view(np.uint64), m5[1][2].view(np.uint64))
+    assert np.array_equal(m5[0][3].view(np.uint64), m5[1][3].view(np.uint64))
+    ip, c_, v = oracle_mod.stencil(kind, n)
+    O = oracle_mod.OracleMat.from_csr(ip.size - 1, ip.size - 1, ip, c_, v)
+    o = O.solve(bh, x0=x0 if guess else None, ksp="cg", pc=pc, rtol=1e-8, max_it=max_it, norm=norm, history=True)
+    assert (m5[0][0], m5[0][1]) == (o["its"], o["reason"]), (m5[0][:2], o["its"], o["reason"])
+    assert np.allclose(m5[0][2], o["history"], rtol=1e-8, atol=0)
+    assert np.linalg.norm(m5[0][3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])

@@ -507,3 +507,145 @@ def test_distributed_fp64_row_pairs(oracle_mod, P, kind, n):
     assert all(r[2] == o["its"] and r[3] == o["reason"] for r in res), ([r[2:4] for r in res], o["its"])
     xs = np.concatenate([r[4] for r in res])
     assert np.linalg.norm(xs - o["x"]) <= REL_TOL * np.linalg.norm(o["x"])
+
+
+# ------------------------------------------------------------------ the north-star partition
+_NS_CACHE = {}
+
+
+def _north_star_oracle(oracle_mod, n, P=8):
+    """The oracle's P-rank model of 3D 7-point n^3: a MatMult of a seeded x and
+    the CG + Jacobi solve of test.py:50 on the hashed right-hand side (the
+    oracle's own threads), cached across the fusion-mode cases."""
+    from _hostinfo import host_threads
+    key = (n, P)
+    if key not in _NS_CACHE:
+        _NS_CACHE.clear()
+        ip, c, v = oracle_mod.stencil("poisson3d", n)
+        M = ip.size - 1
+        O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+        del ip, c, v
+        xr = np.random.default_rng(8).standard_normal(M)
+        y = O.mult(xr)
+        o = O.solve(oracle_mod.rhs_hash(0, M), ksp="cg", nthreads=host_threads())
+        del O
+        _NS_CACHE[key] = (xr, y, o)
+    return _NS_CACHE[key]
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n,fuse", [(128, 3), (128, 2), (256, 3), (256, 2)])
+def test_north_star_partition_p8(oracle_mod, n, fuse):
+    """BASELINE C3's target partition: 3D 7-point n^3 over P = 8 row blocks
+    (test.py:68-74's PetscSplitOwnership: n/8 planes per rank, one ghost plane
+    from each neighbour -- 2 n^2 ghosts on the interior ranks), solved by
+    test.py:50's CG + Jacobi with the fusion mode the 8-GPU node runs:
+    fuse 3 = auto (mode 1 at <= 3M rows/rank: the CG-fused general SELL
+    MatMult, halo packed from r / p_{i-1}, the boundary kernel) and mode 2
+    (the z-march SPLIT kernel with the ghost units flagged, the boundary
+    kernel finishing them).  MatMult bit-exact, its and reason equal to the
+    oracle's P = 8 model, x within rel-L2 1e-10; the dispatch counts show
+    which MatMult kernels ran."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    P = 8
+    xr, y_ref, o = _north_star_oracle(oracle_mod, n)
+    M = n ** 3
+    ranges = oracle_mod.split_ownership(M, P)
+
+    def body(comm):
+        A = DMat.stencil(comm, "poisson3d", n)
+        info = A.info()
+        r0, r1 = ranges[comm.rank], ranges[comm.rank + 1]
+        xl = torch.from_numpy(xr[r0:r1].copy()).cuda()
+        yl = comm.zeros(info["m"])
+        A.mult(xl, yl)
+        b = comm.empty(info["m"])
+        rhs_hash(comm, info["rstart"], b)
+        x = comm.zeros(info["m"])
+        rs = A.solve(b, x, ksp="cg")
+        out = (dict(info), yl.cpu().numpy(), rs["its"], rs["reason"], x.cpu().numpy())
+        A.destroy()
+        return out
+
+    L = _lib.load()
+    old = L.mx_debug_set(9, fuse)
+    dispatch_counts(reset=True)
+    try:
+        res = run_ranks(P, body)
+    finally:
+        L.mx_debug_set(9, old)
+    dc = dispatch_counts(reset=True)
+    plane = n * n
+    for q, (info, *_rest) in enumerate(res):
+        nb = (q > 0) + (q < P - 1)
+        assert info["rstart"] == ranges[q] and info["m"] == M // P == (n // P) * plane
+        assert info["nghost"] == nb * plane and info["nrecv"] == nb * plane and info["nsend"] == nb * plane
+        assert info["nnz_o"] == nb * plane and info["pair_zmarch"] == 1
+    assert np.array_equal(np.concatenate([r[1] for r in res]).view(np.uint64), y_ref.view(np.uint64))
+    assert all(r[2] == o["its"] and r[3] == o["reason"] == 2 for r in res), ([r[2:4] for r in res], o["its"])
+    xs = np.concatenate([r[4] for r in res])
+    assert np.linalg.norm(xs - o["x"]) / np.linalg.norm(o["x"]) <= REL_TOL
+    its = o["its"]
+    # the MatMult above: the z-march SPLIT kernel on every rank + the boundary kernel
+    assert dc["pair_zm_split"] >= P and dc["boundary"] >= P
+    if fuse == 3:     # auto at 2M / 262k rows per rank: mode 1
+        assert dc["sell_cg"] >= P * its and dc["pair_zm_split"] == P, dc
+    else:
+        assert dc["sell_cg"] == 0 and dc["pair_zm_split"] >= P * (its + 1), dc
+    assert dc["boundary"] >= P * (its + 1)
+
+
+@pytest.mark.timeout(900)
+def test_c5_p8_weak_scaling_properties():
+    """BASELINE C5 at P = 8: 27-point 512 x 512 x 512 (512 x 512 x 64 per rank,
+    generated per rank on the device instead of test.py:59-117's rank-0
+    build), CG + Jacobi.  The oracle cannot hold the 3.6 G-entry matrix, so
+    the solve is checked by size-independent properties: per-rank nnz and the
+    A_o split from the grid formula, the 2 MiB ghost planes, the converged
+    reason, and the true preconditioned residual ||D^-1 (b - A x)|| (one
+    distributed MatMult) at the rtol level and equal to the recurrence's final
+    norm; the 27-point z-march SPLIT kernel ran on every rank."""
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    P, nx, ny, nz = 8, 512, 512, 512
+    ranges = np.arange(P + 1, dtype=np.int64) * (nx * ny * nz // P)
+    plane = nx * ny
+    per_plane = (3 * nx - 2) * (3 * ny - 2)
+
+    def body(comm):
+        A = DMat.stencil(comm, "poisson3d27", nx, ny, nz)
+        info = dict(A.info())
+        m = info["m"]
+        b = comm.empty(m)
+        rhs_hash(comm, info["rstart"], b)
+        x = comm.zeros(m)
+        rs = A.solve(b, x, ksp="cg")
+        ax = comm.empty(m)
+        A.mult(x, ax)
+        d = comm.empty(m)
+        A.diagonal(d)
+        z = (b - ax) / d
+        zz = float(torch.dot(z, z))
+        bb = float(torch.dot(b / d, b / d))
+        A.destroy()
+        return info, rs["its"], rs["reason"], rs["rnorm"], zz, bb
+
+    dispatch_counts(reset=True)
+    res = run_ranks(P, body)
+    dc = dispatch_counts(reset=True)
+    for q, (info, *_r) in enumerate(res):
+        z0, z1 = ranges[q] // plane, ranges[q + 1] // plane
+        cz = sum(2 if k in (0, nz - 1) else 3 for k in range(z0, z1))
+        nb = (q > 0) + (q < P - 1)
+        assert info["rstart"] == ranges[q] and info["m"] == 64 * plane
+        assert info["nnz_d"] + info["nnz_o"] == per_plane * cz
+        assert info["nnz_o"] == nb * per_plane
+        assert info["nghost"] == nb * plane and info["nrecv"] * 8 == nb * (2 << 20)
+    its = {r[1] for r in res}
+    assert len(its) == 1 and all(r[2] == 2 for r in res), [r[1:3] for r in res]
+    zr = np.sqrt(sum(r[4] for r in res))
+    zb = np.sqrt(sum(r[5] for r in res))
+    rnorm = res[0][3]
+    assert zr <= 1.5e-5 * zb, (zr, zb)
+    assert abs(zr - rnorm) <= 0.05 * zr + 1e-12 * zb, (zr, rnorm)
+    assert dc["pair_zm27_split"] >= P * next(iter(its)), dc

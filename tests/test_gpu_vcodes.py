@@ -344,7 +344,8 @@ def test_pair_lean_kernel(selfcomm, oracle_mod, kind, n, lean, form):
     other than the unit's edge lane (x-lines of 64 / 96 / 48 rows inside a
     128-row unit) keeps the presence selects.
     The 27-point operator has the z-march form only (nine runs, six carried);
-    its clean layout takes the select body on the units with an empty run.
+    its clean layout skips a unit's empty runs by a wave-uniform branch, the
+    other layout selects by the lane's transposed mask bits.
     Operand values include infinities and NaN: an absent slot must not let them
     into a row that PETSc's product keeps finite."""
     ip, c, v = oracle_mod.stencil(kind, n)
