@@ -67,17 +67,24 @@ def cg_spmv_bytes(m: int, nnz: int, nghost: int) -> int:
     return spmv_bytes(m, nnz, nghost) + 32 * m
 
 
-def cg_iter_bytes_design(m: int, nnz: int, nghost: int, mode: int) -> int:
-    """This design's CG iteration with the uniform Jacobi as a scalar, by fusion
-    mode (knob 9): 0 separate passes, SpMV + 72 B/row (p update 24, x/r update
-    48); 1 MatMult-fused, SpMV + 56 (32 in the MatMult, r update 24); 2 x step
-    deferred into the p update, SpMV + 64 (p/x update 40, r update 24)."""
-    return spmv_bytes(m, nnz, nghost) + {0: 72, 1: 56, 2: 64}[mode] * m
+def pair_meta_bytes(info: dict, m: int, nnz: int, nghost: int) -> int:
+    """The layout's non-vector bytes per product (slice metadata, block ids,
+    the dictionary, A_o): spmv_format_bytes minus x read and y written."""
+    return spmv_format_bytes(info, m, nnz, nghost) - 8 * (m + nghost) - 8 * m
 
 
-def fusion_mode(knob: int, m: int) -> int:
-    """The mode cg_solve runs for knob 9 (3 = auto, mx_ksp.hip)."""
-    return (1 if m <= (3 << 20) else 2) if knob == 3 else knob
+def cg_iter_bytes_design(info: dict, m: int, nnz: int, nghost: int, mode: int) -> int:
+    """This design's CG iteration with the uniform Jacobi as a scalar, by the
+    fusion mode that ran (knob 9): 0 separate passes, MatMult + 72 B/row (p
+    update 24, x/r update 48); 1 MatMult-fused, MatMult + 56 (32 in the
+    MatMult, r update 24); 2 x step deferred into the p update, MatMult + 64
+    (p/x update 40, r update 24); 5 no product stored: the p update (40), the
+    p.Ap pass (p read: 8 + meta) and the residual update (p read again, r read
+    and written: 24 + meta)."""
+    if mode == 5:
+        meta = pair_meta_bytes(info, m, nnz, nghost)
+        return 40 * m + (8 * (m + nghost) + meta) + (8 * (m + nghost) + 16 * m + meta)
+    return spmv_format_bytes(info, m, nnz, nghost) + {0: 72, 1: 56, 2: 64, 4: 48}.get(mode, 64) * m
 
 
 def cpu_threads() -> tuple[int, str]:
@@ -104,7 +111,8 @@ def cpu_threads() -> tuple[int, str]:
 def cpu_baseline(grid: int, threads: int, how: str) -> dict:
     """The oracle's C restatement of PETSc's CG (oracle/petsc_oracle.c) on the
     host cores: the full converged solve of the same system (rtol 1e-5,
-    Jacobi), timed with its matrix build -- a measured time-to-solution."""
+    Jacobi), SURVEY.md §8d's timing -- the median of 3 solves after one
+    warm-up -- plus the host matrix build, a measured time-to-solution."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     t0 = time.perf_counter()
@@ -114,10 +122,13 @@ def cpu_baseline(grid: int, threads: int, how: str) -> dict:
     del ip, c, v
     b = oracle.rhs_hash(0, M)
     setup = time.perf_counter() - t0
-    A.solve(b, ksp="cg", rtol=0.0, max_it=2, nthreads=threads)      # warm threads/pages
-    t0 = time.perf_counter()
-    r = A.solve(b, ksp="cg", pc="jacobi", nthreads=threads)        # converged, default tolerances
-    dt = time.perf_counter() - t0
+    A.solve(b, ksp="cg", rtol=0.0, max_it=20, nthreads=threads)      # warm-up: threads, pages
+    times, r = [], None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        r = A.solve(b, ksp="cg", pc="jacobi", nthreads=threads)    # converged, default tolerances
+        times.append(time.perf_counter() - t0)
+    dt = sorted(times)[1]
     model = "unknown CPU"
     try:
         with open("/proc/cpuinfo") as f:
@@ -126,12 +137,12 @@ def cpu_baseline(grid: int, threads: int, how: str) -> dict:
         pass
     return {"value": round(r["its"] / dt, 3), "unit": "CG iterations/s", "cores": threads,
             "kind": "port", "its": int(r["its"]), "reason": int(r["reason"]),
-            "solve_s": round(dt, 3), "assembly_s": round(setup, 3),
+            "solve_s": round(dt, 3), "solve_s_all": [round(t, 3) for t in times], "assembly_s": round(setup, 3),
             "time_to_solution_s": round(dt + setup, 3), "threads_from": how,
             "sample": f"the full converged CG+Jacobi solve ({r['its']} its, rtol 1e-5) of the {grid}^3 7-point "
-                      f"system, matrix built and assembled on the host first (oracle/petsc_oracle.c, "
-                      f"PETSc-restatement not PETSc, 1 rank x {threads} OpenMP threads on {model}, "
-                      f"nproc {os.cpu_count()}, solve {dt:.1f} s, build {setup:.1f} s)"}
+                      f"system, median of 3 solves after a 20-iteration warm-up, matrix built and assembled on the "
+                      f"host first (oracle/petsc_oracle.c, PETSc-restatement not PETSc, 1 rank x {threads} OpenMP "
+                      f"threads on {model}, nproc {os.cpu_count()}, solve {dt:.1f} s, build {setup:.1f} s)"}
 
 
 def stream_copy_gbps(device, n: int) -> float:
@@ -151,12 +162,14 @@ def stream_copy_gbps(device, n: int) -> float:
     return 2 * 8 * n * 20 / (e0.elapsed_time(e1) * 1e-3) / 1e9
 
 
-def load_traffic(grid: int, n_gpus: int):
+def load_traffic(grid: int, n_gpus: int, mode: int):
+    """Committed PMC traffic of the roofline kernel (profiles/spmv_traffic.json,
+    key "<grid>^3/N<n>" plus "/mode5" for mode 5's residual update)."""
     path = os.path.join(ROOT, "profiles", "spmv_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        key = f"{grid}^3/N{n_gpus}"
+        key = f"{grid}^3/N{n_gpus}" + ("/mode5" if mode == 5 else "")
         return d.get(key)
     except (OSError, ValueError):
         return None
@@ -176,8 +189,6 @@ def main():
     from mxsolve import _lib
     from mxsolve.core import DeviceComm, DMat, rhs_hash, unique_id
     L = _lib.load()
-    fknob = L.mx_debug_set(9, 3)        # read the CG-fusion knob (restored below)
-    L.mx_debug_set(9, fknob)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -265,18 +276,35 @@ def main():
     value = args.steps / dt
 
     # roofline pass: the same CG iterations with a HIP event pair on every
-    # SpMV launch (on the library stream the kernel runs on; one rank: the
-    # events are attached to the kernel's own dispatch by hipExtLaunchKernel,
-    # so they time the kernel alone, as the profiler's trace does).  Kept out
-    # of the K timed steps: the profiled solve runs eagerly (no graph).
+    # MatMult-family launch (on the library stream the kernel runs on; one
+    # rank: the events are attached to the kernel's own dispatch by
+    # hipExtLaunchKernel, so they time the kernel alone, as the profiler's
+    # trace does).  Kept out of the K timed steps: the profiled solve runs
+    # eagerly (no graph).  profile bit 0: the MatMult (mode 5: the p.Ap pass),
+    # bit 1: mode 5's residual update
     x.zero_()
-    rp = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=min(args.steps, 100), profile=True)
+    rp = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=min(args.steps, 100), profile=3)
+    mode = rp["cg_mode"]
     spmv_avg_ms = rp["spmv_ms"] / max(rp["spmv_count"], 1)
     bytes_csr = spmv_bytes(m, nnz_loc, ng)
     bytes_spmv = spmv_format_bytes(info, m, nnz_loc, ng)
-    mode = fusion_mode(fknob, m)
-    bytes_launch = bytes_spmv + (32 * m if mode == 1 else 0)   # SPMV_CG: + r, x r/w, p_i
-    achieved = bytes_launch / (spmv_avg_ms * 1e-3) / 1e9
+    meta = pair_meta_bytes(info, m, nnz_loc, ng)
+    pw = None
+    if mode == 5:
+        # the dominant SpMV-bearing kernel: the residual update (A p recomputed,
+        # r read and written); the p.Ap pass reported beside it
+        upd_avg_ms = rp["upd_ms"] / max(rp["upd_count"], 1)
+        bytes_launch = 8 * (m + ng) + 16 * m + meta
+        avg_ms = upd_avg_ms
+        bytes_pw = 8 * (m + ng) + meta
+        pw = {"kernel": "spmv_pair_zm_kernel<SPMV_PW> (p.Ap partials, product not stored)",
+              "avg_launch_ms": round(spmv_avg_ms, 5), "bytes_per_launch": bytes_pw,
+              "GBps": round(bytes_pw / (spmv_avg_ms * 1e-3) / 1e9, 1),
+              "frac": round(bytes_pw / (spmv_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    else:
+        bytes_launch = bytes_spmv + (32 * m if mode == 1 else 0)   # SPMV_CG: + r, x r/w, p_i
+        avg_ms = spmv_avg_ms
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     # standalone SpMV timing (same kernel, back-to-back)
     y = comm.empty(m)
     spmv_alone_ms, mult_ms = A.bench_mult(b, y, 50)
@@ -327,8 +355,10 @@ def main():
         threads, how = cpu_threads()
         cpu = cpu_baseline(n, threads, how)
 
+    iter_bytes = cg_iter_bytes_design(info, m, nnz_loc, ng, mode)
+    iter_gbps = iter_bytes * value / 1e9
     if rank == 0:
-        traffic = load_traffic(n, world)
+        traffic = load_traffic(n, world, mode)
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "CG iterations/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -340,14 +370,19 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "traffic_source": (traffic.get("source", "") + " -- rocprofv3 PMC (FETCH_SIZE x 2 + "
+                                            "WRITE_SIZE, gfx950 correction) of the same kernel on a builder box, "
+                                            "not counters of this run") if traffic else None,
                          "traffic_detail": traffic,
-                         "kernel": ("spmv_sell_kernel<SPMV_CG> (CG-fused MatMult" if mode == 1 else
+                         "kernel": ("spmv_pair_zm_kernel<SPMV_RUPD> (CG mode 5 residual update: r -= alpha A p "
+                                    "with A p recomputed, [z.z, z.r, r.r] folded" if mode == 5 else
+                                    "spmv_sell_kernel<SPMV_CG> (CG-fused MatMult" if mode == 1 else
                                     ("spmv_pair_zm_kernel<SPMV_DOT> (CG MatMult, lean row-pair z-march" if info.get("pair_zmarch") else
                                      "spmv_pair_lean_kernel<SPMV_DOT> (CG MatMult, lean row-pair" if info.get("pair_lean") else
                                      "spmv_sell_kernel<SPMV_DOT> (CG MatMult")) +
                                    (", HIP events attached to the kernel's dispatch (hipExtLaunchKernel)" if world == 1 else
                                     ", HIP events around the MatMult") + ", rank 0)",
-                         "bytes_per_launch": bytes_launch, "avg_launch_ms": round(spmv_avg_ms, 5),
+                         "bytes_per_launch": bytes_launch, "avg_launch_ms": round(avg_ms, 5),
                          "format": ("value codes (" + str(info.get("value_codes")) + " distinct), " +
                                     ("row pairs" if info.get("pair_shape") else "one row per lane") +
                                     (f", {info['pair_blocks']} distinct code blocks" if info.get("pair_blocks") else "") +
@@ -356,6 +391,7 @@ def main():
                          # how much faster than a CSR SpMV (SURVEY §8d bytes) streaming at HBM peak
                          "csr_bytes_per_launch": bytes_csr,
                          "speedup_vs_csr_at_peak": round((bytes_csr / (HBM_PEAK_GBS * 1e9)) / (spmv_avg_ms * 1e-3), 3)},
+            "pw_pass": pw,
             "cpu_baseline": cpu,
             "converged_its_per_s": solve["its_per_s"] if solve else None,
             "stream_copy_GBps": copy_gbps,
@@ -366,9 +402,11 @@ def main():
                                 "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1)},
             "cg_iter_bytes_survey": cg_iter_bytes(m, nnz_loc, ng),
             "cg_fusion_mode": mode,
-            "cg_iter_bytes_alg": cg_iter_bytes_design(m, nnz_loc, ng, mode) - bytes_csr + bytes_spmv,
-            "cg_iter_GBps_alg": round((cg_iter_bytes_design(m, nnz_loc, ng, mode) - bytes_csr + bytes_spmv)
-                                      * value / 1e9, 1),
+            "cg_iter_bytes_alg": iter_bytes,
+            "cg_iter_GBps_alg": round(iter_gbps, 1),
+            # the whole timed iteration (every kernel, the per-solve start and
+            # finish included) on its algorithmic bytes against HBM peak
+            "cg_iter_frac": round(iter_gbps / HBM_PEAK_GBS, 4),
             "comm_latency": comm_lat,
             "per_rank": per_rank,
             "solve": solve,

@@ -62,7 +62,9 @@ typedef struct {
   double haptol;       /* GMRES happy breakdown, 1e-30                                */
   double breakdowntol; /* GMRES restart consistency check, 0.1                        */
   int poll_every;      /* host polls the device convergence flag every k its (0: 16) */
-  int profile;         /* 1: time every SpMV launch with HIP events                   */
+  int profile;         /* bit 0: time every SpMV launch with HIP events; bit 1: every
+                          CG mode-5 residual-update launch (one rank: events attached
+                          to the kernel's dispatch)                                  */
 } mx_ksp_params;
 
 typedef struct {
@@ -73,6 +75,9 @@ typedef struct {
   double spmv_ms;      /* sum of profiled SpMV launch times (profile = 1)           */
   int spmv_count;      /* SpMV launches profiled                                    */
   int launched_its;    /* iterations enqueued (>= its; the tail are device no-ops)  */
+  int cg_mode;         /* CG: the fusion mode that ran (key 9's modes 0/1/2/4/5)     */
+  double upd_ms;       /* sum of profiled residual-update launch times (profile bit 1) */
+  int upd_count;       /* residual-update launches profiled                         */
 } mx_ksp_result;
 
 typedef struct {
@@ -249,7 +254,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        RCCL communicator (testing, default 0)
  * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
- *        1 for <= 3M local rows, else 2); 4 mode 2 with the direction update and
+ *        5 where it applies, else 1 for <= 3M local rows, else 2); 4 mode 2 with the direction update and
  *        the batched x steps inside the z-march MatMult (one rank, lean z-march
  *        layout, no or uniform Jacobi; else 2; mode 2's bits); 5 mode 2 whose
  *        MatMult stores no product: a p.Ap pass, and the update pass

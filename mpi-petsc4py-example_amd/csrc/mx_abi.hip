@@ -244,7 +244,9 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_uniform = info->pair_shape && info->pair_blocks > 0 && (A->sd.puni.p || A->sd.puni27.p) ? 1 : 0;
     info->pair_lean = pair_lean_kind(A);
     info->pair_zmarch = info->pair_lean && pair_zm_applies(A) ? 1 : 0;
-    info->pair_f64 = pair_f64_kind(A);
+    // the fp64 row-pair z-march runs only where the launch takes it: one rank,
+    // or a product that splits (otherwise the general kernel continues A_o)
+    info->pair_f64 = (A->nghost == 0 || matmult_splits(A)) ? pair_f64_kind(A) : 0;
   });
 }
 

@@ -186,11 +186,13 @@ struct Sell {
   DBuf<PairUni> puni;
   bool pair_clean = false;  // every puni block is select-free (PBLK_RUN0/ELO/EHI flags in pblk)
   DBuf<PairUni27> puni27;   // 27-point uniform-slot dictionary (mx_spmv_pair.hip z-march)
-  // fp64 row pairs (uncoded 5/7-point layouts, one rank): per unit u, slot j,
-  // lane l the values of rows 128u + 2l and + 1 (0.0 where absent) as one
-  // 16-byte pair at pval[(u * K + j) * 64 + l]; pflag[u] = the unit's
-  // select-free flags (PBLK_RUN0 << r, PBLK_ELO / EHI).  Built only when every
-  // unit is select-free (mx_spmv_pair.hip spmv_pair_zmf64_kernel)
+  // fp64 row pairs (uncoded 5/7-point layouts, any rank count): per unit u,
+  // slot j, lane l the values of rows 128u + 2l and + 1 (0.0 where absent) as
+  // one 16-byte pair at pval[(u * K + j) * 64 + l]; pflag[u] = the unit's
+  // select-free flags (PBLK_RUN0 << r, PBLK_ELO / EHI) and, on P > 1 ranks,
+  // PBLK_GHOST_LO / HI (the unit's first / second slice has A_o entries: the
+  // product splits and the boundary kernel finishes those rows).  Built only
+  // when every unit is select-free (mx_spmv_pair.hip spmv_pair_zmf64_kernel)
   DBuf<double> pval;
   DBuf<int32_t> pflag;
   int pair_f64 = 0;         // 5 / 7: the fp64 row-pair layout's shape, 0 none
@@ -210,6 +212,10 @@ constexpr uint32_t PBLK_RUN0 = 1u << 22;
 constexpr uint32_t PBLK_ELO = 1u << 27;
 constexpr uint32_t PBLK_EHI = 1u << 28;
 constexpr uint32_t PBLK_ID = PBLK_RUN0 - 1;   // block ids < 2^22 (units < 2^21, dictionaries <= 2048 blocks)
+// the flag fields must not reach the ghost bits: runs 0..4 (RUN0 << 4), the edges
+static_assert((PBLK_RUN0 << 4) < PBLK_ELO && PBLK_ELO < PBLK_EHI && PBLK_EHI < PBLK_GHOST_LO,
+              "PBLK select-free flags overlap the ghost bits");
+static_assert(((PBLK_RUN0 << 5) - PBLK_RUN0 | PBLK_ELO | PBLK_EHI | PBLK_ID) < PBLK_GHOST_LO, "PBLK field overlap");
 constexpr int64_t PAIR_MAX_ROWS = int64_t(1) << 28;   // operand byte offsets (unsigned 32-bit voffset, bound n * 8 < 2^31)
 constexpr int VCODE_MAX = 256;      // table entries; code 255 marks an absent slot
 constexpr int VCODE_ABSENT = VCODE_MAX - 1;

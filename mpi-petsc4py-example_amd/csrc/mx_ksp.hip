@@ -1169,7 +1169,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // mode 4 (knob 9 = 4): mode 2 whose direction update rides in the z-march
   // MatMult (mx_spmv_pair.hip spmv_pair_zmcg_kernel) -- one rank, a lean
   // z-march layout, no or uniform Jacobi, x steps batched by 2; otherwise 2
-  int fmode = g_knobs.cg_fuse == 3 ? (n <= CG_FUSE_MAX_ROWS ? 1 : 2) : g_knobs.cg_fuse;
+  // auto (3): mode 5 where it applies (one rank, lean 5/7-point z-march), else
+  // 1 up to CG_FUSE_MAX_ROWS local rows, else 2
+  int fmode = g_knobs.cg_fuse == 3 ? (fused && pair_cg5_applies(A, dinv.mode) ? 5 : n <= CG_FUSE_MAX_ROWS ? 1 : 2)
+                                   : g_knobs.cg_fuse;
   if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && g_knobs.cg_xbatch == 2 && poll % 2 == 0 && !p.guess_nonzero))
     fmode = 2;
   // mode 5 (knob 9 = 5): mode 2 whose MatMult stores no product -- a p.Ap
@@ -1190,8 +1193,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   const KspInit kin{p.rtol, p.atol, p.dtol, p.haptol, p.breakdowntol, p.max_it, normtype, !p.guess_nonzero, p.restart};
   ksp_state_init_kernel<<<1, 256, 0, st>>>(sd.p, kin);
   HIPCHECK(hipGetLastError());
-  SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
+  SpmvTimer timer((p.profile & 1) != 0, st, std::min(p.max_it, 4096));
   timer.ext = c->size == 1;
+  SpmvTimer utimer((p.profile & 2) != 0, st, std::min(p.max_it, 4096));   // mode 5's residual update
+  utimer.ext = c->size == 1;
 
   // r = b - A x  (or b)
   if (p.guess_nonzero) {
@@ -1297,6 +1302,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     const double *pcur = fuse_cg ? ((it & 1) ? pv2 : pv.p) : xb > 1 ? pbs.b[it % xb] : pv.p;
     // the update's own partials go after the MatMult's when it folds those
     double *upart = fold_in_update ? part.p + ((nb_spmv + 63) / 64) * 64 : part.p;
+    if (fmode == 5) utimer.begin();
     const int nb_upd =
         fmode == 5 ? pair_cg5_rupd_launch(A, s, pcur, r.p, xb > 1 ? r0 : nullptr, dinv.mode, dinv.c, upart, fupd,
                                           fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb,
@@ -1304,6 +1310,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
                    : cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, upart, fupd,
                                       fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb,
                                       xb > 1 ? r0 : nullptr, poller.hw);
+    if (fmode == 5) utimer.end();
     if (!nb_upd) fail(MX_ERR_INTERNAL, "CG without its update pass");
     if (!fupd.cnt) fold_kernel<3><<<1, 256, 0, st>>>(upart, nb_upd, s->top.red3, done);
     if (!fused) c->allreduce_sum(s->top.red3, 3);
@@ -1398,6 +1405,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   res.solve_ms = (double)ticks / wall_clock_khz(c->device);
   res.launched_its = i;
   timer.collect(res.spmv_ms, res.spmv_count);
+  utimer.collect(res.upd_ms, res.upd_count);
+  res.cg_mode = fmode;
   if (hist_host)
     HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)res.its + 1), hipMemcpyDeviceToHost));
 }

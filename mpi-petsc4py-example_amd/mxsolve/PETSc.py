@@ -1002,7 +1002,24 @@ class KSP:
         self._pc = pc
 
     def setOperators(self, A, P=None):
+        if A is not self._A:
+            self._release_operator()
+            if A is not None:
+                # the solver state lives on the operator (mx_ksp.hip): count the
+                # KSPs sharing it so one's reset leaves the others' state alone
+                A._ksp_users = getattr(A, "_ksp_users", 0) + 1
         self._A = A
+
+    def _release_operator(self):
+        """This KSP stops using its operator; the last user releases the
+        operator's solver state (KSPReset / KSPDestroy leave the Mat itself)."""
+        A, self._A = self._A, None
+        if A is None:
+            return
+        A._ksp_users = max(getattr(A, "_ksp_users", 1) - 1, 0)
+        h = A.getDeviceHandle()
+        if A._ksp_users == 0 and h is not None and h.h:
+            _guard(h.ksp_reset)
 
     def getOperators(self):
         return self._A, self._A
@@ -1154,16 +1171,14 @@ class KSP:
               f"PC Object:\n  type: {self._params()}")
 
     def reset(self):
-        """KSPReset: the solver state kept on the operator (work space, device
-        convergence state, captured CG graph, PCSetUp_Jacobi) is released."""
-        h = self._A.getDeviceHandle() if self._A is not None else None
-        if h is not None and h.h:
-            _guard(h.ksp_reset)
+        """KSPReset: the KSP drops its operator; the solver state kept on the
+        operator (work space, device convergence state, captured CG graph,
+        PCSetUp_Jacobi) is released when no other KSP uses it."""
+        self._release_operator()
         return self
 
     def destroy(self):
         self.reset()
-        self._A = None
         return self
 
 

@@ -313,7 +313,7 @@ class DMat:
         _lib.load().mx_ksp_default_params(C.byref(p))
         p.ksp_type, p.pc_type, p.norm_type = KSP_TYPES[ksp], PC_TYPES[pc], NORM_TYPES[norm]
         p.rtol, p.atol, p.dtol, p.max_it, p.restart = rtol, atol, dtol, max_it, restart
-        p.guess_nonzero, p.profile, p.poll_every = int(guess_nonzero), int(profile), poll_every
+        p.guess_nonzero, p.profile, p.poll_every = int(guess_nonzero), int(profile), poll_every   # profile: bool or bits
         r = KSPResult()
         h = np.zeros(max_it + 2) if history else None
         call("mx_ksp_solve", self.h, C.byref(p), _ptr(b), _ptr(x), C.byref(r),
@@ -325,7 +325,7 @@ class DMat:
 
     def ksp_reset(self):
         """KSPDestroy/KSPReset: drop the solver state kept on this operator."""
-        if self.h:
+        if self.h and self.comm.h:          # (the communicator's stream is synced)
             call("mx_ksp_destroy", self.h)
 
     def destroy(self):

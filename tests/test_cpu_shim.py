@@ -158,6 +158,57 @@ def test_petsc_binary_format_roundtrip(tmp_path, golden):
             petsc_io.read_mat(fh)
 
 
+def test_petsc_binary_known_bytes(tmp_path):
+    """F4 pinned byte for byte against PETSc's documented binary layout (MatView
+    / VecView with a binary viewer, 32-bit indices, big-endian), written out
+    here as literal bytes: MAT_FILE_CLASSID 1211216 = 0x00127B50, M, N, nz,
+    the row lengths, the column indices, the IEEE-754 big-endian values; then
+    VEC_FILE_CLASSID 1211214 = 0x00127B4E, N, the values.  Matrix
+    [[2, 0, 0], [-1, 3, 0], [0, 0.5, -4]], vector [1.5, -2, 0]."""
+    from mxsolve import petsc_io
+    expected = bytes.fromhex(
+        "00127b50" "00000003" "00000003" "00000005"                  # classid, M, N, nz
+        "00000001" "00000002" "00000002"                             # row lengths
+        "00000000" "00000000" "00000001" "00000001" "00000002"       # column indices
+        "4000000000000000" "bff0000000000000" "4008000000000000"     # 2, -1, 3
+        "3fe0000000000000" "c010000000000000"                        # 0.5, -4
+        "00127b4e" "00000003"                                        # Vec classid, N
+        "3ff8000000000000" "c000000000000000" "0000000000000000")    # 1.5, -2, 0
+    f = tmp_path / "k.bin"
+    with open(f, "wb") as fh:
+        petsc_io.write_mat(fh, 3, 3, [0, 1, 3, 5], [0, 0, 1, 1, 2], [2.0, -1.0, 3.0, 0.5, -4.0])
+        petsc_io.write_vec(fh, [1.5, -2.0, 0.0])
+    assert f.read_bytes() == expected
+    with open(f, "rb") as fh:
+        M, N, ip, cj, vv = petsc_io.read_mat(fh)
+        assert (M, N) == (3, 3) and list(ip) == [0, 1, 3, 5] and list(cj) == [0, 0, 1, 1, 2]
+        assert list(vv) == [2.0, -1.0, 3.0, 0.5, -4.0] and list(petsc_io.read_vec(fh)) == [1.5, -2.0, 0.0]
+
+
+def test_petsc_binary_bytes_independent(tmp_path, golden):
+    """The reference system (test.py's 100 x 100 matrix) and its right-hand
+    side: write_mat / write_vec output equals a byte stream built independently
+    with struct ('>i' per int32, '>d' per float64, element by element)."""
+    import struct
+    from mxsolve import petsc_io
+    ip, cj, vv, b = golden["sys_indptr"], golden["sys_indices"], golden["sys_data"], golden["sys_B"]
+    ref = bytearray(struct.pack(">4i", 1211216, 100, 100, int(ip[-1])))
+    for i in range(100):
+        ref += struct.pack(">i", int(ip[i + 1] - ip[i]))
+    for c in cj:
+        ref += struct.pack(">i", int(c))
+    for v in vv:
+        ref += struct.pack(">d", float(v))
+    ref += struct.pack(">2i", 1211214, b.size)
+    for v in b:
+        ref += struct.pack(">d", float(v))
+    f = tmp_path / "sys.bin"
+    with open(f, "wb") as fh:
+        petsc_io.write_mat(fh, 100, 100, ip, cj, vv)
+        petsc_io.write_vec(fh, b)
+    assert f.read_bytes() == bytes(ref)
+
+
 VEC_STASH_SCRIPT = textwrap.dedent('''
     import sys
     import numpy as np, torch

@@ -161,6 +161,30 @@ def test_binary_viewer_roundtrip(PETSc, golden, tmp_path):
     assert np.array_equal(b2.array, golden["sys_B"])
 
 
+def test_binary_viewer_known_bytes(PETSc, tmp_path):
+    """Mat.view / Vec.view through a binary viewer on a matrix assembled on the
+    GPU (unsorted input columns: the file holds the assembled, sorted rows)
+    write PETSc's documented bytes -- the literal stream of
+    tests/test_cpu_shim.py::test_petsc_binary_known_bytes."""
+    expected = bytes.fromhex(
+        "00127b50" "00000003" "00000003" "00000005" "00000001" "00000002" "00000002"
+        "00000000" "00000000" "00000001" "00000001" "00000002"
+        "4000000000000000" "bff0000000000000" "4008000000000000" "3fe0000000000000" "c010000000000000"
+        "00127b4e" "00000003" "3ff8000000000000" "c000000000000000" "0000000000000000")
+    ip = np.array([0, 1, 3, 5], dtype=np.int32)
+    cj = np.array([0, 1, 0, 2, 1], dtype=np.int32)
+    vv = np.array([2.0, 3.0, -1.0, -4.0, 0.5])
+    A = PETSc.Mat().createAIJ(size=(3, 3), csr=(ip, cj, vv))
+    A.assemble()
+    x, b = A.getVecs()
+    b.setArray(np.array([1.5, -2.0, 0.0]))
+    fn = tmp_path / "k.bin"
+    with PETSc.Viewer().createBinary(str(fn), "w") as vw:
+        A.view(vw)
+        b.view(vw)
+    assert fn.read_bytes() == expected
+
+
 def test_ascii_view_petsc_format(PETSc, capsys):
     """A.view() / b.view() (petsc_funcs.py:8, commented out in the reference)
     print PETSc's default ASCII format: "row i: (j, v) ..." with "%g" values."""

@@ -91,7 +91,9 @@ def main():
     # the solve's MatMult: the SpMV kernel with the most device time (the
     # CG-fused SPMV_CG <3,...> at <= 3M rows/rank, SPMV_DOT <2,...> above:
     # the general kernel or the lean row-pair / z-march kernels)
-    cands = [k for k in fetch if k.startswith(("spmv_sell_kernel<3,", "spmv_sell_kernel<2,",
+    # (CG mode 5: the residual update spmv_pair_zm_kernel<7,...> -- SPMV_RUPD --
+    # is the roofline kernel, keyed "/mode5")
+    cands = [k for k in fetch if k.startswith(("spmv_sell_kernel<3,", "spmv_sell_kernel<2,", "spmv_pair_zm_kernel<7,",
                                                "spmv_pair_zm_kernel<2,", "spmv_pair_lean_kernel<2,"))]
     sp = max(cands, key=lambda k: sum(durs.get(k, [0.0]))) if cands else None
     if sp and not sp.startswith("spmv_sell_kernel<3,"):
@@ -110,7 +112,7 @@ def main():
         wr = statistics.median(write[sp]) * 1024
         corr = f16 if f16 else 2.0
         traffic = fr * corr + wr
-        out[f"{grid}^3/N{ngpu}"] = {
+        out[f"{grid}^3/N{ngpu}" + ("/mode5" if sp.startswith("spmv_pair_zm_kernel<7,") else "")] = {
             "bytes_per_launch": round(traffic), "fetch_bytes_raw": round(fr), "write_bytes": round(wr),
             "fetch_correction": round(corr, 4), "calib_8B_per_lane": f8 and round(f8, 4),
             "calib_16B_per_lane": f16 and round(f16, 4), "algorithmic_bytes": alg,
