@@ -459,15 +459,17 @@ def test_local_barrier_then_collectives_skewed():
     assert out == [300 * 4000.0] * 4
 
 
-@pytest.mark.parametrize("P,kind,n", [(2, "poisson3d", 128), (4, "poisson2d", 512)])
-def test_distributed_fp64_row_pairs(oracle_mod, P, kind, n):
+@pytest.mark.parametrize("P,kind,n,overlap", [(2, "poisson3d", 128, 1), (4, "poisson2d", 512, 1), (2, "poisson3d", 128, 0)])
+def test_distributed_fp64_row_pairs(oracle_mod, P, kind, n, overlap):
     """Uncoded (every value distinct: the D A D scaled operator) 5/7-point
     blocks on P ranks: the fp64 row-pair z-march on every rank (the units of
     the planes next to another rank flagged as ghost units, the product split,
     the boundary kernel finishing them): MatMult bit-exact, CG (mode 2) against
-    the oracle."""
+    the oracle; the dispatch counts show the SPLIT fp64 kernel ran.  With the
+    halo overlap off (knob 6 = 0) the product does not split, the general
+    kernel continues A_o, and mx_mat_info.pair_f64 says so (0)."""
     from mxsolve import _lib
-    from mxsolve.core import DMat
+    from mxsolve.core import DMat, dispatch_counts
     ip, c, v = oracle_mod.stencil(kind, n)
     M = ip.size - 1
     rng = np.random.default_rng(31)
@@ -498,11 +500,20 @@ def test_distributed_fp64_row_pairs(oracle_mod, P, kind, n):
 
     L = _lib.load()
     old = L.mx_debug_set(9, 2)
+    old6 = L.mx_debug_set(6, overlap)
+    dispatch_counts(reset=True)
     try:
         res = run_ranks(P, body)
     finally:
         L.mx_debug_set(9, old)
-    assert all(r[0] in (5, 7) for r in res)
+        L.mx_debug_set(6, old6)
+    dc = dispatch_counts(reset=True)
+    if overlap:
+        assert all(r[0] in (5, 7) for r in res)
+        assert dc["pair_zmf64_split"] >= P * (res[0][2] + 1) and dc["boundary"] >= P, dc
+    else:
+        assert all(r[0] == 0 for r in res)
+        assert dc["pair_zmf64_split"] == 0 and dc["pair_zmf64"] == 0 and dc["sell"] >= P, dc
     assert np.array_equal(np.concatenate([r[1] for r in res]).view(np.uint64), y_ref.view(np.uint64))
     assert all(r[2] == o["its"] and r[3] == o["reason"] for r in res), ([r[2:4] for r in res], o["its"])
     xs = np.concatenate([r[4] for r in res])

@@ -161,6 +161,56 @@ def test_binary_viewer_roundtrip(PETSc, golden, tmp_path):
     assert np.array_equal(b2.array, golden["sys_B"])
 
 
+def test_ksp_destroy_keeps_shared_operator_state(PETSc):
+    """Two KSPs on one Mat: destroying one leaves the other's solver state on
+    the operator (PETSc's KSPDestroy leaves the Mat alone) -- its next solve
+    gives the same bits; the last user's reset releases the state and the Mat
+    still multiplies."""
+    from mxsolve.core import dispatch_counts
+    n = 32
+    A = PETSc.Mat().createAIJ(size=(n ** 3, n ** 3), csr=_poisson3d_csr(n))
+    A.assemble()
+    x, b = A.getVecs()
+    b.setArray(np.linspace(0.0, 1.0, n ** 3))
+    k1, k2 = PETSc.KSP().create(), PETSc.KSP().create()
+    for k in (k1, k2):
+        k.setType("cg")
+        k.getPC().setType("jacobi")
+        k.setOperators(A)
+    k1.solve(b, x)
+    x1 = x.array.copy()
+    x.set(0.0)
+    k2.solve(b, x)
+    assert np.array_equal(x.array.view(np.uint64), x1.view(np.uint64))
+    assert A._ksp_users == 2
+    k1.destroy()
+    assert A._ksp_users == 1 and A.getDeviceHandle().h
+    x.set(0.0)
+    k2.solve(b, x)
+    assert np.array_equal(x.array.view(np.uint64), x1.view(np.uint64))
+    k2.destroy()
+    assert A._ksp_users == 0
+    y = x.duplicate()
+    A.mult(b, y)
+    assert np.isfinite(y.array).all()
+
+
+def _poisson3d_csr(n):
+    import itertools
+    rows, cols, vals = [], [], []
+    ip = [0]
+    for k, j, i in itertools.product(range(n), range(n), range(n)):
+        r = i + n * j + n * n * k
+        for dk, dj, di, v in ((-1, 0, 0, -1.0), (0, -1, 0, -1.0), (0, 0, -1, -1.0), (0, 0, 0, 6.0),
+                              (0, 0, 1, -1.0), (0, 1, 0, -1.0), (1, 0, 0, -1.0)):
+            kk, jj, ii = k + dk, j + dj, i + di
+            if 0 <= kk < n and 0 <= jj < n and 0 <= ii < n:
+                cols.append(ii + n * jj + n * n * kk)
+                vals.append(v)
+        ip.append(len(cols))
+    return np.array(ip, np.int32), np.array(cols, np.int32), np.array(vals)
+
+
 def test_binary_viewer_known_bytes(PETSc, tmp_path):
     """Mat.view / Vec.view through a binary viewer on a matrix assembled on the
     GPU (unsorted input columns: the file holds the assembled, sorted rows)
