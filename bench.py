@@ -145,6 +145,109 @@ def cpu_baseline(grid: int, threads: int, how: str) -> dict:
                       f"threads on {model}, nproc {os.cpu_count()}, solve {dt:.1f} s, build {setup:.1f} s)"}
 
 
+HOST_LINK_PEAK_GBS = 64.0   # PCIe 5.0 x16, one direction (the MI355X host link)
+
+
+def host_csr_stencil(nx: int, ny: int, nz: int, kind: str = "7pt"):
+    """test.py's input form for createAIJ(csr=...): host numpy arrays, int32
+    row pointer and columns (petsc4py's default 32-bit PetscInt), fp64 values,
+    rows in natural order, columns ascending -- the 3D 7-point (diag 6, off -1)
+    or 27-point (diag 26, off -1) operator of SURVEY.md §8d, built here with
+    numpy (no oracle code)."""
+    import numpy as np
+    M = nx * ny * nz
+    r = np.arange(M, dtype=np.int64)
+    i, j, k = r % nx, (r // nx) % ny, r // (nx * ny)
+    if kind == "7pt":
+        offs = [(0, 0, -1), (0, -1, 0), (-1, 0, 0), (0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1)]
+        centre = 6.0
+    else:
+        offs = [(di, dj, dk) for dk in (-1, 0, 1) for dj in (-1, 0, 1) for di in (-1, 0, 1)]
+        centre = 26.0
+    cols = np.empty((M, len(offs)), dtype=np.int32)
+    keep = np.empty((M, len(offs)), dtype=bool)
+    for q, (di, dj, dk) in enumerate(offs):
+        ok = (i + di >= 0) & (i + di < nx) & (j + dj >= 0) & (j + dj < ny) & (k + dk >= 0) & (k + dk < nz)
+        keep[:, q] = ok
+        cols[:, q] = (r + di + nx * (dj + ny * dk)).astype(np.int32)
+    del i, j, k
+    vals = np.where(np.array([o == (0, 0, 0) for o in offs])[None, :], centre, -1.0)
+    vals = np.broadcast_to(vals, cols.shape)
+    indptr = np.zeros(M + 1, dtype=np.int32)
+    np.cumsum(keep.sum(axis=1, dtype=np.int32), out=indptr[1:])
+    return indptr, cols[keep], np.ascontiguousarray(vals[keep])
+
+
+def assembly_from_host(comm, nx: int, ny: int, nz: int, kind: str = "7pt") -> dict:
+    """createAIJ(size, csr=(I, J, V)) from host arrays -- the path test.py:24 /
+    petsc_funcs.py:6 take -- timed end to end and by phase (host-to-device
+    copy, row canonicalisation, MPIAIJ split, SpMV layouts), each phase's
+    GB/s on its byte model against the host link or HBM peak."""
+    from mxsolve.core import DMat, assembly_times
+    import torch
+    ip, cj, vv = host_csr_stencil(nx, ny, nz, kind)
+    M, nnz = ip.size - 1, int(cj.size)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    A = DMat.from_csr(comm, M, M, ip, cj, vv)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ph = assembly_times()
+    info = A.info()
+    A.destroy()
+    del ip, cj, vv
+    canon_b = 32 * nnz + 16 * M          # rowptr + int64 cols + vals read, sorted cols + vals + counts written
+    split_b = 36 * nnz + 32 * M          # count pass (cols) + fill pass (cols, vals -> int32 cols, vals, diag)
+    gbs = lambda b, ms: round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
+    return {"workload": f"{kind} {nx}x{ny}x{nz}, int32 I/J + fp64 V host arrays", "rows": M, "nnz": nnz,
+            "wall_s": round(wall, 4), "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
+            "host_bytes": int(ph["host_bytes"]),
+            "h2d_GBps": gbs(ph["host_bytes"], ph["h2d_ms"]), "host_link_peak_GBps": HOST_LINK_PEAK_GBS,
+            "h2d_frac": round(ph["host_bytes"] / (ph["h2d_ms"] * 1e-3) / 1e9 / HOST_LINK_PEAK_GBS, 4)
+            if ph["h2d_ms"] > 0 else None,
+            "canon_bytes": canon_b, "canon_GBps": gbs(canon_b, ph["canon_ms"]),
+            "split_bytes": split_b, "split_GBps": gbs(split_b, ph["split_ms"]),
+            "hbm_peak_GBps": HBM_PEAK_GBS, "nnz_d": info["nnz_d"], "pair_shape": info["pair_shape"]}
+
+
+CPU_CONFIGS = {   # BASELINE.json configurations for the host leg beside the GPU numbers
+    "c2": ("poisson2d", (4096, 4096, 1), "cg", 300),
+    "c3": ("poisson3d", (256, 256, 256), "cg", 200),
+    "c4": ("convdiff3d", (256, 256, 256), "gmres", 120),
+    "c5share": ("poisson3d27", (512, 512, 64), "cg", 60),
+}
+
+
+def cpu_baseline_config(name: str, threads: int, how: str) -> dict:
+    """The oracle's C restatement (PETSc-restatement, not PETSc) on the host
+    cores for another BASELINE configuration: a bounded sample of `its`
+    iterations at rtol = 0 (GMRES: whole restart cycles of 30), the median of 3
+    after a warm-up, reported as iterations/s -- the host figure the GPU's
+    tools/bench_configs.py / tools/bench_general.py numbers stand beside."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    kind, dims, ksp, its = CPU_CONFIGS[name]
+    t0 = time.perf_counter()
+    ip, c, v = oracle.stencil(kind, *dims)
+    M = ip.size - 1
+    A = oracle.OracleMat.from_csr(M, M, ip, c, v)
+    del ip, c, v
+    b = oracle.rhs_hash(0, M)
+    setup = time.perf_counter() - t0
+    A.solve(b, ksp=ksp, rtol=0.0, max_it=10, nthreads=threads)
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        r = A.solve(b, ksp=ksp, pc="jacobi", rtol=0.0, max_it=its, nthreads=threads)
+        times.append(time.perf_counter() - t0)
+    dt = sorted(times)[1]
+    return {"config": name, "kind": kind, "dims": list(dims), "ksp": ksp + ("(30)" if ksp == "gmres" else ""),
+            "value": round(r["its"] / dt, 3), "unit": "iterations/s", "cores": threads, "threads_from": how,
+            "cpu_kind": "port", "sample": f"{r['its']} iterations at rtol 0, median of 3 after a warm-up "
+            f"(oracle/petsc_oracle.c, PETSc-restatement not PETSc), host build {setup:.1f} s",
+            "solve_s_all": [round(t, 3) for t in times]}
+
+
 def stream_copy_gbps(device, n: int) -> float:
     """torch's own device copy of an n-double vector (read + write), the
     same process's HBM reference rate for the numbers above."""
@@ -183,7 +286,14 @@ def main():
     ap.add_argument("--grid", type=int, default=256)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-solve", action="store_true", help="skip the converged solve")
+    ap.add_argument("--no-asm", action="store_true", help="skip the createAIJ-from-host-arrays leg")
+    ap.add_argument("--cpu-config", choices=sorted(CPU_CONFIGS),
+                    help="only the host (oracle) baseline of another BASELINE configuration: one JSON line")
     args = ap.parse_args()
+    if args.cpu_config:
+        threads, how = cpu_threads()
+        print(json.dumps(cpu_baseline_config(args.cpu_config, threads, how)), flush=True)
+        return
 
     import torch
     from mxsolve import _lib
@@ -350,6 +460,10 @@ def main():
 
     copy_gbps = round(stream_copy_gbps(y.device, m), 1)
 
+    asm_host = None
+    if rank == 0 and world == 1 and not args.no_asm:
+        asm_host = assembly_from_host(comm, n, n, n)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         threads, how = cpu_threads()
@@ -410,6 +524,7 @@ def main():
             "comm_latency": comm_lat,
             "per_rank": per_rank,
             "solve": solve,
+            "assembly_host_csr": asm_host,
         }
         print(json.dumps(out), flush=True)
     A.destroy()

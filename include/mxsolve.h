@@ -334,6 +334,13 @@ int mx_debug_set(int key, int value);
  * zeroes them.  Not a PETSc call: it lets the parity tests show which
  * kernel ran (replayed graph launches are not counted).                     */
 int mx_debug_dispatch_counts(int64_t *out, int n, int reset);
+/* Phase times (ms, host wall clock between stream synchronisations) of the
+ * calling thread's last mx_mat_create_csr: 0 host-to-device copy of the CSR
+ * arrays (+ index widening), 1 row canonicalisation (longest row, sort,
+ * duplicate fold), 2 MPIAIJ split (A_d / A_o / garray), 3 SpMV layouts (SELL,
+ * value codes, row pairs, dictionary), 4 halo plan, 5 total, 6 bytes read
+ * from host memory.  Writes min(n, 7) values.                              */
+int mx_debug_assembly_times(double *out, int n);
 /* Calibration stream for PMC byte counters: reads n doubles once with
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,
  * and writes one partial sum per workgroup to out_dev.                      */

@@ -135,6 +135,8 @@ int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
                       const double *vals, int64_t nnz, int insert_mode, int src_is_device, mx_mat *A) {
   return guard([&] {
     Comm *k = C(c);
+    const double t0 = wall_ms();
+    g_asm_times = AsmTimes{};
     if (Mg < 0 || Ng < 0) fail(MX_ERR_ARG, "negative global size");
     if ((indptr_bytes != 4 && indptr_bytes != 8) || (col_bytes != 4 && col_bytes != 8))
       fail(MX_ERR_ARG, "index width must be 4 or 8 bytes");
@@ -175,10 +177,15 @@ int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
       convert_index(cols, col_bytes, nnz, cl.p, st);
       HIPCHECK(hipMemcpyAsync(vl.p, vals, sizeof(double) * nnz, hipMemcpyDeviceToDevice, st));
     }
+    HIPCHECK(hipStreamSynchronize(st));
+    const double t_h2d = wall_ms();
     AssemblyInput in;
     in.rowptr = ip.p; in.cols = cl.p; in.vals = vl.p; in.nnz = nnz;
     in.insert_mode = insert_mode;
     *A = new mx_mat_s{assemble(k, Mg, Ng, m_local, n_local, in)};
+    g_asm_times.h2d_ms = t_h2d - t0;
+    g_asm_times.host_bytes = src_is_device ? 0.0 : (double)(m + 1) * indptr_bytes + (double)nnz * (col_bytes + 8);
+    g_asm_times.total_ms = wall_ms() - t0;
   });
 }
 
@@ -534,6 +541,13 @@ int mx_debug_set(int key, int value) {
     default: break;
   }
   return old;
+}
+
+int mx_debug_assembly_times(double *out, int n) {
+  const AsmTimes &t = g_asm_times;
+  const double v[7] = {t.h2d_ms, t.canon_ms, t.split_ms, t.layout_ms, t.halo_ms, t.total_ms, t.host_bytes};
+  for (int k = 0; k < n && k < 7; ++k) out[k] = v[k];
+  return 0;
 }
 
 int mx_debug_dispatch_counts(int64_t *out, int n, int reset) {

@@ -26,6 +26,7 @@
 //   halo plan: garray owners from the column layout, one count all-to-all,
 //     requested indices sent to their owners, contiguous send ranges detected.
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cstdlib>
 #include <cstring>
@@ -1566,9 +1567,15 @@ static void layout(Comm *c, int64_t G, int64_t local, std::vector<int64_t> &rang
   }
 }
 
+thread_local AsmTimes g_asm_times;
+double wall_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
               const AssemblyInput &in) {
   hipStream_t st = c->stream;
+  const double t_start = wall_ms();
   std::unique_ptr<Mat> A(new Mat());
   A->comm = c;
   A->M = M; A->N = N;
@@ -1680,6 +1687,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   HIPCHECK(hipStreamSynchronize(st));
   if (herr & 4) fail(MX_ERR_ARG, "row pointer array is not nondecreasing");
   if (herr & 1) fail(MX_ERR_OUTOFRANGE, "Column too large: max " + std::to_string(N - 1));
+  const double t_canon = wall_ms();
 
   // ---- split into A_d / A_o with a ghost bitmap
   const bool multi = c->size > 1;
@@ -1723,6 +1731,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   }
   A->garray_h.resize((size_t)A->nghost);
   if (A->nghost) HIPCHECK(hipMemcpyAsync(A->garray_h.data(), A->garray.p, sizeof(int64_t) * A->nghost, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  const double t_split = wall_ms();
 
   // ---- SpMV layouts
   build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
@@ -1731,6 +1741,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   build_pair_f64(A->sd, m, A->n, A->so.nslices ? A->so.width.p : nullptr, st);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
+  const double t_layout = wall_ms();
 
   // ---- halo plan (collective) + the slices that need ghosts
   if (multi) {
@@ -1745,6 +1756,11 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
     if (!lst.empty())
       HIPCHECK(hipMemcpy(A->halo.bnd_slices.p, lst.data(), sizeof(int32_t) * lst.size(), hipMemcpyHostToDevice));
   }
+  const double t_end = wall_ms();
+  g_asm_times.canon_ms = t_canon - t_start;
+  g_asm_times.split_ms = t_split - t_canon;
+  g_asm_times.layout_ms = t_layout - t_split;
+  g_asm_times.halo_ms = t_end - t_layout;
   return A.release();
 }
 

@@ -295,6 +295,15 @@ struct Mat {
   ~Mat() { release_ksp(); }
 };
 
+// Phase times of this thread's last assembly (mx_debug_assembly_times): host
+// wall clock between stream synchronisations, milliseconds.
+struct AsmTimes {
+  double h2d_ms = 0, canon_ms = 0, split_ms = 0, layout_ms = 0, halo_ms = 0, total_ms = 0;
+  double host_bytes = 0;   // bytes read from host memory (createAIJ from host arrays)
+};
+extern thread_local AsmTimes g_asm_times;
+double wall_ms();          // steady clock, milliseconds
+
 // assembly entry (mx_assembly.hip)
 struct AssemblyInput {
   // grouped input: rows [0, m), entries of row i at [rowptr[i], rowptr[i+1])
@@ -402,13 +411,14 @@ int pair_f64_kind(const Mat *A);     // 5 / 7: the fp64 row-pair z-march applies
 bool pair_zmcg_applies(const Mat *A, int jac_mode);
 int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac_c, const double *r, double *pb0,
                      double *pb1, double *x, double *w, double *partials, const Fold *fold, hipStream_t st);
-// CG mode 5: w = A p is never stored -- the p.Ap pass (SPMV_PW) gives p.w,
-// the update pass recomputes A p where it forms r - alpha A p (SPMV_RUPD)
+// CG mode 5: w = A p is not stored -- the p.Ap pass (matmult_overlap with
+// SPMV_PW; on P > 1 ranks only the ghost units' rows are stored and finished
+// by the boundary kernel) gives p.w, the update pass recomputes A p where it
+// forms r - alpha A p (SPMV_RUPD; the ghost units' rows read w)
 bool pair_cg5_applies(const Mat *A, int jac_mode);
-int pair_cg5_pw_launch(Mat *A, const double *p, double *partials, const int *done, const Fold *fold, hipStream_t st);
-int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, double *r, const double *r0, int jac_mode,
-                         double jac_c, double *partials, const Fold &fold, const double *dot_part, int ndot, int xb,
-                         int *hw, hipStream_t st);
+int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, double *r, const double *r0,
+                         int jac_mode, double jac_c, double *partials, const Fold &fold, const double *dot_part,
+                         int ndot, int xb, int *hw, hipStream_t st);
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);

@@ -1172,14 +1172,14 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // auto (3): mode 5 where it applies (one rank, lean 5/7-point z-march), else
   // 1 up to CG_FUSE_MAX_ROWS local rows, else 2
   int fmode = g_knobs.cg_fuse == 3 ? (fused && pair_cg5_applies(A, dinv.mode) ? 5 : n <= CG_FUSE_MAX_ROWS ? 1 : 2)
-                                   : g_knobs.cg_fuse;
+                                   : g_knobs.cg_fuse;   // (multi-rank mode 5: knob 9 = 5 until measured)
   if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && g_knobs.cg_xbatch == 2 && poll % 2 == 0 && !p.guess_nonzero))
     fmode = 2;
   // mode 5 (knob 9 = 5): mode 2 whose MatMult stores no product -- a p.Ap
   // pass, then the update pass recomputes A p (mx_spmv_pair.hip SPMV_PW /
   // SPMV_RUPD) -- one rank, a lean 5/7-point z-march layout, no or uniform
   // Jacobi; otherwise 2
-  if (fmode == 5 && !(fused && pair_cg5_applies(A, dinv.mode))) fmode = 2;
+  if (fmode == 5 && !pair_cg5_applies(A, dinv.mode)) fmode = 2;
   const int xb = ((fmode == 2 || fmode == 4 || fmode == 5) && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 4) &&
                   poll % g_knobs.cg_xbatch == 0)
                      ? g_knobs.cg_xbatch : 1;
@@ -1289,8 +1289,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       if (xb > 1) cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb);
       else cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
       timer.begin();
-      nb_spmv = fmode == 5 ? pair_cg5_pw_launch(A, pi, part.p, done, fdot_p, st)
-                           : matmult_overlap(A, pi, w.p, SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
+      nb_spmv = matmult_overlap(A, pi, w.p, fmode == 5 ? SPMV_PW : SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
       if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG without its MatMult");
     }
@@ -1304,7 +1303,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     double *upart = fold_in_update ? part.p + ((nb_spmv + 63) / 64) * 64 : part.p;
     if (fmode == 5) utimer.begin();
     const int nb_upd =
-        fmode == 5 ? pair_cg5_rupd_launch(A, s, pcur, r.p, xb > 1 ? r0 : nullptr, dinv.mode, dinv.c, upart, fupd,
+        fmode == 5 ? pair_cg5_rupd_launch(A, s, pcur, w.p, r.p, xb > 1 ? r0 : nullptr, dinv.mode, dinv.c, upart, fupd,
                                           fold_in_update ? part.p : nullptr, fold_in_update ? nb_spmv : 0, xb,
                                           poller.hw, st)
                    : cg_update_launch(st, n, s, pcur, w.p, defer_x ? nullptr : x, r.p, dinv, upart, fupd,

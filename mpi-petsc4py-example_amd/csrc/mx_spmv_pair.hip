@@ -98,11 +98,11 @@ __device__ __forceinline__ void pair_unit(const dbl2 (&L)[PairShape<PS>::NR], do
                                           int lane, double &dot) {
   constexpr int C = PairShape<PS>::CENTER_RUN;
   const dbl2 sv = pair_sums<PS, CLEAN>(L, e, bw, puni, lane);
-  if constexpr (MODE != SPMV_PW) *reinterpret_cast<dbl2 *>(y + r0) = sv;
+  // SPLIT: rows with A_o entries store their diagonal-block sum; the boundary
+  // kernel continues them and adds their p.y terms.  SPMV_PW stores only those
+  const bool gh = SPLIT && (bw & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+  if (MODE != SPMV_PW || gh) *reinterpret_cast<dbl2 *>(y + r0) = sv;
   if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
-    // SPLIT: rows with A_o entries stored their diagonal-block sum; the
-    // boundary kernel continues them and adds their p.y terms
-    const bool gh = SPLIT && (bw & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
     if (!gh) {
       dot += L[C].x * sv.x;
       dot += L[C].y * sv.y;
@@ -208,8 +208,13 @@ __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs 
 //   partials, folded in-launch into red3.  p is re-read from the memory-side
 //   cache the PW pass left it in; r is read non-temporally (the direction
 //   update reads the r written here next).
+//   SPLIT (P > 1): the PW pass stored the diagonal-block sums of the units
+//   with A_o entries and the boundary kernel finished them (w = A p there,
+//   plus their p.w terms); the residual update reads those rows' w instead of
+//   its own (diagonal-block only) sums.
 struct PairRuArgs {
   KspState *s;
+  const double *w;             // SPLIT: the finished products of the ghost units' rows
   double *r;                   // r_i in, r_{i+1} out
   const double *r0;            // iteration 0 of a zero-guess solve reads r_0 = b (not copied into r)
   const double *dot_part;      // the PW pass's partials, folded here by every workgroup
@@ -307,7 +312,12 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
         }
         const int r0 = (z + q) * D + cb;
         if constexpr (RU) {
-          const dbl2 w2 = pair_sums<PS, CLEAN>(L[q], e[q], bw[q], puni, lane);
+          dbl2 w2 = pair_sums<PS, CLEAN>(L[q], e[q], bw[q], puni, lane);
+          if constexpr (SPLIT) {
+            if (bw[q] & (PBLK_GHOST_LO | PBLK_GHOST_HI)) {        // wave-uniform, rare
+              if (bw[q] & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) w2 = *reinterpret_cast<const dbl2 *>(ru.w + r0);
+            }
+          }
           const double ra = fma(-alpha, w2.x, rq[q].x), rb = fma(-alpha, w2.y, rq[q].y);
           const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
           nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
@@ -880,7 +890,8 @@ static int pair_f64_launch(Mat *A, int mode, bool split, const double *x, double
 int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials, const int *done,
                      const Fold &fold_in, hipStream_t st) {
   const Sell &S = A->sd;
-  if (mode != SPMV_PLAIN && mode != SPMV_DOT) return 0;
+  if (mode != SPMV_PLAIN && mode != SPMV_DOT && mode != SPMV_PW) return 0;
+  if (mode == SPMV_PW && !pair_cg5_applies(A, 0)) return 0;   // CG mode 5's p.Ap pass: the 5/7-point z-march
   if (pair_f64_kind(A) && (split || A->nghost == 0))   // without a split, A_o continues in the general kernel
     return pair_f64_launch(A, mode, split, x, y, partials, done, fold_in, st);
   const int kind = pair_lean_kind(A);
@@ -952,6 +963,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
 #define ZM_C(MODE, PS) do { if (split) { if (clean) ZM_PICK(MODE, PS, true, true); else ZM_PICK(MODE, PS, true, false); } \
                             else { if (clean) ZM_PICK(MODE, PS, false, true); else ZM_PICK(MODE, PS, false, false); } } while (0)
     if (mode == SPMV_PLAIN) { if (S.pair_shape == 5) ZM_C(SPMV_PLAIN, 5); else ZM_C(SPMV_PLAIN, 7); }
+    else if (mode == SPMV_PW) { if (S.pair_shape == 5) ZM_C(SPMV_PW, 5); else ZM_C(SPMV_PW, 7); }
     else { if (S.pair_shape == 5) ZM_C(SPMV_DOT, 5); else ZM_C(SPMV_DOT, 7); }
 #undef ZM_C
 #undef ZM_PICK
@@ -966,7 +978,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   a.fold = fold;
-  note_dispatch(!zm ? DSP_PAIR_LEAN : split ? DSP_PAIR_ZM_SPLIT : DSP_PAIR_ZM);
+  note_dispatch(mode == SPMV_PW ? DSP_ZM_PW : !zm ? DSP_PAIR_LEAN : split ? DSP_PAIR_ZM_SPLIT : DSP_PAIR_ZM);
   if (zm) launch_timed(fz, grid, st, a, x, y, S.pblk.p, S.puni.p, PairRuArgs{});
   else launch_timed(f, grid, st, a, x, y, S.pblk.p, S.puni.p);
   HIPCHECK(hipGetLastError());
@@ -1021,11 +1033,12 @@ int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac
   return grid;
 }
 
-// CG mode 5 (knob 9 = 5): one rank, a lean 5/7-point z-march layout, no or
-// uniform Jacobi
+// CG mode 5 (knob 9 = 5): a lean 5/7-point z-march layout (the constant-
+// coefficient stencils), no or uniform Jacobi; on P > 1 ranks the product
+// must split (the ghost units' rows are finished by the boundary kernel)
 bool pair_cg5_applies(const Mat *A, int jac_mode) {
-  return A->comm->size == 1 && A->sd.pair_shape != 27 && (jac_mode == 0 || jac_mode == 2) && pair_lean_kind(A) > 0 &&
-         pair_zm_applies(A) && A->nghost == 0 && !A->sd.pair_ghosts;
+  return A->sd.pair_shape != 27 && (jac_mode == 0 || jac_mode == 2) && pair_lean_kind(A) > 0 && pair_zm_applies(A) &&
+         ((A->nghost == 0 && !A->sd.pair_ghosts) || matmult_splits(A));
 }
 
 static int cg5_args(const Mat *A, PairLeanArgs &a) {
@@ -1041,31 +1054,9 @@ static int cg5_args(const Mat *A, PairLeanArgs &a) {
   return zm_tasks(a.P, a.NZ, a.L, a.S);
 }
 
-int pair_cg5_pw_launch(Mat *A, const double *p, double *partials, const int *done, const Fold *fold_in,
-                       hipStream_t st) {
-  if (!pair_cg5_applies(A, 0)) return 0;
-  PairLeanArgs a;
-  const int grid = cg5_args(A, a);
-  a.partials = partials;
-  a.done = done;
-  Fold fold = fold_in ? *fold_in : Fold{};
-  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
-  a.fold = fold;
-  const bool clean = pair_lean_kind(A) == 2, z2 = g_knobs.pair_zm_units == 2;
-  ZmFn f;
-#define PW(PS, CL) f = z2 ? &spmv_pair_zm_kernel<SPMV_PW, PS, false, CL, 2> : &spmv_pair_zm_kernel<SPMV_PW, PS, false, CL, 1>
-  if (A->sd.pair_shape == 5) { if (clean) PW(5, true); else PW(5, false); }
-  else { if (clean) PW(7, true); else PW(7, false); }
-#undef PW
-  note_dispatch(DSP_ZM_PW);
-  launch_timed(f, grid, st, a, p, nullptr, A->sd.pblk.p, A->sd.puni.p, PairRuArgs{});
-  HIPCHECK(hipGetLastError());
-  return grid;
-}
-
-int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, double *r, const double *r0, int jac_mode,
-                         double jac_c, double *partials, const Fold &fold_in, const double *dot_part, int ndot, int xb,
-                         int *hw, hipStream_t st) {
+int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, double *r, const double *r0,
+                         int jac_mode, double jac_c, double *partials, const Fold &fold_in, const double *dot_part,
+                         int ndot, int xb, int *hw, hipStream_t st) {
   if (!pair_cg5_applies(A, jac_mode)) return 0;
   PairLeanArgs a;
   const int grid = cg5_args(A, a);
@@ -1073,15 +1064,18 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, double *r, const 
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   a.fold = fold;
-  const PairRuArgs ru{s, r, r0, dot_part, ndot, xb, jac_c, hw};
+  const bool split = A->sd.pair_ghosts;      // the ghost units' rows: w from the PW pass + boundary kernel
+  const PairRuArgs ru{s, w, r, r0, dot_part, ndot, xb, jac_c, hw};
   const bool clean = pair_lean_kind(A) == 2, z2 = g_knobs.pair_zm_units == 2;
   ZmFn f;
-#define RU(PS, CL, JM) f = z2 ? &spmv_pair_zm_kernel<SPMV_RUPD, PS, false, CL, 2, JM> \
-                              : &spmv_pair_zm_kernel<SPMV_RUPD, PS, false, CL, 1, JM>
-#define RU_J(PS, CL) do { if (jac_mode == 2) RU(PS, CL, 2); else RU(PS, CL, 0); } while (0)
+#define RU(PS, SP, CL, JM) f = z2 ? &spmv_pair_zm_kernel<SPMV_RUPD, PS, SP, CL, 2, JM> \
+                                  : &spmv_pair_zm_kernel<SPMV_RUPD, PS, SP, CL, 1, JM>
+#define RU_S(PS, CL, JM) do { if (split) RU(PS, true, CL, JM); else RU(PS, false, CL, JM); } while (0)
+#define RU_J(PS, CL) do { if (jac_mode == 2) RU_S(PS, CL, 2); else RU_S(PS, CL, 0); } while (0)
   if (A->sd.pair_shape == 5) { if (clean) RU_J(5, true); else RU_J(5, false); }
   else { if (clean) RU_J(7, true); else RU_J(7, false); }
 #undef RU_J
+#undef RU_S
 #undef RU
   note_dispatch(DSP_ZM_RUPD);
   launch_timed(f, grid, st, a, p, nullptr, A->sd.pblk.p, A->sd.puni.p, ru);

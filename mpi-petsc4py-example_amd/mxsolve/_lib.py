@@ -103,6 +103,7 @@ SIGNATURES = {
     "mx_lu_solve_csr": (C.c_int, [P, I64, P, P, P, P, P]),
     "mx_debug_set": (C.c_int, [C.c_int, C.c_int]),
     "mx_debug_dispatch_counts": (C.c_int, [C.POINTER(C.c_int64), C.c_int, C.c_int]),
+    "mx_debug_assembly_times": (C.c_int, [C.POINTER(C.c_double), C.c_int]),
     "mx_debug_stream_read": (C.c_int, [P, P, I64, C.c_int, P]),
     "mx_debug_comm_bench": (C.c_int, [P, P, C.c_int, C.c_int, DP]),
     "mx_debug_comm_stall": (C.c_int, [P, C.c_int]),

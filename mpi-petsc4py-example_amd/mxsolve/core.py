@@ -404,5 +404,15 @@ def dispatch_counts(reset: bool = False) -> dict:
     return {k: int(out[i]) for i, k in enumerate(DISPATCH_KINDS)}
 
 
+ASM_PHASES = ("h2d_ms", "canon_ms", "split_ms", "layout_ms", "halo_ms", "total_ms", "host_bytes")
+
+
+def assembly_times() -> dict:
+    """Phase times of this thread's last createAIJ(csr=...) (mx_debug_assembly_times)."""
+    out = (C.c_double * 7)()
+    call("mx_debug_assembly_times", out, 7)
+    return {k: float(out[i]) for i, k in enumerate(ASM_PHASES)}
+
+
 def rhs_hash(comm, i0: int, out: torch.Tensor):
     call("mx_vec_rhs_hash", comm.h, i0, out.numel(), _ptr(out))

@@ -187,3 +187,16 @@ def test_oracle_maxpy_grouping(oracle_mod):
         for j in range(r, nv, 4):
             u = u + (((a[j] * xs[j] + a[j + 1] * xs[j + 1]) + a[j + 2] * xs[j + 2]) + a[j + 3] * xs[j + 3])
         assert np.array_equal(oracle_mod.vec_maxpy(y, a, xs), u)
+
+
+def test_bench_host_csr_equals_oracle_stencil(oracle_mod):
+    """bench.py builds test.py-style host CSR arrays (int32 I/J, fp64 V) with
+    numpy for its createAIJ-from-host leg: the same matrices as the oracle's
+    stencil generator (7-point and 27-point, non-cubic grids)."""
+    import bench
+    for kind, okind, dims in (("7pt", "poisson3d", (6, 5, 4)), ("27pt", "poisson3d27", (5, 4, 3)),
+                              ("7pt", "poisson3d", (16, 16, 16))):
+        ip, c, v = bench.host_csr_stencil(*dims, kind)
+        oi, oc, ov = oracle_mod.stencil(okind, *dims)
+        assert ip.dtype == np.int32 and c.dtype == np.int32
+        assert np.array_equal(ip, oi) and np.array_equal(c, oc) and np.array_equal(v.view(np.uint64), ov.view(np.uint64))

@@ -660,3 +660,52 @@ def test_c5_p8_weak_scaling_properties():
     assert zr <= 1.5e-5 * zb, (zr, zb)
     assert abs(zr - rnorm) <= 0.05 * zr + 1e-12 * zb, (zr, rnorm)
     assert dc["pair_zm27_split"] >= P * next(iter(its)), dc
+
+
+@pytest.mark.parametrize("P,kind,n,applies", [(2, "poisson3d", 128, True), (8, "poisson3d", 128, True),
+                                              (4, "poisson2d", 512, True), (3, "poisson3d", 64, False)])
+def test_distributed_mode5(oracle_mod, P, kind, n, applies):
+    """CG mode 5 (knob 9 = 5) on P ranks: the p.Ap pass stores only the ghost
+    units' diagonal-block sums, the boundary kernel finishes those rows (A_o
+    over the halo) and adds their p.w terms, and the residual update
+    recomputes A p on the other units and reads w on the ghost units.  Its and
+    reason equal to the oracle's P-rank model, x within rel-L2 1e-10; the
+    dispatch counts show the two mode-5 passes and the boundary kernel.  A
+    partition without whole planes per rank (64^3 over 3) has no z-march and
+    runs mode 2."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+    o = O.solve(oracle_mod.rhs_hash(0, M), ksp="cg")
+
+    def body(comm):
+        A = DMat.stencil(comm, kind, n)
+        info = A.info()
+        b = comm.empty(info["m"])
+        rhs_hash(comm, info["rstart"], b)
+        x = comm.zeros(info["m"])
+        r = A.solve(b, x, ksp="cg")
+        out = (r["its"], r["reason"], x.cpu().numpy(), r["cg_mode"])
+        A.destroy()
+        return out
+
+    L = _lib.load()
+    old = L.mx_debug_set(9, 5)
+    dispatch_counts(reset=True)
+    try:
+        res = run_ranks(P, body)
+    finally:
+        L.mx_debug_set(9, old)
+    dc = dispatch_counts(reset=True)
+    assert all(r[0] == o["its"] and r[1] == o["reason"] for r in res), ([r[:2] for r in res], o["its"])
+    xs = np.concatenate([r[2] for r in res])
+    assert np.linalg.norm(xs - o["x"]) / np.linalg.norm(o["x"]) <= REL_TOL
+    its = o["its"]
+    if applies:
+        assert all(r[3] == 5 for r in res)
+        assert dc["zm_pw"] >= P * its and dc["zm_rupd"] >= P * its and dc["boundary"] >= P * its, dc
+        assert dc["pair_zm_split"] == 0 and dc["sell"] == 0, dc
+    else:
+        assert all(r[3] == 2 for r in res) and dc["zm_pw"] == 0 and dc["zm_rupd"] == 0, dc

@@ -11,6 +11,11 @@ matrices that the value-code / code-dictionary compression does not reach.
             kind of matrix, scipy.sparse.random), diagonally dominant;
             column-index SELL;  GMRES(30) + Jacobi iterations.
   c4      : BASELINE C4, conv-diff 256^3, GMRES(30) + Jacobi, converged.
+  asm     : createAIJ(csr=...) from host int32/fp64 arrays (test.py:24's path)
+            by phase -- C3's 256^3 7-point and C5's per-GPU share (27-point
+            512 x 512 x 64, 451 M entries); bench.py assembly_from_host.
+  (The host baselines of these configurations: python bench.py --cpu-config
+   c2|c3|c4|c5share.)
 
 Both general legs go through createAIJ(csr=...) from host arrays
 (mx_mat_create_csr), exactly the reference's assembly entry point.  Each leg
@@ -33,7 +38,7 @@ import torch  # noqa: E402
 
 from mxsolve.core import DeviceComm, DMat, rhs_hash  # noqa: E402
 sys.path.insert(0, ROOT)
-from bench import spmv_format_bytes  # noqa: E402
+from bench import assembly_from_host, spmv_format_bytes  # noqa: E402
 
 PEAK = 8000.0
 
@@ -184,6 +189,11 @@ def main():
             del ip, c, v
             leg(comm, "random pattern 2^24 rows x 7 (column SELL)", A, "gmres", rtol=0.0, max_it=300, asm_s=asm,
                 jac_vec=True)
+        elif name == "asm":
+            for dims, kind in (((256, 256, 256), "7pt"), ((512, 512, 64), "27pt")):
+                print(json.dumps({"leg": "assembly from host CSR", **assembly_from_host(comm, *dims, kind)}), flush=True)
+                torch.cuda.empty_cache()
+            continue
         elif name == "c4":
             t0 = time.perf_counter()
             A = DMat.stencil(comm, "convdiff3d", 256)
