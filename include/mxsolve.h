@@ -113,6 +113,9 @@ typedef struct {
                                          row pairs -- each unit's values streamed as
                                          16-byte pairs -- and the z-march MatMult runs on
                                          them (one rank, select-free units; key 44)    */
+  int64_t pair_form27;                /* 27-point z-march body: 2 column-zeroed (no branches,
+                                         no selects; key 48), 1 per-run branches, 0 lane
+                                         selects; -1 when the 27-point z-march does not run */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */
@@ -254,7 +257,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        RCCL communicator (testing, default 0)
  * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
- *        5 where it applies, else 1 for <= 3M local rows, else 2); 4 mode 2 with the direction update and
+ *        5 on one rank where it applies, 2 on P > 1 ranks with the z-march
+ *        MatMult, else 1 for <= 3M local rows, else 2); 4 mode 2 with the direction update and
  *        the batched x steps inside the z-march MatMult (one rank, lean z-march
  *        layout, no or uniform Jacobi; else 2; mode 2's bits); 5 mode 2 whose
  *        MatMult stores no product: a p.Ap pass, and the update pass
@@ -317,12 +321,16 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         workgroups; 0 = the resident grid of key 26)
  * key 44: fp64 row-pair layout + z-march MatMult for uncoded 5/7-point blocks
  *         (read at assembly; 0/1, default 1; the same bits)
- * key 45: 27-point z-march resident workgroups per CU (default 3; 0 = key 40)
+ * key 45: 27-point z-march resident workgroups per CU (default 6; 0 = key 40)
  * key 46: CG mode 5: the residual-update pass folds the p.Ap pass's partials
  *         itself (1, default) or a one-block fold kernel runs between (0)
  * key 47: deadline in ms of the RCCL waits that observe no progress (stream /
  *         event waits, setup collectives, barrier); 0 = none (default: a slow
  *         peer is not an error, as with MPI)
+ * key 48: 27-point column words (read at assembly; 0/1, default 1): the
+ *         27-point z-march zeroes empty runs and x-line edges where it loads
+ *         them (no per-run branches, no selects; the same bits)
+ * key 49: 27-point z-march planes per step (1, default, or 2)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

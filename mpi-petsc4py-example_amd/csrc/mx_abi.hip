@@ -254,6 +254,8 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     // the fp64 row-pair z-march runs only where the launch takes it: one rank,
     // or a product that splits (otherwise the general kernel continues A_o)
     info->pair_f64 = (A->nghost == 0 || matmult_splits(A)) ? pair_f64_kind(A) : 0;
+    info->pair_form27 = A->sd.pair_shape == 27 && pair_lean_kind(A)
+                            ? (pair_lean_kind(A) == 2 ? (A->sd.pcol27.p ? 2 : 1) : 0) : -1;
   });
 }
 
@@ -538,6 +540,8 @@ int mx_debug_set(int key, int value) {
     case 45: old = g_knobs.pair_zm27_bpc; g_knobs.pair_zm27_bpc = std::min(std::max(value, 0), 8); break;
     case 46: old = g_knobs.cg5_fold; g_knobs.cg5_fold = value; break;
     case 47: old = g_knobs.comm_wait_ms; g_knobs.comm_wait_ms = std::max(value, 0); break;
+    case 48: old = g_knobs.pair_col27; g_knobs.pair_col27 = value; break;
+    case 49: old = g_knobs.pair_zm27_units; g_knobs.pair_zm27_units = value == 2 ? 2 : 1; break;
     default: break;
   }
   return old;

@@ -1366,6 +1366,41 @@ static void build_pair_uniform27(Sell &S, const std::vector<double> &vt, hipStre
   S.pair_clean27 = all_clean;
 }
 
+// Column words of a clean 27-point layout (Sell::pcol27), when the units'
+// empty runs and x-line edges follow the plane / column rule exactly: unit u =
+// (plane z, column c) must have empty runs = z-boundary runs (z = 0: runs 0-2,
+// z = NZ - 1: runs 6-8) | the column's y-boundary runs (dy = -1: runs 0, 3, 6;
+// dy = +1: 2, 5, 8) and the column's ELO / EHI.  Otherwise none is built.
+static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
+  S.pcol27.reset();
+  if (!S.puni27.p || !S.pair_clean27 || !S.pair_all || S.pat_star_off.size() < 27) return;
+  const int64_t D = S.pat_star_off[22];                   // run 7's centre: +D
+  if (D <= 0 || D % 128 != 0 || m % D != 0 || m > (int64_t(1) << 27)) return;
+  const int64_t P = D / 128, NZ = m / D;
+  const int64_t nb = S.pair_blocks;
+  std::vector<PairUni27> blk((size_t)nb);
+  std::vector<int32_t> pb((size_t)S.nunits);
+  HIPCHECK(hipMemcpyAsync(blk.data(), S.puni27.p, sizeof(PairUni27) * nb, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipMemcpyAsync(pb.data(), S.pblk.p, sizeof(int32_t) * S.nunits, hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  std::vector<int32_t> cw((size_t)P, -1);
+  const uint32_t RUNS = 0x1ffu, EDGES = U27_ELO | U27_EHI;
+  for (int64_t u = 0; u < S.nunits; ++u) {
+    const int64_t z = u / P, c = u % P;
+    const uint32_t f = blk[(size_t)(pb[(size_t)u] & (int32_t)PBLK_ID)].flags;
+    const uint32_t zb = (z == 0 ? 0x007u : 0u) | (z == NZ - 1 ? 0x1c0u : 0u);
+    // the y status from the plane's own runs (dz = 0: runs 3 / 5, never z-boundary runs)
+    uint32_t w = (f & EDGES) | ((f & (1u << 3)) ? U27C_YLO : 0u) | ((f & (1u << 5)) ? U27C_YHI : 0u);
+    const uint32_t ys = ((w & U27C_YLO) ? 0x049u : 0u) | ((w & U27C_YHI) ? 0x124u : 0u);
+    if ((f & RUNS) != (zb | ys)) return;                   // an empty run off the rule
+    if (cw[(size_t)c] >= 0 && (uint32_t)cw[(size_t)c] != w) return;   // the column disagrees with itself
+    cw[(size_t)c] = (int32_t)w;
+  }
+  S.pcol27.alloc((size_t)P);
+  HIPCHECK(hipMemcpyAsync(S.pcol27.p, cw.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, st));
+  HIPCHECK(hipStreamSynchronize(st));
+}
+
 static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st) {
   S.ntab = 0;
   if (S.slots == 0 || !g_knobs.vcodes) return;
@@ -1452,6 +1487,7 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
     }
     // every full unit a pair unit: SpMV reads no per-unit pattern word
     S.pair_all = S.pair_used == m / 128;
+    if (g_knobs.pair_col27) build_pair_col27(S, m, st);
   }
   HIPCHECK(hipStreamSynchronize(st));   // tab / sc are freed on return
   S.ntab = (int)keys.size();

@@ -143,6 +143,8 @@ struct PairUni27 {
 };
 constexpr uint32_t U27_ELO = 1u << 9;
 constexpr uint32_t U27_EHI = 1u << 10;
+constexpr uint32_t U27C_YLO = 1u << 0;   // Sell::pcol27: the column's dy = -1 runs are empty
+constexpr uint32_t U27C_YHI = 1u << 1;   // ... dy = +1
 
 struct Sell {
   int64_t nslices = 0, slots = 0, dia_slices = 0;
@@ -197,6 +199,14 @@ struct Sell {
   DBuf<int32_t> pflag;
   int pair_f64 = 0;         // 5 / 7: the fp64 row-pair layout's shape, 0 none
   bool pair_clean27 = false;  // every puni27 block is select-free
+  // 27-point column words (one per 128-row column of a plane): when every
+  // unit's empty runs are exactly its plane's z-boundary runs (plane 0: dz =
+  // -1, the last plane: dz = +1 -- read out of range anyway) plus its column's
+  // y-boundary runs (U27C_YLO: dy = -1, U27C_YHI: dy = +1) and its x-line
+  // edges are its column's (U27_ELO / U27_EHI), the z-march zeroes those
+  // operands where it loads them (out-of-range reads) and needs neither
+  // per-run branches nor selects (mx_spmv_pair.hip, form 2)
+  DBuf<int32_t> pcol27;
   // 1 / value per code (1 for a zero value and for absent slots): PCJacobi's
   // dinv of a row is dtab[its diagonal slot's code] -- the division the
   // Jacobi setup does, so the Jacobi-fused row-pair MatMult reads no dinv
@@ -231,8 +241,8 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
-                int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 3; int cg5_fold = 1;
-                int comm_wait_ms = 0; };
+                int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
+                int comm_wait_ms = 0; int pair_col27 = 1; int pair_zm27_units = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

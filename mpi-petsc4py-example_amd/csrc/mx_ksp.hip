@@ -1169,10 +1169,17 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // mode 4 (knob 9 = 4): mode 2 whose direction update rides in the z-march
   // MatMult (mx_spmv_pair.hip spmv_pair_zmcg_kernel) -- one rank, a lean
   // z-march layout, no or uniform Jacobi, x steps batched by 2; otherwise 2
-  // auto (3): mode 5 where it applies (one rank, lean 5/7-point z-march), else
-  // 1 up to CG_FUSE_MAX_ROWS local rows, else 2
-  int fmode = g_knobs.cg_fuse == 3 ? (fused && pair_cg5_applies(A, dinv.mode) ? 5 : n <= CG_FUSE_MAX_ROWS ? 1 : 2)
-                                   : g_knobs.cg_fuse;   // (multi-rank mode 5: knob 9 = 5 until measured)
+  // auto (3): mode 5 on one rank where it applies (a lean 5/7-point z-march);
+  // on P > 1 ranks mode 2 where the z-march applies (the interior-rank proxy,
+  // tools/rank_proxy.py, round 3: kernel time per iteration at 2 M rows/rank
+  // mode 1 53.8 / 2 52.6 / 5 54.6 us, and mode 2 ahead at 4 M and 8 M rows);
+  // otherwise (the general SELL kernel) 1 up to CG_FUSE_MAX_ROWS local rows, else 2
+  int fmode = g_knobs.cg_fuse;
+  if (fmode == 3) {
+    if (fused && pair_cg5_applies(A, dinv.mode)) fmode = 5;
+    else if (pair_lean_kind(A) > 0 && pair_zm_applies(A)) fmode = 2;
+    else fmode = n <= CG_FUSE_MAX_ROWS ? 1 : 2;
+  }
   if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && g_knobs.cg_xbatch == 2 && poll % 2 == 0 && !p.guess_nonzero))
     fmode = 2;
   // mode 5 (knob 9 = 5): mode 2 whose MatMult stores no product -- a p.Ap

@@ -42,6 +42,7 @@ namespace mx {
 // element offset added to an absent read: with n <= 2^27 rows every
 // redirected byte offset lies in [2^30, 2^32) -- past the vector, unwrapped
 constexpr int PAIR_OOR = 1 << 28;
+constexpr int PAIR_OOR_EDGE = 1 << 27;   // 27-point form 2's edge redirect (n <= 2^27; may add to PAIR_OOR)
 constexpr int64_t PAIR_CLEAN_MAX_ROWS = int64_t(1) << 27;
 constexpr int LEAN_WAVES = 4;
 
@@ -347,56 +348,61 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
 // at anchors -D-n, -D, -D+n, -n, 0, +n, D-n, D, D+n (each a tri run c-1, c,
 // c+1); marching a column in z, the runs of planes z-1 and z (six pairs and
 // their edge values) are carried and a unit loads only plane z+1's three runs
-// and edges: 3 pair loads + 3 edge loads instead of 9 + 9.
-//   CLEAN (every block select-free, Sell::pair_clean27): a block's absent
-//   entries are whole runs (the y/z-boundary classes) and the x-line's first /
-//   last entry (lane 0 row 0's -1, lane 63 row 1's +1 slots); an empty run is
-//   skipped by a wave-uniform branch (its operands are real x of the
-//   neighbouring line or plane, so it must add nothing, not v * x), and the
-//   x-edge value is zeroed at use (U27_ELO / U27_EHI: lane 0's / lane 63's
-//   edge), so sum + v * 0.0 = sum -- the carried values stay the real x for
-//   the next unit.  The two rows share each slot's value (clean requires
-//   v[j] == v[K + j]): 27 wave-uniform values, no lane masks.
-//   !CLEAN: presence selects from the lane's own 54 mask bits (PairUni27::lane,
-//   one vector load per unit) and the same 27 values.
-template <int MODE, bool SPLIT, bool CLEAN>
+// and edges: 3 pair loads + 3 edge loads instead of 9 + 9.  (A three-way
+// rotation of plane registers instead of the carry copies measured 106-128
+// VGPRs against 78: 4 waves per SIMD instead of 6.)
+// The two rows of a lane share each slot's value (the dictionary build
+// requires v[j] == v[K + j]): 27 wave-uniform values.  Forms:
+//   2 (Sell::pcol27, the column words): every unit's empty runs are its
+//     plane's z-boundary runs -- read out of range (before plane 0, past the
+//     last), so 0.0 -- and its column's y-boundary runs, and its x-line edges
+//     are its column's: the column's empty runs and edges are loaded out of
+//     range too (PAIR_OOR), for the carried planes as well (the same column),
+//     so every absent slot multiplies 0.0 (sum + v * 0.0 = sum, a row sum is
+//     never -0.0) and the unit has neither branches nor selects;
+//   1 (every block select-free, Sell::pair_clean27): an empty run is skipped
+//     by a wave-uniform branch (its operands are real x of the neighbouring
+//     line or plane) and the x-edge value is zeroed at use (U27_ELO /
+//     U27_EHI: lane 0's / lane 63's edge);
+//   0: presence selects from the lane's own 54 mask bits (PairUni27::lane,
+//     one vector load per unit).
+template <int MODE, bool SPLIT, int FORM>
 __device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e)[9], uint32_t bw,
                                             const PairUni27 *__restrict__ puni, double *__restrict__ y, int r0,
                                             int lane, double &dot) {
   constexpr int K = 27;
   const PairUni27 &B = puni[bw & PBLK_ID];                // wave-uniform: scalar loads
+  uint32_t fl = 0;
+  unsigned long long pb = 0;
+  bool zedge = false;
+  if constexpr (FORM == 1) {
+    fl = B.flags;
+    zedge = lane == 0 ? (fl & U27_ELO) != 0 : (fl & U27_EHI) != 0;
+  } else if constexpr (FORM == 0) {
+    pb = B.lane[lane];
+  }
   double s0v = 0.0, s1v = 0.0;
-  if constexpr (CLEAN) {
-    const uint32_t fl = B.flags;
-    const bool zedge = lane == 0 ? (fl & U27_ELO) != 0 : (fl & U27_EHI) != 0;
 #pragma unroll
-    for (int r = 0; r < 9; ++r) {
+  for (int r = 0; r < 9; ++r) {
+    if constexpr (FORM == 1) {
       if (fl & (1u << r)) continue;                       // wave-uniform: an empty run
-      const double er = zedge ? 0.0 : e[r];
-      const double lo = wave_shift<true>(L[r].y, er);     // x[r0 + c - 1]
-      const double hi = wave_shift<false>(L[r].x, er);    // x[r0 + c + 2]
-      const double a0[3] = {lo, L[r].x, L[r].y}, a1[3] = {L[r].x, L[r].y, hi};
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const double v = B.v[3 * r + p];
-        s0v = s0v + v * a0[p];
-        s1v = s1v + v * a1[p];
-      }
     }
-  } else {
-    const unsigned long long pb = B.lane[lane];
+    double er = e[r];
+    if constexpr (FORM == 1) er = zedge ? 0.0 : er;
+    const double lo = wave_shift<true>(L[r].y, er);       // x[r0 + c - 1]
+    const double hi = wave_shift<false>(L[r].x, er);      // x[r0 + c + 2]
+    const double a0[3] = {lo, L[r].x, L[r].y}, a1[3] = {L[r].x, L[r].y, hi};
 #pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      const double lo = wave_shift<true>(L[r].y, e[r]);
-      const double hi = wave_shift<false>(L[r].x, e[r]);
-      const double a0[3] = {lo, L[r].x, L[r].y}, a1[3] = {L[r].x, L[r].y, hi};
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const int j = 3 * r + p;
-        const double v = B.v[j];
-        const double q0 = s0v + v * a0[p], q1 = s1v + v * a1[p];
+    for (int p = 0; p < 3; ++p) {
+      const int j = 3 * r + p;
+      const double v = B.v[j];
+      const double q0 = s0v + v * a0[p], q1 = s1v + v * a1[p];
+      if constexpr (FORM == 0) {
         s0v = ((pb >> j) & 1ull) ? q0 : s0v;
         s1v = ((pb >> (K + j)) & 1ull) ? q1 : s1v;
+      } else {
+        s0v = q0;
+        s1v = q1;
       }
     }
   }
@@ -418,10 +424,11 @@ struct PairLean27Args {
   Fold fold;
 };
 
-template <int MODE, bool SPLIT, bool CLEAN, int ZU>
+template <int MODE, bool SPLIT, int FORM, int ZU>
 __global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
                                                              double *__restrict__ y, const int32_t *__restrict__ pblk,
-                                                             const PairUni27 *__restrict__ puni) {
+                                                             const PairUni27 *__restrict__ puni,
+                                                             const int32_t *__restrict__ pcol) {
   if (a.done && *a.done) return;   // wave-uniform: solver finished
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -447,12 +454,25 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Arg
     const int seg = sb + t / a.P, col = t % a.P;
     const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
     const int cb = col * 128 + 2 * lane;
+    // form 2: the column's empty runs (dy = -1 / +1) and x-line edges read
+    // out of range, in every plane it loads (so the carried runs as well)
+    // (an edge offset 2^27 and a run offset 2^28 may add up: 3 * 2^27 rows is
+    // still past the vector and inside the 32-bit byte offset, n <= 2^27)
+    // (an edge offset 2^27 and a run offset 2^28 may add up: 3 * 2^27 rows is
+    // still past the vector and inside the 32-bit byte offset, n <= 2^27)
+    int oor[3] = {0, 0, 0}, ebe = eb;
+    if constexpr (FORM == 2) {
+      const uint32_t cw = (uint32_t)pcol[col];
+      oor[0] = (cw & U27C_YLO) ? PAIR_OOR : 0;
+      oor[2] = (cw & U27C_YHI) ? PAIR_OOR : 0;
+      ebe += (lane == 0 ? (cw & U27_ELO) : (cw & U27_EHI)) ? PAIR_OOR_EDGE : 0;
+    }
     dbl2 C[6];                                           // runs 0..5 of the current unit (planes z-1, z)
     double Ce[6];
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      C[r] = bload2(xr, z0 * D + cb + a.anchor[r]);
-      Ce[r] = bload1(xr, z0 * D + col * 128 + eb + a.anchor[r]);
+      C[r] = bload2(xr, z0 * D + cb + a.anchor[r] + oor[r % 3]);
+      Ce[r] = bload1(xr, z0 * D + col * 128 + ebe + a.anchor[r] + oor[r % 3]);
     }
     uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
     auto step = [&](int z, auto nq) __attribute__((always_inline)) {
@@ -469,8 +489,8 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Arg
         const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          Nw[q][k] = bload2(xr, r0 + a.anchor[6 + k]);
-          Ne[q][k] = bload1(xr, ub + eb + a.anchor[6 + k]);
+          Nw[q][k] = bload2(xr, r0 + a.anchor[6 + k] + oor[k]);
+          Ne[q][k] = bload1(xr, ub + ebe + a.anchor[6 + k] + oor[k]);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -482,7 +502,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Arg
         for (int r = 0; r < 6; ++r) { L[r] = C[r]; e[r] = Ce[r]; }
 #pragma unroll
         for (int k = 0; k < 3; ++k) { L[6 + k] = Nw[q][k]; e[6 + k] = Ne[q][k]; }
-        pair_unit27<MODE, SPLIT, CLEAN>(L, e, bw[q], puni, y, (z + q) * D + cb, lane, dot);
+        pair_unit27<MODE, SPLIT, FORM>(L, e, bw[q], puni, y, (z + q) * D + cb, lane, dot);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           C[k] = C[3 + k]; Ce[k] = Ce[3 + k];
@@ -905,8 +925,10 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
     const int D = b.anchor[7];
     b.P = D / 128;
     b.NZ = (int)(A->m / D);
-    // 3 workgroups per CU (knob 45): the VALU-bound 27-point body measured
-    // 245 us per CG iteration at C5's share against 249 at 4 and 272 at 2
+    // 6 workgroups per CU (knob 45) with one plane per step (knob 49): the
+    // VALU-bound 27-point body at 78-80 VGPRs keeps 6 waves per SIMD (C5's
+    // share, round 3: CG MatMult 63 us median against 68-74 at 3-4 per CU or
+    // two planes per step, profiles/r03_ab.jsonl)
     int grid = std::max(8, (g_knobs.pair_zm27_bpc > 0 ? g_knobs.pair_zm27_bpc : g_knobs.pair_zm_bpc) * device_cu_count());
     grid &= ~7;
     const int W = grid / 8 * LEAN_WAVES;
@@ -920,16 +942,20 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
     Fold fold = fold_in;
     if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
     b.fold = fold;
-    using F27 = void (*)(PairLean27Args, const double *, double *, const int32_t *, const PairUni27 *);
+    using F27 = void (*)(PairLean27Args, const double *, double *, const int32_t *, const PairUni27 *,
+                         const int32_t *);
     F27 f = nullptr;
-    const bool z2 = g_knobs.pair_zm_units == 2;
-#define Z27(MODE, SP) do { if (clean) f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, true, 2> : &spmv_pair_zm27_kernel<MODE, SP, true, 1>; \
-                           else f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, false, 2> : &spmv_pair_zm27_kernel<MODE, SP, false, 1>; } while (0)
+    const int form = !clean ? 0 : S.pcol27.p ? 2 : 1;
+    const bool z2 = g_knobs.pair_zm27_units == 2;
+#define Z27U(MODE, SP, FM) f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, FM, 2> : &spmv_pair_zm27_kernel<MODE, SP, FM, 1>
+#define Z27(MODE, SP) do { if (form == 2) Z27U(MODE, SP, 2); else if (form == 1) Z27U(MODE, SP, 1); \
+                           else Z27U(MODE, SP, 0); } while (0)
     if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
     else { if (split) Z27(SPMV_DOT, true); else Z27(SPMV_DOT, false); }
 #undef Z27
+#undef Z27U
     note_dispatch(split ? DSP_PAIR_ZM27_SPLIT : DSP_PAIR_ZM27);
-    launch_timed(f, grid, st, b, x, y, S.pblk.p, S.puni27.p);
+    launch_timed(f, grid, st, b, x, y, S.pblk.p, S.puni27.p, S.pcol27.p);
     HIPCHECK(hipGetLastError());
     return grid;
   }

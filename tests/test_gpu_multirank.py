@@ -545,16 +545,16 @@ def _north_star_oracle(oracle_mod, n, P=8):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("n,fuse", [(128, 3), (128, 2), (256, 3), (256, 2)])
+@pytest.mark.parametrize("n,fuse", [(128, 3), (128, 1), (256, 3), (256, 1)])
 def test_north_star_partition_p8(oracle_mod, n, fuse):
     """BASELINE C3's target partition: 3D 7-point n^3 over P = 8 row blocks
     (test.py:68-74's PetscSplitOwnership: n/8 planes per rank, one ghost plane
     from each neighbour -- 2 n^2 ghosts on the interior ranks), solved by
     test.py:50's CG + Jacobi with the fusion mode the 8-GPU node runs:
-    fuse 3 = auto (mode 1 at <= 3M rows/rank: the CG-fused general SELL
-    MatMult, halo packed from r / p_{i-1}, the boundary kernel) and mode 2
-    (the z-march SPLIT kernel with the ghost units flagged, the boundary
-    kernel finishing them).  MatMult bit-exact, its and reason equal to the
+    fuse 3 = auto (mode 2 with the z-march MatMult: the SPLIT kernel with the
+    ghost units flagged, the boundary kernel finishing them) and mode 1 (the
+    CG-fused general SELL MatMult, halo packed from r / p_{i-1}, the boundary
+    kernel; auto before round 3).  MatMult bit-exact, its and reason equal to the
     oracle's P = 8 model, x within rel-L2 1e-10; the dispatch counts show
     which MatMult kernels ran."""
     from mxsolve import _lib
@@ -600,9 +600,9 @@ def test_north_star_partition_p8(oracle_mod, n, fuse):
     its = o["its"]
     # the MatMult above: the z-march SPLIT kernel on every rank + the boundary kernel
     assert dc["pair_zm_split"] >= P and dc["boundary"] >= P
-    if fuse == 3:     # auto at 2M / 262k rows per rank: mode 1
+    if fuse == 1:
         assert dc["sell_cg"] >= P * its and dc["pair_zm_split"] == P, dc
-    else:
+    else:             # auto on P > 1 ranks with the z-march: mode 2
         assert dc["sell_cg"] == 0 and dc["pair_zm_split"] >= P * (its + 1), dc
     assert dc["boundary"] >= P * (its + 1)
 

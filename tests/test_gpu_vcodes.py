@@ -328,7 +328,10 @@ def _with_knobs(L, kv, fn):
 # lean-kernel forms: default (z-march, two planes per step, 4 workgroups per
 # CU, segments of up to 32 planes), the sweep form (39 = 0), one plane per
 # step (42 = 1), short / odd segments with tails (41), other grids (40)
-LEAN_FORMS = [{}, {39: 0}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}, {40: 2}]
+# -- and for the 27-point z-march: its per-run-branch body instead of the
+# column-zeroed one (48 = 0), two planes per step (49 = 2), other grids (45)
+LEAN_FORMS = [{}, {39: 0}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}, {40: 2},
+              {48: 0}, {49: 2, 45: 3}, {48: 0, 49: 2, 41: 5}]
 
 
 @pytest.mark.parametrize("form", range(len(LEAN_FORMS)))
@@ -375,6 +378,9 @@ def test_pair_lean_kernel(selfcomm, oracle_mod, kind, n, lean, form):
         # the 27-point lean kernel exists as a z-march only (knob 39 = 0: the general kernel)
         exp_lean = 0 if kind == "poisson3d27" and LEAN_FORMS[form].get(39) == 0 else lean
         assert i1["pair_uniform"] == 1 and i1["pair_lean"] == exp_lean and i0["pair_lean"] == 0
+        if kind == "poisson3d27" and exp_lean:
+            # a clean layout gets the column words unless knob 48 = 0; the other keeps the selects
+            assert i1["pair_form27"] == (0 if lean == 1 else 1 if LEAN_FORMS[form].get(48) == 0 else 2)
         assert np.array_equal(g1, exp) and np.array_equal(g0, exp)
 
 
