@@ -294,8 +294,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 27: row-pair SpMV layout for 5/7/27-point patterns (read at assembly and
  *         at launch; 0/1, default 1)
  * key 28: resident workgroups per CU for the row-pair SpMV grid (default 4)
- * key 29: CG mode 2 applies the deferred x steps every B iterations from B
- *         rotating direction buffers (1, 2 or 4; default 2)
+ * key 29: CG modes 2/5 apply the deferred x steps every B iterations from B
+ *         rotating direction buffers (1, 2 or 4; default 0 = auto: 4 in mode
+ *         5, else 2)
  * key 33: no-progress deadline in ms of the KSP poller's wait on an RCCL
  *         communicator (re-armed whenever the device's count of iterations
  *         begun moves); past it the communicator is aborted and the call fails

@@ -238,7 +238,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int bnd_grid = 0; int mdot_group = 8;
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
-                int cg_xbatch = 2; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
+                int cg_xbatch = 0; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;

@@ -1110,12 +1110,15 @@ static void cg_p_launch(hipStream_t st, int64_t n, KspState *s, const double *r,
 }
 
 // the direction-update grid (row walk); the zero-guess norms pass runs on
-// the same grid so that its partial sums equal the fused iteration-0 ones
-static unsigned cg_pb_grid(int64_t n) { return cg_vec_grid(n, false, 8192); }
+// the same grid so that its partial sums equal the fused iteration-0 ones.
+// Mode 5 (wide): 12288 workgroups (256^3: 185.8 -> 177.6 us per iteration with
+// x batches of 4, against 180.6 at 8192; profiles/r03_ab.jsonl)
+static unsigned cg_pb_grid(int64_t n, bool wide = false) { return cg_vec_grid(n, false, wide ? 12288 : 8192); }
 
 static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r, const Jac &j, const PBufs &pb,
-                         int B, double *x, double *hist, const double *r0, double *npart, const Fold &fin_in) {
-  const unsigned g = cg_pb_grid(n);
+                         int B, double *x, double *hist, const double *r0, double *npart, const Fold &fin_in,
+                         bool wide) {
+  const unsigned g = cg_pb_grid(n, wide);
   Fold fin = fin_in;
   fin.ntotal = fin.ncount = (int)g;
   const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 1) ? 2 : 0);
@@ -1160,7 +1163,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   int normtype = p.norm_type == MX_NORM_DEFAULT ? MX_NORM_PRECONDITIONED : p.norm_type;
   const size_t nv = (size_t)std::max<int64_t>(n, 1);
   // MatMult partials (+ boundary launch), then the update pass's 3 per workgroup
-  const size_t npart = (size_t)std::max({spmv_blocks(A) + 64, RED_BLOCKS, g_knobs.norm_grid, (int)cg_pb_grid(n)}) * 6 +
+  const size_t npart = (size_t)std::max({spmv_blocks(A) + 64, RED_BLOCKS, g_knobs.norm_grid, (int)cg_pb_grid(n, true)}) * 6 +
                        3 * (size_t)CG_MAX_VEC_GRID + 128;
   const size_t nhist = hist_host ? (size_t)p.max_it + 2 : 1;
   // mode 2 batches B x steps (knob 29; 2 or 4 p buffers) when the batch of
@@ -1180,16 +1183,19 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     else if (pair_lean_kind(A) > 0 && pair_zm_applies(A)) fmode = 2;
     else fmode = n <= CG_FUSE_MAX_ROWS ? 1 : 2;
   }
-  if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && g_knobs.cg_xbatch == 2 && poll % 2 == 0 && !p.guess_nonzero))
+  if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 0) &&
+                      poll % 2 == 0 && !p.guess_nonzero))
     fmode = 2;
   // mode 5 (knob 9 = 5): mode 2 whose MatMult stores no product -- a p.Ap
   // pass, then the update pass recomputes A p (mx_spmv_pair.hip SPMV_PW /
   // SPMV_RUPD) -- one rank, a lean 5/7-point z-march layout, no or uniform
   // Jacobi; otherwise 2
   if (fmode == 5 && !pair_cg5_applies(A, dinv.mode)) fmode = 2;
-  const int xb = ((fmode == 2 || fmode == 4 || fmode == 5) && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 4) &&
-                  poll % g_knobs.cg_xbatch == 0)
-                     ? g_knobs.cg_xbatch : 1;
+  // x-step batch (knob 29; 0 = auto: 4 in mode 5 -- 256^3: -2.8% per iteration
+  // against 2 -- else 2; mode 4 always 2)
+  const int xbk = g_knobs.cg_xbatch == 0 ? (fmode == 5 ? 4 : 2) : fmode == 4 ? 2 : g_knobs.cg_xbatch;
+  const int xb = ((fmode == 2 || fmode == 4 || fmode == 5) && (xbk == 2 || xbk == 4) && poll % xbk == 0) ? xbk : 1;
+  const bool wide_pb = fmode == 5;
   Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist, xb == 4 ? nv : 0, xb == 4 ? nv : 0})));
   struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
   double *pv2 = cv.take(nv);   // fused CG: p_i alternates between pv (i even) and pv2
@@ -1221,7 +1227,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // both give the same bits, then folds in-launch and runs cg_init (one rank)
   // or leaves partials for the all-reduce.
   const bool norms_in_pb = fused && xb > 1 && !p.guess_nonzero;
-  const int ngrid = g_knobs.norm_grid > 0 ? g_knobs.norm_grid : (int)cg_pb_grid(n);
+  const int ngrid = g_knobs.norm_grid > 0 ? g_knobs.norm_grid : (int)cg_pb_grid(n, wide_pb);
   Fold fin;
   if (fused) { fin.cnt = s->fold_upd; fin.out = red; fin.ntotal = fin.ncount = ngrid; }
 #define CGN(...) cg_norms_kernel<__VA_ARGS__><<<ngrid, 256, 0, st>>>
@@ -1293,7 +1299,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG mode 4 without its MatMult");
     } else {
       double *pi = xb > 1 ? pbs.b[it % xb] : pv.p;
-      if (xb > 1) cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb);
+      if (xb > 1) cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb, wide_pb);
       else cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
       timer.begin();
       nb_spmv = matmult_overlap(A, pi, w.p, fmode == 5 ? SPMV_PW : SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);

@@ -279,7 +279,10 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
                                                  ("poisson2d", 384, "jacobi", 10000, {}),
                                                  ("poisson3d", 128, "jacobi", 10000, {"guess": True}),
                                                  ("poisson3d", 128, "jacobi", 10000, {"norm": "natural"}),
-                                                 ("poisson3d", 128, "jacobi", 10000, {"norm": "unpreconditioned"})])
+                                                 ("poisson3d", 128, "jacobi", 10000, {"norm": "unpreconditioned"}),
+                                                 ("poisson3d", 128, "jacobi", 10000, {"xb": 2}),
+                                                 ("poisson3d", 128, "jacobi", 39, {"xb": 2}),
+                                                 ("poisson3d", 128, "jacobi", 38, {})])
 def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
     """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
     gives p.w, and the update pass recomputes A p (the same sums, the same
@@ -288,7 +291,8 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
     2 (the stored-product iteration): the same its and reason, iterates equal
     to rounding (the norms' partials are grouped per z-march column); the
     graph-replayed second solve gives the first one's bits; the dispatch
-    counts show both mode-5 passes ran."""
+    counts show both mode-5 passes ran.  x steps batched by 4 (the mode-5
+    default) and by 2, stops at every position relative to the batch."""
     from mxsolve import _lib
     from mxsolve.core import DMat, dispatch_counts, rhs_hash
     L = _lib.load()
@@ -298,6 +302,7 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
     def run(mode):
         old = L.mx_debug_set(9, mode)
         old27 = L.mx_debug_set(27, 1)           # the row-pair layout (this module's fixture turns it off)
+        old29 = L.mx_debug_set(29, kw.get("xb", 0) if mode == 5 else 0)   # mode 5: x batches of 4 by default
         try:
             A = DMat.stencil(selfcomm, kind, n)
             m = A.info()["m"]
@@ -322,6 +327,7 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
         finally:
             L.mx_debug_set(9, old)
             L.mx_debug_set(27, old27)
+            L.mx_debug_set(29, old29)
 
     m5, dc5, bh, x0 = run(5)
     m2, dc2, _, _ = run(2)
