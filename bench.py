@@ -73,18 +73,24 @@ def pair_meta_bytes(info: dict, m: int, nnz: int, nghost: int) -> int:
     return spmv_format_bytes(info, m, nnz, nghost) - 8 * (m + nghost) - 8 * m
 
 
-def cg_iter_bytes_design(info: dict, m: int, nnz: int, nghost: int, mode: int) -> int:
+def cg_iter_bytes_design(info: dict, m: int, nnz: int, nghost: int, mode: int, xb: int = 1) -> int:
     """This design's CG iteration with the uniform Jacobi as a scalar, by the
     fusion mode that ran (knob 9): 0 separate passes, MatMult + 72 B/row (p
     update 24, x/r update 48); 1 MatMult-fused, MatMult + 56 (32 in the
     MatMult, r update 24); 2 x step deferred into the p update, MatMult + 64
-    (p/x update 40, r update 24); 5 no product stored: the p update (40), the
-    p.Ap pass (p read: 8 + meta) and the residual update (p read again, r read
-    and written: 24 + meta)."""
+    (p/x update 40, r update 24); 5 no product stored: the p update, the p.Ap
+    pass (p read: 8 + meta) and the residual update (p read again, r read and
+    written: 24 + meta).  The p update streams r and p_{i-1} in and p_i out
+    (24 B/row) and, with the x steps batched by B (modes 2/5), every B-th
+    launch also the B - 1 older directions and x in and x out: 24 + (8 (B - 1)
+    + 16) / B B/row per iteration (B = 1: the 40 of the unbatched step)."""
+    pupd = 24 * m + (8 * (xb - 1) + 16) * m // max(xb, 1)
     if mode == 5:
         meta = pair_meta_bytes(info, m, nnz, nghost)
-        return 40 * m + (8 * (m + nghost) + meta) + (8 * (m + nghost) + 16 * m + meta)
-    return spmv_format_bytes(info, m, nnz, nghost) + {0: 72, 1: 56, 2: 64, 4: 48}.get(mode, 64) * m
+        return pupd + (8 * (m + nghost) + meta) + (8 * (m + nghost) + 16 * m + meta)
+    if mode == 2:
+        return spmv_format_bytes(info, m, nnz, nghost) + pupd + 24 * m
+    return spmv_format_bytes(info, m, nnz, nghost) + {0: 72, 1: 56, 4: 48}.get(mode, 64) * m
 
 
 def cpu_threads() -> tuple[int, str]:
@@ -469,7 +475,7 @@ def main():
         threads, how = cpu_threads()
         cpu = cpu_baseline(n, threads, how)
 
-    iter_bytes = cg_iter_bytes_design(info, m, nnz_loc, ng, mode)
+    iter_bytes = cg_iter_bytes_design(info, m, nnz_loc, ng, mode, rp.get("cg_xbatch", 1))
     iter_gbps = iter_bytes * value / 1e9
     if rank == 0:
         traffic = load_traffic(n, world, mode)
@@ -516,6 +522,7 @@ def main():
                                 "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1)},
             "cg_iter_bytes_survey": cg_iter_bytes(m, nnz_loc, ng),
             "cg_fusion_mode": mode,
+            "cg_xbatch": rp.get("cg_xbatch"),
             "cg_iter_bytes_alg": iter_bytes,
             "cg_iter_GBps_alg": round(iter_gbps, 1),
             # the whole timed iteration (every kernel, the per-solve start and

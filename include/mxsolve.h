@@ -78,6 +78,7 @@ typedef struct {
   int cg_mode;         /* CG: the fusion mode that ran (key 9's modes 0/1/2/4/5)     */
   double upd_ms;       /* sum of profiled residual-update launch times (profile bit 1) */
   int upd_count;       /* residual-update launches profiled                         */
+  int cg_xbatch;       /* CG: deferred x steps applied every this many iterations    */
 } mx_ksp_result;
 
 typedef struct {

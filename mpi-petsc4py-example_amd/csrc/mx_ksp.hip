@@ -1419,6 +1419,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   timer.collect(res.spmv_ms, res.spmv_count);
   utimer.collect(res.upd_ms, res.upd_count);
   res.cg_mode = fmode;
+  res.cg_xbatch = xb;
   if (hist_host)
     HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)res.its + 1), hipMemcpyDeviceToHost));
 }
