@@ -117,6 +117,9 @@ typedef struct {
   int64_t pair_form27;                /* 27-point z-march body: 2 column-zeroed (no branches,
                                          no selects; key 48), 1 per-run branches, 0 lane
                                          selects; -1 when the 27-point z-march does not run */
+  int64_t pair_code;                  /* 1: the coded z-march MatMult runs -- 5/7-point code
+                                         dictionary not uniform per slot, every block
+                                         select-free (values from the LDS table; key 52) */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */
@@ -333,6 +336,15 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         27-point z-march zeroes empty runs and x-line edges where it loads
  *         them (no per-run branches, no selects; the same bits)
  * key 49: 27-point z-march planes per step (1, default, or 2)
+ * key 50: GMRES MDot in one pass over w for <= 32 basis vectors (2, default: a
+ *         workgroup holds 2048 rows of w in registers and walks the vectors;
+ *         1: the four waves of a workgroup split the vectors; 0: groups of key 16)
+ * key 51: GMRES MAXPY + norm pass in chunks (1, default: 2048 rows per
+ *         workgroup step, 16-byte pairs; 0: one row per thread)
+ * key 52: coded z-march MatMult for 5/7-point code dictionaries that are not
+ *         uniform per slot (1, default; 0: the general SELL kernel)
+ * key 53: z-march terms of slots whose value is -1, 0 or +1 formed by fma (an
+ *         exact product: the same bits; 1, default; 0: multiply and add)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -256,6 +256,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_f64 = (A->nghost == 0 || matmult_splits(A)) ? pair_f64_kind(A) : 0;
     info->pair_form27 = A->sd.pair_shape == 27 && pair_lean_kind(A)
                             ? (pair_lean_kind(A) == 2 ? (A->sd.pcol27.p ? 2 : 1) : 0) : -1;
+    info->pair_code = pair_code_applies(A) && (A->nghost == 0 || matmult_splits(A)) ? 1 : 0;
   });
 }
 
@@ -542,6 +543,10 @@ int mx_debug_set(int key, int value) {
     case 47: old = g_knobs.comm_wait_ms; g_knobs.comm_wait_ms = std::max(value, 0); break;
     case 48: old = g_knobs.pair_col27; g_knobs.pair_col27 = value; break;
     case 49: old = g_knobs.pair_zm27_units; g_knobs.pair_zm27_units = value == 2 ? 2 : 1; break;
+    case 50: old = g_knobs.mdot_split; g_knobs.mdot_split = value; break;
+    case 51: old = g_knobs.maxpy_pairs; g_knobs.maxpy_pairs = value; break;
+    case 52: old = g_knobs.pair_zmc; g_knobs.pair_zmc = value; break;
+    case 53: old = g_knobs.pair_unitv; g_knobs.pair_unitv = value; break;
     default: break;
   }
   return old;

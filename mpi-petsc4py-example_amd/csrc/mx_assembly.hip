@@ -1217,6 +1217,37 @@ __global__ void pair_clean_flags_kernel(int64_t nunits, const int32_t *__restric
   pblk[u] = (int32_t)((uint32_t)pblk[u] | (uint32_t)bfl[(uint32_t)pblk[u] & PBLK_ID]);
 }
 
+// Select-free ("clean") rule of one 5/7-point row-pair block given its
+// slot-row presence masks pm[0 .. 2K): every absent slot's operand can be made
+// exactly 0.0 by an out-of-range read -- a run whose slot-rows are empty for
+// both rows, or the tri run's edge value when only lane 0 row 0 lacks -1 /
+// lane 63 row 1 lacks +1 -- so no presence select is needed.  f: the flags
+// (PBLK_RUN0 << r, PBLK_ELO / EHI) the z-march kernels read from pblk.
+static bool pair_block_clean(int ps, int K, const unsigned long long *pm, uint32_t &f) {
+  const unsigned long long F = ~0ull;
+  f = 0;
+  const int NR = ps == 5 ? 3 : 5;
+  for (int r = 0; r < NR; ++r) {
+    const bool tri = ps == 5 ? r == 1 : r == 2;
+    const int j = ps == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
+    if (!tri) {
+      const unsigned long long a = pm[j], c = pm[K + j];
+      if (a == 0 && c == 0) f |= PBLK_RUN0 << r;
+      else if (a != F || c != F) return false;
+      continue;
+    }
+    const unsigned long long m0 = pm[j], m1 = pm[j + 1], m2 = pm[j + 2];
+    const unsigned long long n0 = pm[K + j], n1 = pm[K + j + 1], n2 = pm[K + j + 2];
+    if ((m0 | m1 | m2 | n0 | n1 | n2) == 0) { f |= (PBLK_RUN0 << r) | PBLK_ELO | PBLK_EHI; continue; }
+    if (m1 != F || m2 != F || n0 != F || n1 != F) return false;
+    if (m0 != F && m0 != (F & ~1ull)) return false;
+    if (n2 != F && n2 != (F >> 1)) return false;
+    if (m0 != F) f |= PBLK_ELO;
+    if (n2 != F) f |= PBLK_EHI;
+  }
+  return true;
+}
+
 // Uniform-slot form of the code-block dictionary (Sell::puni), 5/7-point
 // shapes: kept only when, in every block, each slot-row's present codes are
 // one code (constant-coefficient stencils: a few dozen boundary classes).
@@ -1260,28 +1291,8 @@ static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream
   std::vector<int32_t> fl((size_t)nb, 0);
   bool clean = true;
   for (int64_t b = 0; b < nb && clean; ++b) {
-    const PairUni &B = u[(size_t)b];
-    const unsigned long long F = ~0ull;
     uint32_t f = 0;
-    const int NR = S.pair_shape == 5 ? 3 : 5;
-    for (int r = 0; r < NR && clean; ++r) {
-      const bool tri = S.pair_shape == 5 ? r == 1 : r == 2;
-      const int j = S.pair_shape == 5 ? (r == 0 ? 0 : r == 1 ? 1 : 4) : (r < 2 ? r : r == 2 ? 2 : r + 2);
-      if (!tri) {
-        const unsigned long long a = B.pm[j], c = B.pm[K + j];
-        if (a == 0 && c == 0) f |= PBLK_RUN0 << r;
-        else if (a != F || c != F) clean = false;
-        continue;
-      }
-      const unsigned long long m0 = B.pm[j], m1 = B.pm[j + 1], m2 = B.pm[j + 2];
-      const unsigned long long n0 = B.pm[K + j], n1 = B.pm[K + j + 1], n2 = B.pm[K + j + 2];
-      if ((m0 | m1 | m2 | n0 | n1 | n2) == 0) { f |= (PBLK_RUN0 << r) | PBLK_ELO | PBLK_EHI; continue; }
-      if (m1 != F || m2 != F || n0 != F || n1 != F) clean = false;
-      else if (m0 != F && m0 != (F & ~1ull)) clean = false;
-      else if (n2 != F && n2 != (F >> 1)) clean = false;
-      if (m0 != F) f |= PBLK_ELO;
-      if (n2 != F) f |= PBLK_EHI;
-    }
+    clean = pair_block_clean(S.pair_shape, K, u[(size_t)b].pm, f);
     fl[(size_t)b] = (int32_t)f;
   }
   S.pair_clean = clean && S.nunits > 0;
@@ -1294,6 +1305,40 @@ static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream
   HIPCHECK(hipStreamSynchronize(st));
 }
 
+// Select-free flags of a non-uniform code dictionary (Sell::pair_code_clean):
+// the coded z-march (mx_spmv_pair.hip spmv_pair_zmc_kernel) reads each unit's
+// code block and looks its values up in LDS, an absent slot's code giving the
+// table's 0.0 and its operand made 0.0 by the same out-of-range reads as the
+// uniform form, so it needs these flags in pblk and no presence select.
+static void build_pair_code_clean(Sell &S, hipStream_t st) {
+  S.pair_code_clean = false;
+  const int K = S.dia_k;
+  if (S.puni.p || S.pair_blocks <= 0 || (S.pair_shape != 5 && S.pair_shape != 7) || K != S.pair_shape || 2 * K > 16)
+    return;
+  const int pb = pair_bytes(K);
+  const int64_t nb = S.pair_blocks;
+  std::vector<uint8_t> d((size_t)nb * 64 * pb);
+  HIPCHECK(hipMemcpyAsync(d.data(), S.pcode.p, d.size(), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  std::vector<int32_t> fl((size_t)nb, 0);
+  for (int64_t b = 0; b < nb; ++b) {
+    unsigned long long pm[16] = {};
+    for (int q = 0; q < 2 * K; ++q)
+      for (int lane = 0; lane < 64; ++lane)
+        if (d[((size_t)b * 64 + lane) * pb + q] != VCODE_ABSENT) pm[q] |= 1ull << lane;
+    uint32_t f = 0;
+    if (!pair_block_clean(S.pair_shape, K, pm, f)) return;
+    fl[(size_t)b] = (int32_t)f;
+  }
+  if (S.nunits <= 0) return;
+  DBuf<int32_t> fd((size_t)nb);
+  HIPCHECK(hipMemcpyAsync(fd.p, fl.data(), sizeof(int32_t) * fl.size(), hipMemcpyHostToDevice, st));
+  pair_clean_flags_kernel<<<(unsigned)cdiv(S.nunits, 256), 256, 0, st>>>(S.nunits, S.dpat.p, fd.p, S.pblk.p);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(st));
+  S.pair_code_clean = true;
+}
+
 // 27-point uniform-slot dictionary (Sell::puni27): kept when every block's
 // 54 slot-rows are uniform; each block also gets its select-free flags (runs
 // empty for both rows, and the x-line edges, which the nine runs of a
@@ -1301,6 +1346,7 @@ static void build_pair_uniform(Sell &S, const std::vector<double> &vt, hipStream
 static void build_pair_uniform27(Sell &S, const std::vector<double> &vt, hipStream_t st) {
   S.puni27.reset();
   S.pair_clean27 = false;
+  S.pair_unit27 = false;
   const int K = 27;
   if (S.pair_blocks <= 0 || S.pair_shape != 27 || S.dia_k != 27) return;
   const int pb = pair_bytes(K);
@@ -1360,10 +1406,16 @@ static void build_pair_uniform27(Sell &S, const std::vector<double> &vt, hipStre
     B.clean = clean ? 1u : 0u;
     all_clean = all_clean && clean;
   }
+  // slot values -1 / 0 / +1 off the diagonal (slot 13): exact products
+  bool unit = true;
+  for (int64_t b = 0; b < nb && unit; ++b)
+    for (int j = 0; j < K && unit; ++j)
+      if (j != 13 && u[(size_t)b].v[j] != -1.0 && u[(size_t)b].v[j] != 0.0 && u[(size_t)b].v[j] != 1.0) unit = false;
   S.puni27.alloc((size_t)nb);
   HIPCHECK(hipMemcpyAsync(S.puni27.p, u.data(), sizeof(PairUni27) * u.size(), hipMemcpyHostToDevice, st));
   HIPCHECK(hipStreamSynchronize(st));
   S.pair_clean27 = all_clean;
+  S.pair_unit27 = unit;
 }
 
 // Column words of a clean 27-point layout (Sell::pcol27), when the units'
@@ -1472,6 +1524,7 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
     }
     dedupe_pair_blocks(S, st);
     build_pair_uniform(S, vt, st);
+    build_pair_code_clean(S, st);
     build_pair_uniform27(S, vt, st);
     S.pair_ghosts = false;
     if (wid_o && S.nunits) {

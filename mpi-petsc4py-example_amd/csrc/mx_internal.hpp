@@ -199,6 +199,9 @@ struct Sell {
   DBuf<int32_t> pflag;
   int pair_f64 = 0;         // 5 / 7: the fp64 row-pair layout's shape, 0 none
   bool pair_clean27 = false;  // every puni27 block is select-free
+  // every puni27 block's slot values but the diagonal's are -1, 0 or +1: the
+  // 27-point z-march forms those slots' terms by fma (exact products, the same bits)
+  bool pair_unit27 = false;
   // 27-point column words (one per 128-row column of a plane): when every
   // unit's empty runs are exactly its plane's z-boundary runs (plane 0: dz =
   // -1, the last plane: dz = +1 -- read out of range anyway) plus its column's
@@ -212,6 +215,9 @@ struct Sell {
   // Jacobi setup does, so the Jacobi-fused row-pair MatMult reads no dinv
   // vector (the same bits)
   DBuf<double> dtab;
+  // a non-uniform code dictionary (pair_blocks > 0, no puni) whose every block
+  // is select-free: the flags are in pblk, and the coded z-march runs on it
+  bool pair_code_clean = false;
 };
 constexpr uint32_t PBLK_GHOST_LO = 1u << 30;
 constexpr uint32_t PBLK_GHOST_HI = 1u << 31;
@@ -242,7 +248,8 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
-                int comm_wait_ms = 0; int pair_col27 = 1; int pair_zm27_units = 1; };
+                int comm_wait_ms = 0; int pair_col27 = 1; int pair_zm27_units = 1;
+                int mdot_split = 2; int maxpy_pairs = 1; int pair_zmc = 1; int pair_unitv = 1; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -405,6 +412,8 @@ enum Dispatch {
   DSP_BOUNDARY = 10,     // spmv_boundary_kernel
   DSP_ZM_PW = 11,        // CG mode 5: the z-march p.Ap pass (no product stored)
   DSP_ZM_RUPD = 12,      // CG mode 5: the z-march residual update (product recomputed)
+  DSP_PAIR_ZMC = 13,     // spmv_pair_zmc_kernel (coded z-march), one rank / no ghost units
+  DSP_PAIR_ZMC_SPLIT = 14,
   DSP_COUNT = 16
 };
 void note_dispatch(int kind);
@@ -413,7 +422,8 @@ int device_cu_count();
 int main_grid(const Mat *A, int mode, const void *kf, bool pairs);   // the SpMV's resident grid
 // lean row-pair MatMult (mx_spmv_pair.hip): launched when it applies (returns its grid, else 0)
 int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials, const int *done,
-                     const Fold &fold, hipStream_t st);
+                     const Fold &fold, hipStream_t st, const Jac &jac = Jac{}, const double *xscale = nullptr);
+bool pair_code_applies(const Mat *A);   // the coded z-march (mx_mat_info.pair_code)
 int pair_lean_kind(const Mat *A);   // 0 general kernel, 1 lean, 2 lean select-free (mx_mat_info.pair_lean)
 bool pair_zm_applies(const Mat *A);  // the lean kernel's z-march form (mx_mat_info.pair_zmarch)
 int pair_f64_kind(const Mat *A);     // 5 / 7: the fp64 row-pair z-march applies (mx_mat_info.pair_f64)

@@ -759,12 +759,153 @@ __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__re
   block_sum_to_partials<NV>(acc, partials + (size_t)j0 * gridDim.x, gridDim.x);
 }
 
+// VecMDot in one pass over w for nv <= 4 * 8 basis vectors: the four waves of
+// a workgroup walk the same rows and split the vectors between them (wave g:
+// vectors [g q, g q + q), q = ceil(nv / 4) = NQ).  w is read from HBM once per
+// step -- the other three waves' reads of a line hit the XCD's L2 -- where
+// mdot_kernel's groups of 8 re-read it per group (ceil(nv / 8) passes), and
+// every load is a 16-byte pair per lane.  Each vector's partial is one wave's
+// sum (no block fold): partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
+template <int NQ>
+__global__ void __launch_bounds__(256) mdot_split_kernel(int64_t n, const double *__restrict__ w,
+                                                         const double *__restrict__ V, int64_t ldv, int nv,
+                                                         const double *__restrict__ vscale,
+                                                         double *__restrict__ partials,
+                                                         const int *__restrict__ stop_flag) {
+  if (*stop_flag) return;
+  const int lane = threadIdx.x & 63;
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j0 = g * NQ, cnt = min(NQ, nv - j0);
+  if (cnt <= 0) return;   // wave-uniform: no vectors for this wave (nv < 4 NQ)
+  constexpr int U = NQ <= 3 ? 2 : 1;   // row pairs per lane per step: >= 6 loads in flight
+  double acc[NQ], sc[NQ];
+  const dbl2 *__restrict__ vk[NQ];
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    const int j = j0 + (k < cnt ? k : cnt - 1);   // past cnt: the last vector again (cached lines, dropped)
+    acc[k] = 0.0;
+    sc[k] = vscale[j];
+    vk[k] = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
+  }
+  const dbl2 *__restrict__ w2 = reinterpret_cast<const dbl2 *>(w);
+  const int64_t n2 = n >> 1, stride = (int64_t)gridDim.x * 64;
+  int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  for (; i + (U - 1) * stride < n2; i += U * stride) {
+    dbl2 wi[U], v[U][NQ];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      wi[u] = w2[i + u * stride];
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) v[u][k] = __builtin_nontemporal_load(vk[k] + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        acc[k] += wi[u].x * (sc[k] * v[u][k].x);
+        acc[k] += wi[u].y * (sc[k] * v[u][k].y);
+      }
+  }
+  if constexpr (U > 1) {
+    if (i < n2) {
+      const dbl2 wi = w2[i];
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        const dbl2 v = __builtin_nontemporal_load(vk[k] + i);
+        acc[k] += wi.x * (sc[k] * v.x);
+        acc[k] += wi.y * (sc[k] * v.y);
+      }
+    }
+  }
+  if ((n & 1) && blockIdx.x == 0 && lane == 0) {   // odd length: the last row
+    const double wl = w[n - 1];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) acc[k] += wl * (sc[k] * V[(int64_t)(j0 + (k < cnt ? k : cnt - 1)) * ldv + n - 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    const double s = wave_sum(acc[k]);
+    if (lane == 0 && k < cnt) partials[(size_t)(j0 + k) * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// VecMDot in one pass over w, chunk form (knob 50 = 2, the default; nv <= 32):
+// a workgroup holds 2048 rows of w in registers (WP = 4 16-byte pairs per
+// thread) and walks the basis vectors one after another, reading 16 KB of
+// each contiguously per step, with nv running sums per thread.  On 2^24 rows
+// this streams at 6.7-6.9 TB/s -- the plain read ceiling -- where the split
+// form (several vectors' 1 KB pieces interleaved per wave step) makes 6.0-6.4
+// (tools/mdot_probe.hip).  partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
+template <int WP>
+__global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double *__restrict__ w,
+                                                         const double *__restrict__ V, int64_t ldv, int nv,
+                                                         const double *__restrict__ vscale,
+                                                         double *__restrict__ partials,
+                                                         const int *__restrict__ stop_flag) {
+  constexpr int NVX = 32;
+  if (*stop_flag) return;
+  double acc[NVX];
+#pragma unroll
+  for (int j = 0; j < NVX; ++j) acc[j] = 0.0;
+  const dbl2 *__restrict__ w2 = reinterpret_cast<const dbl2 *>(w);
+  const int64_t n2 = n >> 1, csz = 256 * WP, nfull = n2 / csz;
+  auto chunk = [&](int64_t c0, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    dbl2 wr[WP];
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+      const int64_t i = c0 + k * 256 + threadIdx.x;
+      wr[k] = (FULL || i < n2) ? w2[i] : dbl2{0.0, 0.0};
+    }
+#pragma unroll
+    for (int j = 0; j < NVX; ++j) {
+      if (j < nv) {                                // wave-uniform
+        const double sj = vscale[j];
+        const dbl2 *__restrict__ vj = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
+        dbl2 t[WP];
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+          const int64_t i = c0 + k * 256 + threadIdx.x;
+          t[k] = (FULL || i < n2) ? __builtin_nontemporal_load(vj + i) : dbl2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+          acc[j] += wr[k].x * (sj * t[k].x);
+          acc[j] += wr[k].y * (sj * t[k].y);
+        }
+      }
+    }
+  };
+  for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
+  if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // odd length: the last row
+    const double wl = w[n - 1];
+#pragma unroll
+    for (int j = 0; j < NVX; ++j)   // compile-time indices: acc stays in registers
+      if (j < nv) acc[j] += wl * (vscale[j] * V[(int64_t)j * ldv + n - 1]);
+  }
+  __shared__ double sh[NVX][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NVX; ++j) {
+    if (j < nv) {
+      const double s = wave_sum(acc[j]);
+      if (lane == 0) sh[j][wid] = s;
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nv)
+    partials[(size_t)threadIdx.x * gridDim.x + blockIdx.x] =
+        (sh[threadIdx.x][0] + sh[threadIdx.x][1]) + (sh[threadIdx.x][2] + sh[threadIdx.x][3]);
+}
+
 // KSPGMRESClassicalGramSchmidtOrthogonalization after the MDot: the
 // coefficients -h_j (h = w.v_j, folded and all-reduced), the Hessenberg
 // column (hh[k][j] = 0 - (-h_j)) and the non-finite check, evaluated by every
 // workgroup (workgroup 0 commits), then VecMAXPY_Seq's grouping (first nv%4
 // vectors, then groups of four) and ||w||^2, folded in-launch (fold.cnt) or
 // as plain partials
+template <bool CHUNK>
 __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
                                                          KspState *__restrict__ s, const double *__restrict__ red_k,
@@ -791,18 +932,84 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
     for (int j = threadIdx.x; j < nv; j += 256) hh[(size_t)(nv - 1) * ld + j] = 0.0 - a[j];
   const int rem = nv & 3;
   double v[1] = {0.0};
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    double u = w[i];
-    int j = 0;
-    auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
-    if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
-    else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
-    else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
-    for (; j < nv; j += 4)
-      u = u + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
-    w[i] = u;
-    v[0] += u * u;
+  if (CHUNK) {
+    // chunk form (knob 51 = 1, the default): a workgroup updates 2048 rows per
+    // step, 4 16-byte pairs of w per thread, and reads each group of four
+    // basis vectors' 16 KB pieces contiguously -- 5.9-6.2 TB/s against
+    // 5.5-6.0 for one row per thread (tools/mdot_probe.hip).  Every row's
+    // expression is the row form's below (VecMAXPY_Seq's grouping), so the
+    // same bits.
+    constexpr int WP = 4;
+    const int64_t n2 = n >> 1, csz = 256 * WP, nfull = n2 / csz;
+    dbl2 *__restrict__ w2 = reinterpret_cast<dbl2 *>(w);
+    auto chunk = [&](int64_t c0, auto fullc) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(fullc)::value;
+      auto in = [&](int k) { return FULL || c0 + k * 256 + threadIdx.x < n2; };
+      auto ld = [&](int j, int k) -> dbl2 {
+        if (!in(k)) return dbl2{0.0, 0.0};
+        const dbl2 t = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv) + c0 +
+                                                  k * 256 + threadIdx.x);
+        return dbl2{sc[j] * t.x, sc[j] * t.y};
+      };
+      dbl2 u[WP];
+#pragma unroll
+      for (int k = 0; k < WP; ++k) u[k] = in(k) ? w2[c0 + k * 256 + threadIdx.x] : dbl2{0.0, 0.0};
+      int j = 0;
+      if (rem) {                                   // the first nv % 4 vectors
+        dbl2 t[3][WP];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+          for (int k = 0; k < WP; ++k) t[q][k] = q < rem ? ld(q, k) : dbl2{0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+          if (rem == 1) {
+            u[k] = dbl2{a[0] * t[0][k].x + u[k].x, a[0] * t[0][k].y + u[k].y};
+          } else if (rem == 2) {
+            u[k] = u[k] + dbl2{a[0] * t[0][k].x + a[1] * t[1][k].x, a[0] * t[0][k].y + a[1] * t[1][k].y};
+          } else {
+            u[k] = u[k] + dbl2{(a[0] * t[0][k].x + a[1] * t[1][k].x) + a[2] * t[2][k].x,
+                               (a[0] * t[0][k].y + a[1] * t[1][k].y) + a[2] * t[2][k].y};
+          }
+        }
+        j = rem;
+      }
+      for (; j < nv; j += 4) {                     // groups of four
+        dbl2 t[4][WP];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int k = 0; k < WP; ++k) t[q][k] = ld(j + q, k);
+#pragma unroll
+        for (int k = 0; k < WP; ++k)
+          u[k] = u[k] + dbl2{((a[j] * t[0][k].x + a[j + 1] * t[1][k].x) + a[j + 2] * t[2][k].x) + a[j + 3] * t[3][k].x,
+                             ((a[j] * t[0][k].y + a[j + 1] * t[1][k].y) + a[j + 2] * t[2][k].y) + a[j + 3] * t[3][k].y};
+      }
+#pragma unroll
+      for (int k = 0; k < WP; ++k) {
+        if (!in(k)) continue;
+        w2[c0 + k * 256 + threadIdx.x] = u[k];
+        v[0] += u[k].x * u[k].x;
+        v[0] += u[k].y * u[k].y;
+      }
+    };
+    for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
+    if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
+  }
+  {
+    const int64_t i0 = CHUNK ? (n & ~(int64_t)1) : 0, stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = i0 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      double u = w[i];
+      int j = 0;
+      auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
+      if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
+      else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
+      else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
+      for (; j < nv; j += 4)
+        u = u + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
+      w[i] = u;
+      v[0] += u * u;
+    }
   }
   block_partials<1>(v, partials, gridDim.x, fold);
 }
@@ -1440,6 +1647,20 @@ static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double
 // buffer holds max_k + 2 rows rounded up to 32; groups are gw wide (knob 16)
 static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
                  const double *vscale, double *partials, const int *stop_flag, int grid) {
+  if (g_knobs.mdot_split == 2 && nv <= 32) {   // one pass over w, chunk form (knob 50)
+    mdot_chunk_kernel<4><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+    HIPCHECK(hipGetLastError());
+    return;
+  }
+  if (g_knobs.mdot_split == 1 && nv <= 32) {   // one pass over w, split form (knob 50)
+    using F = void (*)(int64_t, const double *, const double *, int64_t, int, const double *, double *, const int *);
+    static constexpr F tab[8] = {&mdot_split_kernel<1>, &mdot_split_kernel<2>, &mdot_split_kernel<3>,
+                                 &mdot_split_kernel<4>, &mdot_split_kernel<5>, &mdot_split_kernel<6>,
+                                 &mdot_split_kernel<7>, &mdot_split_kernel<8>};
+    tab[(nv + 3) / 4 - 1]<<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+    HIPCHECK(hipGetLastError());
+    return;
+  }
   const int gw = g_knobs.mdot_group == 16 || g_knobs.mdot_group == 32 || g_knobs.mdot_group == 4 ? g_knobs.mdot_group : 8;
   for (int j0 = 0; j0 < nv; j0 += gw) {
     const int k = std::min(gw, nv - j0);
@@ -1537,7 +1758,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, mgrid, red.p, istop);
       c->allreduce_sum(red.p, k + 1);
       // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
-      maxpy_norm_kernel<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
+      (g_knobs.maxpy_pairs ? &maxpy_norm_kernel<true> : &maxpy_norm_kernel<false>)<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
       c->allreduce_sum(sred, 1);
       gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p);
       HIPCHECK(hipGetLastError());

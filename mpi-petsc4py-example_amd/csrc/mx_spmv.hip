@@ -858,8 +858,8 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
                        const double *xscale) {
   // constant-coefficient 5/7-point blocks: the lean row-pair kernels
   // (mx_spmv_pair.hip; each row's sum has the same bits)
-  if (!cgp && !xscale) {
-    const int lg = pair_lean_launch(A, mode, split, x, y, partials, done_flag, fold_in, st);
+  if (!cgp) {
+    const int lg = pair_lean_launch(A, mode, split, x, y, partials, done_flag, fold_in, st, jac, xscale);
     if (lg) return lg;
   }
   const double *lvec = (A->nghost && !split) ? A->halo.lvec.p : nullptr;

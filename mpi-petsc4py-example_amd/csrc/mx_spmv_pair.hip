@@ -366,7 +366,11 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
 //     U27_EHI: lane 0's / lane 63's edge);
 //   0: presence selects from the lane's own 54 mask bits (PairUni27::lane,
 //     one vector load per unit).
-template <int MODE, bool SPLIT, int FORM>
+//   UV (Sell::pair_unit27, knob 53): every slot value but the diagonal's is
+//     -1, 0 or +1, so v * a is exact and sum + v * a == fma(v, a, sum) bit for
+//     bit (one rounding either way; an exact product cannot overflow or
+//     underflow): one VALU op instead of two for 26 of the 27 slots.
+template <int MODE, bool SPLIT, int FORM, bool UV = false>
 __device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e)[9], uint32_t bw,
                                             const PairUni27 *__restrict__ puni, double *__restrict__ y, int r0,
                                             int lane, double &dot) {
@@ -396,7 +400,14 @@ __device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e
     for (int p = 0; p < 3; ++p) {
       const int j = 3 * r + p;
       const double v = B.v[j];
-      const double q0 = s0v + v * a0[p], q1 = s1v + v * a1[p];
+      double q0, q1;
+      if (UV && j != 13) {
+        q0 = __builtin_fma(v, a0[p], s0v);
+        q1 = __builtin_fma(v, a1[p], s1v);
+      } else {
+        q0 = s0v + v * a0[p];
+        q1 = s1v + v * a1[p];
+      }
       if constexpr (FORM == 0) {
         s0v = ((pb >> j) & 1ull) ? q0 : s0v;
         s1v = ((pb >> (K + j)) & 1ull) ? q1 : s1v;
@@ -424,8 +435,12 @@ struct PairLean27Args {
   Fold fold;
 };
 
-template <int MODE, bool SPLIT, int FORM, int ZU>
-__global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
+// The column-word form keeps 6 waves per SIMD (<= 80 VGPRs; the VALU-bound
+// body measured fastest there, knob 45); the fma form (UV) otherwise
+// allocates 86-105 (one plane per step; two would spill at that bound).
+template <int MODE, bool SPLIT, int FORM, int ZU, bool UV = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UV && ZU == 1 ? 6 : 1)))
+spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
                                                              double *__restrict__ y, const int32_t *__restrict__ pblk,
                                                              const PairUni27 *__restrict__ puni,
                                                              const int32_t *__restrict__ pcol) {
@@ -502,7 +517,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27_kernel(const PairLean27Arg
         for (int r = 0; r < 6; ++r) { L[r] = C[r]; e[r] = Ce[r]; }
 #pragma unroll
         for (int k = 0; k < 3; ++k) { L[6 + k] = Nw[q][k]; e[6 + k] = Ne[q][k]; }
-        pair_unit27<MODE, SPLIT, FORM>(L, e, bw[q], puni, y, (z + q) * D + cb, lane, dot);
+        pair_unit27<MODE, SPLIT, FORM, UV>(L, e, bw[q], puni, y, (z + q) * D + cb, lane, dot);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           C[k] = C[3 + k]; Ce[k] = Ce[3 + k];
@@ -618,6 +633,164 @@ __global__ void __launch_bounds__(256) spmv_pair_zmf64_kernel(const PairLeanArgs
           // SPLIT: rows with A_o entries stored their diagonal-block sum; the
           // boundary kernel continues them and adds their p.y terms
           const bool gh = SPLIT && (fl[q] & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+          if (!gh) {
+            dot += L[q][C].x * s0v;
+            dot += L[q][C].y * s1v;
+          }
+        }
+      }
+      if constexpr (NQ == 1) zm = c;
+      else zm = zp[NQ - 2];
+      c = zp[NQ - 1];
+    };
+    int z = z0;
+    for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
+    for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
+  }
+  if constexpr (MODE == SPMV_DOT) {
+    double v[1] = {dot};
+    block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  }
+}
+
+// Coded z-march (Sell::pair_code_clean): spmv_pair_zm_kernel's march for
+// 5/7-point layouts whose dictionary blocks are not uniform per slot-row --
+// variable coefficients with few distinct values, e.g. BASELINE C4's
+// convection-diffusion operator (10 values, period 4 in x: a slot's value
+// differs between lanes).  Per unit: one 16-byte code load per lane from the
+// L2-resident dictionary (pcode block pblk[u] & PBLK_ID), the values from the
+// LDS table (the absent code's entry is 0.0, and the clean flags' out-of-range
+// reads make an absent slot's operand 0.0: sum + 0.0 * 0.0 = sum, no presence
+// select), and for the Jacobi modes dinv from dtab by the diagonal slot's code
+// (the Jacobi setup's division per code: the same bits as the dinv vector).
+// Modes: PLAIN, DOT, JACOBI, and GMRES's PLAIN_S / JACOBI_S -- the operand is
+// fl(s * x) with s = *xscale (the basis vector kept unnormalised), formed
+// once per loaded value and carried formed.  Each row sums its slots in
+// ascending column order: the general kernel's bits (tests/test_gpu_vcodes.py).
+struct PairCodeArgs {
+  const uint8_t *pcode;        // the code dictionary (64 lanes x 16 bytes per block)
+  const double *vtab, *dtab;   // [VCODE_MAX]: values (absent / unused: 0.0), 1 / value
+  const double *xscale;        // *_S modes
+  Jac jac;                     // JACOBI modes without dtab (DT = false)
+};
+
+template <int MODE, int PS, bool SPLIT, int ZU, bool DT>
+__global__ void __launch_bounds__(256) spmv_pair_zmc_kernel(const PairLeanArgs a, const double *__restrict__ x,
+                                                            double *__restrict__ y, const int32_t *__restrict__ pblk,
+                                                            const PairCodeArgs ca) {
+  if (a.done && *a.done) return;   // wave-uniform: solver finished
+  __shared__ double vtab[VCODE_MAX];
+  __shared__ double dtab[DT ? VCODE_MAX : 1];
+  for (int i = threadIdx.x; i < VCODE_MAX; i += 256) {
+    vtab[i] = ca.vtab[i];
+    if constexpr (DT) dtab[i] = ca.dtab[i];
+  }
+  __syncthreads();
+  constexpr bool SC = spmv_scaled(MODE), JAC = spmv_jac(MODE);
+  const double xs = SC ? *ca.xscale : 1.0;
+  using SH = PairShape<PS>;
+  constexpr int K = SH::K, NR = SH::NR, C = SH::CENTER_RUN, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
+  constexpr int JC = SH::first(SH::CENTER_RUN) + 1;   // the diagonal slot
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[LAST];
+  const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
+  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
+  auto scl = [&](dbl2 v) __attribute__((always_inline)) { return SC ? dbl2{xs * v.x, xs * v.y} : v; };
+  const u32x4 *__restrict__ cd = reinterpret_cast<const u32x4 *>(ca.pcode) + lane;
+  double dot = 0.0;
+  const int ntask = (se - sb) * a.P;
+  for (int t = w; t < ntask; t += W) {
+    const int seg = sb + t / a.P, col = t % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;
+    dbl2 zm = scl(bload2(xr, z0 * D + cb - D)), c = scl(bload2(xr, z0 * D + cb));
+    uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
+    auto step = [&](int z, auto nq) __attribute__((always_inline)) {
+      constexpr int NQ = decltype(nq)::value;
+      dbl2 L[NQ][NR], zp[NQ];
+      double e[NQ];
+      u32x4 cw[NQ];
+      uint32_t bw[NQ];
+      bw[0] = bwn;
+#pragma unroll
+      for (int q = 1; q < NQ; ++q) bw[q] = (uint32_t)pblk[(z + q) * a.P + col];
+      if (z + NQ < z1) bwn = (uint32_t)pblk[(z + NQ) * a.P + col];   // next step's, ahead
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
+        zp[q] = bload2(xr, r0 + D);
+#pragma unroll
+        for (int r = 1; r < LAST; ++r)
+          if (r != TR) L[q][r] = bload2(xr, r0 + a.anchor[r] + ((bw[q] & (PBLK_RUN0 << r)) ? PAIR_OOR : 0));
+        const int eo = ecst + (lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0));
+        e[q] = bload1(xr, ub + eo);
+        cw[q] = cd[(size_t)(bw[q] & PBLK_ID) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        zp[q] = scl(zp[q]);
+#pragma unroll
+        for (int r = 1; r < LAST; ++r)
+          if (r != TR) L[q][r] = scl(L[q][r]);
+        if constexpr (SC) e[q] = xs * e[q];
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        L[q][0] = q == 0 ? zm : q == 1 ? c : zp[q - 2];
+        L[q][TR] = q == 0 ? c : zp[q - 1];
+        L[q][LAST] = zp[q];
+        if (bw[q] & CARRY) {                       // wave-uniform, rare: an empty carried run
+          if (bw[q] & PBLK_RUN0) L[q][0] = dbl2{0.0, 0.0};
+          if (bw[q] & (PBLK_RUN0 << TR)) L[q][TR] = dbl2{0.0, 0.0};
+          if (bw[q] & (PBLK_RUN0 << LAST)) L[q][LAST] = dbl2{0.0, 0.0};
+        }
+        auto code = [&](int i) -> int { return (int)((cw[q][i >> 2] >> (8 * (i & 3))) & 0xffu); };
+        const int r0 = (z + q) * D + cb;
+        double s0v = 0.0, s1v = 0.0, lo = 0.0, hi = 0.0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int r = SH::run(j), p = SH::pos(j);
+          if (SH::tri(r) && p < 0) {
+            lo = wave_shift<true>(L[q][r].y, e[q]);
+            hi = wave_shift<false>(L[q][r].x, e[q]);
+          }
+          double a0, a1;
+          if (!SH::tri(r)) { a0 = L[q][r].x; a1 = L[q][r].y; }
+          else if (p < 0) { a0 = lo; a1 = L[q][r].x; }
+          else if (p == 0) { a0 = L[q][r].x; a1 = L[q][r].y; }
+          else { a0 = L[q][r].y; a1 = hi; }
+          s0v = s0v + vtab[code(j)] * a0;
+          s1v = s1v + vtab[code(K + j)] * a1;
+        }
+        // SPLIT: rows with A_o entries store their diagonal-block sum; the
+        // boundary kernel continues them and applies the epilogue
+        const bool gh = SPLIT && (bw[q] & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+        double o0 = s0v, o1 = s1v;
+        if constexpr (JAC) {
+          if (!gh) {
+            if constexpr (DT) { o0 = s0v * dtab[code(JC)]; o1 = s1v * dtab[code(K + JC)]; }
+            else { o0 = papply(ca.jac, s0v, r0); o1 = papply(ca.jac, s1v, r0 + 1); }
+          }
+        }
+        *reinterpret_cast<dbl2 *>(y + r0) = dbl2{o0, o1};
+        if constexpr (MODE == SPMV_DOT) {
           if (!gh) {
             dot += L[q][C].x * s0v;
             dot += L[q][C].y * s1v;
@@ -907,9 +1080,70 @@ static int pair_f64_launch(Mat *A, int mode, bool split, const double *x, double
 // Launch the lean MatMult for this product; returns its grid, or 0 when it
 // does not apply (the general kernel then runs).  A fold (fold.cnt set)
 // counts this launch's workgroups.
-int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials, const int *done,
-                     const Fold &fold_in, hipStream_t st) {
+// the coded z-march (spmv_pair_zmc_kernel) applies: 5 / 7-point row pairs
+// from a non-uniform, select-free code dictionary, z-march geometry
+bool pair_code_applies(const Mat *A) {
   const Sell &S = A->sd;
+  if (!g_knobs.pair_zmc || !g_knobs.pair_zm || !g_knobs.vcodes || !g_knobs.spmv_pairs || g_knobs.spmv_ynt ||
+      g_knobs.spmv_rev || !S.pair_code_clean || S.ntab <= 0 || S.puni.p || S.pair_blocks <= 0 || !S.pair_all ||
+      (S.pair_shape != 5 && S.pair_shape != 7) || !S.pcode.p || !S.vtab.p)
+    return false;
+  if (A->m % 128 != 0 || A->m > PAIR_CLEAN_MAX_ROWS || A->n > PAIR_CLEAN_MAX_ROWS || S.nunits * 128 != A->m) return false;
+  int anchor[5];
+  pair_anchors(S, anchor);
+  return zm_plane(A, S.pair_shape, anchor) > 0;
+}
+
+static int pair_code_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials,
+                            const int *done, const Fold &fold_in, const Jac &jac, const double *xscale,
+                            hipStream_t st) {
+  const Sell &S = A->sd;
+  PairLeanArgs a{};
+  a.m = (int)A->m;
+  a.n = (int)A->n;
+  a.nunits = (int)S.nunits;
+  pair_anchors(S, a.anchor);
+  const int D = zm_plane(A, S.pair_shape, a.anchor);
+  a.P = D / 128;
+  a.NZ = (int)(A->m / D);
+  const int grid = zm_tasks(a.P, a.NZ, a.L, a.S);
+  a.partials = partials;
+  a.done = done;
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  a.fold = fold;
+  // Jacobi by diagonal code: the operator's own vector Jacobi (knob 37)
+  const bool dt = spmv_jac(mode) && jac.mode == 1 && jac.d == A->jac_dinv.p && S.dtab.p && g_knobs.pair_dtab;
+  const PairCodeArgs ca{S.pcode.p, S.vtab.p, S.dtab.p, xscale, jac};
+  using F = void (*)(PairLeanArgs, const double *, double *, const int32_t *, PairCodeArgs);
+  F f = nullptr;
+  const bool z2 = g_knobs.pair_zm_units == 2;
+#define ZMC_U(MODE, PS, SP, DTV) f = z2 ? &spmv_pair_zmc_kernel<MODE, PS, SP, 2, DTV> : &spmv_pair_zmc_kernel<MODE, PS, SP, 1, DTV>
+#define ZMC_S(MODE, PS, DTV) do { if (split) ZMC_U(MODE, PS, true, DTV); else ZMC_U(MODE, PS, false, DTV); } while (0)
+#define ZMC_P(MODE, DTV) do { if (S.pair_shape == 5) ZMC_S(MODE, 5, DTV); else ZMC_S(MODE, 7, DTV); } while (0)
+  switch (mode) {
+    case SPMV_PLAIN: ZMC_P(SPMV_PLAIN, false); break;
+    case SPMV_DOT: ZMC_P(SPMV_DOT, false); break;
+    case SPMV_PLAIN_S: ZMC_P(SPMV_PLAIN_S, false); break;
+    case SPMV_JACOBI: if (dt) ZMC_P(SPMV_JACOBI, true); else ZMC_P(SPMV_JACOBI, false); break;
+    case SPMV_JACOBI_S: if (dt) ZMC_P(SPMV_JACOBI_S, true); else ZMC_P(SPMV_JACOBI_S, false); break;
+    default: return 0;
+  }
+#undef ZMC_P
+#undef ZMC_S
+#undef ZMC_U
+  note_dispatch(split ? DSP_PAIR_ZMC_SPLIT : DSP_PAIR_ZMC);
+  launch_timed(f, grid, st, a, x, y, S.pblk.p, ca);
+  HIPCHECK(hipGetLastError());
+  return grid;
+}
+
+int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials, const int *done,
+                     const Fold &fold_in, hipStream_t st, const Jac &jac, const double *xscale) {
+  const Sell &S = A->sd;
+  if (pair_code_applies(A) && (split || (A->nghost == 0 && !S.pair_ghosts)))
+    return pair_code_launch(A, mode, split, x, y, partials, done, fold_in, jac, xscale, st);
+  if (xscale) return 0;
   if (mode != SPMV_PLAIN && mode != SPMV_DOT && mode != SPMV_PW) return 0;
   if (mode == SPMV_PW && !pair_cg5_applies(A, 0)) return 0;   // CG mode 5's p.Ap pass: the 5/7-point z-march
   if (pair_f64_kind(A) && (split || A->nghost == 0))   // without a split, A_o continues in the general kernel
@@ -947,9 +1181,11 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
     F27 f = nullptr;
     const int form = !clean ? 0 : S.pcol27.p ? 2 : 1;
     const bool z2 = g_knobs.pair_zm27_units == 2;
+    const bool uv = form == 2 && S.pair_unit27 && g_knobs.pair_unitv && !z2;   // one plane per step only
 #define Z27U(MODE, SP, FM) f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, FM, 2> : &spmv_pair_zm27_kernel<MODE, SP, FM, 1>
-#define Z27(MODE, SP) do { if (form == 2) Z27U(MODE, SP, 2); else if (form == 1) Z27U(MODE, SP, 1); \
-                           else Z27U(MODE, SP, 0); } while (0)
+#define Z27(MODE, SP) do { if (form == 2) { if (uv) f = &spmv_pair_zm27_kernel<MODE, SP, 2, 1, true>; \
+                                            else Z27U(MODE, SP, 2); } \
+                           else if (form == 1) Z27U(MODE, SP, 1); else Z27U(MODE, SP, 0); } while (0)
     if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
     else { if (split) Z27(SPMV_DOT, true); else Z27(SPMV_DOT, false); }
 #undef Z27

@@ -51,7 +51,8 @@ class MatInfo(C.Structure):
                 ("value_codes", C.c_int64), ("code_bytes", C.c_int64), ("pair_shape", C.c_int64),
                 ("pair_units", C.c_int64), ("pair_blocks", C.c_int64), ("pair_block_bytes", C.c_int64),
                 ("pair_uniform", C.c_int64), ("pair_lean", C.c_int64),
-                ("pair_zmarch", C.c_int64), ("pair_f64", C.c_int64), ("pair_form27", C.c_int64)]
+                ("pair_zmarch", C.c_int64), ("pair_f64", C.c_int64), ("pair_form27", C.c_int64),
+                ("pair_code", C.c_int64)]
 
 
 P = C.c_void_p

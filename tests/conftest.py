@@ -15,6 +15,42 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
 
 
+_HEARTBEAT_S = float(os.environ.get("MX_TEST_HEARTBEAT_S", "60"))
+
+
+@pytest.hookimpl(hookwrapper=True)
+def pytest_runtest_call(item):
+    """A test running longer than a minute (the full-size oracle parity runs:
+    C2's 7,723 oracle iterations take 2-3 min) prints a line to stderr every
+    MX_TEST_HEARTBEAT_S seconds, so a runner that takes a silent process for a
+    hung one sees progress."""
+    import threading
+    import time
+    done = threading.Event()
+
+    capman = item.config.pluginmanager.getplugin("capturemanager")
+
+    def beat():
+        t0 = time.time()
+        while not done.wait(_HEARTBEAT_S):
+            msg = f"[still running {item.nodeid}: {time.time() - t0:.0f} s]\n"
+            if capman is not None:       # past the output capture, to the real stderr
+                with capman.global_and_fixture_disabled():
+                    sys.stderr.write(msg)
+                    sys.stderr.flush()
+            else:
+                sys.stderr.write(msg)
+                sys.stderr.flush()
+
+    th = threading.Thread(target=beat, daemon=True)
+    if _HEARTBEAT_S > 0:
+        th.start()
+    try:
+        yield
+    finally:
+        done.set()
+
+
 def pytest_collection_modifyitems(config, items):
     import torch
     if torch.cuda.is_available():

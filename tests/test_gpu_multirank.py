@@ -709,3 +709,47 @@ def test_distributed_mode5(oracle_mod, P, kind, n, applies):
         assert dc["pair_zm_split"] == 0 and dc["sell"] == 0, dc
     else:
         assert all(r[3] == 2 for r in res) and dc["zm_pw"] == 0 and dc["zm_rupd"] == 0, dc
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_distributed_code_zmarch(oracle_mod, P):
+    """BASELINE C4's operator (conv-diff, non-uniform code dictionary) on P
+    ranks: the coded z-march on every rank with the ghost units split off to
+    the boundary kernel (the dispatch counts show the SPLIT kernel ran):
+    MatMult bit-exact, GMRES(30) + Jacobi against the oracle's P-rank model."""
+    from mxsolve.core import DMat, dispatch_counts
+    from _hostinfo import host_threads
+    ip, c, v = oracle_mod.stencil("convdiff3d", 128)
+    M = ip.size - 1
+    rng = np.random.default_rng(43)
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+    ranges = oracle_mod.split_ownership(M, P)
+    x = rng.standard_normal(M)
+    y_ref = O.mult(x)
+    bvec = rng.random(M)
+    o = O.solve(bvec, ksp="gmres", rtol=1e-8, max_it=400, nthreads=host_threads())
+
+    def body(comm):
+        r = comm.rank
+        lip, lc, lv = local_csr(ip, c, v, ranges[r], ranges[r + 1])
+        A = DMat.from_csr(comm, M, M, lip, lc, lv)
+        info = A.info()
+        xl = torch.from_numpy(x[ranges[r]:ranges[r + 1]].copy()).cuda()
+        yl = torch.zeros(ranges[r + 1] - ranges[r], dtype=torch.float64, device="cuda")
+        A.mult(xl, yl)
+        bl = torch.from_numpy(bvec[ranges[r]:ranges[r + 1]].copy()).cuda()
+        xs = torch.zeros_like(bl)
+        rs = A.solve(bl, xs, ksp="gmres", rtol=1e-8, max_it=400)
+        out = (info["pair_code"], yl.cpu().numpy(), rs["its"], rs["reason"], xs.cpu().numpy())
+        A.destroy()
+        return out
+
+    dispatch_counts(reset=True)
+    res = run_ranks(P, body)
+    dc = dispatch_counts(reset=True)
+    assert all(r[0] == 1 for r in res)
+    assert dc["pair_zmc_split"] >= P * (res[0][2] + 1) and dc["boundary"] >= P, dc
+    assert np.array_equal(np.concatenate([r[1] for r in res]).view(np.uint64), y_ref.view(np.uint64))
+    assert all(r[3] == o["reason"] and abs(r[2] - o["its"]) <= 1 for r in res), ([r[2:4] for r in res], o["its"])
+    xs = np.concatenate([r[4] for r in res])
+    assert np.linalg.norm(xs - o["x"]) <= REL_TOL * np.linalg.norm(o["x"])

@@ -329,9 +329,10 @@ def _with_knobs(L, kv, fn):
 # CU, segments of up to 32 planes), the sweep form (39 = 0), one plane per
 # step (42 = 1), short / odd segments with tails (41), other grids (40)
 # -- and for the 27-point z-march: its per-run-branch body instead of the
-# column-zeroed one (48 = 0), two planes per step (49 = 2), other grids (45)
+# column-zeroed one (48 = 0), two planes per step (49 = 2), other grids (45),
+# multiply-and-add for the -1 slots instead of their exact-product fma (53 = 0)
 LEAN_FORMS = [{}, {39: 0}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}, {40: 2},
-              {48: 0}, {49: 2, 45: 3}, {48: 0, 49: 2, 41: 5}]
+              {48: 0}, {49: 2, 45: 3}, {48: 0, 49: 2, 41: 5}, {53: 0}]
 
 
 @pytest.mark.parametrize("form", range(len(LEAN_FORMS)))
@@ -463,3 +464,95 @@ def test_pair_f64_zmarch(selfcomm, oracle_mod, kind, n, f64):
     o = O.solve(b, ksp="cg", rtol=1e-8)
     assert r["reason"] == o["reason"] and abs(r["its"] - o["its"]) <= 1
     assert np.linalg.norm(xs.cpu().numpy() - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
+
+
+def _periodic_2d(oracle_mod, n):
+    """2D 5-point operator with row scales of period 4 in x (four distinct row
+    factors): a code dictionary that is not uniform per slot-row (a slot's
+    value differs between lanes), nonsymmetric."""
+    ip, c, v = oracle_mod.stencil("poisson2d", n)
+    M = ip.size - 1
+    f = np.array([1.0, 1.25, 1.5, 2.0])[np.arange(M) % n % 4]
+    rows = np.repeat(np.arange(M), np.diff(ip))
+    return ip, c, v * f[rows]
+
+
+ZMC_FORMS = [{}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}]
+
+
+@pytest.mark.parametrize("form", range(len(ZMC_FORMS)))
+@pytest.mark.parametrize("kind,n,applies", [("convdiff3d", 128, 1), ("periodic2d", 256, 1), ("convdiff3d", 64, 0)])
+def test_pair_code_zmarch(selfcomm, oracle_mod, kind, n, applies, form):
+    """Coded z-march MatMult (spmv_pair_zmc_kernel, knob 52 = 1, the default)
+    for 5/7-point code dictionaries that are not uniform per slot-row --
+    BASELINE C4's convection-diffusion operator (kappa of period 4 in x) and a
+    periodic-coefficient 2D operator: bit-exact against the oracle and against
+    the general SELL kernel (knob 52 = 0), operands with infinities and NaN
+    included, in every z-march form.  x-lines of 64 rows (not select-free)
+    keep the general kernel (mx_mat_info.pair_code = 0)."""
+    from mxsolve.core import DMat, dispatch_counts
+    ip, c, v = _periodic_2d(oracle_mod, n) if kind == "periodic2d" else oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    L = lib()
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    rng = np.random.default_rng(37)
+    for special in (False, True):
+        x = rng.standard_normal(M)
+        if special:
+            x[rng.integers(0, M, 40)] = np.inf
+            x[rng.integers(0, M, 40)] = -np.inf
+            x[rng.integers(0, M, 40)] = np.nan
+        exp = O.mult(x).view(np.uint64)
+        outs = []
+        for knob in (1, 0):
+            def run():
+                A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+                y = torch.zeros(M, dtype=torch.float64, device="cuda")
+                dispatch_counts(reset=True)
+                A.mult(torch.from_numpy(x).cuda(), y)
+                dc = dispatch_counts(reset=True)
+                info = A.info()
+                A.destroy()
+                return info, y.cpu().numpy().view(np.uint64), dc
+            outs.append(_with_knobs(L, {52: knob, **ZMC_FORMS[form]}, run))
+        (i1, g1, d1), (i0, g0, d0) = outs
+        assert i1["pair_uniform"] == 0 and i1["pair_code"] == applies and i0["pair_code"] == 0
+        assert d1["pair_zmc"] == applies and d0["pair_zmc"] == 0
+        assert np.array_equal(g1, exp) and np.array_equal(g0, exp)
+
+
+@pytest.mark.parametrize("kind,n,pc", [("convdiff3d", 128, "jacobi"), ("periodic2d", 256, "none"),
+                                       ("periodic2d", 512, "jacobi")])
+def test_pair_code_zmarch_gmres(selfcomm, oracle_mod, kind, n, pc):
+    """GMRES(30) on the coded z-march: its MatMult forms the operand fl(s x)
+    of the unnormalised basis vector and applies Jacobi by the diagonal code
+    (JACOBI_S) or nothing (PLAIN_S).  The same per-row sums as the general
+    kernel, so the whole solve -- iterations, history, solution -- is bitwise
+    that of knob 52 = 0; both against the oracle."""
+    from mxsolve.core import DMat, dispatch_counts
+    ip, c, v = _periodic_2d(oracle_mod, n) if kind == "periodic2d" else oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    L = lib()
+    b = np.random.default_rng(41).random(M)
+
+    def run():
+        A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+        bt = torch.from_numpy(b).cuda()
+        x = torch.zeros(M, dtype=torch.float64, device="cuda")
+        dispatch_counts(reset=True)
+        r = A.solve(bt, x, ksp="gmres", pc=pc, rtol=1e-8, max_it=400, history=True)
+        dc = dispatch_counts(reset=True)
+        A.destroy()
+        return r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy(), dc
+
+    on = run()
+    off = _with_knob(L, 52, 0, run)
+    assert on[4]["pair_zmc"] >= on[0] and off[4]["pair_zmc"] == 0
+    assert on[:2] == off[:2]
+    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
+    assert np.array_equal(on[3].view(np.uint64), off[3].view(np.uint64))
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    from _hostinfo import host_threads
+    o = O.solve(b, ksp="gmres", pc=pc, rtol=1e-8, max_it=400, nthreads=host_threads())
+    assert on[1] == o["reason"] and abs(on[0] - o["its"]) <= 1
+    assert np.linalg.norm(on[3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])

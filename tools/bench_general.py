@@ -127,7 +127,8 @@ def gather_bytes(info) -> int:
 
 def leg(comm, name, A, ksp, rtol=1e-5, max_it=10000, asm_s=None, jac_vec=False):
     """jac_vec: the GMRES MatMult applies a non-uniform Jacobi diagonal to its
-    output (SPMV_JACOBI_S), reading the dinv vector: + 8 B per row."""
+    output (SPMV_JACOBI_S), reading the dinv vector: + 8 B per row (not on
+    value-coded row pairs, whose dinv comes from the per-code table)."""
     info = A.info()
     m, nnz = info["m"], info["nnz_d"] + info["nnz_o"]
     b = comm.empty(m)
@@ -145,6 +146,10 @@ def leg(comm, name, A, ksp, rtol=1e-5, max_it=10000, asm_s=None, jac_vec=False):
     spmv_ms = rp["spmv_ms"] / max(rp["spmv_count"], 1)
     y = comm.empty(m)
     alone_ms, _ = A.bench_mult(b, y, 30)
+    # row-pair layouts with value codes apply Jacobi from the per-code dinv
+    # table (dtab, knob 37): no dinv vector is read
+    if info.get("value_codes") and info.get("pair_shape"):
+        jac_vec = False
     sb = streamed_bytes(info) + (8 * m if jac_vec else 0)
     csr = 12 * nnz + 4 * (m + 1) + 16 * m
     rec = {"leg": name, "rows": m, "nnz": nnz, "ksp": ksp, "value_codes": info["value_codes"],
@@ -152,6 +157,8 @@ def leg(comm, name, A, ksp, rtol=1e-5, max_it=10000, asm_s=None, jac_vec=False):
            "assembly_s": None if asm_s is None else round(asm_s, 3),
            "its": r["its"], "reason": r["reason"], "solve_s": round(ts, 4), "its_per_s": round(r["its"] / ts, 1),
            "spmv_in_solve_ms": round(spmv_ms, 5), "spmv_standalone_ms": round(alone_ms, 5),
+           "spmv_kernel": ("pair_zmc" if info.get("pair_code") else "pair_zmf64" if info.get("pair_f64")
+                           else "pair_lean" if info.get("pair_lean") else "sell"),
            "roofline": {"bound": "hbm", "peak": PEAK, "unit": "GB/s",
                         "streamed_bytes": sb, "achieved": round(sb / spmv_ms / 1e6, 1),
                         "frac": round(sb / spmv_ms / 1e6 / PEAK, 4),

@@ -1,14 +1,18 @@
 #!/usr/bin/env python3
 """GMRES(30)+Jacobi on conv-diff 256^3 (config C4) for a fixed number of
 iterations: a kernel-trace source for the GMRES inner step.
-    python tools/gmres_trace.py [n] [its]"""
+    python tools/gmres_trace.py [n] [its] [knob=value+...]"""
 import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-petsc4py-example_amd"))
 import torch  # noqa: E402
+from mxsolve import _lib  # noqa: E402
 from mxsolve.core import DeviceComm, DMat, rhs_hash  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 its = int(sys.argv[2]) if len(sys.argv) > 2 else 60
+for kv in (sys.argv[3].split("+") if len(sys.argv) > 3 else []):
+    k, v = kv.split("=")
+    _lib.load().mx_debug_set(int(k), int(v))
 comm = DeviceComm.self_comm(0)
 A = DMat.stencil(comm, "convdiff3d", n)
 m = A.info()["m"]

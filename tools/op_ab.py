@@ -2,7 +2,7 @@
 """Operators assembled under different knob settings (e.g. format choices read
 at assembly), side by side in one process: interleaved CG and standalone
 MatMult timing, products checked bitwise equal.
-    python tools/op_ab.py kind n rounds "19=1" "19=0" ..."""
+    python tools/op_ab.py kind n rounds "19=1" "19=0" ...   (n: an edge, or NXxNYxNZ)"""
 import json, os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-petsc4py-example_amd"))
 import numpy as np, torch  # noqa: E401,E402
@@ -10,7 +10,8 @@ from mxsolve import _lib  # noqa: E402
 from mxsolve.core import DeviceComm, DMat, rhs_hash  # noqa: E402
 
 L = _lib.load()
-kind, n, rounds = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+kind, n, rounds = sys.argv[1], sys.argv[2], int(sys.argv[3])
+dims = [int(t) for t in n.split("x")]
 variants = sys.argv[4:]
 comm = DeviceComm.self_comm(0)
 
@@ -26,7 +27,7 @@ def setv(v):
 ops = {}
 for v in variants:
     old = setv(v)
-    A = DMat.stencil(comm, kind, n)
+    A = DMat.stencil(comm, kind, *dims)
     m = A.info()["m"]
     b = comm.empty(m); rhs_hash(comm, 0, b); x = comm.zeros(m); y = comm.empty(m)
     A.solve(b, x, ksp="cg", rtol=0.0, max_it=20)
