@@ -339,8 +339,11 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 50: GMRES MDot in one pass over w for <= 32 basis vectors (2, default: a
  *         workgroup holds 2048 rows of w in registers and walks the vectors;
  *         1: the four waves of a workgroup split the vectors; 0: groups of key 16)
- * key 51: GMRES MAXPY + norm pass in chunks (1, default: 2048 rows per
- *         workgroup step, 16-byte pairs; 0: one row per thread)
+ * key 51: GMRES MAXPY + norm pass in chunks (1: 2048 rows per workgroup
+ *         step, 16-byte pairs; 0, default: one row per thread -- measured
+ *         0.5% faster per GMRES(30) step beside the chunk MDot)
+ * key 54: GMRES basis stride padding in rows (multiple of 32; default 256:
+ *         2 KB between the vectors' rows, -1.8% per GMRES(30) step at 256^3)
  * key 52: coded z-march MatMult for 5/7-point code dictionaries that are not
  *         uniform per slot (1, default; 0: the general SELL kernel)
  * key 53: z-march terms of slots whose value is -1, 0 or +1 formed by fma (an

@@ -832,10 +832,12 @@ __global__ void __launch_bounds__(256) mdot_split_kernel(int64_t n, const double
 // VecMDot in one pass over w, chunk form (knob 50 = 2, the default; nv <= 32):
 // a workgroup holds 2048 rows of w in registers (WP = 4 16-byte pairs per
 // thread) and walks the basis vectors one after another, reading 16 KB of
-// each contiguously per step, with nv running sums per thread.  On 2^24 rows
-// this streams at 6.7-6.9 TB/s -- the plain read ceiling -- where the split
-// form (several vectors' 1 KB pieces interleaved per wave step) makes 6.0-6.4
-// (tools/mdot_probe.hip).  partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
+// each contiguously per step.  Each vector's chunk sum is reduced across the
+// wave at once and added to lane j's running total (one accumulator register
+// instead of nv: 49 VGPRs).  On 2^24 rows this streams at 7.0-7.1 TB/s, the
+// plain read ceiling, where the split form (several vectors' 1 KB pieces
+// interleaved per wave step) makes 6.0-6.4 (tools/mdot_probe.hip chunk4r).
+// partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
 template <int WP>
 __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
@@ -844,9 +846,8 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
                                                          const int *__restrict__ stop_flag) {
   constexpr int NVX = 32;
   if (*stop_flag) return;
-  double acc[NVX];
-#pragma unroll
-  for (int j = 0; j < NVX; ++j) acc[j] = 0.0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double acc = 0.0;                                // lane j: vector j's running total
   const dbl2 *__restrict__ w2 = reinterpret_cast<const dbl2 *>(w);
   const int64_t n2 = n >> 1, csz = 256 * WP, nfull = n2 / csz;
   auto chunk = [&](int64_t c0, auto fullc) __attribute__((always_inline)) {
@@ -868,31 +869,23 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
           const int64_t i = c0 + k * 256 + threadIdx.x;
           t[k] = (FULL || i < n2) ? __builtin_nontemporal_load(vj + i) : dbl2{0.0, 0.0};
         }
+        double a = 0.0;
 #pragma unroll
         for (int k = 0; k < WP; ++k) {
-          acc[j] += wr[k].x * (sj * t[k].x);
-          acc[j] += wr[k].y * (sj * t[k].y);
+          a += wr[k].x * (sj * t[k].x);
+          a += wr[k].y * (sj * t[k].y);
         }
+        a = wave_sum(a);
+        if (lane == j) acc += a;
       }
     }
   };
   for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
   if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // odd length: the last row
-    const double wl = w[n - 1];
-#pragma unroll
-    for (int j = 0; j < NVX; ++j)   // compile-time indices: acc stays in registers
-      if (j < nv) acc[j] += wl * (vscale[j] * V[(int64_t)j * ldv + n - 1]);
-  }
+  if ((n & 1) && blockIdx.x == 0 && wid == 0 && lane < nv)   // odd length: the last row, lane j's term
+    acc += w[n - 1] * (vscale[lane] * V[(int64_t)lane * ldv + n - 1]);
   __shared__ double sh[NVX][4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < NVX; ++j) {
-    if (j < nv) {
-      const double s = wave_sum(acc[j]);
-      if (lane == 0) sh[j][wid] = s;
-    }
-  }
+  if (lane < nv) sh[lane][wid] = acc;
   __syncthreads();
   if ((int)threadIdx.x < nv)
     partials[(size_t)threadIdx.x * gridDim.x + blockIdx.x] =
@@ -1689,7 +1682,9 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   const int max_k = p.restart > 0 ? p.restart : 30;
   if (max_k > MAX_RESTART) fail(MX_ERR_UNSUPPORTED, "GMRES restart above 1000");
   const int ld = max_k + 2;
-  const int64_t ldv = (std::max<int64_t>(n, 1) + 31) / 32 * 32;
+  // basis stride: n rounded up to 32 rows, plus knob 54's extra rows (the
+  // vectors' relative placement in HBM: an A/B lever for the MDot / MAXPY)
+  const int64_t ldv = (std::max<int64_t>(n, 1) + 31) / 32 * 32 + std::max(0, g_knobs.gm_pad) / 32 * 32;
   const size_t nV = (size_t)ldv * (max_k + 1), nh = (size_t)ld * (max_k + 1);
   const size_t prow = std::max<size_t>((size_t)max_k + 2, ((size_t)max_k + 1 + 31) / 32 * 32);   // MDot groups of 32
   const size_t npart = (size_t)RED_BLOCKS * prow + (size_t)spmv_blocks(A) + 128;

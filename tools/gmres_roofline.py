@@ -35,15 +35,18 @@ maxpy_b = sum(8 * m * (j + 3) for j in steps)
 spmv_b = len(steps) * (16 * m + 4 * (m // 128))
 
 
-def total(prefix, lo=20.0):      # working launches (the no-ops after a stop are shorter)
-    return sum(t for k, v in d.items() if k.startswith(prefix) for t in v if t >= lo)
+def total(prefixes, lo=20.0):    # working launches (the no-ops after a stop are shorter)
+    return sum(t for k, v in d.items() if k.startswith(prefixes) for t in v if t >= lo)
 
 
 share = 1.0
 out = {}
-for name, prefix, b in (("MDot (mdot_kernel<NV>)", "mdot_kernel", mdot_b),
-                        ("MAXPY+norm (maxpy_norm_kernel)", "maxpy_norm_kernel", maxpy_b),
-                        ("MatMult (spmv_sell_kernel<5,...>, Jacobi)", "spmv_sell_kernel<5,", spmv_b)):
+# MDot: mdot_kernel<NV> groups, mdot_split_kernel, mdot_chunk_kernel (knob 50);
+# MatMult: the coded z-march (knob 52) or the general kernel, JACOBI_S (mode 5)
+for name, prefix, b in (("MDot (mdot_*_kernel)", ("mdot_",), mdot_b),
+                        ("MAXPY+norm (maxpy_norm_kernel)", ("maxpy_norm_kernel",), maxpy_b),
+                        ("MatMult (JACOBI_S: spmv_pair_zmc_kernel / spmv_sell_kernel)",
+                         ("spmv_pair_zmc_kernel<5,", "spmv_sell_kernel<5,"), spmv_b)):
     t_us = total(prefix) * share
     out[name] = {"alg_bytes": b, "time_us": round(t_us, 1), "TBps": round(b / t_us / 1e6, 3),
                  "frac_of_8TBps": round(b / t_us / 1e6 / 8.0, 3)}

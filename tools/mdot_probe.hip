@@ -123,6 +123,64 @@ __global__ void __launch_bounds__(256) chunk_kernel(int64_t n, const double *__r
 }
 
 
+// chunk with the basis scale applied on read (the product's form: acc +=
+// w (s_j v)); RED: per-chunk wave sums, vector j's total kept in lane j
+// (one accumulator register instead of nv)
+template <int WP, bool RED>
+__global__ void __launch_bounds__(256) chunks_kernel(int64_t n, const double *__restrict__ w, const double *__restrict__ V,
+                                                     int64_t ldv, int nv, const double *__restrict__ vs,
+                                                     double *__restrict__ partials) {
+  double acc[RED ? 1 : NVMAX];
+#pragma unroll
+  for (int j = 0; j < (RED ? 1 : NVMAX); ++j) acc[j] = 0.0;
+  const int lane = threadIdx.x & 63;
+  const dbl2 *__restrict__ w2 = reinterpret_cast<const dbl2 *>(w);
+  const int64_t n2 = n >> 1, csz = 256 * WP;
+  for (int64_t c0 = blockIdx.x * csz; c0 < n2; c0 += (int64_t)gridDim.x * csz) {
+    dbl2 wr[WP];
+#pragma unroll
+    for (int k = 0; k < WP; ++k) wr[k] = w2[c0 + k * 256 + threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < NVMAX; ++j) {
+      if (j < nv) {
+        const double sj = vs[j];
+        const dbl2 *__restrict__ vj = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv) + c0 + threadIdx.x;
+        dbl2 t[WP];
+#pragma unroll
+        for (int k = 0; k < WP; ++k) t[k] = __builtin_nontemporal_load(vj + k * 256);
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+          a += wr[k].x * (sj * t[k].x);
+          a += wr[k].y * (sj * t[k].y);
+        }
+        if constexpr (RED) {
+          a = wave_sum(a);
+          if (lane == j) acc[0] += a;
+        } else {
+          acc[j] += a;
+        }
+      }
+    }
+  }
+  __shared__ double sh[NVMAX][4];
+  const int wid = threadIdx.x >> 6;
+  if constexpr (RED) {
+    if (lane < nv) sh[lane][wid] = acc[0];
+  } else {
+#pragma unroll
+    for (int j = 0; j < NVMAX; ++j) {
+      if (j < nv) {
+        const double s = wave_sum(acc[j]);
+        if (lane == 0) sh[j][wid] = s;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) partials[(size_t)threadIdx.x * gridDim.x + blockIdx.x] =
+      (sh[threadIdx.x][0] + sh[threadIdx.x][1]) + (sh[threadIdx.x][2] + sh[threadIdx.x][3]);
+}
+
 // VecMAXPY + ||w||^2 (GMRES's maxpy_norm_kernel body): w -= sum_j a_j v_j in
 // VecMAXPY_Seq's grouping (first nv % 4 vectors, then groups of four)
 __global__ void __launch_bounds__(256) maxpy_row_kernel(int64_t n, double *__restrict__ w, const double *__restrict__ V,
@@ -255,10 +313,15 @@ int main(int argc, char **argv) {
         default: split_kernel<8, U2><<<grid, 256>>>(N, w, V, ldv, nv, part); break;                       \
       }                                                                                                  \
     }
-    rep("split", time_it(SPLIT(1), reps));
-    rep("split2", time_it(SPLIT(2), reps));
+    if (argc > 2) {
+      rep("split", time_it(SPLIT(1), reps));
+      rep("split2", time_it(SPLIT(2), reps));
+    }
     rep("chunk4", time_it([&] { chunk_kernel<4><<<grid, 256>>>(N, w, V, ldv, nv, part); }, reps));
     rep("chunk2", time_it([&] { chunk_kernel<2><<<grid, 256>>>(N, w, V, ldv, nv, part); }, reps));
+    rep("chunk4s", time_it([&] { chunks_kernel<4, false><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
+    rep("chunk4r", time_it([&] { chunks_kernel<4, true><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
+    rep("chunk8r", time_it([&] { chunks_kernel<8, true><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
     const double mbytes = 8.0 * N * (nv + 2);
     auto repm = [&](const char *name, float ms) {
       printf("{\"variant\": \"%s\", \"nv\": %d, \"grid\": %d, \"us\": %.1f, \"TBps\": %.3f}\n", name, nv, grid, ms * 1e3,
