@@ -370,10 +370,9 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
 //     -1, 0 or +1, so v * a is exact and sum + v * a == fma(v, a, sum) bit for
 //     bit (one rounding either way; an exact product cannot overflow or
 //     underflow): one VALU op instead of two for 26 of the 27 slots.
-template <int MODE, bool SPLIT, int FORM, bool UV = false>
-__device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e)[9], uint32_t bw,
-                                            const PairUni27 *__restrict__ puni, double *__restrict__ y, int r0,
-                                            int lane, double &dot) {
+template <int FORM, bool UV = false>
+__device__ __forceinline__ dbl2 pair_sums27(const dbl2 (&L)[9], const double (&e)[9], uint32_t bw,
+                                            const PairUni27 *__restrict__ puni, int lane) {
   constexpr int K = 27;
   const PairUni27 &B = puni[bw & PBLK_ID];                // wave-uniform: scalar loads
   uint32_t fl = 0;
@@ -417,14 +416,7 @@ __device__ __forceinline__ void pair_unit27(const dbl2 (&L)[9], const double (&e
       }
     }
   }
-  *reinterpret_cast<dbl2 *>(y + r0) = dbl2{s0v, s1v};
-  if constexpr (MODE == SPMV_DOT) {
-    const bool gh = SPLIT && (bw & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
-    if (!gh) {
-      dot += L[4].x * s0v;
-      dot += L[4].y * s1v;
-    }
-  }
+  return dbl2{s0v, s1v};
 }
 
 struct PairLean27Args {
@@ -438,13 +430,36 @@ struct PairLean27Args {
 // The column-word form keeps 6 waves per SIMD (<= 80 VGPRs; the VALU-bound
 // body measured fastest there, knob 45); the fma form (UV) otherwise
 // allocates 86-105 (one plane per step; two would spill at that bound).
-template <int MODE, bool SPLIT, int FORM, int ZU, bool UV = false>
+// CG mode 5 on the 27-point operator (one rank, no ghost units): SPMV_PW
+// (the p.Ap partials, nothing stored) and SPMV_RUPD (alpha from the PW
+// partials, A p recomputed, r = r - alpha A p, z = c r and the three norms),
+// as spmv_pair_zm_kernel's (the same sums as the MatMult's, bit for bit).
+template <int MODE, bool SPLIT, int FORM, int ZU, bool UV = false, int JM = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UV && ZU == 1 ? 6 : 1)))
 spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
                                                              double *__restrict__ y, const int32_t *__restrict__ pblk,
                                                              const PairUni27 *__restrict__ puni,
-                                                             const int32_t *__restrict__ pcol) {
-  if (a.done && *a.done) return;   // wave-uniform: solver finished
+                                                             const int32_t *__restrict__ pcol, const PairRuArgs ru) {
+  constexpr bool RU = MODE == SPMV_RUPD;
+  static_assert(!SPLIT || (MODE != SPMV_PW && !RU), "27-point mode 5: one rank");
+  double alpha = 0.0;
+  const double *rin = nullptr;
+  if constexpr (RU) {
+    KspState *s = ru.s;
+    if (s->top.done) {
+      if (ru.hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(ru.hw + HW_DONE, 1);
+      return;
+    }
+    const double pw = ru.ndot > 0 ? block_sum_array<16>(ru.dot_part, ru.ndot) : s->red1;
+    const CgAlpha al = cg_alpha(s, pw);
+    if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, ru.xb, false, ru.hw);
+    if (al.reason) return;
+    alpha = al.alpha;
+    rin = (ru.r0 && al.i == 0) ? ru.r0 : ru.r;
+  } else {
+    if (a.done && *a.done) return;   // wave-uniform: solver finished
+  }
+  double nv[3] = {0.0, 0.0, 0.0};                  // RU: [z.z, z.r, r.r]
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int sb, se, W, w;
@@ -492,7 +507,7 @@ spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
     uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
     auto step = [&](int z, auto nq) __attribute__((always_inline)) {
       constexpr int NQ = decltype(nq)::value;
-      dbl2 Nw[NQ][3];
+      dbl2 Nw[NQ][3], rq[NQ];
       double Ne[NQ][3];
       uint32_t bw[NQ];
       bw[0] = bwn;
@@ -507,6 +522,7 @@ spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
           Nw[q][k] = bload2(xr, r0 + a.anchor[6 + k] + oor[k]);
           Ne[q][k] = bload1(xr, ub + ebe + a.anchor[6 + k] + oor[k]);
         }
+        if constexpr (RU) rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -517,7 +533,24 @@ spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
         for (int r = 0; r < 6; ++r) { L[r] = C[r]; e[r] = Ce[r]; }
 #pragma unroll
         for (int k = 0; k < 3; ++k) { L[6 + k] = Nw[q][k]; e[6 + k] = Ne[q][k]; }
-        pair_unit27<MODE, SPLIT, FORM, UV>(L, e, bw[q], puni, y, (z + q) * D + cb, lane, dot);
+        const int r0 = (z + q) * D + cb;
+        const dbl2 sv = pair_sums27<FORM, UV>(L, e, bw[q], puni, lane);
+        if constexpr (RU) {
+          const double ra = fma(-alpha, sv.x, rq[q].x), rb = fma(-alpha, sv.y, rq[q].y);
+          const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
+          nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
+          nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
+          *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+        } else {
+          if constexpr (MODE != SPMV_PW) *reinterpret_cast<dbl2 *>(y + r0) = sv;
+          if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
+            const bool gh = SPLIT && (bw[q] & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+            if (!gh) {
+              dot += L[4].x * sv.x;
+              dot += L[4].y * sv.y;
+            }
+          }
+        }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           C[k] = C[3 + k]; Ce[k] = Ce[3 + k];
@@ -529,9 +562,11 @@ spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
     for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
     for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
   }
-  if constexpr (MODE == SPMV_DOT) {
+  if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
     double v[1] = {dot};
     block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  } else if constexpr (RU) {
+    block_partials<3>(nv, a.partials, gridDim.x, a.fold);
   }
 }
 
@@ -1077,6 +1112,64 @@ static int pair_f64_launch(Mat *A, int mode, bool split, const double *x, double
   return grid;
 }
 
+// The 27-point z-march launch: PLAIN / DOT (the MatMult), and CG mode 5's PW
+// and RUPD passes (one rank, column-word form; ru / jm for RUPD)
+static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x, double *y, double *partials,
+                       const int *done, const Fold &fold_in, hipStream_t st, const PairRuArgs &ru, int jm) {
+  const Sell &S = A->sd;
+  PairLean27Args b{};
+  b.n = (int)A->n;
+  for (int r = 0; r < 9; ++r) b.anchor[r] = S.pat_star_off[(size_t)(3 * r + 1)];
+  const int D = b.anchor[7];
+  b.P = D / 128;
+  b.NZ = (int)(A->m / D);
+  // 6 workgroups per CU (knob 45) with one plane per step (knob 49): the
+  // VALU-bound 27-point body at 78-80 VGPRs keeps 6 waves per SIMD (C5's
+  // share, round 3: CG MatMult 63 us median against 68-74 at 3-4 per CU or
+  // two planes per step, profiles/r03_ab.jsonl)
+  int grid = std::max(8, (g_knobs.pair_zm27_bpc > 0 ? g_knobs.pair_zm27_bpc : g_knobs.pair_zm_bpc) * device_cu_count());
+  grid &= ~7;
+  const int W = grid / 8 * LEAN_WAVES;
+  const int slab = (b.NZ + 7) / 8;
+  int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
+  while (L > 1 && (int64_t)b.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
+  b.L = L;
+  b.S = (b.NZ + L - 1) / L;
+  b.partials = partials;
+  b.done = done;
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  b.fold = fold;
+  using F27 = void (*)(PairLean27Args, const double *, double *, const int32_t *, const PairUni27 *,
+                       const int32_t *, PairRuArgs);
+  F27 f = nullptr;
+  const int form = !clean ? 0 : S.pcol27.p ? 2 : 1;
+  const bool z2 = g_knobs.pair_zm27_units == 2;
+  const bool uv = form == 2 && S.pair_unit27 && g_knobs.pair_unitv && !z2;   // one plane per step only
+  if (mode == SPMV_PW || mode == SPMV_RUPD) {      // CG mode 5: form 2, one rank, one plane per step
+    if (form != 2 || split) return 0;
+    if (mode == SPMV_PW) f = uv ? &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, true> : &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, false>;
+    // the residual update without the fma form: with it the kernel holds
+    // 101 VGPRs and spills SGPRs (the same bits either way)
+    else if (jm == 2) f = &spmv_pair_zm27_kernel<SPMV_RUPD, false, 2, 1, false, 2>;
+    else f = &spmv_pair_zm27_kernel<SPMV_RUPD, false, 2, 1, false, 0>;
+    note_dispatch(mode == SPMV_PW ? DSP_ZM_PW : DSP_ZM_RUPD);
+  } else {
+#define Z27U(MODE, SP, FM) f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, FM, 2> : &spmv_pair_zm27_kernel<MODE, SP, FM, 1>
+#define Z27(MODE, SP) do { if (form == 2) { if (uv) f = &spmv_pair_zm27_kernel<MODE, SP, 2, 1, true>; \
+                                            else Z27U(MODE, SP, 2); } \
+                           else if (form == 1) Z27U(MODE, SP, 1); else Z27U(MODE, SP, 0); } while (0)
+    if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
+    else { if (split) Z27(SPMV_DOT, true); else Z27(SPMV_DOT, false); }
+#undef Z27
+#undef Z27U
+    note_dispatch(split ? DSP_PAIR_ZM27_SPLIT : DSP_PAIR_ZM27);
+  }
+  launch_timed(f, grid, st, b, x, y, S.pblk.p, S.puni27.p, S.pcol27.p, ru);
+  HIPCHECK(hipGetLastError());
+  return grid;
+}
+
 // Launch the lean MatMult for this product; returns its grid, or 0 when it
 // does not apply (the general kernel then runs).  A fold (fold.cnt set)
 // counts this launch's workgroups.
@@ -1152,49 +1245,7 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   if (!kind) return 0;
   if (!split && (A->nghost > 0 || S.pair_ghosts)) return 0;   // A_o continues in the general kernel
   const bool clean = kind == 2;
-  if (S.pair_shape == 27) {
-    PairLean27Args b{};
-    b.n = (int)A->n;
-    for (int r = 0; r < 9; ++r) b.anchor[r] = S.pat_star_off[(size_t)(3 * r + 1)];
-    const int D = b.anchor[7];
-    b.P = D / 128;
-    b.NZ = (int)(A->m / D);
-    // 6 workgroups per CU (knob 45) with one plane per step (knob 49): the
-    // VALU-bound 27-point body at 78-80 VGPRs keeps 6 waves per SIMD (C5's
-    // share, round 3: CG MatMult 63 us median against 68-74 at 3-4 per CU or
-    // two planes per step, profiles/r03_ab.jsonl)
-    int grid = std::max(8, (g_knobs.pair_zm27_bpc > 0 ? g_knobs.pair_zm27_bpc : g_knobs.pair_zm_bpc) * device_cu_count());
-    grid &= ~7;
-    const int W = grid / 8 * LEAN_WAVES;
-    const int slab = (b.NZ + 7) / 8;
-    int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
-    while (L > 1 && (int64_t)b.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
-    b.L = L;
-    b.S = (b.NZ + L - 1) / L;
-    b.partials = partials;
-    b.done = done;
-    Fold fold = fold_in;
-    if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
-    b.fold = fold;
-    using F27 = void (*)(PairLean27Args, const double *, double *, const int32_t *, const PairUni27 *,
-                         const int32_t *);
-    F27 f = nullptr;
-    const int form = !clean ? 0 : S.pcol27.p ? 2 : 1;
-    const bool z2 = g_knobs.pair_zm27_units == 2;
-    const bool uv = form == 2 && S.pair_unit27 && g_knobs.pair_unitv && !z2;   // one plane per step only
-#define Z27U(MODE, SP, FM) f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, FM, 2> : &spmv_pair_zm27_kernel<MODE, SP, FM, 1>
-#define Z27(MODE, SP) do { if (form == 2) { if (uv) f = &spmv_pair_zm27_kernel<MODE, SP, 2, 1, true>; \
-                                            else Z27U(MODE, SP, 2); } \
-                           else if (form == 1) Z27U(MODE, SP, 1); else Z27U(MODE, SP, 0); } while (0)
-    if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
-    else { if (split) Z27(SPMV_DOT, true); else Z27(SPMV_DOT, false); }
-#undef Z27
-#undef Z27U
-    note_dispatch(split ? DSP_PAIR_ZM27_SPLIT : DSP_PAIR_ZM27);
-    launch_timed(f, grid, st, b, x, y, S.pblk.p, S.puni27.p, S.pcol27.p);
-    HIPCHECK(hipGetLastError());
-    return grid;
-  }
+  if (S.pair_shape == 27) return zm27_launch(A, mode, split, clean, x, y, partials, done, fold_in, st, PairRuArgs{}, 0);
   PairLeanArgs a{};
   a.m = (int)A->m;
   a.n = (int)A->n;
@@ -1298,9 +1349,12 @@ int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac
 // CG mode 5 (knob 9 = 5): a lean 5/7-point z-march layout (the constant-
 // coefficient stencils), no or uniform Jacobi; on P > 1 ranks the product
 // must split (the ghost units' rows are finished by the boundary kernel)
+// 27-point (knob 55): one rank, the clean column-word layout
 bool pair_cg5_applies(const Mat *A, int jac_mode) {
-  return A->sd.pair_shape != 27 && (jac_mode == 0 || jac_mode == 2) && pair_lean_kind(A) > 0 && pair_zm_applies(A) &&
-         ((A->nghost == 0 && !A->sd.pair_ghosts) || matmult_splits(A));
+  if (jac_mode != 0 && jac_mode != 2) return false;
+  if (A->sd.pair_shape == 27)
+    return g_knobs.cg5_27 && pair_lean_kind(A) == 2 && A->sd.pcol27.p && A->nghost == 0 && !A->sd.pair_ghosts;
+  return pair_lean_kind(A) > 0 && pair_zm_applies(A) && ((A->nghost == 0 && !A->sd.pair_ghosts) || matmult_splits(A));
 }
 
 static int cg5_args(const Mat *A, PairLeanArgs &a) {
@@ -1320,6 +1374,10 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
                          int jac_mode, double jac_c, double *partials, const Fold &fold_in, const double *dot_part,
                          int ndot, int xb, int *hw, hipStream_t st) {
   if (!pair_cg5_applies(A, jac_mode)) return 0;
+  if (A->sd.pair_shape == 27) {
+    const PairRuArgs ru{s, w, r, r0, dot_part, ndot, xb, jac_c, hw};
+    return zm27_launch(A, SPMV_RUPD, false, true, p, nullptr, partials, nullptr, fold_in, st, ru, jac_mode);
+  }
   PairLeanArgs a;
   const int grid = cg5_args(A, a);
   a.partials = partials;

@@ -282,7 +282,11 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
                                                  ("poisson3d", 128, "jacobi", 10000, {"norm": "unpreconditioned"}),
                                                  ("poisson3d", 128, "jacobi", 10000, {"xb": 2}),
                                                  ("poisson3d", 128, "jacobi", 39, {"xb": 2}),
-                                                 ("poisson3d", 128, "jacobi", 38, {})])
+                                                 ("poisson3d", 128, "jacobi", 38, {}),
+                                                 ("poisson3d27", 128, "jacobi", 10000, {}),
+                                                 ("poisson3d27", 128, "jacobi", 37, {}),
+                                                 ("poisson3d27", 128, "none", 10000, {"guess": True}),
+                                                 ("poisson3d27", 128, "jacobi", 39, {"xb": 2})])
 def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
     """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
     gives p.w, and the update pass recomputes A p (the same sums, the same
@@ -292,7 +296,8 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
     to rounding (the norms' partials are grouped per z-march column); the
     graph-replayed second solve gives the first one's bits; the dispatch
     counts show both mode-5 passes ran.  x steps batched by 4 (the mode-5
-    default) and by 2, stops at every position relative to the batch."""
+    default) and by 2, stops at every position relative to the batch.  The
+    27-point operator (knob 55) runs both passes on its column-word z-march."""
     from mxsolve import _lib
     from mxsolve.core import DMat, dispatch_counts, rhs_hash
     L = _lib.load()
@@ -332,8 +337,9 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
     m5, dc5, bh, x0 = run(5)
     m2, dc2, _, _ = run(2)
     # (a nonzero guess forms r = b - A x with the stored-product MatMult first)
-    assert dc5["zm_pw"] > 0 and dc5["zm_rupd"] > 0 and dc5["pair_zm"] == (1 if guess else 0), dc5
-    assert dc2["zm_pw"] == 0 and dc2["pair_zm"] > 0, dc2
+    zk = "pair_zm27" if kind == "poisson3d27" else "pair_zm"
+    assert dc5["zm_pw"] > 0 and dc5["zm_rupd"] > 0 and dc5[zk] == (1 if guess else 0), dc5
+    assert dc2["zm_pw"] == 0 and dc2[zk] > 0, dc2
     for a, c in zip(m5, m2):
         assert a[:2] == c[:2], (a[:2], c[:2])
         assert np.allclose(a[2], c[2], rtol=1e-10, atol=0)
