@@ -1127,7 +1127,12 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // VALU-bound 27-point body at 78-80 VGPRs keeps 6 waves per SIMD (C5's
   // share, round 3: CG MatMult 63 us median against 68-74 at 3-4 per CU or
   // two planes per step, profiles/r03_ab.jsonl)
-  int grid = std::max(8, (g_knobs.pair_zm27_bpc > 0 ? g_knobs.pair_zm27_bpc : g_knobs.pair_zm_bpc) * device_cu_count());
+  // CG mode 5's residual update holds 96 VGPRs (5 waves per SIMD): its grid
+  // is the 5 workgroups per CU that fit at once (knob 56; 6 left a partial
+  // second generation: 99 -> 89 us per launch, -5% per C5 iteration)
+  const int bpc = mode == SPMV_RUPD && g_knobs.pair_zm27_ru_bpc > 0 ? g_knobs.pair_zm27_ru_bpc
+                  : g_knobs.pair_zm27_bpc > 0 ? g_knobs.pair_zm27_bpc : g_knobs.pair_zm_bpc;
+  int grid = std::max(8, bpc * device_cu_count());
   grid &= ~7;
   const int W = grid / 8 * LEAN_WAVES;
   const int slab = (b.NZ + 7) / 8;
@@ -1145,21 +1150,24 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   F27 f = nullptr;
   const int form = !clean ? 0 : S.pcol27.p ? 2 : 1;
   const bool z2 = g_knobs.pair_zm27_units == 2;
-  const bool uv = form == 2 && S.pair_unit27 && g_knobs.pair_unitv && !z2;   // one plane per step only
+  // the fma form: one plane per step, no ghost units (the SPLIT variant
+  // spills a VGPR at the 6-wave bound)
+  const bool uv = form == 2 && S.pair_unit27 && g_knobs.pair_unitv && !z2 && !split;
   if (mode == SPMV_PW || mode == SPMV_RUPD) {      // CG mode 5: form 2, one rank, one plane per step
     if (form != 2 || split) return 0;
     if (mode == SPMV_PW) f = uv ? &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, true> : &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, false>;
-    // the residual update without the fma form: with it the kernel holds
-    // 101 VGPRs and spills SGPRs (the same bits either way)
+    // the residual update without the fma form: with it the kernel holds 101
+    // VGPRs, spills SGPRs and measured no faster (101 vs 89 us at C5's share)
     else if (jm == 2) f = &spmv_pair_zm27_kernel<SPMV_RUPD, false, 2, 1, false, 2>;
     else f = &spmv_pair_zm27_kernel<SPMV_RUPD, false, 2, 1, false, 0>;
     note_dispatch(mode == SPMV_PW ? DSP_ZM_PW : DSP_ZM_RUPD);
   } else {
 #define Z27U(MODE, SP, FM) f = z2 ? &spmv_pair_zm27_kernel<MODE, SP, FM, 2> : &spmv_pair_zm27_kernel<MODE, SP, FM, 1>
-#define Z27(MODE, SP) do { if (form == 2) { if (uv) f = &spmv_pair_zm27_kernel<MODE, SP, 2, 1, true>; \
-                                            else Z27U(MODE, SP, 2); } \
-                           else if (form == 1) Z27U(MODE, SP, 1); else Z27U(MODE, SP, 0); } while (0)
-    if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
+#define Z27(MODE, SP) do { if (form == 2) Z27U(MODE, SP, 2); else if (form == 1) Z27U(MODE, SP, 1); \
+                           else Z27U(MODE, SP, 0); } while (0)
+    if (uv) f = mode == SPMV_PLAIN ? &spmv_pair_zm27_kernel<SPMV_PLAIN, false, 2, 1, true>
+                                   : &spmv_pair_zm27_kernel<SPMV_DOT, false, 2, 1, true>;
+    else if (mode == SPMV_PLAIN) { if (split) Z27(SPMV_PLAIN, true); else Z27(SPMV_PLAIN, false); }
     else { if (split) Z27(SPMV_DOT, true); else Z27(SPMV_DOT, false); }
 #undef Z27
 #undef Z27U
