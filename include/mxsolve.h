@@ -348,6 +348,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         the 27-point column-word z-march on one rank (1, default; 0: mode 2)
  * key 56: workgroups per CU of that 27-point residual update (default 5, the
  *         resident count at its 96 VGPRs; 0: key 45's)
+ * key 57: workgroups per CU of CG mode 5's 5/7-point p.Ap pass (0, default:
+ *         key 40's)
+ * key 58: workgroups per CU of CG mode 5's 5/7-point residual update (0,
+ *         default: key 40's)
  * key 52: coded z-march MatMult for 5/7-point code dictionaries that are not
  *         uniform per slot (1, default; 0: the general SELL kernel)
  * key 53: z-march terms of slots whose value is -1, 0 or +1 formed by fma (an

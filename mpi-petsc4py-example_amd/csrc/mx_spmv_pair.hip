@@ -1051,8 +1051,8 @@ static int zm_plane(const Mat *A, int ps, const int anchor[5]) {
 }
 
 // grid, segment length and segments of a z-march over NZ planes of P columns
-static int zm_tasks(int P, int NZ, int &L, int &S) {
-  int grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
+static int zm_tasks(int P, int NZ, int &L, int &S, int bpc = 0) {
+  int grid = std::max(8, (bpc > 0 ? bpc : g_knobs.pair_zm_bpc) * device_cu_count());
   grid &= ~7;
   const int W = grid / 8 * LEAN_WAVES;               // waves per XCD
   const int slab = (NZ + 7) / 8;                      // planes per XCD
@@ -1269,7 +1269,8 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   if (zm) {
     a.P = D / 128;
     a.NZ = (int)(A->m / D);
-    grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
+    // CG mode 5's p.Ap pass may take its own grid (knob 57)
+    grid = std::max(8, (mode == SPMV_PW && g_knobs.pw_bpc > 0 ? g_knobs.pw_bpc : g_knobs.pair_zm_bpc) * device_cu_count());
     grid &= ~7;
     const int W = grid / 8 * LEAN_WAVES;               // waves per XCD
     const int slab = (a.NZ + 7) / 8;                    // planes per XCD
@@ -1365,7 +1366,7 @@ bool pair_cg5_applies(const Mat *A, int jac_mode) {
   return pair_lean_kind(A) > 0 && pair_zm_applies(A) && ((A->nghost == 0 && !A->sd.pair_ghosts) || matmult_splits(A));
 }
 
-static int cg5_args(const Mat *A, PairLeanArgs &a) {
+static int cg5_args(const Mat *A, PairLeanArgs &a, int bpc = 0) {
   const Sell &S = A->sd;
   a = PairLeanArgs{};
   a.m = (int)A->m;
@@ -1375,7 +1376,7 @@ static int cg5_args(const Mat *A, PairLeanArgs &a) {
   const int D = a.anchor[S.pair_shape == 5 ? 2 : 4];
   a.P = D / 128;
   a.NZ = (int)(A->m / D);
-  return zm_tasks(a.P, a.NZ, a.L, a.S);
+  return zm_tasks(a.P, a.NZ, a.L, a.S, bpc);
 }
 
 int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, double *r, const double *r0,
@@ -1387,7 +1388,7 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
     return zm27_launch(A, SPMV_RUPD, false, true, p, nullptr, partials, nullptr, fold_in, st, ru, jac_mode);
   }
   PairLeanArgs a;
-  const int grid = cg5_args(A, a);
+  const int grid = cg5_args(A, a, g_knobs.ru_bpc);   // knob 58 (0: key 40's)
   a.partials = partials;
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
