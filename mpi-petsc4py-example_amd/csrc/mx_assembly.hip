@@ -1425,6 +1425,7 @@ static void build_pair_uniform27(Sell &S, const std::vector<double> &vt, hipStre
 // dy = +1: 2, 5, 8) and the column's ELO / EHI.  Otherwise none is built.
 static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
   S.pcol27.reset();
+  S.pair_sym27 = false;
   if (!S.puni27.p || !S.pair_clean27 || !S.pair_all || S.pat_star_off.size() < 27) return;
   const int64_t D = S.pat_star_off[22];                   // run 7's centre: +D
   if (D <= 0 || D % 128 != 0 || m % D != 0 || m > (int64_t(1) << 27)) return;
@@ -1451,6 +1452,22 @@ static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
   S.pcol27.alloc((size_t)P);
   HIPCHECK(hipMemcpyAsync(S.pcol27.p, cw.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, st));
   HIPCHECK(hipStreamSynchronize(st));
+  // symmetry (Sell::pair_sym27): one value per off-diagonal slot over every
+  // block's present slots, and that value equal to the mirrored slot's
+  double V[27];
+  bool have[27] = {};
+  bool sym = true;
+  for (int64_t b = 0; b < nb && sym; ++b)
+    for (int j = 0; j < 27 && sym; ++j) {
+      if (j == 13 || !(blk[(size_t)b].pm[j] | blk[(size_t)b].pm[27 + j])) continue;
+      const double v = blk[(size_t)b].v[j];
+      if (!have[j]) { V[j] = v; have[j] = true; }
+      else if (std::memcmp(&V[j], &v, sizeof(double)) != 0) sym = false;
+    }
+  for (int j = 0; j < 27 && sym; ++j)
+    if (j != 13 && have[j] != have[26 - j]) sym = false;
+    else if (j != 13 && have[j] && std::memcmp(&V[j], &V[26 - j], sizeof(double)) != 0) sym = false;
+  S.pair_sym27 = sym;
 }
 
 static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st) {

@@ -202,6 +202,11 @@ struct Sell {
   // every puni27 block's slot values but the diagonal's are -1, 0 or +1: the
   // 27-point z-march forms those slots' terms by fma (exact products, the same bits)
   bool pair_unit27 = false;
+  // the column-word 27-point layout is symmetric: every block's off-diagonal
+  // slot values are one value per slot across blocks and v[j] == v[26 - j]
+  // (with the box-boundary presence of the column words, a_ij == a_ji): CG
+  // mode 5's p.Ap pass sums each row's forward half (mx_spmv_pair.hip pair_fwd27)
+  bool pair_sym27 = false;
   // 27-point column words (one per 128-row column of a plane): when every
   // unit's empty runs are exactly its plane's z-boundary runs (plane 0: dz =
   // -1, the last plane: dz = +1 -- read out of range anyway) plus its column's
@@ -249,7 +254,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 0; int pair_col27 = 1; int pair_zm27_units = 1;
-                int mdot_split = 2; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 0; };
+                int mdot_split = 2; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 0; int pw_sym27 = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

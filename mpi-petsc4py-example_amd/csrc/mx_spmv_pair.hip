@@ -419,6 +419,42 @@ __device__ __forceinline__ dbl2 pair_sums27(const dbl2 (&L)[9], const double (&e
   return dbl2{s0v, s1v};
 }
 
+// CG mode 5's p.Ap pass on a symmetric 27-point operator (Sell::pair_sym27,
+// knob 59): p^T A p = sum_i p_i (a_ii p_i + 2 sum_{d > 0} a_{i,i+d} p_{i+d}),
+// so a row needs only its 13 forward slots (14..26: the +1 of the centre run,
+// the dy = +1 run of its plane and the three runs of the next plane) -- half
+// the products of the full row.  Returns the rows' t_i = a_ii p_i + 2 fwd_i:
+// p.Ap equals mode 2's p.w to rounding (a different order of the same exact
+// terms), not bit for bit.
+template <bool UV>
+__device__ __forceinline__ dbl2 pair_fwd27(const dbl2 (&L)[9], const double (&e)[9], uint32_t bw,
+                                           const PairUni27 *__restrict__ puni) {
+  const PairUni27 &B = puni[bw & PBLK_ID];                // wave-uniform: scalar loads
+  double f0 = 0.0, f1 = 0.0;
+#pragma unroll
+  for (int r = 4; r < 9; ++r) {
+    const double hi = wave_shift<false>(L[r].x, e[r]);    // x[r0 + c + 2]
+    double lo = 0.0;
+    if (r > 4) lo = wave_shift<true>(L[r].y, e[r]);       // x[r0 + c - 1]
+    const double a0[3] = {lo, L[r].x, L[r].y}, a1[3] = {L[r].x, L[r].y, hi};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int j = 3 * r + q;
+      if (j <= 13) continue;
+      const double v = B.v[j];
+      if (UV) {
+        f0 = __builtin_fma(v, a0[q], f0);
+        f1 = __builtin_fma(v, a1[q], f1);
+      } else {
+        f0 = f0 + v * a0[q];
+        f1 = f1 + v * a1[q];
+      }
+    }
+  }
+  const double d = B.v[13];
+  return dbl2{fma(2.0, f0, d * L[4].x), fma(2.0, f1, d * L[4].y)};
+}
+
 struct PairLean27Args {
   int n, P, NZ, L, S;
   int anchor[9];
@@ -434,7 +470,7 @@ struct PairLean27Args {
 // (the p.Ap partials, nothing stored) and SPMV_RUPD (alpha from the PW
 // partials, A p recomputed, r = r - alpha A p, z = c r and the three norms),
 // as spmv_pair_zm_kernel's (the same sums as the MatMult's, bit for bit).
-template <int MODE, bool SPLIT, int FORM, int ZU, bool UV = false, int JM = 0>
+template <int MODE, bool SPLIT, int FORM, int ZU, bool UV = false, int JM = 0, bool SYM = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UV && ZU == 1 ? 6 : 1)))
 spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
                                                              double *__restrict__ y, const int32_t *__restrict__ pblk,
@@ -534,14 +570,20 @@ spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
 #pragma unroll
         for (int k = 0; k < 3; ++k) { L[6 + k] = Nw[q][k]; e[6 + k] = Ne[q][k]; }
         const int r0 = (z + q) * D + cb;
-        const dbl2 sv = pair_sums27<FORM, UV>(L, e, bw[q], puni, lane);
-        if constexpr (RU) {
+        if constexpr (SYM) {                             // PW on a symmetric operator: forward half
+          static_assert(MODE == SPMV_PW && FORM == 2 && !SPLIT, "symmetric p.Ap pass only");
+          const dbl2 t = pair_fwd27<UV>(L, e, bw[q], puni);
+          dot += L[4].x * t.x;
+          dot += L[4].y * t.y;
+        } else if constexpr (RU) {
+          const dbl2 sv = pair_sums27<FORM, UV>(L, e, bw[q], puni, lane);
           const double ra = fma(-alpha, sv.x, rq[q].x), rb = fma(-alpha, sv.y, rq[q].y);
           const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
           nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
           nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
           *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
         } else {
+          const dbl2 sv = pair_sums27<FORM, UV>(L, e, bw[q], puni, lane);
           if constexpr (MODE != SPMV_PW) *reinterpret_cast<dbl2 *>(y + r0) = sv;
           if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
             const bool gh = SPLIT && (bw[q] & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
@@ -1155,7 +1197,11 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   const bool uv = form == 2 && S.pair_unit27 && g_knobs.pair_unitv && !z2 && !split;
   if (mode == SPMV_PW || mode == SPMV_RUPD) {      // CG mode 5: form 2, one rank, one plane per step
     if (form != 2 || split) return 0;
-    if (mode == SPMV_PW) f = uv ? &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, true> : &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, false>;
+    // the symmetric operator's p.Ap pass: forward half of every row (knob 59)
+    const bool sym = S.pair_sym27 && g_knobs.pw_sym27;
+    if (mode == SPMV_PW && sym) f = uv ? &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, true, 0, true>
+                                       : &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, false, 0, true>;
+    else if (mode == SPMV_PW) f = uv ? &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, true> : &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, false>;
     // the residual update without the fma form: with it the kernel holds 101
     // VGPRs, spills SGPRs and measured no faster (101 vs 89 us at C5's share)
     else if (jm == 2) f = &spmv_pair_zm27_kernel<SPMV_RUPD, false, 2, 1, false, 2>;

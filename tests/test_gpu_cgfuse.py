@@ -286,7 +286,9 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
                                                  ("poisson3d27", 128, "jacobi", 10000, {}),
                                                  ("poisson3d27", 128, "jacobi", 37, {}),
                                                  ("poisson3d27", 128, "none", 10000, {"guess": True}),
-                                                 ("poisson3d27", 128, "jacobi", 39, {"xb": 2})])
+                                                 ("poisson3d27", 128, "jacobi", 39, {"xb": 2}),
+                                                 ("poisson3d27", 128, "jacobi", 10000, {"sym": 0}),
+                                                 ("poisson3d27", 256, "jacobi", 10000, {})])
 def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
     """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
     gives p.w, and the update pass recomputes A p (the same sums, the same
@@ -297,7 +299,9 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
     graph-replayed second solve gives the first one's bits; the dispatch
     counts show both mode-5 passes ran.  x steps batched by 4 (the mode-5
     default) and by 2, stops at every position relative to the batch.  The
-    27-point operator (knob 55) runs both passes on its column-word z-march."""
+    27-point operator (knob 55) runs both passes on its column-word z-march,
+    its p.Ap pass summing each row's forward half (the operator is symmetric:
+    knob 59; p.Ap then equals mode 2's p.w to rounding, the bar above)."""
     from mxsolve import _lib
     from mxsolve.core import DMat, dispatch_counts, rhs_hash
     L = _lib.load()
@@ -308,6 +312,7 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
         old = L.mx_debug_set(9, mode)
         old27 = L.mx_debug_set(27, 1)           # the row-pair layout (this module's fixture turns it off)
         old29 = L.mx_debug_set(29, kw.get("xb", 0) if mode == 5 else 0)   # mode 5: x batches of 4 by default
+        old59 = L.mx_debug_set(59, kw.get("sym", 1))   # 27-point: the symmetric forward-half p.Ap pass
         try:
             A = DMat.stencil(selfcomm, kind, n)
             m = A.info()["m"]
@@ -333,6 +338,7 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
             L.mx_debug_set(9, old)
             L.mx_debug_set(27, old27)
             L.mx_debug_set(29, old29)
+            L.mx_debug_set(59, old59)
 
     m5, dc5, bh, x0 = run(5)
     m2, dc2, _, _ = run(2)
