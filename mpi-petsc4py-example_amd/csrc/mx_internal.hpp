@@ -302,6 +302,9 @@ struct Mat {
   DBuf<double> jac_dinv;
   int jac_mode = -1;       // -1: not set up; 1: vector; 2: uniform scalar
   double jac_c = 1.0;
+  // A_d symmetric, entries and values (one rank, checked once by
+  // pair_sym_prepare for CG mode 5's forward-half p.Ap pass): -1 not checked
+  int sym = -1;
   // captured CG iteration batch (hipGraph), reused while its key matches
   hipGraphExec_t cg_graph = nullptr;
   std::vector<uintptr_t> cg_key;
@@ -429,6 +432,7 @@ int main_grid(const Mat *A, int mode, const void *kf, bool pairs);   // the SpMV
 int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, double *partials, const int *done,
                      const Fold &fold, hipStream_t st, const Jac &jac = Jac{}, const double *xscale = nullptr);
 bool pair_code_applies(const Mat *A);   // the coded z-march (mx_mat_info.pair_code)
+void pair_sym_prepare(Mat *A);          // Mat::sym, once per operator, before a CG solve's capture
 int pair_lean_kind(const Mat *A);   // 0 general kernel, 1 lean, 2 lean select-free (mx_mat_info.pair_lean)
 bool pair_zm_applies(const Mat *A);  // the lean kernel's z-march form (mx_mat_info.pair_zmarch)
 int pair_f64_kind(const Mat *A);     // 5 / 7: the fp64 row-pair z-march applies (mx_mat_info.pair_f64)

@@ -1393,6 +1393,9 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   if (fmode == 5 && !pair_cg5_applies(A, dinv.mode)) fmode = 2;
   // x-step batch (knob 29; 0 = auto: 4 in mode 5 -- 256^3: -2.8% per iteration
   // against 2 -- else 2; mode 4 always 2)
+  // mode 5 on a symmetric 5/7-point operator: the forward-half p.Ap pass
+  // (checked once per operator, before any capture)
+  if (fmode == 5) pair_sym_prepare(A);
   const int xbk = g_knobs.cg_xbatch == 0 ? (fmode == 5 ? 4 : 2) : fmode == 4 ? 2 : g_knobs.cg_xbatch;
   const int xb = ((fmode == 2 || fmode == 4 || fmode == 5) && (xbk == 2 || xbk == 4) && poll % xbk == 0) ? xbk : 1;
   const bool wide_pb = fmode == 5;

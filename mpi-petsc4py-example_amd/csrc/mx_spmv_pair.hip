@@ -186,6 +186,28 @@ __global__ void __launch_bounds__(256) spmv_pair_lean_kernel(const PairLeanArgs 
   }
 }
 
+// CG mode 5's p.Ap pass on a symmetric 5/7-point operator (Mat::sym57,
+// checked once per operator by sym_check_kernel; knob 59): each row sums only
+// its forward slots (+1, and for 7-point +n and +D; 5-point: +1, +D),
+// t_i = a_ii p_i + 2 fwd_i, and p.Ap = sum_i p_i t_i -- mode 2's p.w to
+// rounding (the same exact terms, another order).  The -n run is not loaded.
+template <int PS>
+__device__ __forceinline__ dbl2 pair_fwd(const dbl2 (&L)[PairShape<PS>::NR], double e, uint32_t bw,
+                                         const PairUni *__restrict__ puni) {
+  using SH = PairShape<PS>;
+  constexpr int K = SH::K, C = SH::CENTER_RUN, JD = SH::first(C) + 1;   // the diagonal slot
+  const PairUni &B = puni[bw & PBLK_ID];                  // wave-uniform: scalar loads
+  const double hi = wave_shift<false>(L[C].x, e);         // x[r0 + c + 2]: row 1's +1
+  double f0 = B.v[JD + 1] * L[C].y, f1 = B.v[K + JD + 1] * hi;
+#pragma unroll
+  for (int j = JD + 2; j < K; ++j) {                      // the singleton runs past the centre
+    const int r = SH::run(j);
+    f0 = f0 + B.v[j] * L[r].x;
+    f1 = f1 + B.v[K + j] * L[r].y;
+  }
+  return dbl2{fma(2.0, f0, B.v[JD] * L[C].x), fma(2.0, f1, B.v[K + JD] * L[C].y)};
+}
+
 // Z-march form.  The pattern's first and last runs are -D and +D (D = P
 // units: a 3D plane, a 2D line); unit u and unit u + P are one plane apart.
 // A task is (segment of L planes, column of units); XCD x takes segments
@@ -224,7 +246,7 @@ struct PairRuArgs {
   int *hw;                     // the host's pinned words (Poller)
 };
 
-template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0>
+template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0, bool SYM = false>
 __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a, const double *__restrict__ x,
                                                            double *__restrict__ y, const int32_t *__restrict__ pblk,
                                                            const PairUni *__restrict__ puni, const PairRuArgs ru) {
@@ -247,7 +269,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
     if (a.done && *a.done) return;   // wave-uniform: solver finished
   }
   using SH = PairShape<PS>;
-  constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
+  constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1, C = SH::CENTER_RUN;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int sb, se, W, w;
@@ -292,7 +314,8 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
         zp[q] = bload2(xr, r0 + D);
 #pragma unroll
         for (int r = 1; r < LAST; ++r)
-          if (r != TR) L[q][r] = bload2(xr, r0 + a.anchor[r] + (CLEAN && (bw[q] & (PBLK_RUN0 << r)) ? PAIR_OOR : 0));
+          if (r != TR && !(SYM && r < TR))                 // SYM: no backward inner run
+            L[q][r] = bload2(xr, r0 + a.anchor[r] + (CLEAN && (bw[q] & (PBLK_RUN0 << r)) ? PAIR_OOR : 0));
         int eo = ecst;
         if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
         e[q] = bload1(xr, ub + eo);
@@ -324,6 +347,11 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
           nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
           nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
           *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+        } else if constexpr (SYM) {
+          static_assert(MODE == SPMV_PW && CLEAN && !SPLIT, "symmetric p.Ap pass: one rank, select-free");
+          const dbl2 t = pair_fwd<PS>(L[q], e[q], bw[q], puni);
+          dot += L[q][C].x * t.x;
+          dot += L[q][C].y * t.y;
         } else {
           pair_unit<MODE, PS, SPLIT, CLEAN>(L[q], e[q], bw[q], puni, y, r0, lane, dot);
         }
@@ -1224,6 +1252,47 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   return grid;
 }
 
+// Symmetry of A_d (one rank): every off-diagonal entry (i, j, v) has its
+// mirror (j, i) with the same bits (canonical rows are sorted: a binary
+// search of row j).  A vector store of 1 on a mismatch (benign race).
+__global__ void sym_check_kernel(int64_t m, const int64_t *__restrict__ ptr, const int32_t *__restrict__ col,
+                                 const double *__restrict__ val, int *__restrict__ bad) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    for (int64_t k = ptr[i]; k < ptr[i + 1]; ++k) {
+      const int64_t j = col[k];
+      if (j == i) continue;
+      if (j < 0 || j >= m) { *bad = 1; return; }
+      int64_t lo = ptr[j], hi = ptr[j + 1];
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (col[mid] < i) lo = mid + 1; else hi = mid;
+      }
+      if (lo == ptr[j + 1] || col[lo] != i || __double_as_longlong(val[lo]) != __double_as_longlong(val[k])) {
+        *bad = 1;
+        return;
+      }
+    }
+  }
+}
+
+void pair_sym_prepare(Mat *A) {
+  if (A->sym >= 0) return;
+  A->sym = 0;
+  if (!g_knobs.pw_sym27 || A->comm->size != 1 || A->nghost != 0 || A->m != A->n || A->m <= 0 ||
+      (A->sd.pair_shape != 5 && A->sd.pair_shape != 7) || !A->dptr.p)
+    return;
+  hipStream_t st = A->comm->stream;
+  DBuf<int> bad(1);
+  HIPCHECK(hipMemsetAsync(bad.p, 0, sizeof(int), st));
+  sym_check_kernel<<<grid_for(A->m, 256, 8192), 256, 0, st>>>(A->m, A->dptr.p, A->dcol.p, A->dval.p, bad.p);
+  HIPCHECK(hipGetLastError());
+  int h = 1;
+  HIPCHECK(hipMemcpyAsync(&h, bad.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIPCHECK(hipStreamSynchronize(st));
+  A->sym = h == 0 ? 1 : 0;
+}
+
 // Launch the lean MatMult for this product; returns its grid, or 0 when it
 // does not apply (the general kernel then runs).  A fold (fold.cnt set)
 // counts this launch's workgroups.
@@ -1331,6 +1400,12 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
 #define ZM_C(MODE, PS) do { if (split) { if (clean) ZM_PICK(MODE, PS, true, true); else ZM_PICK(MODE, PS, true, false); } \
                             else { if (clean) ZM_PICK(MODE, PS, false, true); else ZM_PICK(MODE, PS, false, false); } } while (0)
     if (mode == SPMV_PLAIN) { if (S.pair_shape == 5) ZM_C(SPMV_PLAIN, 5); else ZM_C(SPMV_PLAIN, 7); }
+    else if (mode == SPMV_PW && clean && !split && A->sym == 1 && g_knobs.pw_sym27) {   // symmetric: forward half
+      if (S.pair_shape == 5) fz = g_knobs.pair_zm_units == 2 ? &spmv_pair_zm_kernel<SPMV_PW, 5, false, true, 2, 0, true>
+                                                             : &spmv_pair_zm_kernel<SPMV_PW, 5, false, true, 1, 0, true>;
+      else fz = g_knobs.pair_zm_units == 2 ? &spmv_pair_zm_kernel<SPMV_PW, 7, false, true, 2, 0, true>
+                                           : &spmv_pair_zm_kernel<SPMV_PW, 7, false, true, 1, 0, true>;
+    }
     else if (mode == SPMV_PW) { if (S.pair_shape == 5) ZM_C(SPMV_PW, 5); else ZM_C(SPMV_PW, 7); }
     else { if (S.pair_shape == 5) ZM_C(SPMV_DOT, 5); else ZM_C(SPMV_DOT, 7); }
 #undef ZM_C

@@ -288,6 +288,8 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
                                                  ("poisson3d27", 128, "none", 10000, {"guess": True}),
                                                  ("poisson3d27", 128, "jacobi", 39, {"xb": 2}),
                                                  ("poisson3d27", 128, "jacobi", 10000, {"sym": 0}),
+                                                 ("poisson3d", 128, "jacobi", 10000, {"sym": 0}),
+                                                 ("poisson2d", 256, "jacobi", 10000, {"sym": 0}),
                                                  ("poisson3d27", 256, "jacobi", 10000, {})])
 def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
     """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
@@ -359,3 +361,39 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
     assert (m5[0][0], m5[0][1]) == (o["its"], o["reason"]), (m5[0][:2], o["its"], o["reason"])
     assert np.allclose(m5[0][2], o["history"], rtol=1e-8, atol=0)
     assert np.linalg.norm(m5[0][3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
+
+
+def test_mode5_nonsymmetric_full_rows(selfcomm, oracle_mod):
+    """CG mode 5 on a constant-coefficient 7-point operator that is not
+    symmetric (+D coupling -1.5, -D -1): the symmetry check (Mat::sym, once per
+    operator) refuses the forward-half p.Ap pass, so the pass sums full rows
+    and the solve matches the oracle (a forward-half pass would not: p.Ap of a
+    nonsymmetric A is not p_i (a_ii p_i + 2 fwd_i))."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts
+    L = _lib.load()
+    n = 128
+    ip, c, v = oracle_mod.stencil("poisson3d", n)
+    M = ip.size - 1
+    rows = np.repeat(np.arange(M), np.diff(ip))
+    v = np.where(c - rows == n * n, -1.5, v)
+    b = np.random.default_rng(47).random(M)
+    old = L.mx_debug_set(9, 5)
+    old27 = L.mx_debug_set(27, 1)           # the row-pair layout (this module's fixture turns it off)
+    try:
+        A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+        assert A.info()["pair_uniform"] == 1
+        x = torch.zeros(M, dtype=torch.float64, device="cuda")
+        dispatch_counts(reset=True)
+        r = A.solve(torch.from_numpy(b).cuda(), x, ksp="cg", pc="jacobi", rtol=1e-8, max_it=300, history=True)
+        dc = dispatch_counts(reset=True)
+        A.destroy()
+    finally:
+        L.mx_debug_set(9, old)
+        L.mx_debug_set(27, old27)
+    assert dc["zm_pw"] > 0 and dc["zm_rupd"] > 0, dc
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
+    o = O.solve(b, ksp="cg", pc="jacobi", rtol=1e-8, max_it=300, history=True)
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"]), (r["its"], r["reason"], o["its"], o["reason"])
+    assert np.allclose(r["history"], o["history"], rtol=1e-8, atol=0)
+    assert np.linalg.norm(x.cpu().numpy() - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
