@@ -356,6 +356,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         forward half, p^T A p = sum_i p_i (a_ii p_i + 2 fwd_i) -- 27-point:
  *         symmetry from the column-word layout; 5/7-point: A_d checked once
  *         per operator (1, default; 0: the full rows -- mode 2's p.w bits)
+ * key 60: 27-point column-word z-march plane-pipelined -- each loaded plane
+ *         advances three units' running sums, nothing but two sums and the
+ *         centre pair carried (1, default; 0: six operand pairs carried)
  * key 52: coded z-march MatMult for 5/7-point code dictionaries that are not
  *         uniform per slot (1, default; 0: the general SELL kernel)
  * key 53: z-march terms of slots whose value is -1, 0 or +1 formed by fma (an

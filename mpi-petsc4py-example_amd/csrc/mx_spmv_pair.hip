@@ -641,6 +641,162 @@ spmv_pair_zm27_kernel(const PairLean27Args a, const double *__restrict__ x,
 }
 
 
+// Plane-pipelined 27-point z-march (column-word form, knob 60).  A unit's 27
+// slots are three dz groups of nine (plane z-1, z, z+1), summed in slot
+// order; so when a wave loads plane q it advances three units at once: it
+// finishes unit q-1 (its dz = +1 group), continues unit q (dz = 0) and starts
+// unit q+1 (dz = -1), each with its own dictionary block's nine values.  What
+// crosses a step is two running row sums and the centre pair (12 VGPRs)
+// instead of six operand pairs and their edges (36), and each plane's +-1
+// neighbours take one pair of wave shifts per run instead of three.  The
+// same operations in the same order as spmv_pair_zm27_kernel: the same bits.
+struct Plane27 { dbl2 L[3]; double lo[3], hi[3]; };
+
+template <bool UV>
+__device__ __forceinline__ dbl2 plane27_add(dbl2 s, const PairUni27 &B, int g, const Plane27 &P) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double a0[3] = {P.lo[k], P.L[k].x, P.L[k].y}, a1[3] = {P.L[k].x, P.L[k].y, P.hi[k]};
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int j = 9 * g + 3 * k + p;
+      const double v = B.v[j];
+      if (UV && j != 13) {
+        s.x = __builtin_fma(v, a0[p], s.x);
+        s.y = __builtin_fma(v, a1[p], s.y);
+      } else {
+        s.x = s.x + v * a0[p];
+        s.y = s.y + v * a1[p];
+      }
+    }
+  }
+  return s;
+}
+
+template <int MODE, bool SPLIT, bool UV, int JM = 0>
+__global__ void __launch_bounds__(256) spmv_pair_zm27p_kernel(const PairLean27Args a, const double *__restrict__ x,
+                                                              double *__restrict__ y, const int32_t *__restrict__ pblk,
+                                                              const PairUni27 *__restrict__ puni,
+                                                              const int32_t *__restrict__ pcol, const PairRuArgs ru) {
+  constexpr bool RU = MODE == SPMV_RUPD;
+  static_assert(!SPLIT || (MODE != SPMV_PW && !RU), "27-point mode 5: one rank");
+  double alpha = 0.0;
+  const double *rin = nullptr;
+  if constexpr (RU) {
+    KspState *s = ru.s;
+    if (s->top.done) {
+      if (ru.hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(ru.hw + HW_DONE, 1);
+      return;
+    }
+    const double pw = ru.ndot > 0 ? block_sum_array<16>(ru.dot_part, ru.ndot) : s->red1;
+    const CgAlpha al = cg_alpha(s, pw);
+    if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, ru.xb, false, ru.hw);
+    if (al.reason) return;
+    alpha = al.alpha;
+    rin = (ru.r0 && al.i == 0) ? ru.r0 : ru.r;
+  } else {
+    if (a.done && *a.done) return;   // wave-uniform: solver finished
+  }
+  double nv[3] = {0.0, 0.0, 0.0};   // RU: [z.z, z.r, r.r]
+  double dot = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[7];
+  const int eb = lane == 0 ? -1 : 128;                   // edge: lane 0 x[ub + c - 1], others x[ub + 128 + c]
+  const int ntask = (se - sb) * a.P;
+  for (int t = w; t < ntask; t += W) {
+    const int seg = sb + t / a.P, col = t % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;
+    // the column's empty dy runs and x-line edges read out of range (form 2)
+    const uint32_t cw = (uint32_t)pcol[col];
+    const int oor[3] = {(cw & U27C_YLO) ? PAIR_OOR : 0, 0, (cw & U27C_YHI) ? PAIR_OOR : 0};
+    const int ebe = eb + ((lane == 0 ? (cw & U27_ELO) : (cw & U27_EHI)) ? PAIR_OOR_EDGE : 0);
+    // plane q's three dy runs (anchors 3..5: -n, 0, +n within the plane), their edges and shifts
+    auto load = [&](int q, Plane27 &P, double (&e)[3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        P.L[k] = bload2(xr, q * D + cb + a.anchor[3 + k] + oor[k]);
+        e[k] = bload1(xr, q * D + col * 128 + ebe + a.anchor[3 + k] + oor[k]);
+      }
+    };
+    auto shift = [&](Plane27 &P, const double (&e)[3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        P.lo[k] = wave_shift<true>(P.L[k].y, e[k]);      // x[r0 + c - 1]
+        P.hi[k] = wave_shift<false>(P.L[k].x, e[k]);     // x[r0 + c + 2]
+      }
+    };
+    auto blk = [&](int z) -> uint32_t { return (uint32_t)pblk[min(z, a.NZ - 1) * a.P + col]; };
+    uint32_t bz = blk(z0), bz1 = blk(z0 + 1);
+    Plane27 P;
+    double e[3];
+    // prologue: plane z0 - 1 starts unit z0, plane z0 continues it and starts z0 + 1
+    load(z0 - 1, P, e);
+    shift(P, e);
+    dbl2 m1 = plane27_add<UV>(dbl2{0.0, 0.0}, puni[bz & PBLK_ID], 0, P);
+    load(z0, P, e);
+    shift(P, e);
+    m1 = plane27_add<UV>(m1, puni[bz & PBLK_ID], 1, P);
+    dbl2 m0 = plane27_add<UV>(dbl2{0.0, 0.0}, puni[bz1 & PBLK_ID], 0, P);
+    dbl2 cz = P.L[1];                                    // unit z0's own rows
+    for (int z = z0; z < z1; ++z) {
+      const uint32_t bz2 = blk(z + 2);                   // (past the last plane: a stand-in, never emitted)
+      const int r0 = z * D + cb;
+      dbl2 rq;
+      load(z + 1, P, e);
+      if constexpr (RU) rq = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
+      shift(P, e);
+      // one block's nine values live at a time (the barriers keep the three
+      // groups' scalar loads from being hoisted together: 54 SGPRs spilled)
+      const dbl2 out = plane27_add<UV>(m1, puni[bz & PBLK_ID], 2, P);   // unit z finished
+      __builtin_amdgcn_sched_barrier(0);
+      m1 = plane27_add<UV>(m0, puni[bz1 & PBLK_ID], 1, P);              // unit z + 1: 18 slots
+      __builtin_amdgcn_sched_barrier(0);
+      m0 = plane27_add<UV>(dbl2{0.0, 0.0}, puni[bz2 & PBLK_ID], 0, P);  // unit z + 2: 9 slots
+      if constexpr (RU) {
+        const double ra = fma(-alpha, out.x, rq.x), rb = fma(-alpha, out.y, rq.y);
+        const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
+        nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
+        nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
+        *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+      } else {
+        if constexpr (MODE != SPMV_PW) *reinterpret_cast<dbl2 *>(y + r0) = out;
+        if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
+          const bool gh = SPLIT && (bz & (lane < 32 ? PBLK_GHOST_LO : PBLK_GHOST_HI)) != 0;
+          if (!gh) {
+            dot += cz.x * out.x;
+            dot += cz.y * out.y;
+          }
+        }
+      }
+      cz = P.L[1];
+      bz = bz1;
+      bz1 = bz2;
+    }
+  }
+  if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
+    double v[1] = {dot};
+    block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  } else if constexpr (RU) {
+    block_partials<3>(nv, a.partials, gridDim.x, a.fold);
+  }
+}
+
 // fp64 row pairs (Sell::pval, uncoded 5/7-point layouts whose every unit is
 // select-free): the z-march with the unit's values streamed (K 16-byte pairs
 // per lane, non-temporal) instead of a dictionary block's uniform values.
@@ -1223,10 +1379,35 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // the fma form: one plane per step, no ghost units (the SPLIT variant
   // spills a VGPR at the 6-wave bound)
   const bool uv = form == 2 && S.pair_unit27 && g_knobs.pair_unitv && !z2 && !split;
-  if (mode == SPMV_PW || mode == SPMV_RUPD) {      // CG mode 5: form 2, one rank, one plane per step
+  // the plane-pipelined form (knob 60): column words; the symmetric p.Ap pass
+  // keeps the carried-operand kernel
+  const bool sym = S.pair_sym27 && g_knobs.pw_sym27;
+  if (form == 2 && g_knobs.pair_zm27p && !(mode == SPMV_PW && sym)) {
+    const bool uvp = S.pair_unit27 && g_knobs.pair_unitv;
+    switch (mode) {
+      case SPMV_PLAIN:
+        if (split) f = uvp ? &spmv_pair_zm27p_kernel<SPMV_PLAIN, true, true> : &spmv_pair_zm27p_kernel<SPMV_PLAIN, true, false>;
+        else f = uvp ? &spmv_pair_zm27p_kernel<SPMV_PLAIN, false, true> : &spmv_pair_zm27p_kernel<SPMV_PLAIN, false, false>;
+        break;
+      case SPMV_DOT:
+        if (split) f = uvp ? &spmv_pair_zm27p_kernel<SPMV_DOT, true, true> : &spmv_pair_zm27p_kernel<SPMV_DOT, true, false>;
+        else f = uvp ? &spmv_pair_zm27p_kernel<SPMV_DOT, false, true> : &spmv_pair_zm27p_kernel<SPMV_DOT, false, false>;
+        break;
+      case SPMV_PW:
+        if (split) return 0;
+        f = uvp ? &spmv_pair_zm27p_kernel<SPMV_PW, false, true> : &spmv_pair_zm27p_kernel<SPMV_PW, false, false>;
+        break;
+      case SPMV_RUPD:
+        if (split) return 0;
+        if (jm == 2) f = uvp ? &spmv_pair_zm27p_kernel<SPMV_RUPD, false, true, 2> : &spmv_pair_zm27p_kernel<SPMV_RUPD, false, false, 2>;
+        else f = uvp ? &spmv_pair_zm27p_kernel<SPMV_RUPD, false, true, 0> : &spmv_pair_zm27p_kernel<SPMV_RUPD, false, false, 0>;
+        break;
+      default: return 0;
+    }
+    note_dispatch(mode == SPMV_PW ? DSP_ZM_PW : mode == SPMV_RUPD ? DSP_ZM_RUPD : split ? DSP_PAIR_ZM27_SPLIT : DSP_PAIR_ZM27);
+  } else if (mode == SPMV_PW || mode == SPMV_RUPD) {      // CG mode 5: form 2, one rank, one plane per step
     if (form != 2 || split) return 0;
     // the symmetric operator's p.Ap pass: forward half of every row (knob 59)
-    const bool sym = S.pair_sym27 && g_knobs.pw_sym27;
     if (mode == SPMV_PW && sym) f = uv ? &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, true, 0, true>
                                        : &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, false, 0, true>;
     else if (mode == SPMV_PW) f = uv ? &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, true> : &spmv_pair_zm27_kernel<SPMV_PW, false, 2, 1, false>;

@@ -288,6 +288,7 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
                                                  ("poisson3d27", 128, "none", 10000, {"guess": True}),
                                                  ("poisson3d27", 128, "jacobi", 39, {"xb": 2}),
                                                  ("poisson3d27", 128, "jacobi", 10000, {"sym": 0}),
+                                                 ("poisson3d27", 128, "jacobi", 10000, {"sym": 0, "k60": 0}),
                                                  ("poisson3d", 128, "jacobi", 10000, {"sym": 0}),
                                                  ("poisson2d", 256, "jacobi", 10000, {"sym": 0}),
                                                  ("poisson3d27", 256, "jacobi", 10000, {})])
@@ -315,6 +316,7 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
         old27 = L.mx_debug_set(27, 1)           # the row-pair layout (this module's fixture turns it off)
         old29 = L.mx_debug_set(29, kw.get("xb", 0) if mode == 5 else 0)   # mode 5: x batches of 4 by default
         old59 = L.mx_debug_set(59, kw.get("sym", 1))   # 27-point: the symmetric forward-half p.Ap pass
+        old60 = L.mx_debug_set(60, kw.get("k60", 1))   # 27-point: the plane-pipelined z-march
         try:
             A = DMat.stencil(selfcomm, kind, n)
             m = A.info()["m"]
@@ -341,6 +343,7 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
             L.mx_debug_set(27, old27)
             L.mx_debug_set(29, old29)
             L.mx_debug_set(59, old59)
+            L.mx_debug_set(60, old60)
 
     m5, dc5, bh, x0 = run(5)
     m2, dc2, _, _ = run(2)

@@ -330,9 +330,10 @@ def _with_knobs(L, kv, fn):
 # step (42 = 1), short / odd segments with tails (41), other grids (40)
 # -- and for the 27-point z-march: its per-run-branch body instead of the
 # column-zeroed one (48 = 0), two planes per step (49 = 2), other grids (45),
-# multiply-and-add for the -1 slots instead of their exact-product fma (53 = 0)
+# multiply-and-add for the -1 slots instead of their exact-product fma (53 = 0),
+# the carried-operand body instead of the plane-pipelined one (60 = 0)
 LEAN_FORMS = [{}, {39: 0}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}, {40: 2},
-              {48: 0}, {49: 2, 45: 3}, {48: 0, 49: 2, 41: 5}, {53: 0}]
+              {48: 0}, {49: 2, 45: 3}, {48: 0, 49: 2, 41: 5}, {53: 0}, {60: 0}, {60: 0, 53: 0}]
 
 
 @pytest.mark.parametrize("form", range(len(LEAN_FORMS)))
