@@ -291,7 +291,7 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
                                                  ("poisson3d27", 128, "jacobi", 10000, {"sym": 0, "k60": 0}),
                                                  ("poisson3d", 128, "jacobi", 10000, {"sym": 0}),
                                                  ("poisson2d", 256, "jacobi", 10000, {"sym": 0}),
-                                                 ("poisson3d27", 256, "jacobi", 10000, {})])
+                                                 ])
 def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
     """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
     gives p.w, and the update pass recomputes A p (the same sums, the same
@@ -360,7 +360,9 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
     assert np.array_equal(m5[0][3].view(np.uint64), m5[1][3].view(np.uint64))
     ip, c_, v = oracle_mod.stencil(kind, n)
     O = oracle_mod.OracleMat.from_csr(ip.size - 1, ip.size - 1, ip, c_, v)
-    o = O.solve(bh, x0=x0 if guess else None, ksp="cg", pc=pc, rtol=1e-8, max_it=max_it, norm=norm, history=True)
+    from _hostinfo import host_threads
+    o = O.solve(bh, x0=x0 if guess else None, ksp="cg", pc=pc, rtol=1e-8, max_it=max_it, norm=norm, history=True,
+                nthreads=host_threads())
     assert (m5[0][0], m5[0][1]) == (o["its"], o["reason"]), (m5[0][:2], o["its"], o["reason"])
     assert np.allclose(m5[0][2], o["history"], rtol=1e-8, atol=0)
     assert np.linalg.norm(m5[0][3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
