@@ -1008,68 +1008,109 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
 }
 
 // normalise vv[k+1], happy breakdown, KSPGMRESUpdateHessenberg, convergence
+// The column and the rotations are staged in LDS by the whole workgroup
+// (coalesced loads) and thread 0 works there: the rotation loop's dependent
+// global loads took ~20 us per step at k ~ 15 (the same operations in the
+// same order, so the same bits).
 __global__ void __launch_bounds__(256) gm_step_kernel(KspState *s, int k, const double *partials, int nblocks,
                                                       int fused, double *hh, int ld, double *grs, double *cc,
                                                       double *ss, double *hist, double *vscale) {
   if (s->inner_stop) return;
-  if (!gather_red<1>(s, partials, nblocks, fused)) return;
-  const double tt = sqrt(s->red[0]);
-  s->scale = tt != 0.0 ? 1.0 / tt : 1.0;
-  vscale[k + 1] = s->scale;   // VecScale(vv[k+1], 1/tt), applied where it is read
-  if (not_finite(tt)) { stop(s, R_DIVERGED_NANORINF); return; }
+  (void)gather_red<1>(s, partials, nblocks, fused);   // every thread: the fold syncs the workgroup
+  __shared__ double hs[MAX_RESTART + 2], cs[MAX_RESTART + 1], sn[MAX_RESTART + 1];
+  __shared__ int wb;
   double *h = hh + (size_t)k * ld;   // column k
-  h[k + 1] = tt;
-  double hapbnd = fabs(tt / grs[k]);
-  if (hapbnd > s->haptol) hapbnd = s->haptol;
-  const bool hapend = tt < hapbnd;
-  // apply the previous rotations to column k
-  for (int j = 1; j <= k; ++j) {
-    const double t = h[j - 1];
-    h[j - 1] = cc[j - 1] * t + ss[j - 1] * h[j];
-    h[j] = cc[j - 1] * h[j] - (ss[j - 1] * t);
+  for (int j = threadIdx.x; j <= k + 1; j += blockDim.x) hs[j] = h[j];
+  for (int j = threadIdx.x; j < k; j += blockDim.x) {
+    cs[j] = cc[j];
+    sn[j] = ss[j];
   }
-  double res;
-  if (!hapend) {
-    const double t = sqrt(h[k] * h[k] + h[k + 1] * h[k + 1]);
-    if (t == 0.0) { stop(s, R_DIVERGED_NULL); return; }
-    cc[k] = h[k] / t;
-    ss[k] = h[k + 1] / t;
-    grs[k + 1] = -(ss[k] * grs[k]);
-    grs[k] = cc[k] * grs[k];
-    h[k] = cc[k] * h[k] + ss[k] * h[k + 1];
-    res = fabs(grs[k + 1]);
-  } else {
-    res = 0.0;
+  if (threadIdx.x == 0) wb = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    [&] {
+      const double tt = sqrt(s->red[0]);
+      s->scale = tt != 0.0 ? 1.0 / tt : 1.0;
+      vscale[k + 1] = s->scale;   // VecScale(vv[k+1], 1/tt), applied where it is read
+      if (not_finite(tt)) { stop(s, R_DIVERGED_NANORINF); return; }
+      wb = 1;
+      hs[k + 1] = tt;
+      double hapbnd = fabs(tt / grs[k]);
+      if (hapbnd > s->haptol) hapbnd = s->haptol;
+      const bool hapend = tt < hapbnd;
+      // apply the previous rotations to column k
+      for (int j = 1; j <= k; ++j) {
+        const double t = hs[j - 1];
+        hs[j - 1] = cs[j - 1] * t + sn[j - 1] * hs[j];
+        hs[j] = cs[j - 1] * hs[j] - (sn[j - 1] * t);
+      }
+      double res;
+      if (!hapend) {
+        const double t = sqrt(hs[k] * hs[k] + hs[k + 1] * hs[k + 1]);
+        if (t == 0.0) { stop(s, R_DIVERGED_NULL); return; }
+        const double ck = hs[k] / t, sk = hs[k + 1] / t;
+        cc[k] = ck;
+        ss[k] = sk;
+        const double g = grs[k];
+        grs[k + 1] = -(sk * g);
+        grs[k] = ck * g;
+        hs[k] = ck * hs[k] + sk * hs[k + 1];
+        res = fabs(grs[k + 1]);
+      } else {
+        res = 0.0;
+      }
+      s->it = k + 1;
+      s->its += 1;
+      s->ksp_rnorm = res;
+      s->res = tt;
+      if (hist) hist[s->its] = res;
+      int reason = dev_converged(s, s->its, res, true, 0.0);
+      if (hapend && !reason) reason = R_DIVERGED_BREAKDOWN;
+      if (reason) { stop(s, reason); return; }
+      if (s->it >= s->max_k || s->its >= s->top.max_it) s->inner_stop = 1;
+    }();
   }
-  s->it = k + 1;
-  s->its += 1;
-  s->ksp_rnorm = res;
-  s->res = tt;
-  if (hist) hist[s->its] = res;
-  int reason = dev_converged(s, s->its, res, true, 0.0);
-  if (hapend && !reason) reason = R_DIVERGED_BREAKDOWN;
-  if (reason) { stop(s, reason); return; }
-  if (s->it >= s->max_k || s->its >= s->top.max_it) s->inner_stop = 1;
+  __syncthreads();
+  if (wb)
+    for (int j = threadIdx.x; j <= k + 1; j += blockDim.x) h[j] = hs[j];
 }
 
-// KSPGMRESBuildSoln: back substitution into grs (in place)
-__global__ void gm_buildsoln_kernel(KspState *s, const double *hh, int ld, double *grs) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  s->nv = 0;
+// KSPGMRESBuildSoln: back substitution into grs (in place).  Up to restart
+// 63 the workgroup stages the Hessenberg block and grs in LDS first (thread 0
+// then runs the same operations there: the same bits, without a dependent
+// global load per term).
+constexpr int GM_LDS_K = 64;
+__global__ void __launch_bounds__(256) gm_buildsoln_kernel(KspState *s, const double *hh, int ld, double *grs) {
+  if (blockIdx.x != 0) return;
   const int it = s->it - 1;
+  const bool stage = it >= 0 && it < GM_LDS_K && ld <= GM_LDS_K + 1;
+  __shared__ double hl[GM_LDS_K * (GM_LDS_K + 1)], gl[GM_LDS_K];
+  if (stage) {
+    for (int q = threadIdx.x; q < (it + 1) * ld; q += blockDim.x) hl[q] = hh[q];   // columns 0 .. it
+    for (int q = threadIdx.x; q <= it; q += blockDim.x) gl[q] = grs[q];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s->nv = 0;
   if (it < 0 || s->reason == R_DIVERGED_NULL || s->reason == R_DIVERGED_NANORINF) return;
   if (s->reason == R_DIVERGED_BREAKDOWN && s->ksp_rnorm > 0.0 && s->it == 0) return;
-#define HHd(a, b) hh[(size_t)(b) * ld + (a)]
+  const double *H = stage ? hl : hh;
+  double *G = stage ? gl : grs;
+#define HHd(a, b) H[(size_t)(b) * ld + (a)]
   if (HHd(it, it) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->top.done = 1; return; }
-  grs[it] = grs[it] / HHd(it, it);
+  G[it] = G[it] / HHd(it, it);
   for (int ii = 1; ii <= it; ++ii) {
     const int k = it - ii;
-    double t = grs[k];
-    for (int j = k + 1; j <= it; ++j) t = t - HHd(k, j) * grs[j];
-    if (HHd(k, k) == 0.0) { s->reason = R_DIVERGED_BREAKDOWN; s->top.done = 1; return; }
-    grs[k] = t / HHd(k, k);
+    double t = G[k];
+    for (int j = k + 1; j <= it; ++j) t = t - HHd(k, j) * G[j];
+    if (HHd(k, k) == 0.0) {
+      if (stage) for (int q = 0; q <= it; ++q) grs[q] = gl[q];
+      s->reason = R_DIVERGED_BREAKDOWN; s->top.done = 1; return;
+    }
+    G[k] = t / HHd(k, k);
   }
 #undef HHd
+  if (stage) for (int q = 0; q <= it; ++q) grs[q] = gl[q];
   s->nv = it + 1;
 }
 
@@ -1762,7 +1803,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       HIPCHECK(hipGetLastError());
       ++launched;
     }
-    gm_buildsoln_kernel<<<1, 64, 0, st>>>(s, hh.p, ld, grs.p);
+    gm_buildsoln_kernel<<<1, 256, 0, st>>>(s, hh.p, ld, grs.p);
     gm_update_x_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, ldv, vsc.p, grs.p, x);
     gm_cycle_end_kernel<<<1, 64, 0, st>>>(s);
     HIPCHECK(hipGetLastError());
