@@ -244,7 +244,6 @@ struct PairRuArgs {
   int ndot, xb;
   double c;                    // JM 2: the uniform Jacobi scalar 1 / d
   int *hw;                     // the host's pinned words (Poller)
-  int cache = 0;               // knob 61 (5/7-point): bit 0 r stored non-temporally, bit 1 r read temporally
 };
 
 template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0, bool SYM = false>
@@ -320,10 +319,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
         int eo = ecst;
         if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
         e[q] = bload1(xr, ub + eo);
-        if constexpr (RU) {
-          if (ru.cache & 2) rq[q] = *reinterpret_cast<const dbl2 *>(rin + r0);
-          else rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
-        }
+        if constexpr (RU) rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -350,8 +346,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
           const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
           nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
           nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
-          if (ru.cache & 1) __builtin_nontemporal_store(dbl2{ra, rb}, reinterpret_cast<dbl2 *>(ru.r + r0));
-          else *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+          *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
         } else if constexpr (SYM) {
           static_assert(MODE == SPMV_PW && CLEAN && !SPLIT, "symmetric p.Ap pass: one rank, select-free");
           const dbl2 t = pair_fwd<PS>(L[q], e[q], bw[q], puni);
@@ -1701,7 +1696,7 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   a.fold = fold;
   const bool split = A->sd.pair_ghosts;      // the ghost units' rows: w from the PW pass + boundary kernel
-  const PairRuArgs ru{s, w, r, r0, dot_part, ndot, xb, jac_c, hw, g_knobs.ru_cache};
+  const PairRuArgs ru{s, w, r, r0, dot_part, ndot, xb, jac_c, hw};
   const bool clean = pair_lean_kind(A) == 2, z2 = g_knobs.pair_zm_units == 2;
   ZmFn f;
 #define RU(PS, SP, CL, JM) f = z2 ? &spmv_pair_zm_kernel<SPMV_RUPD, PS, SP, CL, 2, JM> \
