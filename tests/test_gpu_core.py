@@ -143,7 +143,9 @@ def rel(a, b):
 
 @pytest.mark.parametrize("kind,n,ksp", [("poisson3d", 24, "cg"), ("poisson2d", 64, "cg"),
                                        ("poisson3d27", 12, "cg"), ("convdiff3d", 12, "gmres"),
-                                       ("poisson3d", 12, "gmres")])
+                                       ("poisson3d", 12, "gmres"),
+                                       # odd row counts: the chunk MDot's partial chunk and last row
+                                       ("convdiff3d", 13, "gmres"), ("convdiff3d", 29, "gmres")])
 def test_ksp_parity(selfcomm, oracle_mod, kind, n, ksp):
     from mxsolve.core import DMat, rhs_hash
     ip, c, v = oracle_mod.stencil(kind, n)
