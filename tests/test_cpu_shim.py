@@ -22,6 +22,33 @@ def _free_port() -> int:
         return so.getsockname()[1]
 
 
+def _run_gloo_ranks(script, P, attempts=2):
+    """Start P gloo ranks of `script` on a free port; wait for all.  A failed
+    attempt is retried once on a new port (the rendezvous port can be taken
+    between the probe and rank 0's bind); a real failure fails both times and
+    reports both attempts' stderr."""
+    errs = []
+    for _ in range(attempts):
+        port = str(_free_port())
+        procs = []
+        for r in range(P):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True))
+        outs = []
+        for p in procs:
+            try:
+                outs.append(p.communicate(timeout=120))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                outs.append(p.communicate())
+        if all(p.returncode == 0 for p in procs):
+            return outs
+        errs.append("\n".join(e[-1500:] for p, (o, e) in zip(procs, outs) if p.returncode != 0))
+    raise AssertionError("gloo ranks failed:\n" + "\n---\n".join(errs))
+
+
 def test_options_parsing():
     from mxsolve import PETSc
     PETSc.init(["prog", "-ksp_type", "cg", "-ksp_rtol", "1e-8", "-ksp_monitor", "-pc_type", "jacobi",
@@ -124,16 +151,7 @@ def test_mpi_shim_gloo(tmp_path, P):
     script = tmp_path / "rank.py"
     script.write_text(RANK_SCRIPT.format(pkg=PKG, oracle=os.path.join(ROOT, "oracle"),
                                          golden=os.path.join(ROOT, "tests", "golden", "reference_systems.npz")))
-    port = str(_free_port())
-    procs = []
-    for r in range(P):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
-                                      stderr=subprocess.PIPE, text=True))
-    outs = [p.communicate(timeout=120) for p in procs]
-    for p, (o, e) in zip(procs, outs):
-        assert p.returncode == 0, e[-2000:]
+    outs = _run_gloo_ranks(script, P)
     assert outs[0][0].strip().splitlines()[-1] == f"OK {P}"
 
 
@@ -257,14 +275,5 @@ def test_vec_stash_gloo(tmp_path, P):
     """VecSetValues on off-process entries reach their owner at assemblyEnd."""
     script = tmp_path / "vec.py"
     script.write_text(VEC_STASH_SCRIPT.format(pkg=PKG))
-    port = str(_free_port())
-    procs = []
-    for r in range(P):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(P), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
-                                      stderr=subprocess.PIPE, text=True))
-    outs = [p.communicate(timeout=120) for p in procs]
-    for p, (o, e) in zip(procs, outs):
-        assert p.returncode == 0, e[-2000:]
+    outs = _run_gloo_ranks(script, P)
     assert outs[0][0].strip().splitlines()[-1] == f"OK {P}"
