@@ -856,8 +856,10 @@ static int pair_flags(const Mat *A) {
 static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                        int *done_flag, bool split, hipStream_t st, const CgFuse *cgp, const Fold &fold_in,
                        const double *xscale) {
-  // constant-coefficient 5/7-point blocks: the lean row-pair kernels
-  // (mx_spmv_pair.hip; each row's sum has the same bits)
+  // row-pair z-march kernels (mx_spmv_pair.hip; each row's sum has the same
+  // bits): constant-coefficient 5/7/27-point blocks, fp64 row pairs, and the
+  // coded z-march for non-uniform code dictionaries (every non-CG mode,
+  // GMRES's scaled operand included)
   if (!cgp) {
     const int lg = pair_lean_launch(A, mode, split, x, y, partials, done_flag, fold_in, st, jac, xscale);
     if (lg) return lg;
