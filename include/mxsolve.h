@@ -63,8 +63,9 @@ typedef struct {
   double breakdowntol; /* GMRES restart consistency check, 0.1                        */
   int poll_every;      /* host polls the device convergence flag every k its (0: 16) */
   int profile;         /* bit 0: time every SpMV launch with HIP events; bit 1: every
-                          CG mode-5 residual-update launch (one rank: events attached
-                          to the kernel's dispatch)                                  */
+                          CG mode-5 residual-update launch; bit 2: every CG direction-
+                          update launch with batched x steps (cg_pb_kernel; one rank:
+                          events attached to the kernel's dispatch)                  */
 } mx_ksp_params;
 
 typedef struct {
@@ -79,6 +80,8 @@ typedef struct {
   double upd_ms;       /* sum of profiled residual-update launch times (profile bit 1) */
   int upd_count;       /* residual-update launches profiled                         */
   int cg_xbatch;       /* CG: deferred x steps applied every this many iterations    */
+  double pb_ms;        /* sum of profiled direction-update launch times (profile bit 2) */
+  int pb_count;        /* direction-update launches profiled                        */
 } mx_ksp_result;
 
 typedef struct {

@@ -34,6 +34,7 @@
 #include "mx_cg.hpp"
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
+#include "mx_launch.hpp"
 
 namespace mx {
 
@@ -1363,8 +1364,8 @@ static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r
   Fold fin = fin_in;
   fin.ntotal = fin.ncount = (int)g;
   const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 1) ? 2 : 0);
-#define CGPB(JM, BB) cg_pb_kernel<JM, BB><<<g, 256, 0, st>>>(n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], pb.b[3], \
-                                                           x, hist, unr, r0, npart, fin)
+#define CGPB(JM, BB) launch_timed(&cg_pb_kernel<JM, BB>, (int)g, st, n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], \
+                                     pb.b[3], x, hist, unr, r0, npart, fin)
 #define CGPB_J(JM) do { if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
   switch (j.mode) { case 1: CGPB_J(1); break; case 2: CGPB_J(2); break; default: CGPB_J(0); }
 #undef CGPB_J
@@ -1454,6 +1455,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   timer.ext = c->size == 1;
   SpmvTimer utimer((p.profile & 2) != 0, st, std::min(p.max_it, 4096));   // mode 5's residual update
   utimer.ext = c->size == 1;
+  SpmvTimer ptimer((p.profile & 4) != 0, st, std::min(p.max_it, 4096));   // the batched direction update
+  ptimer.ext = c->size == 1;
 
   // r = b - A x  (or b)
   if (p.guess_nonzero) {
@@ -1543,8 +1546,11 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG mode 4 without its MatMult");
     } else {
       double *pi = xb > 1 ? pbs.b[it % xb] : pv.p;
-      if (xb > 1) cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb, wide_pb);
-      else cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
+      if (xb > 1) {
+        ptimer.begin();
+        cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb, wide_pb);
+        ptimer.end();
+      } else cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
       timer.begin();
       nb_spmv = matmult_overlap(A, pi, w.p, fmode == 5 ? SPMV_PW : SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
       timer.end();
@@ -1662,6 +1668,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   res.launched_its = i;
   timer.collect(res.spmv_ms, res.spmv_count);
   utimer.collect(res.upd_ms, res.upd_count);
+  ptimer.collect(res.pb_ms, res.pb_count);
   res.cg_mode = fmode;
   res.cg_xbatch = xb;
   if (hist_host)

@@ -39,7 +39,7 @@ class KSPResult(C.Structure):
     _fields_ = [("its", C.c_int), ("reason", C.c_int), ("rnorm", C.c_double),
                 ("solve_ms", C.c_double), ("spmv_ms", C.c_double), ("spmv_count", C.c_int),
                 ("launched_its", C.c_int), ("cg_mode", C.c_int), ("upd_ms", C.c_double), ("upd_count", C.c_int),
-                ("cg_xbatch", C.c_int)]
+                ("cg_xbatch", C.c_int), ("pb_ms", C.c_double), ("pb_count", C.c_int)]
 
 
 class MatInfo(C.Structure):

@@ -200,3 +200,37 @@ def test_bench_host_csr_equals_oracle_stencil(oracle_mod):
         oi, oc, ov = oracle_mod.stencil(okind, *dims)
         assert ip.dtype == np.int32 and c.dtype == np.int32
         assert np.array_equal(ip, oi) and np.array_equal(c, oc) and np.array_equal(v.view(np.uint64), ov.view(np.uint64))
+
+
+def test_bench_general_leg_checker(oracle_mod):
+    """bench.py's spmv_general leg: the variable-coefficient 7-point operator
+    (canonical CSR: ascending columns, 7n^3 - 6n^2 entries, symmetric, diagonal
+    = the sum of the face kappas) and the row-ordered product it checks the
+    GPU MatMult against, which must equal the oracle's MatMult_SeqAIJ bit for
+    bit (the checker cannot be weaker than the oracle)."""
+    import bench
+    n = 12
+    N, ip, c, v = bench.varcoef_csr(n)
+    assert N == n ** 3 and ip[-1] == 7 * n ** 3 - 6 * n ** 2
+    assert all(np.all(np.diff(c[ip[i]:ip[i + 1]]) > 0) for i in range(N))
+    import scipy.sparse as sp
+    A = sp.csr_matrix((v, c, ip), shape=(N, N))
+    assert abs(A - A.T).max() == 0.0
+    d = A.diagonal()
+    assert len(np.unique(v)) > 2 * N and np.all(d > 0)
+    O = oracle_mod.OracleMat.from_csr(N, N, ip, c, v)
+    for seed in range(3):
+        x = np.random.default_rng(seed).standard_normal(N)
+        got = bench.csr_rowsum_reference(ip, c, v, x)
+        assert np.array_equal(got.view(np.uint64), O.mult(x).view(np.uint64))
+
+
+def test_bench_parity_record():
+    """bench.py's parity block: ok only with equal its, equal reason and
+    rel-L2 <= 1e-10."""
+    import bench
+    o = {"its": 560, "reason": 2, "P": 1, "solve_s": 1.0}
+    assert bench.parity_record(560, 2, 3e-14, o)["ok"]
+    assert not bench.parity_record(561, 2, 3e-14, o)["ok"]
+    assert not bench.parity_record(560, 3, 3e-14, o)["ok"]
+    assert not bench.parity_record(560, 2, 2e-10, o)["ok"]

@@ -1,0 +1,64 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces round 3's one-off gpu_r3*.sh).
+#
+#   gpurun --timeout S -- bash tools/gpu_run.sh TAG STEP [STEP ...]
+#
+# Each STEP runs under its own time limit, writes gpurun_out/TAG_STEP.log (or
+# .json), and appends the exact command to gpurun_out/TAG_commands.txt so every
+# summary copied into profiles/ can name the command that produced it.  The
+# first failing step ends the run (no GPU step after a failure).
+#
+# Steps:
+#   suite            the whole GPU test suite (as the driver runs it)
+#   tests:EXPR       pytest -m gpu -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench20          bench.py --steps 20 --warmup 5 (the driver's K/W class)
+#   bench            bench.py with its defaults (K = 500)
+#   benchfast        bench.py --steps 100 --no-cpu --no-asm --no-general
+#   shm2             N = 2 rehearsal on one GPU (MXSOLVE_TRANSPORT=shm, torchrun)
+#   prof             tools/profile.sh (trace + FETCH/WRITE PMC passes + calibration)
+#   configs          tools/bench_configs.py (C2/C3/C4/C5-share converged solves)
+#   general:LEGS     tools/bench_general.py LEGS (comma separated)
+#   py:SCRIPT[:ARGS] python3 SCRIPT ARGS (ARGS comma separated)
+set -o pipefail
+TAG=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+O=gpurun_out
+mkdir -p $O
+export TMPDIR=/tmp
+(while true; do date > $O/hb; sleep 30; done) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+
+run() {   # run NAME SECONDS CMD... ; output to $O/TAG_NAME.log
+  local name=$1 secs=$2; shift 2
+  local log=$O/${TAG}_${name}.log
+  echo "[$(date +%T)] $name: $*" | tee -a $O/${TAG}_commands.txt
+  timeout -k 10 "$secs" "$@" > "$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "step $name failed rc=$rc"; tail -40 "$log"; exit $rc
+  fi
+  tail -3 "$log"
+}
+
+for step in "$@"; do
+  case $step in
+    suite) run suite 1100 python3 -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread --durations=20 ;;
+    tests:*) run "tests_${step#tests:}" 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${step#tests:}" ;;
+    smoke) run smoke 400 python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench20) run bench20 500 python3 -u bench.py --steps 20 --warmup 5 ;;
+    bench) run bench 500 python3 -u bench.py ;;
+    benchfast) run benchfast 300 python3 -u bench.py --steps 100 --no-cpu --no-asm --no-general ;;
+    shm2) MXSOLVE_TRANSPORT=shm run shm2 400 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 50 --warmup 5 ;;
+    prof) run prof 1000 bash tools/profile.sh ;;
+    configs) run configs 700 python3 -u tools/bench_configs.py ;;
+    general:*) run general 700 python3 -u tools/bench_general.py $(echo "${step#general:}" | tr , ' ') ;;
+    py:*) s=${step#py:}; scr=${s%%:*}; a=""; [ "$s" != "$scr" ] && a=$(echo "${s#*:}" | tr , ' ')
+          run "py_$(basename "$scr" .py)" 900 python3 -u "$scr" $a ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps done"
