@@ -273,14 +273,15 @@ def stream_copy_gbps(device, n: int) -> float:
     return 2 * 8 * n * 20 / (e0.elapsed_time(e1) * 1e-3) / 1e9
 
 
-def load_traffic(grid: int, n_gpus: int, mode: int):
+def load_traffic(grid: int, n_gpus: int, mode: int, suffix: str | None = None):
     """Committed PMC traffic of the roofline kernel (profiles/spmv_traffic.json,
-    key "<grid>^3/N<n>" plus "/mode5" for mode 5's residual update)."""
+    key "<grid>^3/N<n>" plus "/mode5" for mode 5's residual update, or the
+    given suffix: "/pb" for the direction update)."""
     path = os.path.join(ROOT, "profiles", "spmv_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        key = f"{grid}^3/N{n_gpus}" + ("/mode5" if mode == 5 else "")
+        key = f"{grid}^3/N{n_gpus}" + (suffix if suffix is not None else "/mode5" if mode == 5 else "")
         return d.get(key)
     except (OSError, ValueError):
         return None
@@ -687,6 +688,9 @@ def main():
                "avg_launch_ms": round(pb_ms, 5), "launches": rp["pb_count"], "bytes_per_launch": pb_bytes,
                "GBps": round(pb_bytes / (pb_ms * 1e-3) / 1e9, 1),
                "frac": round(pb_bytes / (pb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        tp = load_traffic(n, world, mode, "/pb")
+        dom.update({"traffic": tp["bytes_per_launch"] if tp else None,
+                    "traffic_source": tp.get("source") if tp else None})
     # standalone SpMV timing (same kernel, back-to-back)
     y = comm.empty(m)
     spmv_alone_ms, mult_ms = A.bench_mult(b, y, 50)

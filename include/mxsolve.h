@@ -265,9 +265,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 9: CG fusion: 0 separate passes; 1 direction update + x step inside the
  *        MatMult; 2 x step deferred into the direction update; 3 auto (default:
  *        5 on one rank where it applies, 2 on P > 1 ranks with the z-march
- *        MatMult, else 1 for <= 3M local rows, else 2); 4 mode 2 with the direction update and
- *        the batched x steps inside the z-march MatMult (one rank, lean z-march
- *        layout, no or uniform Jacobi; else 2; mode 2's bits); 5 mode 2 whose
+ *        MatMult, else 1 for <= 3M local rows, else 2); 4 (retired in round 4:
+ *        runs as 2); 5 mode 2 whose
  *        MatMult stores no product: a p.Ap pass, and the update pass
  *        recomputes A p where it forms r - alpha A p (one rank, lean 5/7-point
  *        z-march layout, no or uniform Jacobi; else 2)
@@ -283,9 +282,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         vector is aligned (0/1, default 0: one row per thread per step)
  * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
  * key 15: grid cap of the halo-boundary SpMV launch (0 = default 2048)
- * key 16: GMRES VecMDot vectors per pass over w (4, 8, 16 or 32; default 8: one
- *         pass over w per 8 basis vectors measured 1.4% faster per GMRES(30) step
- *         than 32 at 256^3 -- the 32-wide kernel holds 139 VGPRs)
+ * key 16: GMRES VecMDot vectors per pass over w with key 50 = 0 (4 or 8;
+ *         default 8: measured 1.4% faster per GMRES(30) step than 32 at 256^3;
+ *         the 16/32-wide kernels were dropped in round 4 -- they spilled 30 / 142
+ *         SGPRs)
  * key 18: library buffers >= 64 MiB physically contiguous when the driver can
  *         provide them (hipDeviceMallocContiguous, else hipMalloc; 0/1, default 1)
  * key 19: one-byte row masks for aligned-offset slices when every slice has
@@ -333,8 +333,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 46: CG mode 5: the residual-update pass folds the p.Ap pass's partials
  *         itself (1, default) or a one-block fold kernel runs between (0)
  * key 47: deadline in ms of the RCCL waits that observe no progress (stream /
- *         event waits, setup collectives, barrier); 0 = none (default: a slow
- *         peer is not an error, as with MPI)
+ *         event waits, setup collectives, barrier); 0 = none (default 600000:
+ *         a slow peer is not an error, a dead one fails the call after 10 min).
+ *         The GMRES restart read-back observes the step count (key 33)
  * key 48: 27-point column words (read at assembly; 0/1, default 1): the
  *         27-point z-march zeroes empty runs and x-line edges where it loads
  *         them (no per-run branches, no selects; the same bits)
@@ -366,6 +367,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         uniform per slot (1, default; 0: the general SELL kernel)
  * key 53: z-march terms of slots whose value is -1, 0 or +1 formed by fma (an
  *         exact product: the same bits; 1, default; 0: multiply and add)
+ * key 61: testing: a device stall of this many us before each GMRES restart
+ *         read-back (default 0), so the no-progress deadline can be driven
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -146,9 +146,12 @@ struct RcclComm : Comm {
   // the count of iterations begun, which the device advances) fails after
   // knob 33 ms (default 120 s) WITHOUT progress -- the timer re-arms whenever
   // the count moves, so a long healthy solve never trips it; a wait that
-  // cannot (stream/event waits, setup collectives, barrier) has no deadline
-  // unless knob 47 sets one (ms, default 0 = wait as MPI would: a slow peer,
-  // e.g. one still building its CSR on the host, is not an error).
+  // cannot (stream/event waits, setup collectives, barrier) fails after knob
+  // 47 ms (default 600 s: a slow peer, e.g. one still building its CSR on the
+  // host, is not an error, but a dead one on a transport that reports no
+  // asynchronous error does not hang the rank forever; 0 = no deadline).
+  // GMRES's restart read-back observes progress (gm_step_kernel stores a step
+  // count into the host word), so it runs under knob 33 like the CG poller.
   template <class Q> void watch(Q query, const char *what, const std::function<long long()> &progress = {}) {
     const int limit = progress ? g_knobs.comm_timeout_ms : g_knobs.comm_wait_ms;
     auto t0 = std::chrono::steady_clock::now();

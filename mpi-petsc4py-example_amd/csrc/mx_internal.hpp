@@ -253,8 +253,8 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
-                int comm_wait_ms = 0; int pair_col27 = 1; int pair_zm27_units = 1;
-                int mdot_split = 2; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 0; int pw_sym27 = 1; int pair_zm27p = 1; };
+                int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
+                int mdot_split = 2; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 0; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -416,7 +416,7 @@ enum Dispatch {
   DSP_PAIR_ZM27_SPLIT = 6,
   DSP_PAIR_ZMF64 = 7,
   DSP_PAIR_ZMF64_SPLIT = 8,
-  DSP_PAIR_ZMCG = 9,     // CG mode 4
+  DSP_PAIR_ZMCG = 9,     // retired (round 2's CG mode 4, removed in round 4); slot kept for the ABI's order
   DSP_BOUNDARY = 10,     // spmv_boundary_kernel
   DSP_ZM_PW = 11,        // CG mode 5: the z-march p.Ap pass (no product stored)
   DSP_ZM_RUPD = 12,      // CG mode 5: the z-march residual update (product recomputed)
@@ -436,10 +436,6 @@ void pair_sym_prepare(Mat *A);          // Mat::sym, once per operator, before a
 int pair_lean_kind(const Mat *A);   // 0 general kernel, 1 lean, 2 lean select-free (mx_mat_info.pair_lean)
 bool pair_zm_applies(const Mat *A);  // the lean kernel's z-march form (mx_mat_info.pair_zmarch)
 int pair_f64_kind(const Mat *A);     // 5 / 7: the fp64 row-pair z-march applies (mx_mat_info.pair_f64)
-// CG mode 4: the direction update inside the z-march MatMult (mx_spmv_pair.hip)
-bool pair_zmcg_applies(const Mat *A, int jac_mode);
-int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac_c, const double *r, double *pb0,
-                     double *pb1, double *x, double *w, double *partials, const Fold *fold, hipStream_t st);
 // CG mode 5: w = A p is not stored -- the p.Ap pass (matmult_overlap with
 // SPMV_PW; on P > 1 ranks only the ghost units' rows are stored and finished
 // by the boundary kernel) gives p.w, the update pass recomputes A p where it

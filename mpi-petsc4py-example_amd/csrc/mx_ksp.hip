@@ -859,25 +859,43 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
       const int64_t i = c0 + k * 256 + threadIdx.x;
       wr[k] = (FULL || i < n2) ? w2[i] : dbl2{0.0, 0.0};
     }
+    // vectors two at a time (the loads of both in flight before either sum);
+    // round 3's fully unrolled walk over 32 guarded vectors kept every
+    // vector's base address and scale live in SGPRs: 126 SGPR spills
+    for (int j = 0; j < nv; j += 2) {              // wave-uniform
+      const bool two = j + 1 < nv;
+      const double s0 = vscale[j], s1 = two ? vscale[j + 1] : 0.0;
+      const dbl2 *__restrict__ v0 = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
+      const dbl2 *__restrict__ v1 = reinterpret_cast<const dbl2 *>(V + (int64_t)(two ? j + 1 : j) * ldv);
+      dbl2 t0[WP], t1[WP];
 #pragma unroll
-    for (int j = 0; j < NVX; ++j) {
-      if (j < nv) {                                // wave-uniform
-        const double sj = vscale[j];
-        const dbl2 *__restrict__ vj = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
-        dbl2 t[WP];
+      for (int k = 0; k < WP; ++k) {
+        const int64_t i = c0 + k * 256 + threadIdx.x;
+        t0[k] = (FULL || i < n2) ? __builtin_nontemporal_load(v0 + i) : dbl2{0.0, 0.0};
+      }
+      if (two) {
 #pragma unroll
         for (int k = 0; k < WP; ++k) {
           const int64_t i = c0 + k * 256 + threadIdx.x;
-          t[k] = (FULL || i < n2) ? __builtin_nontemporal_load(vj + i) : dbl2{0.0, 0.0};
+          t1[k] = (FULL || i < n2) ? __builtin_nontemporal_load(v1 + i) : dbl2{0.0, 0.0};
         }
-        double a = 0.0;
+      }
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < WP; ++k) {
+        a0 += wr[k].x * (s0 * t0[k].x);
+        a0 += wr[k].y * (s0 * t0[k].y);
+      }
+      a0 = wave_sum(a0);
+      if (lane == j) acc += a0;
+      if (two) {
 #pragma unroll
         for (int k = 0; k < WP; ++k) {
-          a += wr[k].x * (sj * t[k].x);
-          a += wr[k].y * (sj * t[k].y);
+          a1 += wr[k].x * (s1 * t1[k].x);
+          a1 += wr[k].y * (s1 * t1[k].y);
         }
-        a = wave_sum(a);
-        if (lane == j) acc += a;
+        a1 = wave_sum(a1);
+        if (lane == j + 1) acc += a1;
       }
     }
   };
@@ -1015,7 +1033,11 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
 // same order, so the same bits).
 __global__ void __launch_bounds__(256) gm_step_kernel(KspState *s, int k, const double *partials, int nblocks,
                                                       int fused, double *hh, int ld, double *grs, double *cc,
-                                                      double *ss, double *hist, double *vscale) {
+                                                      double *ss, double *hist, double *vscale, int *hw,
+                                                      int step) {
+  // the host's progress word: this launch (a no-op after a stop too) ran --
+  // the restart read-back's wait re-arms its no-progress deadline on it
+  if (hw && threadIdx.x == 0) host_store(hw + HW_PROGRESS, step);
   if (s->inner_stop) return;
   (void)gather_red<1>(s, partials, nblocks, fused);   // every thread: the fold syncs the workgroup
   __shared__ double hs[MAX_RESTART + 2], cs[MAX_RESTART + 1], sn[MAX_RESTART + 1];
@@ -1261,7 +1283,7 @@ void init_state(KspState &h, const mx_ksp_params &p, int normtype) {
 
 // device state -> host through the operator's pinned staging buffer (a
 // pageable copy is staged and synchronous in the runtime)
-void read_state(Mat *A, hipStream_t st, const KspState *d, KspState &h) {
+[[maybe_unused]] void read_state(Mat *A, hipStream_t st, const KspState *d, KspState &h) {
   solve_resources(A);
   HIPCHECK(hipMemcpyAsync(A->state_pinned, d, sizeof(KspState), hipMemcpyDeviceToHost, st));
   A->comm->wait_stream(st);
@@ -1367,7 +1389,7 @@ static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r
 #define CGPB(JM, BB) launch_timed(&cg_pb_kernel<JM, BB>, (int)g, st, n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], \
                                      pb.b[3], x, hist, unr, r0, npart, fin)
 #define CGPB_J(JM) do { if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
-  switch (j.mode) { case 1: CGPB_J(1); break; case 2: CGPB_J(2); break; default: CGPB_J(0); }
+  switch (j.mode) { case 1: CGPB(1, 2); break; case 2: CGPB_J(2); break; default: CGPB_J(0); }
 #undef CGPB_J
 #undef CGPB
   HIPCHECK(hipGetLastError());
@@ -1411,9 +1433,6 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // mode 2 batches B x steps (knob 29; 2 or 4 p buffers) when the batch of
   // launched iterations (poll) is a multiple of B; 1 = the x step every iteration
   const int poll = p.poll_every > 0 ? p.poll_every : 16;
-  // mode 4 (knob 9 = 4): mode 2 whose direction update rides in the z-march
-  // MatMult (mx_spmv_pair.hip spmv_pair_zmcg_kernel) -- one rank, a lean
-  // z-march layout, no or uniform Jacobi, x steps batched by 2; otherwise 2
   // auto (3): mode 5 on one rank where it applies (a lean 5/7-point z-march);
   // on P > 1 ranks mode 2 where the z-march applies (the interior-rank proxy,
   // tools/rank_proxy.py, round 3: kernel time per iteration at 2 M rows/rank
@@ -1425,21 +1444,23 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     else if (pair_lean_kind(A) > 0 && pair_zm_applies(A)) fmode = 2;
     else fmode = n <= CG_FUSE_MAX_ROWS ? 1 : 2;
   }
-  if (fmode == 4 && !(pair_zmcg_applies(A, dinv.mode) && (g_knobs.cg_xbatch == 2 || g_knobs.cg_xbatch == 0) &&
-                      poll % 2 == 0 && !p.guess_nonzero))
-    fmode = 2;
+  if (fmode == 4) fmode = 2;   // round 2's mode 4 (the direction update inside the MatMult) is retired
   // mode 5 (knob 9 = 5): mode 2 whose MatMult stores no product -- a p.Ap
   // pass, then the update pass recomputes A p (mx_spmv_pair.hip SPMV_PW /
   // SPMV_RUPD) -- one rank, a lean 5/7-point z-march layout, no or uniform
   // Jacobi; otherwise 2
   if (fmode == 5 && !pair_cg5_applies(A, dinv.mode)) fmode = 2;
   // x-step batch (knob 29; 0 = auto: 4 in mode 5 -- 256^3: -2.8% per iteration
-  // against 2 -- else 2; mode 4 always 2)
+  // against 2 -- else 2)
   // mode 5 on a symmetric 5/7-point operator: the forward-half p.Ap pass
   // (checked once per operator, before any capture)
   if (fmode == 5) pair_sym_prepare(A);
-  const int xbk = g_knobs.cg_xbatch == 0 ? (fmode == 5 ? 4 : 2) : fmode == 4 ? 2 : g_knobs.cg_xbatch;
-  const int xb = ((fmode == 2 || fmode == 4 || fmode == 5) && (xbk == 2 || xbk == 4) && poll % xbk == 0) ? xbk : 1;
+  // (batches of 4 only with no or a uniform Jacobi: the vector-Jacobi
+  // direction update with four p buffers spilled SGPRs and is not on any
+  // default path -- mode 5, the only one batching by 4, needs a uniform one)
+  const int xbk = g_knobs.cg_xbatch == 0 ? (fmode == 5 ? 4 : 2) : (g_knobs.cg_xbatch == 4 && dinv.mode == 1) ? 2
+                                                                                                           : g_knobs.cg_xbatch;
+  const int xb = ((fmode == 2 || fmode == 5) && (xbk == 2 || xbk == 4) && poll % xbk == 0) ? xbk : 1;
   const bool wide_pb = fmode == 5;
   Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist, xb == 4 ? nv : 0, xb == 4 ? nv : 0})));
   struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
@@ -1539,11 +1560,6 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       timer.begin();
       nb_spmv = matmult_overlap(A, nullptr, w.p, SPMV_CG, Jac{}, part.p, done, &cg, fdot_p);
       timer.end();
-    } else if (fmode == 4 && it > 0) {
-      timer.begin();
-      nb_spmv = pair_zmcg_launch(A, s, hist_d, dinv.mode, dinv.c, r.p, pbs.b[0], pbs.b[1], x, w.p, part.p, fdot_p, st);
-      timer.end();
-      if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG mode 4 without its MatMult");
     } else {
       double *pi = xb > 1 ? pbs.b[it % xb] : pv.p;
       if (xb > 1) {
@@ -1632,9 +1648,6 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       graph = false;
     }
   };
-  // mode 4: iteration 0 (its direction update also forms the initial norms)
-  // runs as mode 2, eagerly; the captured batches start at iteration 1
-  if (fmode == 4 && p.max_it > 0) iteration(i++);
   if (graph && !use_graph && c->size == 1 && i < p.max_it) capture();
   for (; i < p.max_it;) {
     if (use_graph && p.max_it - i >= poll) {
@@ -1705,14 +1718,12 @@ static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, in
     HIPCHECK(hipGetLastError());
     return;
   }
-  const int gw = g_knobs.mdot_group == 16 || g_knobs.mdot_group == 32 || g_knobs.mdot_group == 4 ? g_knobs.mdot_group : 8;
+  const int gw = g_knobs.mdot_group == 4 ? 4 : 8;
   for (int j0 = 0; j0 < nv; j0 += gw) {
     const int k = std::min(gw, nv - j0);
     if (k <= 2) launch_mdot<2>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
     else if (k <= 4) launch_mdot<4>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
-    else if (k <= 8) launch_mdot<8>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
-    else if (k <= 16) launch_mdot<16>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
-    else launch_mdot<32>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
+    else launch_mdot<8>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
     HIPCHECK(hipGetLastError());
   }
 }
@@ -1779,6 +1790,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   }
   int first = 1, launched = 0;
   int *istop = &s->inner_stop;
+  Poller poller(A, st);            // its pinned words: the step count (HW_PROGRESS)
   Fold fnorm;                      // ||w||^2 of the MAXPY pass, folded in-launch into s->red[0]
   fnorm.cnt = s->fold_upd; fnorm.out = sred; fnorm.ntotal = fnorm.ncount = RED_BLOCKS;
   while (true) {
@@ -1806,15 +1818,20 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
       (g_knobs.maxpy_pairs ? &maxpy_norm_kernel<true> : &maxpy_norm_kernel<false>)<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
       c->allreduce_sum(sred, 1);
-      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p);
-      HIPCHECK(hipGetLastError());
       ++launched;
+      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p,
+                                        poller.hw, launched);
+      HIPCHECK(hipGetLastError());
     }
     gm_buildsoln_kernel<<<1, 256, 0, st>>>(s, hh.p, ld, grs.p);
     gm_update_x_kernel<<<egrid, 256, 0, st>>>(n, s, V.p, ldv, vsc.p, grs.p, x);
     gm_cycle_end_kernel<<<1, 64, 0, st>>>(s);
     HIPCHECK(hipGetLastError());
-    read_state(A, st, s, hs);
+    if (g_knobs.gm_stall_us > 0) debug_stall(st, g_knobs.gm_stall_us);   // knob 61: the deadline tests
+    // the cycle's state read-back: a wait that observes the step count
+    HIPCHECK(hipMemcpyAsync(A->state_pinned, s, sizeof(KspState), hipMemcpyDeviceToHost, st));
+    c->wait_until([] { return false; }, st, [&] { return (long long)poller.word(HW_PROGRESS); });
+    std::memcpy(&hs, A->state_pinned, sizeof(KspState));
     if (hs.top.done) break;
   }
   HIPCHECK(hipEventRecord(ev.b, st));

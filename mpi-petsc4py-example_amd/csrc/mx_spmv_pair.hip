@@ -1072,157 +1072,6 @@ __global__ void __launch_bounds__(256) spmv_pair_zmc_kernel(const PairLeanArgs a
   }
 }
 
-// CG mode 4 (knob 9 = 4): the direction update rides in the z-march MatMult.
-// Every operand value is formed where it is read, p_i(j) = z(j) + b p_{i-1}(j)
-// with z = r (JM 0) or c r (JM 2, uniform Jacobi) -- cg_pb_kernel's row(),
-// the same expression, so the same bits -- from r and p_{i-1}, which no
-// kernel of this launch writes.  Along a column the formed -D and centre
-// pairs are carried, so the +D plane (r and p_{i-1}: the lines read from HBM
-// for the first time) is formed once per unit; the +-n pairs and the edge
-// values are formed from L2-resident r / p_{i-1} lines.  At its own rows a
-// unit stores p_i (the centre pair) into buffer i % 2 and, every second
-// iteration, applies the two pending x steps (x = fma(a_{i-1}, p_{i-1},
-// fma(a_{i-2}, p_{i-2}, x)), reading p_{i-2} from that buffer before p_i
-// overwrites it -- cg_pb_kernel's batch).  The grid, the task order and the
-// per-lane p.w order are the plain z-march MatMult's, so mode 4 gives mode
-// 2's bits (tests/test_gpu_cgfuse.py).  One rank; iteration 0 runs as mode 2
-// (its direction update also forms the initial norms).
-struct PairCgArgs {
-  KspState *s;
-  double *hist;
-  double c;                    // JM 2: the uniform Jacobi scalar 1 / d
-};
-
-template <int PS, bool CLEAN, int ZU, int JM>
-__global__ void __launch_bounds__(256) spmv_pair_zmcg_kernel(const PairLeanArgs a, const PairCgArgs cga,
-                                                             const double *__restrict__ r, double *__restrict__ pb0,
-                                                             double *__restrict__ pb1, double *__restrict__ xv,
-                                                             double *__restrict__ y, const int32_t *__restrict__ pblk,
-                                                             const PairUni *__restrict__ puni) {
-  const CgTopIn top = cga.s->top;
-  if (top.done) return;                            // wave-uniform: solver finished
-  const CgTop t = cg_top(top);
-  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(cga.s, t, cga.hist);
-  if (t.reason) return;
-  const int it = t.i;
-  const double bb = t.b, jc = cga.c;
-  // p_{i-1} in buffer (i - 1) % 2, p_i into buffer i % 2 (wave-uniform selects)
-  const double *__restrict__ pprev = (it & 1) ? pb0 : pb1;
-  double *__restrict__ pout = (it & 1) ? pb1 : pb0;
-  const bool xbatch = (it & 1) == 0 && top.xhi == it && top.xlo == it - 2;
-  const double al0 = top.xal[0], al1 = top.xal[1];
-  const bool xz = top.xlo == 0 && cga.s->guess_zero;   // x's first write: not read (+0.0)
-  auto form = [&](double rr, double po) __attribute__((always_inline)) -> double {
-    const double z = JM == 2 ? rr * jc : rr;
-    return (bb == 0.0) ? z : z + bb * po;             // VecAYPX_Seq (b == 0 copies)
-  };
-  auto form2 = [&](dbl2 rv, dbl2 pv) __attribute__((always_inline)) -> dbl2 {
-    return dbl2{form(rv.x, pv.x), form(rv.y, pv.y)};
-  };
-  using SH = PairShape<PS>;
-  constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int sb, se, W, w;
-  if ((gridDim.x & 7) == 0) {
-    const int xcd = blockIdx.x & 7;
-    W = (gridDim.x >> 3) * LEAN_WAVES;
-    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
-    sb = a.S * xcd / 8;
-    se = a.S * (xcd + 1) / 8;
-  } else {
-    W = gridDim.x * LEAN_WAVES;
-    w = blockIdx.x * LEAN_WAVES + wid;
-    sb = 0;
-    se = a.S;
-  }
-  const __amdgpu_buffer_rsrc_t rr_ = vec_rsrc(r, a.n), pr_ = vec_rsrc(pprev, a.n);
-  const int D = a.anchor[LAST];
-  const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
-  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
-  double dot = 0.0;
-  const int ntask = (se - sb) * a.P;
-  for (int tk = w; tk < ntask; tk += W) {
-    const int seg = sb + tk / a.P, col = tk % a.P;
-    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
-    const int cb = col * 128 + 2 * lane;
-    // carried: the formed -D and centre pairs, and p_{i-1} at the centre
-    dbl2 pcr = bload2(pr_, z0 * D + cb);
-    dbl2 zm = form2(bload2(rr_, z0 * D + cb - D), bload2(pr_, z0 * D + cb - D)), c = form2(bload2(rr_, z0 * D + cb), pcr);
-    uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
-    auto step = [&](int z, auto nq) __attribute__((always_inline)) {
-      constexpr int NQ = decltype(nq)::value;
-      dbl2 Rr[NQ][NR], Pp[NQ][NR];             // raw r / p_{i-1} of the loaded runs
-      double er[NQ], ep[NQ];
-      dbl2 xo[NQ], po2[NQ];
-      uint32_t bw[NQ];
-      bw[0] = bwn;
-#pragma unroll
-      for (int q = 1; q < NQ; ++q) bw[q] = (uint32_t)pblk[(z + q) * a.P + col];
-      if (z + NQ < z1) bwn = (uint32_t)pblk[(z + NQ) * a.P + col];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
-        Rr[q][LAST] = bload2(rr_, r0 + D);
-        Pp[q][LAST] = bload2(pr_, r0 + D);
-#pragma unroll
-        for (int rn = 1; rn < LAST; ++rn)
-          if (rn != TR) {
-            const int o = r0 + a.anchor[rn] + (CLEAN && (bw[q] & (PBLK_RUN0 << rn)) ? PAIR_OOR : 0);
-            Rr[q][rn] = bload2(rr_, o);
-            Pp[q][rn] = bload2(pr_, o);
-          }
-        int eo = ecst;
-        if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
-        er[q] = bload1(rr_, ub + eo);
-        ep[q] = bload1(pr_, ub + eo);
-        if (xbatch) {                            // p_{i-2} and x at the own rows (own lanes only)
-          po2[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(pout + r0));
-          xo[q] = xz ? dbl2{0.0, 0.0} : __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(xv + r0));
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int r0 = (z + q) * D + cb;
-        dbl2 L[NR];
-        const dbl2 pnext = form2(Rr[q][LAST], Pp[q][LAST]);
-#pragma unroll
-        for (int rn = 1; rn < LAST; ++rn)
-          if (rn != TR) L[rn] = form2(Rr[q][rn], Pp[q][rn]);
-        L[0] = zm;
-        L[TR] = c;
-        L[LAST] = pnext;
-        const double e = form(er[q], ep[q]);
-        // own rows: p_i (the centre pair), then the batched x steps from
-        // p_{i-2} (read above, before this store) and p_{i-1}
-        if (xbatch) {
-          const dbl2 xx = dbl2{fma(al0, po2[q].x, xo[q].x), fma(al0, po2[q].y, xo[q].y)};
-          const dbl2 xn = dbl2{fma(al1, pcr.x, xx.x), fma(al1, pcr.y, xx.y)};
-          __builtin_nontemporal_store(xn, reinterpret_cast<dbl2 *>(xv + r0));
-        }
-        *reinterpret_cast<dbl2 *>(pout + r0) = c;
-        if constexpr (CLEAN) {
-          if (bw[q] & CARRY) {                     // wave-uniform, rare: an empty carried run
-            if (bw[q] & PBLK_RUN0) L[0] = dbl2{0.0, 0.0};
-            if (bw[q] & (PBLK_RUN0 << TR)) L[TR] = dbl2{0.0, 0.0};
-            if (bw[q] & (PBLK_RUN0 << LAST)) L[LAST] = dbl2{0.0, 0.0};
-          }
-        }
-        pair_unit<SPMV_DOT, PS, false, CLEAN>(L, e, bw[q], puni, y, r0, lane, dot);
-        zm = c;
-        c = pnext;
-        pcr = Pp[q][LAST];
-      }
-    };
-    int z = z0;
-    for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
-    for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
-  }
-  double v[1] = {dot};
-  block_partials<1>(v, a.partials, gridDim.x, a.fold);
-}
-
 using LeanFn = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const PairUni *);
 using ZmFn = void (*)(PairLeanArgs, const double *, double *, const int32_t *, const PairUni *, PairRuArgs);
 
@@ -1457,10 +1306,12 @@ __global__ void sym_check_kernel(int64_t m, const int64_t *__restrict__ ptr, con
   }
 }
 
+// (the result is cached per operator; knob 59 is read where the pass is
+// launched, so turning it on later still gets the check)
 void pair_sym_prepare(Mat *A) {
-  if (A->sym >= 0) return;
+  if (A->sym >= 0 || !g_knobs.pw_sym27) return;
   A->sym = 0;
-  if (!g_knobs.pw_sym27 || A->comm->size != 1 || A->nghost != 0 || A->m != A->n || A->m <= 0 ||
+  if (A->comm->size != 1 || A->nghost != 0 || A->m != A->n || A->m <= 0 ||
       (A->sd.pair_shape != 5 && A->sd.pair_shape != 7) || !A->dptr.p)
     return;
   hipStream_t st = A->comm->stream;
@@ -1605,54 +1456,6 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   note_dispatch(mode == SPMV_PW ? DSP_ZM_PW : !zm ? DSP_PAIR_LEAN : split ? DSP_PAIR_ZM_SPLIT : DSP_PAIR_ZM);
   if (zm) launch_timed(fz, grid, st, a, x, y, S.pblk.p, S.puni.p, PairRuArgs{});
   else launch_timed(f, grid, st, a, x, y, S.pblk.p, S.puni.p);
-  HIPCHECK(hipGetLastError());
-  return grid;
-}
-
-// CG mode 4 (spmv_pair_zmcg_kernel): applies on one rank to a lean z-march
-// layout with no or uniform Jacobi; returns the grid, 0 when it does not apply
-bool pair_zmcg_applies(const Mat *A, int jac_mode) {
-  return A->comm->size == 1 && A->sd.pair_shape != 27 && (jac_mode == 0 || jac_mode == 2) && pair_lean_kind(A) > 0 &&
-         pair_zm_applies(A) &&
-         A->nghost == 0 && !A->sd.pair_ghosts;
-}
-
-int pair_zmcg_launch(Mat *A, KspState *s, double *hist, int jac_mode, double jac_c, const double *r, double *pb0,
-                     double *pb1, double *x, double *w, double *partials, const Fold *fold_in, hipStream_t st) {
-  if (!pair_zmcg_applies(A, jac_mode)) return 0;
-  const Sell &S = A->sd;
-  PairLeanArgs a{};
-  a.m = (int)A->m;
-  a.n = (int)A->n;
-  a.nunits = (int)S.nunits;
-  pair_anchors(S, a.anchor);
-  a.partials = partials;
-  const int D = a.anchor[S.pair_shape == 5 ? 2 : 4];
-  a.P = D / 128;
-  a.NZ = (int)(A->m / D);
-  int grid = std::max(8, g_knobs.pair_zm_bpc * device_cu_count());
-  grid &= ~7;
-  const int W = grid / 8 * LEAN_WAVES;
-  const int slab = (a.NZ + 7) / 8;
-  int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
-  while (L > 1 && (int64_t)a.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
-  a.L = L;
-  a.S = (a.NZ + L - 1) / L;
-  Fold fold = fold_in ? *fold_in : Fold{};
-  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
-  a.fold = fold;
-  const PairCgArgs c{s, hist, jac_c};
-  const bool clean = pair_lean_kind(A) == 2;
-  using F = void (*)(PairLeanArgs, PairCgArgs, const double *, double *, double *, double *, double *,
-                     const int32_t *, const PairUni *);
-  F f = nullptr;
-#define ZMCG(PS, CL) do { if (jac_mode == 2) f = g_knobs.pair_zm_units == 2 ? &spmv_pair_zmcg_kernel<PS, CL, 2, 2> : &spmv_pair_zmcg_kernel<PS, CL, 1, 2>; \
-                          else f = g_knobs.pair_zm_units == 2 ? &spmv_pair_zmcg_kernel<PS, CL, 2, 0> : &spmv_pair_zmcg_kernel<PS, CL, 1, 0>; } while (0)
-  if (S.pair_shape == 5) { if (clean) ZMCG(5, true); else ZMCG(5, false); }
-  else { if (clean) ZMCG(7, true); else ZMCG(7, false); }
-#undef ZMCG
-  note_dispatch(DSP_PAIR_ZMCG);
-  launch_timed(f, grid, st, a, c, r, pb0, pb1, x, w, S.pblk.p, S.puni.p);
   HIPCHECK(hipGetLastError());
   return grid;
 }

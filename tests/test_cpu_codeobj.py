@@ -4,8 +4,11 @@ row-pair unit's registers on the stack (432 bytes per lane) and halved the
 SpMV's speed with every parity test still green; this check catches that
 class of regression on the CPU, from the kernel descriptors' metadata.  The
 lean row-pair MatMults (the 5/7/27-point z-march, the fp64 row-pair z-march,
-the sweep form: C2-C5's hot kernels) must also spill no SGPR or VGPR: round 2's 27-point form spilled 119 SGPRs (its
-54 slot values and lane masks) and ran VALU-bound at 0.39 of HBM peak."""
+the sweep form: C2-C5's hot kernels) and the Krylov vector kernels (CG's
+direction / residual updates, GMRES's MDot, MAXPY and step kernels) must also
+spill no SGPR or VGPR: round 2's 27-point form spilled 119 SGPRs (its 54 slot
+values and lane masks) and ran VALU-bound at 0.39 of HBM peak; round 3's
+chunk MDot spilled 126 SGPRs."""
 import os
 import re
 import shutil
@@ -19,7 +22,8 @@ LIB = os.path.join(ROOT, "mpi-petsc4py-example_amd", "lib", "libmxsolve.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 HOT = re.compile(r"spmv_sell_kernel|spmv_pair_lean|spmv_pair_zm|cg_|mdot|maxpy|fold_kernel")
-NOSPILL = re.compile(r"spmv_pair_zm_kernel|spmv_pair_zm27|spmv_pair_zmf64|spmv_pair_lean")
+NOSPILL = re.compile(r"spmv_pair_zm_kernel|spmv_pair_zm27|spmv_pair_zmf64|spmv_pair_zmc|spmv_pair_lean|mdot|maxpy|cg_pb|"
+                     r"cg_update|cg_norms|cg_finish|gm_|fold_kernel|finish_many")
 
 
 def code_objects(fatbin: bytes):
@@ -75,5 +79,6 @@ def test_hot_kernels_use_no_scratch(tmp_path):
 def test_zmarch_kernels_spill_nothing(tmp_path):
     zm = {k: v for k, v in kernel_descriptors(tmp_path).items() if NOSPILL.search(k)}
     assert any("zm27" in k for k in zm) and any("zmf64" in k for k in zm), sorted(zm)
+    assert any("mdot_chunk" in k for k in zm) and any("cg_pb" in k for k in zm), sorted(zm)
     bad = {k: v for k, v in zm.items() if v[1] or v[2]}
     assert not bad, f"z-march kernels with register spills (scratch, SGPR, VGPR): {bad}"

@@ -23,10 +23,11 @@ def _free_port() -> int:
 
 
 def _run_gloo_ranks(script, P, attempts=2):
-    """Start P gloo ranks of `script` on a free port; wait for all.  A failed
-    attempt is retried once on a new port (the rendezvous port can be taken
-    between the probe and rank 0's bind); a real failure fails both times and
-    reports both attempts' stderr."""
+    """Start P gloo ranks of `script` on a free port; wait for all.  An
+    attempt is retried on a new port only when a failed rank's stderr shows a
+    lost rendezvous port (taken between the probe and rank 0's bind: EADDRINUSE
+    / 'Address already in use'); any other failure fails at once, so an
+    intermittent bug (a barrier race) cannot pass on a second try."""
     errs = []
     for _ in range(attempts):
         port = str(_free_port())
@@ -46,6 +47,10 @@ def _run_gloo_ranks(script, P, attempts=2):
         if all(p.returncode == 0 for p in procs):
             return outs
         errs.append("\n".join(e[-1500:] for p, (o, e) in zip(procs, outs) if p.returncode != 0))
+        bind = any(p.returncode != 0 and ("EADDRINUSE" in e or "Address already in use" in e)
+                   for p, (o, e) in zip(procs, outs))
+        if not bind:
+            break
     raise AssertionError("gloo ranks failed:\n" + "\n---\n".join(errs))
 
 

@@ -216,60 +216,6 @@ def test_batched_x_steps_equal_separate(selfcomm, oracle_mod, kind, kw, B):
     _same(a, _run(selfcomm, oracle_mod, kind, 0, **dict(kw)))
 
 
-@pytest.mark.parametrize("kind,n,pc,max_it", [("poisson3d", 128, "jacobi", 10000), ("poisson3d", 64, "jacobi", 10000),
-                                              ("poisson2d", 256, "none", 10000), ("poisson3d", 128, "jacobi", 37),
-                                              ("poisson3d", 128, "jacobi", 1), ("poisson3d", 128, "jacobi", 2),
-                                              ("poisson2d", 384, "jacobi", 10000)])
-def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it):
-    """CG mode 4 (knob 9 = 4): the direction update p_i = z + b p_{i-1} and the
-    batched x steps ride in the z-march MatMult (operands formed where read,
-    p_i stored at the own rows).  The same grid, task order and per-lane p.w
-    order as mode 2's z-march MatMult, so the same iterations, history and
-    solution bits as mode 2 -- for converged solves, max_it stops at odd and
-    even counts (the pending x steps), 1 and 2 iterations (iteration 0 runs as
-    mode 2), select-free and select layouts, no / uniform Jacobi -- and against
-    the oracle."""
-    from mxsolve import _lib
-    from mxsolve.core import DMat, rhs_hash
-    L = _lib.load()
-
-    def run(mode):
-        old = L.mx_debug_set(9, mode)
-        old27 = L.mx_debug_set(27, 1)           # the row-pair layout (this module's fixture turns it off)
-        try:
-            A = DMat.stencil(selfcomm, kind, n)
-            m = A.info()["m"]
-            b = selfcomm.empty(m)
-            rhs_hash(selfcomm, 0, b)
-            x = selfcomm.zeros(m)
-            outs = []
-            for _ in range(2):                  # the second solve replays the cached graph
-                x.zero_()
-                r = A.solve(b, x, ksp="cg", pc=pc, rtol=1e-8, max_it=max_it, history=True)
-                outs.append((r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy()))
-            zm = A.info()["pair_zmarch"]
-            A.destroy()
-            return outs, zm, b.cpu().numpy()
-        finally:
-            L.mx_debug_set(9, old)
-            L.mx_debug_set(27, old27)
-
-    m4, zm4, bh = run(4)
-    m2, zm2, _ = run(2)
-    assert zm4 == 1 and zm2 == 1
-    for a, c in zip(m4, m2):
-        assert a[:2] == c[:2]
-        assert np.array_equal(a[2].view(np.uint64), c[2].view(np.uint64))
-        assert np.array_equal(a[3].view(np.uint64), c[3].view(np.uint64))
-    assert np.array_equal(m4[0][3].view(np.uint64), m4[1][3].view(np.uint64))
-    if max_it == 10000:
-        ip, c_, v = oracle_mod.stencil(kind, n)
-        O = oracle_mod.OracleMat.from_csr(ip.size - 1, ip.size - 1, ip, c_, v)
-        o = O.solve(bh, ksp="cg", pc=pc, rtol=1e-8)
-        assert m4[0][1] == o["reason"] and abs(m4[0][0] - o["its"]) <= 1
-        assert np.linalg.norm(m4[0][3] - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
-
-
 @pytest.mark.parametrize("kind,n,pc,max_it,kw", [("poisson3d", 128, "jacobi", 10000, {}),
                                                  ("poisson3d", 64, "jacobi", 10000, {}),
                                                  ("poisson2d", 256, "none", 10000, {}),
@@ -291,11 +237,22 @@ def test_mode4_zmarch_direction_update(selfcomm, oracle_mod, kind, n, pc, max_it
                                                  ("poisson3d27", 128, "jacobi", 10000, {"sym": 0, "k60": 0}),
                                                  ("poisson3d", 128, "jacobi", 10000, {"sym": 0}),
                                                  ("poisson2d", 256, "jacobi", 10000, {"sym": 0}),
+                                                 # x step every iteration (xb = 1: the residual update
+                                                 # reads r, no r0): poll not a multiple of 4, or knob 29 = 1
+                                                 ("poisson3d", 128, "jacobi", 10000, {"poll": 6}),
+                                                 ("poisson3d", 128, "jacobi", 10000, {"xb": 1}),
+                                                 ("poisson3d", 128, "jacobi", 41, {"xb": 1}),
+                                                 ("poisson3d27", 128, "jacobi", 10000, {"poll": 6}),
+                                                 ("poisson2d", 256, "jacobi", 10000, {"xb": 1, "guess": True}),
                                                  ])
 def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
     """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
-    gives p.w, and the update pass recomputes A p (the same sums, the same
-    bits) where it forms r - alpha A p and the norms.  Against the oracle: its
+    gives p.w, and the update pass recomputes A p (the same row sums as a
+    stored product, bit for bit) where it forms r - alpha A p and the norms.
+    The p.Ap scalar itself is not PETSc's VecDot(p, A p) bit for bit: the
+    symmetric forward-half pass sums p_i (a_ii p_i + 2 fwd_i), the same exact
+    terms in another order, so the iterates match to rounding (the bars
+    below).  Against the oracle: its
     and reason equal, history within 1e-8, x within rel-L2 1e-10; against mode
     2 (the stored-product iteration): the same its and reason, iterates equal
     to rounding (the norms' partials are grouped per z-march column); the
@@ -332,7 +289,10 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
             for k in range(2):                  # the second solve replays the cached graph
                 x.copy_(x0)
                 r = A.solve(b, x, ksp="cg", pc=pc, rtol=1e-8, max_it=max_it, history=True, norm=norm,
-                            guess_nonzero=guess)
+                            guess_nonzero=guess, poll_every=kw.get("poll", 16))
+                if mode == 5:
+                    exp_xb = 1 if (kw.get("xb") == 1 or kw.get("poll", 16) % kw.get("xb", 4)) else kw.get("xb", 4)
+                    assert r["cg_mode"] == 5 and r["cg_xbatch"] == exp_xb, (r["cg_mode"], r["cg_xbatch"], exp_xb)
                 outs.append((r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy()))
                 if k == 0:
                     dc = dispatch_counts(reset=True)

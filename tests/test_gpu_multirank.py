@@ -711,7 +711,7 @@ def test_distributed_mode5(oracle_mod, P, kind, n, applies):
         assert all(r[3] == 2 for r in res) and dc["zm_pw"] == 0 and dc["zm_rupd"] == 0, dc
 
 
-@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("P", [2, 4, 8])
 def test_distributed_code_zmarch(oracle_mod, P):
     """BASELINE C4's operator (conv-diff, non-uniform code dictionary) on P
     ranks: the coded z-march on every rank with the ghost units split off to
@@ -750,6 +750,68 @@ def test_distributed_code_zmarch(oracle_mod, P):
     assert all(r[0] == 1 for r in res)
     assert dc["pair_zmc_split"] >= P * (res[0][2] + 1) and dc["boundary"] >= P, dc
     assert np.array_equal(np.concatenate([r[1] for r in res]).view(np.uint64), y_ref.view(np.uint64))
-    assert all(r[3] == o["reason"] and abs(r[2] - o["its"]) <= 1 for r in res), ([r[2:4] for r in res], o["its"])
+    # equal iteration counts: the GPU's dot products sum in another (fixed)
+    # order than the oracle's, which moves the residual history by rounding
+    # only (SURVEY Appendix A orderprobe: identical its); a count that differed
+    # would mean a stop decided on a different residual
+    assert all(r[3] == o["reason"] and r[2] == o["its"] for r in res), ([r[2:4] for r in res], o["its"])
     xs = np.concatenate([r[4] for r in res])
     assert np.linalg.norm(xs - o["x"]) <= REL_TOL * np.linalg.norm(o["x"])
+
+
+_C4_CACHE = {}
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n", [128, 256])
+def test_c4_p8_partition(oracle_mod, n):
+    """BASELINE C4 at P = 8 (conv-diff n^3, GMRES(30) + Jacobi, 1/2/4/8 GPUs):
+    the operator generated per rank on the device (the bench path), n/8
+    planes per rank, the coded z-march SPLIT kernel with the ghost units
+    finished by the boundary kernel, the default solver options (rtol 1e-5).
+    MatMult bit-exact against the oracle's P = 8 model; its and reason EQUAL
+    to it; x within rel-L2 1e-10."""
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    from _hostinfo import host_threads
+    P = 8
+    M = n ** 3
+    if n not in _C4_CACHE:
+        ip, c, v = oracle_mod.stencil("convdiff3d", n)
+        O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+        del ip, c, v
+        xr = np.random.default_rng(44).standard_normal(M)
+        y = O.mult(xr)
+        o = O.solve(oracle_mod.rhs_hash(0, M), ksp="gmres", pc="jacobi", nthreads=host_threads())
+        del O
+        _C4_CACHE[n] = (xr, y, o)
+    xr, y_ref, o = _C4_CACHE[n]
+    ranges = oracle_mod.split_ownership(M, P)
+
+    def body(comm):
+        A = DMat.stencil(comm, "convdiff3d", n)
+        info = dict(A.info())
+        r0, r1 = ranges[comm.rank], ranges[comm.rank + 1]
+        xl = torch.from_numpy(xr[r0:r1].copy()).cuda()
+        yl = comm.zeros(info["m"])
+        A.mult(xl, yl)
+        b = comm.empty(info["m"])
+        rhs_hash(comm, info["rstart"], b)
+        x = comm.zeros(info["m"])
+        rs = A.solve(b, x, ksp="gmres", pc="jacobi")
+        out = (info, yl.cpu().numpy(), rs["its"], rs["reason"], x.cpu().numpy())
+        A.destroy()
+        return out
+
+    dispatch_counts(reset=True)
+    res = run_ranks(P, body)
+    dc = dispatch_counts(reset=True)
+    plane = n * n
+    for q, (info, *_r) in enumerate(res):
+        nb = (q > 0) + (q < P - 1)
+        assert info["rstart"] == ranges[q] and info["m"] == M // P
+        assert info["nghost"] == nb * plane and info["pair_code"] == 1
+    assert np.array_equal(np.concatenate([r[1] for r in res]).view(np.uint64), y_ref.view(np.uint64))
+    assert all(r[2] == o["its"] and r[3] == o["reason"] == 2 for r in res), ([r[2:4] for r in res], o["its"])
+    xs = np.concatenate([r[4] for r in res])
+    assert np.linalg.norm(xs - o["x"]) <= REL_TOL * np.linalg.norm(o["x"])
+    assert dc["pair_zmc_split"] >= P * o["its"] and dc["boundary"] >= P * o["its"], dc

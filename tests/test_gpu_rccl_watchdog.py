@@ -19,7 +19,7 @@ def test_rccl_wait_deadline_aborts_communicator():
     L = _lib.load()
     rc = DeviceComm.rccl(0, 1, unique_id(), device=0)
     try:
-        # no deadline by default on a wait that observes no progress
+        # the default deadline (600 s) does not trip a 0.3 s wait that observes no progress
         _lib.call("mx_debug_comm_stall", rc.h, 300_000)
         old = L.mx_debug_set(47, 50)              # 50 ms deadline
         try:
@@ -81,4 +81,41 @@ def test_rccl_poller_deadline_rearms_on_progress():
         if A is not None:
             A.destroy()
         torch.cuda.synchronize()
+        rc.destroy()
+
+
+def test_rccl_gmres_readback_deadline():
+    """GMRES(30)'s restart read-back waits under the no-progress deadline
+    (knob 33): with a 0.4 s device stall before the read-back (knob 61) and a
+    50 ms deadline the solve fails with MX_ERR_COMM and the communicator is
+    aborted; without the stall the same solve completes (the step kernels keep
+    the progress word moving)."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, DeviceComm, rhs_hash, unique_id
+    L = _lib.load()
+    rc = DeviceComm.rccl(0, 1, unique_id(), device=0)
+    old = {k: L.mx_debug_set(k, v) for k, v in ((8, 1), (33, 50))}   # collective path, 50 ms
+    mats = []
+    try:
+        A = DMat.stencil(rc, "convdiff3d", 32)
+        mats.append(A)
+        m = A.info()["m"]
+        b, x = rc.empty(m), rc.zeros(m)
+        rhs_hash(rc, 0, b)
+        r = A.solve(b, x, ksp="gmres", pc="jacobi", rtol=1e-8)
+        assert r["reason"] > 0, r
+        old61 = L.mx_debug_set(61, 400_000)
+        try:
+            x.zero_()
+            with pytest.raises(_lib.MxError) as ei:
+                A.solve(b, x, ksp="gmres", pc="jacobi", rtol=1e-8)
+            assert ei.value.code == _lib.MX_ERR_COMM and "no progress" in ei.value.msg, ei.value.msg
+        finally:
+            L.mx_debug_set(61, old61)
+    finally:
+        for k, v in old.items():
+            L.mx_debug_set(k, v)
+        torch.cuda.synchronize()                 # the bounded stall has drained
+        for A in mats:
+            A.destroy()
         rc.destroy()

@@ -100,6 +100,7 @@ def main():
         alg = spmv_alg
     # the profiled bench's own figure (bench.py spmv_format_bytes: code-block
     # dictionary, value codes) when its JSON line is in the trace log
+    js = []
     try:
         with open(os.path.join(src, "trace.log")) as f:
             js = [json.loads(ln) for ln in f if ln.startswith("{")]
@@ -122,6 +123,37 @@ def main():
         lines += ["", f"{sp} per launch: FETCH_SIZE {fr/1e6:.1f} MB raw x {corr:.3f} (calibrated, 16 B/lane NT stream; "
                   f"8 B/lane factor {f8 and round(f8, 3)}) + WRITE_SIZE {wr/1e6:.1f} MB = {traffic/1e6:.1f} MB "
                   f"vs {alg/1e6:.1f} MB algorithmic ({traffic/alg:.3f}x)."]
+    # beside the roofline kernel: the direction update (mode 5's longest
+    # kernel, cg_pb_kernel<JM, 4>) and the streamed-values MatMult of bench.py's
+    # spmv_general leg (spmv_pair_zmf64_kernel), each against the bench line's
+    # own algorithmic bytes
+    js_last = js[-1] if js else {}
+    corr = f16 if f16 else 2.0
+    extra = []
+    dom = (js_last.get("roofline") or {}).get("dominant_kernel") or {}
+    gen = js_last.get("spmv_general") or {}
+    xb = js_last.get("cg_xbatch") or 4
+    pbk = [k for k in fetch if k.startswith("cg_pb_kernel<") and k.endswith(f",{xb}>")]
+    if pbk and dom.get("bytes_per_launch"):
+        extra.append((f"{grid}^3/N{ngpu}/pb", max(pbk, key=lambda k: sum(durs.get(k, [0.0]))), dom["bytes_per_launch"]))
+    gk = [k for k in fetch if k.startswith("spmv_pair_zmf64_kernel<2,")]
+    if gk and gen.get("streamed_bytes"):
+        extra.append((f"varcoef{grid}^3/N{ngpu}", gk[0], gen["streamed_bytes"]))
+    for key, k, a in extra:
+        if k in fetch and k in write:
+            fr, wr = statistics.median(fetch[k]) * 1024, statistics.median(write[k]) * 1024
+            t = fr * corr + wr
+            out[key] = {"bytes_per_launch": round(t), "fetch_bytes_raw": round(fr), "write_bytes": round(wr),
+                        "fetch_correction": round(corr, 4), "algorithmic_bytes": a,
+                        "traffic_over_algorithmic": round(t / a, 4), "kernel": k,
+                        "median_launch_us": round(statistics.median(durs[k]), 1) if k in durs else None,
+                        "source": f"profiles/{tag}_summary.md"}
+            lines += [f"{k} per launch ({key}): FETCH_SIZE {fr/1e6:.1f} MB raw x {corr:.3f} + WRITE_SIZE "
+                      f"{wr/1e6:.1f} MB = {t/1e6:.1f} MB vs {a/1e6:.1f} MB algorithmic ({t/a:.3f}x)."]
+    lines += ["", "Produced by: `bash tools/gpu_run.sh <tag> prof` (tools/profile.sh: rocprofv3 --kernel-trace --stats, "
+              "then --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of `bench.py --steps 50 --warmup 5 --no-cpu "
+              "--no-solve --no-asm`, and the tools/calib_stream.py calibration pass), then "
+              f"`python tools/summarize_profile.py {src} {tag} {grid} {ngpu}`."]
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     tj = os.path.join(dst, "spmv_traffic.json")
