@@ -19,6 +19,7 @@
 #   prof             tools/profile.sh (trace + FETCH/WRITE PMC passes + calibration)
 #   configs          tools/bench_configs.py (C2/C3/C4/C5-share converged solves)
 #   general:LEGS     tools/bench_general.py LEGS (comma separated)
+#   c4prof           rocprofv3 kernel trace of bench_general.py c4 + gmres_roofline.py
 #   py:SCRIPT[:ARGS] python3 SCRIPT ARGS (ARGS comma separated)
 set -o pipefail
 TAG=$1; shift
@@ -55,6 +56,9 @@ for step in "$@"; do
             --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 50 --warmup 5 ;;
     prof) run prof 1000 bash tools/profile.sh ;;
     configs) run configs 700 python3 -u tools/bench_configs.py ;;
+    c4prof) run c4prof 600 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_c4trace -o run -- \
+              python3 -u tools/bench_general.py c4
+            run c4roof 120 python3 tools/gmres_roofline.py $O/${TAG}_c4trace 530 ;;
     general:*) run general 700 python3 -u tools/bench_general.py $(echo "${step#general:}" | tr , ' ') ;;
     py:*) s=${step#py:}; scr=${s%%:*}; a=""; [ "$s" != "$scr" ] && a=$(echo "${s#*:}" | tr , ' ')
           run "py_$(basename "$scr" .py)" 900 python3 -u "$scr" $a ;;
