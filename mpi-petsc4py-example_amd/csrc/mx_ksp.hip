@@ -830,12 +830,25 @@ __global__ void __launch_bounds__(256) mdot_split_kernel(int64_t n, const double
   }
 }
 
+// Four lane-distributed partials a0..a3 summed over the wave together: the
+// xor-32 step exchanges two values, the xor-16 step one, then four plain
+// steps -- lanes 16 q .. 16 q + 15 end with value q = 2 (l >> 5 & 1) + (l >> 4 & 1)'s total
+__device__ __forceinline__ double red4(double a0, double a1, double a2, double a3, int lane) {
+  const bool b5 = lane & 32, b4 = lane & 16;
+  const double c0 = (b5 ? a2 : a0) + __shfl_xor(b5 ? a0 : a2, 32, 64);
+  const double c1 = (b5 ? a3 : a1) + __shfl_xor(b5 ? a1 : a3, 32, 64);
+  double c = (b4 ? c1 : c0) + __shfl_xor(b4 ? c0 : c1, 16, 64);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  return c;
+}
+
 // VecMDot in one pass over w, chunk form (knob 50 = 2, the default; nv <= 32):
 // a workgroup holds 2048 rows of w in registers (WP = 4 16-byte pairs per
-// thread) and walks the basis vectors one after another, reading 16 KB of
-// each contiguously per step.  Each vector's chunk sum is reduced across the
-// wave at once and added to lane j's running total (one accumulator register
-// instead of nv: 49 VGPRs).  On 2^24 rows this streams at 7.0-7.1 TB/s, the
+// thread) and walks the basis vectors four at a time, reading 16 KB of each
+// contiguously per step.  Each vector's chunk sum is reduced across the wave
+// at once and added to one lane's running total (one accumulator register
+// instead of nv).  On 2^24 rows this streams at 7.0-7.1 TB/s, the
 // plain read ceiling, where the split form (several vectors' 1 KB pieces
 // interleaved per wave step) makes 6.0-6.4 (tools/mdot_probe.hip chunk4r).
 // partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
@@ -859,52 +872,50 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
       const int64_t i = c0 + k * 256 + threadIdx.x;
       wr[k] = (FULL || i < n2) ? w2[i] : dbl2{0.0, 0.0};
     }
-    // vectors two at a time (the loads of both in flight before either sum);
-    // round 3's fully unrolled walk over 32 guarded vectors kept every
-    // vector's base address and scale live in SGPRs: 126 SGPR spills
-    for (int j = 0; j < nv; j += 2) {              // wave-uniform
-      const bool two = j + 1 < nv;
-      const double s0 = vscale[j], s1 = two ? vscale[j + 1] : 0.0;
-      const dbl2 *__restrict__ v0 = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
-      const dbl2 *__restrict__ v1 = reinterpret_cast<const dbl2 *>(V + (int64_t)(two ? j + 1 : j) * ldv);
-      dbl2 t0[WP], t1[WP];
+    // vectors four at a time: their 16 loads in flight together (clamped to
+    // the last vector, so branch-free), then the four lane partials reduced
+    // together by a transposed butterfly (red4: 7 fp64 shuffles instead of 4
+    // wave sums of 6); vector j's chunk total lands in lanes 16 (j & 3) ..
+    // 16 (j & 3) + 15 and is kept in lane 16 (j & 3) + (j >> 2).  Round 3's
+    // fully unrolled walk over 32 guarded vectors kept every vector's address
+    // and scale in SGPRs (126 spills); tools/mdot_probe.hip chunk4grp4.
+    for (int j = 0; j < nv; j += 4) {              // wave-uniform
+      dbl2 t[4][WP];
+      double sq[4];
 #pragma unroll
-      for (int k = 0; k < WP; ++k) {
-        const int64_t i = c0 + k * 256 + threadIdx.x;
-        t0[k] = (FULL || i < n2) ? __builtin_nontemporal_load(v0 + i) : dbl2{0.0, 0.0};
-      }
-      if (two) {
+      for (int q = 0; q < 4; ++q) {
+        const int jq = min(j + q, nv - 1);
+        sq[q] = j + q < nv ? vscale[jq] : 0.0;
+        const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)jq * ldv);
 #pragma unroll
         for (int k = 0; k < WP; ++k) {
           const int64_t i = c0 + k * 256 + threadIdx.x;
-          t1[k] = (FULL || i < n2) ? __builtin_nontemporal_load(v1 + i) : dbl2{0.0, 0.0};
+          t[q][k] = (FULL || i < n2) ? __builtin_nontemporal_load(vq + i) : dbl2{0.0, 0.0};
         }
       }
-      double a0 = 0.0, a1 = 0.0;
+      double a[4];
 #pragma unroll
-      for (int k = 0; k < WP; ++k) {
-        a0 += wr[k].x * (s0 * t0[k].x);
-        a0 += wr[k].y * (s0 * t0[k].y);
-      }
-      a0 = wave_sum(a0);
-      if (lane == j) acc += a0;
-      if (two) {
+      for (int q = 0; q < 4; ++q) {
+        a[q] = 0.0;
 #pragma unroll
         for (int k = 0; k < WP; ++k) {
-          a1 += wr[k].x * (s1 * t1[k].x);
-          a1 += wr[k].y * (s1 * t1[k].y);
+          a[q] += wr[k].x * (sq[q] * t[q][k].x);
+          a[q] += wr[k].y * (sq[q] * t[q][k].y);
         }
-        a1 = wave_sum(a1);
-        if (lane == j + 1) acc += a1;
       }
+      const double r = red4(a[0], a[1], a[2], a[3], lane);
+      if ((lane & 15) == (j >> 2)) acc += r;
     }
   };
   for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
   if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
-  if ((n & 1) && blockIdx.x == 0 && wid == 0 && lane < nv)   // odd length: the last row, lane j's term
-    acc += w[n - 1] * (vscale[lane] * V[(int64_t)lane * ldv + n - 1]);
+  // lane l keeps vector 4 (l & 15) + 2 (l >> 5 & 1) + (l >> 4 & 1)
+  const int vj = 4 * (lane & 15) + 2 * ((lane >> 5) & 1) + ((lane >> 4) & 1);
+  const bool mine = (lane & 15) < NVX / 4 && vj < nv;
+  if ((n & 1) && blockIdx.x == 0 && wid == 0 && mine)   // odd length: the last row, vector vj's term
+    acc += w[n - 1] * (vscale[vj] * V[(int64_t)vj * ldv + n - 1]);
   __shared__ double sh[NVX][4];
-  if (lane < nv) sh[lane][wid] = acc;
+  if (mine) sh[vj][wid] = acc;
   __syncthreads();
   if ((int)threadIdx.x < nv)
     partials[(size_t)threadIdx.x * gridDim.x + blockIdx.x] =

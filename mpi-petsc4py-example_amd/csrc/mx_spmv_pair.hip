@@ -797,6 +797,143 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p_kernel(const PairLean27Ar
   }
 }
 
+// CG mode 5's two passes on a 27-point "box" operator (Sell::pair_box27: the
+// column-word layout, every present off-diagonal slot holding one value v and
+// every diagonal one value c -- C5's 26 / -1 stencil).  Then
+//   (A p)_i = (c - v) p_i + v B_i,   B_i = sum of p over the 3 x 3 x 3 box
+// (absent neighbours read as 0.0, as the column words already arrange), and
+// the box sum is separable: per loaded plane, each of its three lines' x
+// triples (lo + p_x + p_x+1 and p_x + p_x+1 + hi: three adds for the lane's
+// two rows), the plane's y sum of those, and the z sum of three consecutive
+// planes' sums -- 17 adds for the lane's two rows where the slot-order sum
+// takes 54 multiply-adds.  The round-3 kernels were VALU-issue-bound on those
+// (217 VALU instructions per unit, 36% of wave cycles issue-stalled); this
+// form is an HBM stream.  The sums are reassociated, so A p is not the
+// MatMult's bits (mx_mat_mult keeps PETSc's slot order): it equals them to
+// rounding, and the CG iterates equal the oracle's within the north-star bar
+// (its and reason equal, x within rel-L2 1e-10; tests/test_gpu_cgfuse.py).
+// What crosses a step: the two previous planes' sums and the centre pair.
+// PW: the p.Ap partials (full rows, nothing stored); RUPD: alpha from the PW
+// partials, r = r - alpha A p (daxpy's fma), z = c_J r, [z.z, z.r, r.r].
+template <int MODE, int JM = 0>
+__global__ void __launch_bounds__(256) spmv_pair_zm27b_kernel(const PairLean27Args a, const double *__restrict__ x,
+                                                              const int32_t *__restrict__ pcol, const double cmv,
+                                                              const double bv, const PairRuArgs ru) {
+  static_assert(MODE == SPMV_PW || MODE == SPMV_RUPD, "CG mode 5's passes");
+  constexpr bool RU = MODE == SPMV_RUPD;
+  double alpha = 0.0;
+  const double *rin = nullptr;
+  if constexpr (RU) {
+    KspState *s = ru.s;
+    if (s->top.done) {
+      if (ru.hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(ru.hw + HW_DONE, 1);
+      return;
+    }
+    const double pw = ru.ndot > 0 ? block_sum_array<16>(ru.dot_part, ru.ndot) : s->red1;
+    const CgAlpha al = cg_alpha(s, pw);
+    if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, ru.xb, false, ru.hw);
+    if (al.reason) return;
+    alpha = al.alpha;
+    rin = (ru.r0 && al.i == 0) ? ru.r0 : ru.r;
+  } else {
+    if (a.done && *a.done) return;   // wave-uniform: solver finished
+  }
+  double nv[3] = {0.0, 0.0, 0.0};   // RU: [z.z, z.r, r.r]
+  double dot = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[7];
+  const int eb = lane == 0 ? -1 : 128;                   // edge: lane 0 x[ub + c - 1], others x[ub + 128 + c]
+  const int ntask = (se - sb) * a.P;
+  for (int t = w; t < ntask; t += W) {
+    const int seg = sb + t / a.P, col = t % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;
+    const uint32_t cw = (uint32_t)pcol[col];
+    const int oor[3] = {(cw & U27C_YLO) ? PAIR_OOR : 0, 0, (cw & U27C_YHI) ? PAIR_OOR : 0};
+    const int ebe = eb + ((lane == 0 ? (cw & U27_ELO) : (cw & U27_EHI)) ? PAIR_OOR_EDGE : 0);
+    // plane q's three lines (dy = -1, 0, +1) and their edge values
+    auto load = [&](int q, dbl2 (&L)[3], double (&e)[3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        L[k] = bload2(xr, q * D + cb + a.anchor[3 + k] + oor[k]);
+        e[k] = bload1(xr, q * D + col * 128 + ebe + a.anchor[3 + k] + oor[k]);
+      }
+    };
+    // the plane's box-row sums for the lane's two rows
+    auto psum = [&](const dbl2 (&L)[3], const double (&e)[3]) __attribute__((always_inline)) -> dbl2 {
+      dbl2 t[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double lo = wave_shift<true>(L[k].y, e[k]);   // x[r0 + c - 1]
+        const double hi = wave_shift<false>(L[k].x, e[k]);  // x[r0 + c + 2]
+        const double u = L[k].x + L[k].y;
+        t[k] = dbl2{lo + u, u + hi};
+      }
+      return dbl2{(t[0].x + t[1].x) + t[2].x, (t[0].y + t[1].y) + t[2].y};
+    };
+    // software-pipelined by one plane: plane z + 2's loads (and row z + 1's
+    // r) are issued before plane z + 1 is summed, so every wave keeps a
+    // plane's reads in flight while it computes (the slot-order kernels, at
+    // 73-98 VGPRs, could not afford the second set)
+    dbl2 L[3], Ln[3];
+    double e[3], en[3];
+    dbl2 rq, rqn;
+    load(z0 - 1, L, e);                                  // (plane -1: out of range, 0.0)
+    load(z0, Ln, en);
+    dbl2 sm = psum(L, e);
+    dbl2 s0 = psum(Ln, en);
+    dbl2 cz = Ln[1];                                     // unit z0's own rows
+    load(z0 + 1, L, e);                                  // (past the last plane: 0.0)
+    if constexpr (RU) rq = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + z0 * D + cb));
+    for (int z = z0; z < z1; ++z) {
+      const int r0 = z * D + cb;
+      if (z + 1 < z1) {                                  // wave-uniform: the next step's reads
+        load(z + 2, Ln, en);
+        if constexpr (RU) rqn = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0 + D));
+      }
+      const dbl2 sp = psum(L, e);
+      const dbl2 bx = dbl2{(sm.x + s0.x) + sp.x, (sm.y + s0.y) + sp.y};
+      const dbl2 ap = dbl2{fma(cmv, cz.x, bv * bx.x), fma(cmv, cz.y, bv * bx.y)};
+      if constexpr (RU) {
+        const double ra = fma(-alpha, ap.x, rq.x), rb = fma(-alpha, ap.y, rq.y);
+        const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
+        nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
+        nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
+        *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+      } else {
+        dot += cz.x * ap.x;
+        dot += cz.y * ap.y;
+      }
+      sm = s0;
+      s0 = sp;
+      cz = L[1];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { L[k] = Ln[k]; e[k] = en[k]; }
+      if constexpr (RU) rq = rqn;
+    }
+  }
+  if constexpr (RU) block_partials<3>(nv, a.partials, gridDim.x, a.fold);
+  else {
+    double v[1] = {dot};
+    block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  }
+}
+
 // fp64 row pairs (Sell::pval, uncoded 5/7-point layouts whose every unit is
 // select-free): the z-march with the unit's values streamed (K 16-byte pairs
 // per lane, non-temporal) instead of a dictionary block's uniform values.
@@ -1231,6 +1368,25 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // the plane-pipelined form (knob 60): column words; the symmetric p.Ap pass
   // keeps the carried-operand kernel
   const bool sym = S.pair_sym27 && g_knobs.pw_sym27;
+  if ((mode == SPMV_PW || mode == SPMV_RUPD) && form == 2 && !split && S.pair_box27 && g_knobs.box27) {
+    // the box operator's separable sums (knob 62), on knob 63 workgroups per CU
+    if (g_knobs.box27_bpc > 0) {
+      grid = std::max(8, g_knobs.box27_bpc * device_cu_count()) & ~7;
+      const int Wb = grid / 8 * LEAN_WAVES;
+      int Lb = std::min(std::max(1, g_knobs.pair_zm_len), slab);
+      while (Lb > 1 && (int64_t)b.P * ((slab + Lb - 1) / Lb) < Wb) Lb = (Lb + 1) / 2;
+      b.L = Lb;
+      b.S = (b.NZ + Lb - 1) / Lb;
+      if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
+    }
+    using FB = void (*)(PairLean27Args, const double *, const int32_t *, double, double, PairRuArgs);
+    FB fb = mode == SPMV_PW ? &spmv_pair_zm27b_kernel<SPMV_PW> : jm == 2 ? &spmv_pair_zm27b_kernel<SPMV_RUPD, 2>
+                                                                         : &spmv_pair_zm27b_kernel<SPMV_RUPD, 0>;
+    note_dispatch(mode == SPMV_PW ? DSP_ZM_PW : DSP_ZM_RUPD);
+    launch_timed(fb, grid, st, b, x, S.pcol27.p, S.box_c - S.box_v, S.box_v, ru);
+    HIPCHECK(hipGetLastError());
+    return grid;
+  }
   if (form == 2 && g_knobs.pair_zm27p && !(mode == SPMV_PW && sym)) {
     const bool uvp = S.pair_unit27 && g_knobs.pair_unitv;
     switch (mode) {

@@ -20,7 +20,9 @@
 #   configs          tools/bench_configs.py (C2/C3/C4/C5-share converged solves)
 #   general:LEGS     tools/bench_general.py LEGS (comma separated)
 #   c4prof           rocprofv3 kernel trace of bench_general.py c4 + gmres_roofline.py
-#   py:SCRIPT[:ARGS] python3 SCRIPT ARGS (ARGS comma separated)
+#   py:SCRIPT[:ARGS] python3 SCRIPT ARGS (ARGS separated by @)
+#   trace:SCRIPT[:ARGS] rocprofv3 kernel trace of python3 SCRIPT ARGS + trace_medians.py
+#   bin:PATH[:ARGS]  a prebuilt probe binary (e.g. tools/mdot_probe)
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -60,8 +62,14 @@ for step in "$@"; do
               python3 -u tools/bench_general.py c4
             run c4roof 120 python3 tools/gmres_roofline.py $O/${TAG}_c4trace 530 ;;
     general:*) run general 700 python3 -u tools/bench_general.py $(echo "${step#general:}" | tr , ' ') ;;
-    py:*) s=${step#py:}; scr=${s%%:*}; a=""; [ "$s" != "$scr" ] && a=$(echo "${s#*:}" | tr , ' ')
+    py:*) s=${step#py:}; scr=${s%%:*}; a=""; [ "$s" != "$scr" ] && a=$(echo "${s#*:}" | tr @ ' ')
           run "py_$(basename "$scr" .py)" 900 python3 -u "$scr" $a ;;
+    trace:*) s=${step#trace:}; scr=${s%%:*}; a=""; [ "$s" != "$scr" ] && a=$(echo "${s#*:}" | tr @ ' ')
+             nm=$(basename "$scr" .py)
+             run "trace_$nm" 600 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_trace_$nm -o run -- python3 -u "$scr" $a
+             run "med_$nm" 120 python3 tools/trace_medians.py $O/${TAG}_trace_$nm ;;
+    bin:*) s=${step#bin:}; b=${s%%:*}; a=""; [ "$s" != "$b" ] && a=$(echo "${s#*:}" | tr @ ' ')
+           run "bin_$(basename "$b")" 300 "$b" $a ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -24,6 +25,11 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+__global__ void initv_kernel(double *p, int64_t ldv, int nv) {   // vector j: 1 + j / 64 + (i % 7) / 1024
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ldv * nv; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 1.0 + (double)(i / ldv) / 64.0 + (double)((i % ldv) % 7) / 1024.0;
 }
 
 __global__ void init_kernel(double *p, int64_t n, double s) {
@@ -181,6 +187,99 @@ __global__ void __launch_bounds__(256) chunks_kernel(int64_t n, const double *__
       (sh[threadIdx.x][0] + sh[threadIdx.x][1]) + (sh[threadIdx.x][2] + sh[threadIdx.x][3]);
 }
 
+// round 4 variants of the RED form without the fully unrolled guarded walk
+// (which kept 32 vector addresses and scales in SGPRs: 126 spills):
+//   pair : two vectors per step (the product after round 4's first fix)
+//   grp4 : four vectors per step, loads clamped to the last vector (branch-free),
+//          the four lane partials reduced together by a transposed butterfly
+//          (7 fp64 shuffles instead of 4 x 6); vector 4g + q's total lands in
+//          the lanes 16q..16q+15 and is kept in lane 16q + g
+__device__ __forceinline__ double red4(double a0, double a1, double a2, double a3, int lane) {
+  const bool b5 = lane & 32, b4 = lane & 16;
+  const double k0 = b5 ? a2 : a0, s0 = b5 ? a0 : a2;
+  const double k1 = b5 ? a3 : a1, s1 = b5 ? a1 : a3;
+  const double c0 = k0 + __shfl_xor(s0, 32, 64);
+  const double c1 = k1 + __shfl_xor(s1, 32, 64);
+  double c = (b4 ? c1 : c0) + __shfl_xor(b4 ? c0 : c1, 16, 64);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  return c;                                  // lane l: vector 2 (l >> 5 & 1) + (l >> 4 & 1) of the group
+}
+
+template <int WP, int MODE>   // MODE 0 pair, 1 grp4
+__global__ void __launch_bounds__(256) chunkv_kernel(int64_t n, const double *__restrict__ w, const double *__restrict__ V,
+                                                     int64_t ldv, int nv, const double *__restrict__ vs,
+                                                     double *__restrict__ partials) {
+  double acc = 0.0;
+  const int lane = threadIdx.x & 63;
+  const dbl2 *__restrict__ w2 = reinterpret_cast<const dbl2 *>(w);
+  const int64_t n2 = n >> 1, csz = 256 * WP;
+  for (int64_t c0 = blockIdx.x * csz; c0 < n2; c0 += (int64_t)gridDim.x * csz) {
+    dbl2 wr[WP];
+#pragma unroll
+    for (int k = 0; k < WP; ++k) wr[k] = w2[c0 + k * 256 + threadIdx.x];
+    if constexpr (MODE == 0) {
+      for (int j = 0; j < nv; j += 2) {
+        const bool two = j + 1 < nv;
+        const double s0 = vs[j], s1 = two ? vs[j + 1] : 0.0;
+        const dbl2 *__restrict__ v0 = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv) + c0 + threadIdx.x;
+        const dbl2 *__restrict__ v1 = reinterpret_cast<const dbl2 *>(V + (int64_t)(two ? j + 1 : j) * ldv) + c0 + threadIdx.x;
+        dbl2 t0[WP], t1[WP];
+#pragma unroll
+        for (int k = 0; k < WP; ++k) t0[k] = __builtin_nontemporal_load(v0 + k * 256);
+        if (two) {
+#pragma unroll
+          for (int k = 0; k < WP; ++k) t1[k] = __builtin_nontemporal_load(v1 + k * 256);
+        }
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < WP; ++k) { a0 += wr[k].x * (s0 * t0[k].x); a0 += wr[k].y * (s0 * t0[k].y); }
+        a0 = wave_sum(a0);
+        if (lane == j) acc += a0;
+        if (two) {
+#pragma unroll
+          for (int k = 0; k < WP; ++k) { a1 += wr[k].x * (s1 * t1[k].x); a1 += wr[k].y * (s1 * t1[k].y); }
+          a1 = wave_sum(a1);
+          if (lane == j + 1) acc += a1;
+        }
+      }
+    } else {
+      for (int j = 0; j < nv; j += 4) {
+        dbl2 t[4][WP];
+        double sq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int jq = min(j + q, nv - 1);
+          sq[q] = j + q < nv ? vs[jq] : 0.0;
+          const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)jq * ldv) + c0 + threadIdx.x;
+#pragma unroll
+          for (int k = 0; k < WP; ++k) t[q][k] = __builtin_nontemporal_load(vq + k * 256);
+        }
+        double a[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a[q] = 0.0;
+#pragma unroll
+          for (int k = 0; k < WP; ++k) { a[q] += wr[k].x * (sq[q] * t[q][k].x); a[q] += wr[k].y * (sq[q] * t[q][k].y); }
+        }
+        const double r = red4(a[0], a[1], a[2], a[3], lane);
+        if ((lane & 15) == (j >> 2)) acc += r;
+      }
+    }
+  }
+  __shared__ double sh[NVMAX][4];
+  const int wid = threadIdx.x >> 6;
+  if constexpr (MODE == 0) {
+    if (lane < nv) sh[lane][wid] = acc;
+  } else {
+    const int vj = 4 * (lane & 15) + 2 * ((lane >> 5) & 1) + ((lane >> 4) & 1);
+    if ((lane & 15) < 8 && vj < nv) sh[vj][wid] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < nv) partials[(size_t)threadIdx.x * gridDim.x + blockIdx.x] =
+      (sh[threadIdx.x][0] + sh[threadIdx.x][1]) + (sh[threadIdx.x][2] + sh[threadIdx.x][3]);
+}
+
 // VecMAXPY + ||w||^2 (GMRES's maxpy_norm_kernel body): w -= sum_j a_j v_j in
 // VecMAXPY_Seq's grouping (first nv % 4 vectors, then groups of four)
 __global__ void __launch_bounds__(256) maxpy_row_kernel(int64_t n, double *__restrict__ w, const double *__restrict__ V,
@@ -288,7 +387,7 @@ int main(int argc, char **argv) {
   double *al;
   CK(hipMalloc(&al, sizeof(double) * NVMAX));
   init_kernel<<<1, 64>>>(al, NVMAX, 1e-3);
-  init_kernel<<<4096, 256>>>(V, ldv * NVMAX, 1.0);
+  initv_kernel<<<4096, 256>>>(V, ldv, NVMAX);
   init_kernel<<<4096, 256>>>(w, N, 0.5);
   init_kernel<<<4096, 256>>>(big, N * 16, 0.25);
   CK(hipDeviceSynchronize());
@@ -322,6 +421,25 @@ int main(int argc, char **argv) {
     rep("chunk4s", time_it([&] { chunks_kernel<4, false><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
     rep("chunk4r", time_it([&] { chunks_kernel<4, true><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
     rep("chunk8r", time_it([&] { chunks_kernel<8, true><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
+    rep("chunk4pair", time_it([&] { chunkv_kernel<4, 0><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
+    rep("chunk4grp4", time_it([&] { chunkv_kernel<4, 1><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
+    rep("chunk2grp4", time_it([&] { chunkv_kernel<2, 1><<<grid, 256>>>(N, w, V, ldv, nv, al, part); }, reps));
+    {   // the variants' totals agree (different sum orders: to rounding)
+      auto totals = [&](auto launch) {
+        launch();
+        CK(hipDeviceSynchronize());
+        std::vector<double> h((size_t)nv * grid), t(nv, 0.0);
+        CK(hipMemcpy(h.data(), part, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+        for (int j = 0; j < nv; ++j) for (int b = 0; b < grid; ++b) t[j] += h[(size_t)j * grid + b];
+        return t;
+      };
+      auto r0 = totals([&] { chunks_kernel<4, true><<<grid, 256>>>(N, w, V, ldv, nv, al, part); });
+      auto r1 = totals([&] { chunkv_kernel<4, 0><<<grid, 256>>>(N, w, V, ldv, nv, al, part); });
+      auto r2 = totals([&] { chunkv_kernel<4, 1><<<grid, 256>>>(N, w, V, ldv, nv, al, part); });
+      double e = 0.0;
+      for (int j = 0; j < nv; ++j) e = fmax(e, fmax(fabs(r1[j] - r0[j]), fabs(r2[j] - r0[j])) / fabs(r0[j]));
+      printf("{\"check\": \"variant totals\", \"nv\": %d, \"max_rel_diff\": %.3e}\n", nv, e);
+    }
     const double mbytes = 8.0 * N * (nv + 2);
     auto repm = [&](const char *name, float ms) {
       printf("{\"variant\": \"%s\", \"nv\": %d, \"grid\": %d, \"us\": %.1f, \"TBps\": %.3f}\n", name, nv, grid, ms * 1e3,
