@@ -11,6 +11,7 @@ and reductions run over RCCL inside libmxsolve.so.
 """
 from __future__ import annotations
 
+import atexit
 import os
 import pickle
 
@@ -63,6 +64,27 @@ def _buf(spec):
     return spec, []
 
 
+def _finalize(dist):
+    """MPI_Finalize at interpreter exit (mpi4py registers the same): a last
+    barrier, then the process group torn down while every rank is still
+    there.  Without it a rank could exit while a peer's gloo threads were
+    still live, and that peer's teardown died in std::terminate ('terminate
+    called without an active exception', about one run in ten)."""
+    if not dist.is_initialized():
+        return
+    try:
+        # bounded: a rank that died (or is stuck in another collective) must
+        # not hold its peers' exit forever
+        import datetime
+        dist.monitored_barrier(timeout=datetime.timedelta(seconds=300))
+    except Exception:  # noqa: BLE001 -- a peer already gone: tear down anyway
+        pass
+    try:
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        pass
+
+
 class Comm:
     """COMM_WORLD over torch.distributed (gloo) -- or a world of one."""
 
@@ -74,6 +96,7 @@ class Comm:
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 dist.init_process_group("gloo")
+                atexit.register(_finalize, dist)
             self._dist = dist
             self._rank, self._size = dist.get_rank(), dist.get_world_size()
         else:
