@@ -144,7 +144,13 @@ class DeviceComm:
         return device_vector(max(int(n), 0), self.device).zero_()
 
     def destroy(self):
+        """Destroys the communicator (its stream goes with it): when that
+        stream is this thread's current torch stream, the device's default
+        stream becomes current again, so later torch work is not enqueued on
+        a destroyed stream."""
         if self.h:
+            if torch.cuda.current_stream(self.device).cuda_stream == self.stream_ptr:
+                torch.cuda.set_stream(torch.cuda.default_stream(self.device))
             call("mx_comm_destroy", self.h)
             self.h = None
 

@@ -73,8 +73,23 @@ def oracle_mod():
     return oracle
 
 
+_SELF = []
+
+
 @pytest.fixture(scope="session")
 def selfcomm():
     from mxsolve.core import DeviceComm
     c = DeviceComm.self_comm(0)
+    _SELF.append(c)
     yield c
+
+
+@pytest.fixture(autouse=True)
+def _selfcomm_stream():
+    """Every test starts with the session communicator's stream as torch's
+    current stream: a test that created (and destroyed) another communicator
+    made that one current, and torch ops on the session's vectors would
+    otherwise be ordered on a different stream than the library's kernels."""
+    if _SELF and _SELF[0].h:
+        _SELF[0].activate()
+    yield
