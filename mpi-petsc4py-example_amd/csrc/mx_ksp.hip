@@ -852,7 +852,7 @@ __device__ __forceinline__ double red4(double a0, double a1, double a2, double a
 // plain read ceiling, where the split form (several vectors' 1 KB pieces
 // interleaved per wave step) makes 6.0-6.4 (tools/mdot_probe.hip chunk4r).
 // partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
-template <int WP>
+template <int WP, int FORM = 0>
 __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
                                                          const double *__restrict__ vscale,
@@ -879,9 +879,7 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
     // 16 (j & 3) + 15 and is kept in lane 16 (j & 3) + (j >> 2).  Round 3's
     // fully unrolled walk over 32 guarded vectors kept every vector's address
     // and scale in SGPRs (126 spills); tools/mdot_probe.hip chunk4grp4.
-    for (int j = 0; j < nv; j += 4) {              // wave-uniform
-      dbl2 t[4][WP];
-      double sq[4];
+    auto group = [&](int j, dbl2 (&t)[4][WP], double (&sq)[4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int jq = min(j + q, nv - 1);
@@ -893,6 +891,8 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
           t[q][k] = (FULL || i < n2) ? __builtin_nontemporal_load(vq + i) : dbl2{0.0, 0.0};
         }
       }
+    };
+    auto finish = [&](int j, const dbl2 (&t)[4][WP], const double (&sq)[4]) __attribute__((always_inline)) {
       double a[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -905,6 +905,29 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
       }
       const double r = red4(a[0], a[1], a[2], a[3], lane);
       if ((lane & 15) == (j >> 2)) acc += r;
+    };
+    if constexpr (FORM == 1) {
+      // knob 50 = 4: the next group's 16 loads issued before this group's sums
+      dbl2 t[4][WP], tn[4][WP];
+      double sq[4], sqn[4];
+      group(0, t, sq);
+      for (int j = 0; j < nv; j += 4) {            // wave-uniform
+        if (j + 4 < nv) group(j + 4, tn, sqn);
+        finish(j, t, sq);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sq[q] = sqn[q];
+#pragma unroll
+          for (int k = 0; k < WP; ++k) t[q][k] = tn[q][k];
+        }
+      }
+    } else {
+      for (int j = 0; j < nv; j += 4) {            // wave-uniform
+        dbl2 t[4][WP];
+        double sq[4];
+        group(j, t, sq);
+        finish(j, t, sq);
+      }
     }
   };
   for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
@@ -1715,8 +1738,10 @@ static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double
 // buffer holds max_k + 2 rows rounded up to 32; groups are gw wide (knob 16)
 static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
                  const double *vscale, double *partials, const int *stop_flag, int grid) {
-  if (g_knobs.mdot_split == 2 && nv <= 32) {   // one pass over w, chunk form (knob 50)
-    mdot_chunk_kernel<4><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+  if ((g_knobs.mdot_split == 2 || g_knobs.mdot_split == 4 || g_knobs.mdot_split == 5) && nv <= 32) {   // one pass over w, chunk form (knob 50)
+    if (g_knobs.mdot_split == 4) mdot_chunk_kernel<4, 1><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+    else if (g_knobs.mdot_split == 5) mdot_chunk_kernel<2, 1><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+    else mdot_chunk_kernel<4><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
     HIPCHECK(hipGetLastError());
     return;
   }

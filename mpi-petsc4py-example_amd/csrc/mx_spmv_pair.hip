@@ -1667,6 +1667,17 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
 #undef RU_J
 #undef RU_S
 #undef RU
+  // knob 64: 3 or 4 planes per step for the clean one-rank residual update
+  // (more of its HBM reads in flight per wave)
+  if (clean && !split && (g_knobs.ru_units == 3 || g_knobs.ru_units == 4)) {
+    const bool u4 = g_knobs.ru_units == 4, j2 = jac_mode == 2;
+    if (A->sd.pair_shape == 5)
+      f = u4 ? (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 4, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 4, 0>)
+             : (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 3, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 3, 0>);
+    else
+      f = u4 ? (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 4, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 4, 0>)
+             : (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 3, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 3, 0>);
+  }
   note_dispatch(DSP_ZM_RUPD);
   launch_timed(f, grid, st, a, p, nullptr, A->sd.pblk.p, A->sd.puni.p, ru);
   HIPCHECK(hipGetLastError());
