@@ -1263,8 +1263,8 @@ static int zm_plane(const Mat *A, int ps, const int anchor[5]) {
 }
 
 // grid, segment length and segments of a z-march over NZ planes of P columns
-static int zm_tasks(int P, int NZ, int &L, int &S, int bpc = 0) {
-  int grid = std::max(8, (bpc > 0 ? bpc : g_knobs.pair_zm_bpc) * device_cu_count());
+static int zm_geom(int P, int NZ, int &L, int &S, int bpc) {
+  int grid = std::max(8, bpc * device_cu_count());
   grid &= ~7;
   const int W = grid / 8 * LEAN_WAVES;               // waves per XCD
   const int slab = (NZ + 7) / 8;                      // planes per XCD
@@ -1272,6 +1272,27 @@ static int zm_tasks(int P, int NZ, int &L, int &S, int bpc = 0) {
   while (L > 1 && (int64_t)P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
   S = (NZ + L - 1) / L;
   return grid;
+}
+
+// Knob 65: the workgroups per CU (at most the requested, at least 2) whose
+// z-march tasks fill the XCD's waves in whole rounds.  A wave takes tasks
+// (segment, column) in turn, so T tasks over W waves take ceil(T / W) rounds
+// and a partial last round idles the rest: C5's share (2,048 columns x one
+// 8-plane segment per XCD) on 5 workgroups per CU gives 640 waves 3.2 tasks
+// each -- four rounds, the last one a fifth full.
+static int zm_tasks(int P, int NZ, int &L, int &S, int bpc = 0) {
+  const int want = bpc > 0 ? bpc : g_knobs.pair_zm_bpc;
+  if (!g_knobs.zm_balance) return zm_geom(P, NZ, L, S, want);
+  int best = want;
+  double best_eff = -1.0;
+  for (int b = want; b >= std::min(2, want); --b) {
+    int l, sg;
+    const int grid = zm_geom(P, NZ, l, sg, b);
+    const int64_t W = grid / 8 * LEAN_WAVES, T = (int64_t)P * ((sg + 7) / 8);
+    const double eff = (double)T / (double)(W * ((T + W - 1) / W));
+    if (eff > best_eff + 0.02) { best_eff = eff; best = b; }
+  }
+  return zm_geom(P, NZ, L, S, best);
 }
 
 // fp64 row-pair z-march (Sell::pval): uncoded 5/7-point layouts
@@ -1344,14 +1365,10 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // second generation: 99 -> 89 us per launch, -5% per C5 iteration)
   const int bpc = mode == SPMV_RUPD && g_knobs.pair_zm27_ru_bpc > 0 ? g_knobs.pair_zm27_ru_bpc
                   : g_knobs.pair_zm27_bpc > 0 ? g_knobs.pair_zm27_bpc : g_knobs.pair_zm_bpc;
-  int grid = std::max(8, bpc * device_cu_count());
-  grid &= ~7;
-  const int W = grid / 8 * LEAN_WAVES;
-  const int slab = (b.NZ + 7) / 8;
-  int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
-  while (L > 1 && (int64_t)b.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
+  int L, Sg;
+  int grid = zm_tasks(b.P, b.NZ, L, Sg, bpc);
   b.L = L;
-  b.S = (b.NZ + L - 1) / L;
+  b.S = Sg;
   b.partials = partials;
   b.done = done;
   Fold fold = fold_in;
@@ -1371,12 +1388,7 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   if ((mode == SPMV_PW || mode == SPMV_RUPD) && form == 2 && !split && S.pair_box27 && g_knobs.box27) {
     // the box operator's separable sums (knob 62), on knob 63 workgroups per CU
     if (g_knobs.box27_bpc > 0) {
-      grid = std::max(8, g_knobs.box27_bpc * device_cu_count()) & ~7;
-      const int Wb = grid / 8 * LEAN_WAVES;
-      int Lb = std::min(std::max(1, g_knobs.pair_zm_len), slab);
-      while (Lb > 1 && (int64_t)b.P * ((slab + Lb - 1) / Lb) < Wb) Lb = (Lb + 1) / 2;
-      b.L = Lb;
-      b.S = (b.NZ + Lb - 1) / Lb;
+      grid = zm_tasks(b.P, b.NZ, b.L, b.S, g_knobs.box27_bpc);
       if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
     }
     using FB = void (*)(PairLean27Args, const double *, const int32_t *, double, double, PairRuArgs);
@@ -1572,17 +1584,10 @@ int pair_lean_launch(Mat *A, int mode, bool split, const double *x, double *y, d
   if (zm) {
     a.P = D / 128;
     a.NZ = (int)(A->m / D);
-    // CG mode 5's p.Ap pass may take its own grid (knob 57)
-    grid = std::max(8, (mode == SPMV_PW && g_knobs.pw_bpc > 0 ? g_knobs.pw_bpc : g_knobs.pair_zm_bpc) * device_cu_count());
-    grid &= ~7;
-    const int W = grid / 8 * LEAN_WAVES;               // waves per XCD
-    const int slab = (a.NZ + 7) / 8;                    // planes per XCD
-    // segments of up to 32 planes, shorter when one slab's columns do not
-    // give every wave a task
-    int L = std::min(std::max(1, g_knobs.pair_zm_len), slab);
-    while (L > 1 && (int64_t)a.P * ((slab + L - 1) / L) < W) L = (L + 1) / 2;
-    a.L = L;
-    a.S = (a.NZ + L - 1) / L;
+    // CG mode 5's p.Ap pass may take its own grid (knob 57); segments of up
+    // to 32 planes, shorter when one slab's columns do not give every wave a
+    // task (zm_geom)
+    grid = zm_tasks(a.P, a.NZ, a.L, a.S, mode == SPMV_PW && g_knobs.pw_bpc > 0 ? g_knobs.pw_bpc : g_knobs.pair_zm_bpc);
 #define ZM_PICK(MODE, PS, SP, CL) \
     fz = g_knobs.pair_zm_units == 2 ? &spmv_pair_zm_kernel<MODE, PS, SP, CL, 2> : &spmv_pair_zm_kernel<MODE, PS, SP, CL, 1>
 #define ZM_C(MODE, PS) do { if (split) { if (clean) ZM_PICK(MODE, PS, true, true); else ZM_PICK(MODE, PS, true, false); } \
