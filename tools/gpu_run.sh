@@ -23,6 +23,8 @@
 #   py:SCRIPT[:ARGS] python3 SCRIPT ARGS (ARGS separated by @)
 #   trace:SCRIPT[:ARGS] rocprofv3 kernel trace of python3 SCRIPT ARGS + trace_medians.py
 #   bin:PATH[:ARGS]  a prebuilt probe binary (e.g. tools/mdot_probe)
+#   pmc:REGEX:SCRIPT[:ARGS] tools/pmc_kernels.sh (one rocprofv3 --pmc pass per counter
+#                    group) over python3 SCRIPT ARGS for kernels matching REGEX, then pmc_table.py
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -70,6 +72,9 @@ for step in "$@"; do
              run "med_$nm" 120 python3 tools/trace_medians.py $O/${TAG}_trace_$nm ;;
     bin:*) s=${step#bin:}; b=${s%%:*}; a=""; [ "$s" != "$b" ] && a=$(echo "${s#*:}" | tr @ ' ')
            run "bin_$(basename "$b")" 300 "$b" $a ;;
+    pmc:*) s=${step#pmc:}; rx=${s%%:*}; s=${s#*:}; scr=${s%%:*}; a=""; [ "$s" != "$scr" ] && a=$(echo "${s#*:}" | tr @ ' ')
+           TAG=${TAG}_pmc REGEX="$rx" run "pmc_$(basename "$scr" .py)" 900 bash tools/pmc_kernels.sh python3 "$R/$scr" $a
+           run "pmctab_$(basename "$scr" .py)" 120 python3 tools/pmc_table.py $O/pmc_${TAG}_pmc ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
