@@ -443,6 +443,10 @@ def oracle_check(grid: int, P: int, threads: int) -> dict:
 PARITY_BAR = "its and reason equal to the oracle's, x within relative L2 1e-10 (north_star)"
 
 
+def rnd(v, k):
+    return None if v is None else round(v, k)
+
+
 def parity_record(its: int, reason: int, rel: float, o: dict) -> dict:
     return {"checker": f"oracle/petsc_oracle.c CG + Jacobi, P = {o['P']} row-block model, converged "
                        f"(rtol 1e-5), {o['solve_s']} s on the host",
@@ -575,16 +579,24 @@ def main():
     if world == 1:
         leg_specs = [("auto", {})]
     else:
-        leg_specs = [("mode2/eager", {9: 2, 7: 1}), ("mode2/graph", {9: 2, 7: 2}),
-                     ("mode5/eager", {9: 5, 7: 1}), ("mode5/graph", {9: 5, 7: 2})]
+        # eager legs first: a multi-rank RCCL capture has only ever run on the
+        # driver's node, so if it fails there (an RCCL error, or no progress
+        # for 30 s: knob 33), the eager legs are already measured and the
+        # line is still printed from them
+        leg_specs = [("mode2/eager", {9: 2, 7: 1}), ("mode5/eager", {9: 5, 7: 1}),
+                     ("mode2/graph", {9: 2, 7: 2, 33: 30000}), ("mode5/graph", {9: 5, 7: 2, 33: 30000})]
 
     def set_knobs(kn):
         return {k: L.mx_debug_set(k, v) for k, v in kn.items()}
 
     legs = []
+    comm_dead = None
     for name, kn in leg_specs:
         old = set_knobs(kn)
         try:
+            # rehearsal hook: the failure path of a leg (MXSOLVE_BENCH_FAIL_LEG=<leg name>)
+            if os.environ.get("MXSOLVE_BENCH_FAIL_LEG") == name:
+                raise _lib.MxError(_lib.MX_ERR_COMM, f"injected failure of leg {name}")
             if args.warmup > 0:
                 A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=args.warmup)
             barrier()
@@ -594,7 +606,8 @@ def main():
             dt_local = time.perf_counter() - t0
             dt = max_over_ranks(dt_local)
             assert r["its"] == args.steps, r
-            leg = {"leg": name, "knobs": kn, "cg_mode": r["cg_mode"], "value": round(args.steps / dt, 3),
+            leg = {"leg": name, "knobs": kn, "cg_mode": r["cg_mode"], "cg_xbatch": r["cg_xbatch"],
+                   "value": round(args.steps / dt, 3),
                    "ms_per_step": round(dt / args.steps * 1e3, 4), "_dt": dt,
                    "per_rank_timed_s": [round(v, 5) for v in gather(dt_local)]}
             if not args.no_solve:
@@ -606,8 +619,17 @@ def main():
                 ts = max_over_ranks(time.perf_counter() - t0)
                 leg.update({"its": rs["its"], "reason": rs["reason"], "solve_s": ts, "_x": x.clone()})
             legs.append(leg)
+        except _lib.MxError as e:
+            if not legs:
+                raise
+            # the communicator is aborted: no further GPU legs or collectives
+            legs.append({"leg": name, "knobs": kn, "error": str(e)})
+            comm_dead = str(e)
+            break
         finally:
             set_knobs(old)
+    failed = [lg for lg in legs if "error" in lg]
+    legs = [lg for lg in legs if "error" not in lg]
 
     # parity: every leg's converged solve against the oracle (the checker, run
     # on rank 0 after the GPU work; at N = 1 it is the cpu_baseline leg's own
@@ -645,76 +667,83 @@ def main():
     chosen = max(passing or legs[:1], key=lambda lg: lg["value"])
     set_knobs(chosen["knobs"])          # the chosen leg's settings for the measurements below
     value, dt = chosen["value"], chosen["_dt"]
+    legs += failed
 
-    # roofline pass: the same CG iterations with a HIP event pair on every
-    # MatMult-family launch (on the library stream the kernel runs on; one
-    # rank: the events are attached to the kernel's own dispatch by
-    # hipExtLaunchKernel, so they time the kernel alone, as the profiler's
-    # trace does).  Kept out of the K timed steps: the profiled solve runs
-    # eagerly (no graph).  profile bit 0: the MatMult (mode 5: the p.Ap pass),
-    # bit 1: mode 5's residual update, bit 2: the batched direction update
-    x.zero_()
-    rp = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=min(args.steps, 100), profile=7)
-    mode = rp["cg_mode"]
-    xb = rp.get("cg_xbatch", 1)
-    spmv_avg_ms = rp["spmv_ms"] / max(rp["spmv_count"], 1)
+    mode, xb = chosen["cg_mode"], chosen.get("cg_xbatch", 1)
     bytes_csr = spmv_bytes(m, nnz_loc, ng)
     bytes_spmv = spmv_format_bytes(info, m, nnz_loc, ng)
-    meta = pair_meta_bytes(info, m, nnz_loc, ng)
-    pw = None
-    if mode == 5:
-        # the SpMV-bearing kernel: the residual update (A p recomputed, r read
-        # and written); the p.Ap pass reported beside it
-        upd_avg_ms = rp["upd_ms"] / max(rp["upd_count"], 1)
-        bytes_launch = 8 * (m + ng) + 16 * m + meta
-        avg_ms = upd_avg_ms
-        bytes_pw = 8 * (m + ng) + meta
-        pw = {"kernel": "spmv_pair_zm_kernel<SPMV_PW> (p.Ap partials, product not stored)",
-              "avg_launch_ms": round(spmv_avg_ms, 5), "bytes_per_launch": bytes_pw,
-              "GBps": round(bytes_pw / (spmv_avg_ms * 1e-3) / 1e9, 1),
-              "frac": round(bytes_pw / (spmv_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-    else:
-        bytes_launch = bytes_spmv + (32 * m if mode == 1 else 0)   # SPMV_CG: + r, x r/w, p_i
-        avg_ms = spmv_avg_ms
-    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    # the direction update (the iteration's longest kernel in mode 5): r and
-    # p_{i-1} in, p_i out (24 B/row), and every xb-th launch the xb - 1 older
-    # directions and x in, x out -- per launch on average 24 + (8 (xb - 1) + 16) / xb B/row
-    dom = None
-    if rp.get("pb_count"):
-        pb_ms = rp["pb_ms"] / rp["pb_count"]
-        pb_bytes = 24 * m + (8 * (xb - 1) + 16) * m // max(xb, 1)
-        dom = {"kernel": f"cg_pb_kernel<JM, {xb}> (direction update p_i = z + b p_(i-1), the x steps batched by {xb})",
-               "avg_launch_ms": round(pb_ms, 5), "launches": rp["pb_count"], "bytes_per_launch": pb_bytes,
-               "GBps": round(pb_bytes / (pb_ms * 1e-3) / 1e9, 1),
-               "frac": round(pb_bytes / (pb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        tp = load_traffic(n, world, mode, "/pb")
-        dom.update({"traffic": tp["bytes_per_launch"] if tp else None,
-                    "traffic_source": tp.get("source") if tp else None})
-    # standalone SpMV timing (same kernel, back-to-back)
-    y = comm.empty(m)
-    spmv_alone_ms, mult_ms = A.bench_mult(b, y, 50)
-    # cold-cache MatMult: stream 512 MB through the caches first
-    flush = torch.empty(1 << 26, dtype=torch.float64, device=y.device)
-    cold = []
-    for _ in range(3):
-        flush.fill_(1.0)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        A.mult(b, y)
-        e1.record()
-        e1.synchronize()
-        cold.append(e0.elapsed_time(e1))
-    del flush
-    cold_ms = sorted(cold)[1]
+    pw = dom = comm_lat = None
+    achieved = avg_ms = spmv_avg_ms = spmv_alone_ms = mult_ms = cold_ms = bytes_launch = None
+    if comm_dead is None:       # (an aborted communicator runs nothing more)
+        # roofline pass: the same CG iterations with a HIP event pair on every
+        # MatMult-family launch (on the library stream the kernel runs on; one
+        # rank: the events are attached to the kernel's own dispatch by
+        # hipExtLaunchKernel, so they time the kernel alone, as the profiler's
+        # trace does).  Kept out of the K timed steps: the profiled solve runs
+        # eagerly (no graph).  profile bit 0: the MatMult (mode 5: the p.Ap pass),
+        # bit 1: mode 5's residual update, bit 2: the batched direction update
+        x.zero_()
+        rp = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=min(args.steps, 100), profile=7)
+        mode = rp["cg_mode"]
+        xb = rp.get("cg_xbatch", 1)
+        spmv_avg_ms = rp["spmv_ms"] / max(rp["spmv_count"], 1)
+        bytes_csr = spmv_bytes(m, nnz_loc, ng)
+        bytes_spmv = spmv_format_bytes(info, m, nnz_loc, ng)
+        meta = pair_meta_bytes(info, m, nnz_loc, ng)
+        pw = None
+        if mode == 5:
+            # the SpMV-bearing kernel: the residual update (A p recomputed, r read
+            # and written); the p.Ap pass reported beside it
+            upd_avg_ms = rp["upd_ms"] / max(rp["upd_count"], 1)
+            bytes_launch = 8 * (m + ng) + 16 * m + meta
+            avg_ms = upd_avg_ms
+            bytes_pw = 8 * (m + ng) + meta
+            pw = {"kernel": "spmv_pair_zm_kernel<SPMV_PW> (p.Ap partials, product not stored)",
+                  "avg_launch_ms": round(spmv_avg_ms, 5), "bytes_per_launch": bytes_pw,
+                  "GBps": round(bytes_pw / (spmv_avg_ms * 1e-3) / 1e9, 1),
+                  "frac": round(bytes_pw / (spmv_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        else:
+            bytes_launch = bytes_spmv + (32 * m if mode == 1 else 0)   # SPMV_CG: + r, x r/w, p_i
+            avg_ms = spmv_avg_ms
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+        # the direction update (the iteration's longest kernel in mode 5): r and
+        # p_{i-1} in, p_i out (24 B/row), and every xb-th launch the xb - 1 older
+        # directions and x in, x out -- per launch on average 24 + (8 (xb - 1) + 16) / xb B/row
+        dom = None
+        if rp.get("pb_count"):
+            pb_ms = rp["pb_ms"] / rp["pb_count"]
+            pb_bytes = 24 * m + (8 * (xb - 1) + 16) * m // max(xb, 1)
+            dom = {"kernel": f"cg_pb_kernel<JM, {xb}> (direction update p_i = z + b p_(i-1), the x steps batched by {xb})",
+                   "avg_launch_ms": round(pb_ms, 5), "launches": rp["pb_count"], "bytes_per_launch": pb_bytes,
+                   "GBps": round(pb_bytes / (pb_ms * 1e-3) / 1e9, 1),
+                   "frac": round(pb_bytes / (pb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            tp = load_traffic(n, world, mode, "/pb")
+            dom.update({"traffic": tp["bytes_per_launch"] if tp else None,
+                        "traffic_source": tp.get("source") if tp else None})
+        # standalone SpMV timing (same kernel, back-to-back)
+        y = comm.empty(m)
+        spmv_alone_ms, mult_ms = A.bench_mult(b, y, 50)
+        # cold-cache MatMult: stream 512 MB through the caches first
+        flush = torch.empty(1 << 26, dtype=torch.float64, device=y.device)
+        cold = []
+        for _ in range(3):
+            flush.fill_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            A.mult(b, y)
+            e1.record()
+            e1.synchronize()
+            cold.append(e0.elapsed_time(e1))
+        del flush
+        cold_ms = sorted(cold)[1]
 
-    # communication latency on the library stream (N > 1): the two CG
-    # all-reduces and the halo exchange, back to back; diagnostics for scaling
-    comm_lat = None
-    if world > 1:
-        comm_lat = {"allreduce_1_us": round(comm.comm_bench(0, 200), 2),
-                    "allreduce_3_us": round(comm.comm_bench(1, 200), 2),
-                    "halo_us": round(comm.comm_bench(2, 200, A), 2)}
+        # communication latency on the library stream (N > 1): the two CG
+        # all-reduces and the halo exchange, back to back; diagnostics for scaling
+        comm_lat = None
+        if world > 1:
+            comm_lat = {"allreduce_1_us": round(comm.comm_bench(0, 200), 2),
+                        "allreduce_3_us": round(comm.comm_bench(1, 200), 2),
+                        "halo_us": round(comm.comm_bench(2, 200, A), 2)}
 
     solve = None
     if "its" in chosen:
@@ -725,7 +754,7 @@ def main():
                  "time_to_solution_s": round(ts + t_asm + t_setup, 3),
                  "process_init_s": round(t_init, 3)}
 
-    copy_gbps = round(stream_copy_gbps(y.device, m), 1)
+    copy_gbps = round(stream_copy_gbps(x.device, m), 1) if comm_dead is None else None
 
     asm_host = None
     if rank == 0 and world == 1 and not args.no_asm:
@@ -752,8 +781,8 @@ def main():
                        "rows": info["M"], "nnz": int(7 * n**3 - 6 * n**2),
                        "parallelism": (f"row-block x{world} (" + ("shared-memory rehearsal" if shm else "RCCL halo + allreduce") + ")") if world > 1 else "single GPU"},
             "parity": chosen.get("parity"),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "hbm", "achieved": rnd(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": rnd(achieved and achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic["bytes_per_launch"] if traffic else None,
                          "traffic_source": (traffic.get("source", "") + " -- rocprofv3 PMC (FETCH_SIZE x 2 + "
                                             "WRITE_SIZE, gfx950 correction) of the same kernel on a builder box, "
@@ -767,7 +796,7 @@ def main():
                                      "spmv_sell_kernel<SPMV_DOT> (CG MatMult")) +
                                    (", HIP events attached to the kernel's dispatch (hipExtLaunchKernel)" if world == 1 else
                                     ", HIP events around the MatMult") + ", rank 0)",
-                         "bytes_per_launch": bytes_launch, "avg_launch_ms": round(avg_ms, 5),
+                         "bytes_per_launch": bytes_launch, "avg_launch_ms": rnd(avg_ms, 5),
                          "format": ("value codes (" + str(info.get("value_codes")) + " distinct), " +
                                     ("row pairs" if info.get("pair_shape") else "one row per lane") +
                                     (f", {info['pair_blocks']} distinct code blocks" if info.get("pair_blocks") else "") +
@@ -779,7 +808,8 @@ def main():
                                        "frac": round(iter_gbps / HBM_PEAK_GBS, 4)},
                          # how much faster than a CSR SpMV (SURVEY §8d bytes) streaming at HBM peak
                          "csr_bytes_per_launch": bytes_csr,
-                         "speedup_vs_csr_at_peak": round((bytes_csr / (HBM_PEAK_GBS * 1e9)) / (spmv_avg_ms * 1e-3), 3)},
+                         "speedup_vs_csr_at_peak": rnd(spmv_avg_ms and (bytes_csr / (HBM_PEAK_GBS * 1e9)) / (spmv_avg_ms * 1e-3), 3)},
+            "comm_failure": comm_dead,
             "pw_pass": pw,
             "cpu_baseline": cpu,
             "legs": legs,
@@ -789,7 +819,7 @@ def main():
                                 "GBps": round(bytes_spmv / (spmv_alone_ms * 1e-3) / 1e9, 1),
                                 "matmult_ms": round(mult_ms, 5),
                                 "cold_matmult_ms": round(cold_ms, 5),
-                                "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1)},
+                                "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1)} if spmv_alone_ms else None,
             "spmv_general": general,
             "cg_iter_bytes_survey": cg_iter_bytes(m, nnz_loc, ng),
             "cg_fusion_mode": mode,
@@ -804,8 +834,12 @@ def main():
             "assembly_host_csr": asm_host,
         }
         print(json.dumps(out), flush=True)
-    A.destroy()
-    comm.destroy()
+    try:
+        A.destroy()
+        comm.destroy()
+    except _lib.MxError:
+        if comm_dead is None:
+            raise
     if dist is not None:
         dist.destroy_process_group()
 

@@ -16,6 +16,7 @@
 #   bench            bench.py with its defaults (K = 500)
 #   benchfast        bench.py --steps 100 --no-cpu --no-asm --no-general
 #   shm2             N = 2 rehearsal on one GPU (MXSOLVE_TRANSPORT=shm, torchrun)
+#   shm2fail         the same with the mode2/graph leg failing (the line must still print)
 #   prof             tools/profile.sh (trace + FETCH/WRITE PMC passes + calibration)
 #   configs          tools/bench_configs.py (C2/C3/C4/C5-share converged solves)
 #   general:LEGS     tools/bench_general.py LEGS (comma separated)
@@ -58,6 +59,8 @@ for step in "$@"; do
     benchfast) run benchfast 300 python3 -u bench.py --steps 100 --no-cpu --no-asm --no-general ;;
     shm2) MXSOLVE_TRANSPORT=shm run shm2 400 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
             --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 50 --warmup 5 ;;
+    shm2fail) MXSOLVE_TRANSPORT=shm MXSOLVE_BENCH_FAIL_LEG=mode2/graph run shm2fail 400 python3 -u -m torch.distributed.run \
+                --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 50 --warmup 5 ;;
     prof) run prof 1000 bash tools/profile.sh ;;
     configs) run configs 700 python3 -u tools/bench_configs.py ;;
     c4prof) run c4prof 600 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_c4trace -o run -- \
