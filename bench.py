@@ -443,6 +443,14 @@ def oracle_check(grid: int, P: int, threads: int) -> dict:
 PARITY_BAR = "its and reason equal to the oracle's, x within relative L2 1e-10 (north_star)"
 
 
+def choose_leg(legs: list, no_solve: bool = False) -> dict:
+    """The leg `value` is taken from: the fastest whose converged solve
+    passed the parity check (every leg when no converged solves ran); when
+    none passed, the first leg -- its parity record then says so."""
+    passing = [lg for lg in legs if lg.get("parity", {}).get("ok", no_solve)]
+    return max(passing or legs[:1], key=lambda lg: lg["value"])
+
+
 def rnd(v, k):
     return None if v is None else round(v, k)
 
@@ -663,8 +671,7 @@ def main():
     elif rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(n, threads, how)
         cpu.pop("_oracle")
-    passing = [lg for lg in legs if lg.get("parity", {}).get("ok", args.no_solve)]
-    chosen = max(passing or legs[:1], key=lambda lg: lg["value"])
+    chosen = choose_leg(legs, args.no_solve)
     set_knobs(chosen["knobs"])          # the chosen leg's settings for the measurements below
     value, dt = chosen["value"], chosen["_dt"]
     legs += failed

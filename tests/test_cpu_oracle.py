@@ -234,3 +234,16 @@ def test_bench_parity_record():
     assert not bench.parity_record(561, 2, 3e-14, o)["ok"]
     assert not bench.parity_record(560, 3, 3e-14, o)["ok"]
     assert not bench.parity_record(560, 2, 2e-10, o)["ok"]
+
+
+def test_bench_choose_leg():
+    """bench.py takes value from the fastest parity-passing leg; a faster leg
+    that failed parity is never chosen; with no passing leg, the first."""
+    import bench
+    legs = [{"leg": "a", "value": 10.0, "parity": {"ok": True}},
+            {"leg": "b", "value": 30.0, "parity": {"ok": False}},
+            {"leg": "c", "value": 20.0, "parity": {"ok": True}}]
+    assert bench.choose_leg(legs)["leg"] == "c"
+    assert bench.choose_leg([dict(l, parity={"ok": False}) for l in legs])["leg"] == "a"
+    assert bench.choose_leg([{"leg": "x", "value": 1.0}, {"leg": "y", "value": 2.0}], no_solve=True)["leg"] == "y"
+    assert bench.rnd(None, 3) is None and bench.rnd(1.23456, 2) == 1.23
