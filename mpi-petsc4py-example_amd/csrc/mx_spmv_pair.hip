@@ -246,7 +246,11 @@ struct PairRuArgs {
   int *hw;                     // the host's pinned words (Poller)
 };
 
-template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0, bool SYM = false>
+// RPF (knob 66, residual update only): the next step's r pairs are loaded
+// one step ahead, so every wave keeps its own HBM stream (r is read from
+// memory: the direction update read it non-temporally) in flight while it
+// sums the current planes
+template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0, bool SYM = false, bool RPF = false>
 __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a, const double *__restrict__ x,
                                                            double *__restrict__ y, const int32_t *__restrict__ pblk,
                                                            const PairUni *__restrict__ puni, const PairRuArgs ru) {
@@ -298,9 +302,20 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
     const int cb = col * 128 + 2 * lane;       // the lane's rows within a plane
     dbl2 zm = bload2(xr, z0 * D + cb - D), c = bload2(xr, z0 * D + cb);
     uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
+    constexpr bool PF = RPF && RU;
+    dbl2 rn[ZU];                                // PF: the next full step's r, loaded ahead
+    bool have = false;
+    if constexpr (PF) {
+      if (z0 + ZU <= z1) {
+#pragma unroll
+        for (int q = 0; q < ZU; ++q) rn[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + (z0 + q) * D + cb));
+        have = true;
+      }
+    }
     // NQ units (planes z .. z + NQ - 1) with all their loads in flight
     auto step = [&](int z, auto nq) __attribute__((always_inline)) {
       constexpr int NQ = decltype(nq)::value;
+      constexpr bool PFS = PF && NQ == ZU;      // a full step: its r came with the previous one
       dbl2 L[NQ][NR], zp[NQ], rq[NQ];
       double e[NQ];
       uint32_t bw[NQ];
@@ -319,7 +334,18 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
         int eo = ecst;
         if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
         e[q] = bload1(xr, ub + eo);
-        if constexpr (RU) rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
+        if constexpr (RU) {
+          if constexpr (PFS) rq[q] = have ? rn[q % ZU] : __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
+          else rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
+        }
+      }
+      if constexpr (PFS) {                         // the next full step's r
+        have = z + 2 * ZU <= z1;
+        if (have) {
+#pragma unroll
+          for (int q = 0; q < ZU; ++q)
+            rn[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + (z + ZU + q) * D + cb));
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1672,6 +1698,15 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
 #undef RU_J
 #undef RU_S
 #undef RU
+  // knob 66: the next step's r loaded one step ahead (clean, one rank, 2 planes per step)
+  if (clean && !split && g_knobs.ru_rpf && z2 && g_knobs.ru_units != 3 && g_knobs.ru_units != 4) {
+    if (A->sd.pair_shape == 5)
+      f = jac_mode == 2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 2, 2, false, true>
+                        : &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 2, 0, false, true>;
+    else
+      f = jac_mode == 2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 2, 2, false, true>
+                        : &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 2, 0, false, true>;
+  }
   // knob 64: 3 or 4 planes per step for the clean one-rank residual update
   // (more of its HBM reads in flight per wave)
   if (clean && !split && (g_knobs.ru_units == 3 || g_knobs.ru_units == 4)) {
