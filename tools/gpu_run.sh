@@ -37,9 +37,12 @@ export TMPDIR=/tmp
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
 
-run() {   # run NAME SECONDS CMD... ; output to $O/TAG_NAME.log
+NSTEP=0
+run() {   # run NAME SECONDS CMD... ; output to $O/TAG_NAME.log (TAG_NAME_<n>.log when NAME repeats)
   local name=$1 secs=$2; shift 2
+  NSTEP=$((NSTEP + 1))
   local log=$O/${TAG}_${name}.log
+  [ -e "$log" ] && log=$O/${TAG}_${name}_${NSTEP}.log
   echo "[$(date +%T)] $name: $*" | tee -a $O/${TAG}_commands.txt
   timeout -k 10 "$secs" "$@" > "$log" 2>&1
   local rc=$?
