@@ -341,8 +341,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         them (no per-run branches, no selects; the same bits)
  * key 49: 27-point z-march planes per step (1, default, or 2)
  * key 50: GMRES MDot in one pass over w for <= 32 basis vectors (2, default: a
- *         workgroup holds 2048 rows of w in registers and walks the vectors;
- *         1: the four waves of a workgroup split the vectors; 0: groups of key 16)
+ *         workgroup holds 2048 rows of w in registers and walks the vectors
+ *         four at a time; 4: the same with the next four's loads issued
+ *         first (170 VGPRs), 5: that with 1024-row chunks; 1: the four waves
+ *         of a workgroup split the vectors; 0: groups of key 16)
  * key 51: GMRES MAXPY + norm pass in chunks (1: 2048 rows per workgroup
  *         step, 16-byte pairs; 0, default: one row per thread -- measured
  *         0.5% faster per GMRES(30) step beside the chunk MDot)
@@ -369,6 +371,19 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         exact product: the same bits; 1, default; 0: multiply and add)
  * key 61: testing: a device stall of this many us before each GMRES restart
  *         read-back (default 0), so the no-progress deadline can be driven
+ * key 62: CG mode 5's 27-point passes by separable box sums on a "box"
+ *         operator (one off-diagonal value, one diagonal value; A p =
+ *         (c - v) p + v box(p), reassociated: A p to rounding, not the
+ *         MatMult's bits) -- 1 on, 0 (default: measured 1-2% slower per C5
+ *         iteration than the slot-order passes, which are not VALU-bound)
+ * key 63: workgroups per CU of the key-62 kernels (0: the 27-point defaults)
+ * key 64: residual update planes per z-march step, 3 or 4 (0, default: key 42's)
+ * key 65: z-march grids that fill whole task rounds (1, default: the
+ *         workgroups per CU, at most the configured, whose tasks per XCD are
+ *         a whole number of rounds of its waves -- C5's share: 4 instead of 5
+ *         for the residual update; 0: the configured counts)
+ * key 66: residual update with the next step's r loaded one step ahead (0/1,
+ *         default 0: -0.3% per C3 iteration, within noise)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches
