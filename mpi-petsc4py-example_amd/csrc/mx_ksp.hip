@@ -906,7 +906,42 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
       const double r = red4(a[0], a[1], a[2], a[3], lane);
       if ((lane & 15) == (j >> 2)) acc += r;
     };
-    if constexpr (FORM == 1) {
+    if constexpr (FORM == 2) {
+      // knob 50 = 6: one vector at a time (the workgroup streams one 16 KB
+      // piece of one vector, as round 3's walk did: few DRAM streams at once),
+      // the next vector's loads issued before this one's sums; the four lane
+      // partials of a group reduced together (red4)
+      auto vload = [&](int j, dbl2 (&t)[WP]) __attribute__((always_inline)) {
+        const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+          const int64_t i = c0 + k * 256 + threadIdx.x;
+          t[k] = (FULL || i < n2) ? __builtin_nontemporal_load(vq + i) : dbl2{0.0, 0.0};
+        }
+      };
+      dbl2 ta[WP], tb[WP];
+      vload(0, ta);
+      for (int j = 0; j < nv; j += 4) {            // wave-uniform
+        double a[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          dbl2 (&cur)[WP] = (q & 1) ? tb : ta;
+          dbl2 (&nxt)[WP] = (q & 1) ? ta : tb;
+          if (j + q + 1 < nv) vload(j + q + 1, nxt);
+          a[q] = 0.0;
+          if (j + q < nv) {
+            const double sj = vscale[j + q];
+#pragma unroll
+            for (int k = 0; k < WP; ++k) {
+              a[q] += wr[k].x * (sj * cur[k].x);
+              a[q] += wr[k].y * (sj * cur[k].y);
+            }
+          }
+        }
+        const double r = red4(a[0], a[1], a[2], a[3], lane);
+        if ((lane & 15) == (j >> 2)) acc += r;
+      }
+    } else if constexpr (FORM == 1) {
       // knob 50 = 4: the next group's 16 loads issued before this group's sums
       dbl2 t[4][WP], tn[4][WP];
       double sq[4], sqn[4];
@@ -1738,9 +1773,11 @@ static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double
 // buffer holds max_k + 2 rows rounded up to 32; groups are gw wide (knob 16)
 static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
                  const double *vscale, double *partials, const int *stop_flag, int grid) {
-  if ((g_knobs.mdot_split == 2 || g_knobs.mdot_split == 4 || g_knobs.mdot_split == 5) && nv <= 32) {   // one pass over w, chunk form (knob 50)
+  if ((g_knobs.mdot_split == 2 || (g_knobs.mdot_split >= 4 && g_knobs.mdot_split <= 7)) && nv <= 32) {   // one pass over w, chunk form (knob 50)
     if (g_knobs.mdot_split == 4) mdot_chunk_kernel<4, 1><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
     else if (g_knobs.mdot_split == 5) mdot_chunk_kernel<2, 1><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+    else if (g_knobs.mdot_split == 6) mdot_chunk_kernel<4, 2><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+    else if (g_knobs.mdot_split == 7) mdot_chunk_kernel<8, 2><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
     else mdot_chunk_kernel<4><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
     HIPCHECK(hipGetLastError());
     return;
