@@ -1095,6 +1095,98 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
   block_partials<1>(v, partials, gridDim.x, fold);
 }
 
+// The MAXPY + norm pass one vector at a time (knob 51 = 2 / 3: WP = 4 / 8
+// pairs per thread): a workgroup holds 512 WP rows of w in registers and
+// walks the basis in order, loading the next vector's piece before adding the
+// current one (few DRAM streams at once, the next one in flight: the MDot's
+// mdot_chunk_kernel<WP, 2> form).  VecMAXPY_Seq's grouping is kept exactly:
+// a group's products are summed in order, g = a_j0 v_j0, g = g + a_j v_j,
+// then u = u + g at the group's end (the first nv % 4 vectors, then fours),
+// fl(s_j v) applied on read -- every row's bits are maxpy_norm_kernel's.
+template <int WP>
+__global__ void __launch_bounds__(256) maxpy_seq_kernel(int64_t n, double *__restrict__ w,
+                                                        const double *__restrict__ V, int64_t ldv, int nv,
+                                                        KspState *__restrict__ s, const double *__restrict__ red_k,
+                                                        const double *__restrict__ vscale,
+                                                        double *__restrict__ hh, int ld,
+                                                        double *__restrict__ partials, const Fold fold) {
+  if (s->inner_stop) return;
+  __shared__ double a[MAX_RESTART + 1], sc[MAX_RESTART + 1];
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  for (int j = threadIdx.x; j < nv; j += 256) {
+    const double h = red_k[j];
+    if (not_finite(h)) bad = 1;
+    a[j] = -h;                                   // lhh[j] = -h_j
+    sc[j] = vscale[j];
+  }
+  __syncthreads();
+  if (bad) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) stop(s, R_DIVERGED_NANORINF);
+    return;
+  }
+  if (blockIdx.x == 0)
+    for (int j = threadIdx.x; j < nv; j += 256) hh[(size_t)(nv - 1) * ld + j] = 0.0 - a[j];
+  const int rem = nv & 3;
+  double v[1] = {0.0};
+  const int64_t n2 = n >> 1, csz = 256 * WP, nfull = n2 / csz;
+  dbl2 *__restrict__ w2 = reinterpret_cast<dbl2 *>(w);
+  auto chunk = [&](int64_t c0, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    auto in = [&](int k) { return FULL || c0 + k * 256 + threadIdx.x < n2; };
+    auto vload = [&](int j, dbl2 (&t)[WP]) __attribute__((always_inline)) {
+      const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
+#pragma unroll
+      for (int k = 0; k < WP; ++k)
+        t[k] = in(k) ? __builtin_nontemporal_load(vq + c0 + k * 256 + threadIdx.x) : dbl2{0.0, 0.0};
+    };
+    dbl2 u[WP], g[WP], ta[WP], tb[WP];
+#pragma unroll
+    for (int k = 0; k < WP; ++k) u[k] = in(k) ? w2[c0 + k * 256 + threadIdx.x] : dbl2{0.0, 0.0};
+    vload(0, ta);
+    auto step = [&](int j, dbl2 (&cur)[WP], dbl2 (&nxt)[WP]) __attribute__((always_inline)) {
+      if (j + 1 < nv) vload(j + 1, nxt);         // wave-uniform
+      const bool first = j == 0 || (j >= rem && (j - rem) % 4 == 0);
+      const bool last = (j < rem) ? j == rem - 1 : (j - rem) % 4 == 3;
+      const double aj = a[j], sj = sc[j];
+#pragma unroll
+      for (int k = 0; k < WP; ++k) {
+        const dbl2 p = dbl2{aj * (sj * cur[k].x), aj * (sj * cur[k].y)};
+        g[k] = first ? p : dbl2{g[k].x + p.x, g[k].y + p.y};
+        if (last) u[k] = dbl2{u[k].x + g[k].x, u[k].y + g[k].y};
+      }
+    };
+    for (int j = 0; j < nv; j += 2) {
+      step(j, ta, tb);
+      if (j + 1 < nv) step(j + 1, tb, ta);
+    }
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+      if (!in(k)) continue;
+      w2[c0 + k * 256 + threadIdx.x] = u[k];
+      v[0] += u[k].x * u[k].x;
+      v[0] += u[k].y * u[k].y;
+    }
+  };
+  for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
+  if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // odd length: the last row (row form)
+    const int64_t i = n - 1;
+    double uu = w[i];
+    int j = 0;
+    auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
+    if (rem == 1) { uu = a[0] * vj(0) + uu; j = 1; }
+    else if (rem == 2) { uu = uu + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
+    else if (rem == 3) { uu = uu + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
+    for (; j < nv; j += 4)
+      uu = uu + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
+    w[i] = uu;
+    v[0] += uu * uu;
+  }
+  block_partials<1>(v, partials, gridDim.x, fold);
+}
+
 // normalise vv[k+1], happy breakdown, KSPGMRESUpdateHessenberg, convergence
 // The column and the rotations are staged in LDS by the whole workgroup
 // (coalesced loads) and thread 0 works there: the rotation loop's dependent
@@ -1889,7 +1981,10 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, mgrid, red.p, istop);
       c->allreduce_sum(red.p, k + 1);
       // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
-      (g_knobs.maxpy_pairs ? &maxpy_norm_kernel<true> : &maxpy_norm_kernel<false>)<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
+      if (g_knobs.maxpy_pairs == 2 || g_knobs.maxpy_pairs == 3)   // one vector at a time (knob 51)
+        (g_knobs.maxpy_pairs == 3 ? &maxpy_seq_kernel<8> : &maxpy_seq_kernel<4>)<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
+      else
+        (g_knobs.maxpy_pairs ? &maxpy_norm_kernel<true> : &maxpy_norm_kernel<false>)<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
       c->allreduce_sum(sred, 1);
       ++launched;
       gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p,
