@@ -313,7 +313,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         whose fused iteration-0 norms it must match bit for bit)
  * key 35: row-pair SpMV reads uniform-slot dictionary blocks as slot values +
  *         lane masks when the matrix has them (0/1, default 1)
- * key 36: grid of the GMRES MDot pass (0 = default 1024 workgroups)
+ * key 36: grid of the GMRES MDot pass (0 = default: 3 per CU for key 50 = 7, else 1024)
  * key 37: the Jacobi-fused row-pair MatMult (GMRES) takes dinv from a table
  *         indexed by the rows' diagonal code instead of reading the dinv
  *         vector (0/1, default 1; the same bits)
@@ -340,12 +340,16 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         27-point z-march zeroes empty runs and x-line edges where it loads
  *         them (no per-run branches, no selects; the same bits)
  * key 49: 27-point z-march planes per step (1, default, or 2)
- * key 50: GMRES MDot in one pass over w for <= 32 basis vectors (2, default: a
- *         workgroup holds 2048 rows of w in registers and walks the vectors
- *         four at a time; 4: the same with the next four's loads issued
- *         first (170 VGPRs), 5: that with 1024-row chunks; 1: the four waves
- *         of a workgroup split the vectors; 0: groups of key 16)
- * key 51: GMRES MAXPY + norm pass in chunks (1: 2048 rows per workgroup
+ * key 50: GMRES MDot in one pass over w for <= 32 basis vectors (7, default:
+ *         a workgroup holds 4096 rows of w in registers and walks the basis
+ *         one vector at a time, the next vector's loads issued before the
+ *         current one's sums, four lane partials reduced together -- -2 to
+ *         -3% per GMRES(30) step against 2; 6: the same with 2048 rows; 2: 2048
+ *         rows, four vectors' loads at once; 4 / 5: 2 with the next four's
+ *         loads first (4096 / 1024 rows); 1: the four waves of a workgroup
+ *         split the vectors; 0: groups of key 16)
+ * key 51: GMRES MAXPY + norm pass in chunks (2 / 3: one vector at a time with
+ *         the next in flight, 2048 / 4096 rows -- measured 3% slower; 1: 2048 rows per workgroup
  *         step, 16-byte pairs; 0, default: one row per thread -- measured
  *         0.5% faster per GMRES(30) step beside the chunk MDot)
  * key 54: GMRES basis stride padding in rows (multiple of 32; default 256:

@@ -1853,7 +1853,13 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
 // finish): knob 36, default RED_BLOCKS.  mdot_kernel<32> holds 139 VGPRs (3
 // waves per SIMD, 768 resident workgroups), yet its resident grid measured
 // 1.1% slower per GMRES(30) step than 1024 and 512 0.8% (tools/gmres_ab.py)
-static int mdot_grid() { return g_knobs.mdot_grid > 0 ? g_knobs.mdot_grid : RED_BLOCKS; }
+// (knob 50 = 7, the default chunk form, holds 153 VGPRs: three workgroups per
+// CU are resident, so its grid is one generation of them -- 768 on 256 CUs --
+// instead of 1024 in two uneven generations)
+static int mdot_grid() {
+  if (g_knobs.mdot_grid > 0) return g_knobs.mdot_grid;
+  return g_knobs.mdot_split == 7 ? std::min(RED_BLOCKS, 3 * device_cu_count()) : RED_BLOCKS;
+}
 
 template <int NV>
 static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int j0, int k,
