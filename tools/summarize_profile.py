@@ -141,7 +141,10 @@ def main():
         extra.append((f"varcoef{grid}^3/N{ngpu}", gk[0], gen["streamed_bytes"]))
     for key, k, a in extra:
         if k in fetch and k in write:
-            fr, wr = statistics.median(fetch[k]) * 1024, statistics.median(write[k]) * 1024
+            # the direction update's launches differ (every xb-th one carries the
+            # x batch): its algorithmic bytes are a per-launch mean, so is its traffic
+            agg = statistics.mean if key.endswith("/pb") else statistics.median
+            fr, wr = agg(fetch[k]) * 1024, agg(write[k]) * 1024
             t = fr * corr + wr
             out[key] = {"bytes_per_launch": round(t), "fetch_bytes_raw": round(fr), "write_bytes": round(wr),
                         "fetch_correction": round(corr, 4), "algorithmic_bytes": a,
