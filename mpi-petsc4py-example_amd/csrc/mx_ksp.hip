@@ -439,9 +439,13 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
   // rows per thread in the same order as cg_norms_kernel on this grid, so the
   // same bits -- folded in-launch, the last workgroup running cg_init
   double nv[3] = {0.0, 0.0, 0.0};
-  auto walk = [&](auto ntc, const double *__restrict__ rs, auto nrmc) __attribute__((always_inline)) {
+  // NP (b == 0: iteration 0, or a restart of the direction): p_i = z, so
+  // p_{i-1} is not read at all (VecAYPX_Seq with b == 0 copies) -- iteration
+  // 0 of every solve used to stream the unused buffer (+20 us at 256^3)
+  auto walk = [&](auto ntc, const double *__restrict__ rs, auto nrmc, auto npc) __attribute__((always_inline)) {
     constexpr bool NTL = decltype(ntc)::value;
     constexpr bool NRM = decltype(nrmc)::value;
+    constexpr bool NP = decltype(npc)::value;
     auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
       if constexpr (NTL) return __builtin_nontemporal_load(q);
       else return *q;
@@ -457,7 +461,7 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
         double po[4], rr[4], dd[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          po[u] = ldv(pprev + k + u * stride);
+          po[u] = NP ? 0.0 : ldv(pprev + k + u * stride);
           rr[u] = ldv(rs + k + u * stride);
           dd[u] = JM == 1 ? dv[k + u * stride] : 0.0;
         }
@@ -470,19 +474,24 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
     }
     for (; k < n; k += stride) {
       const double rr = ldv(rs + k), dd = JM == 1 ? dv[k] : 0.0;
-      pout[k] = row(rr, dd, ldv(pprev + k));
+      pout[k] = row(rr, dd, NP ? 0.0 : ldv(pprev + k));
       norms(rr, dd);
     }
   };
-  if (r0 && i == 0) {
+  const std::true_type T{};
+  const std::false_type F{};
+  if (r0 && i == 0) {                            // (b == 0 at iteration 0)
     if (fin.cnt) {
-      if (unr & 2) walk(std::true_type{}, r0, std::true_type{});
-      else walk(std::false_type{}, r0, std::true_type{});
+      if (unr & 2) walk(T, r0, T, T);
+      else walk(F, r0, T, T);
       if (block_fold<3>(nv, npart, fin) && threadIdx.x == 0) cg_init_body<3>(s, hist);
-    } else if (unr & 2) walk(std::true_type{}, r0, std::false_type{});
-    else walk(std::false_type{}, r0, std::false_type{});
-  } else if (unr & 2) walk(std::true_type{}, r, std::false_type{});
-  else walk(std::false_type{}, r, std::false_type{});
+    } else if (unr & 2) walk(T, r0, F, T);
+    else walk(F, r0, F, T);
+  } else if (b == 0.0) {                          // wave-uniform
+    if (unr & 2) walk(T, r, F, T);
+    else walk(F, r, F, T);
+  } else if (unr & 2) walk(T, r, F, F);
+  else walk(F, r, F, F);
 }
 
 // x += a p, r -= a w (BLAS daxpy = fma), z = d.*r, [z.z, z.r, r.r] folded
@@ -1811,7 +1820,11 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   };
   if (graph && !use_graph && c->size == 1 && i < p.max_it) capture();
   for (; i < p.max_it;) {
-    if (use_graph && p.max_it - i >= poll) {
+    // knob 67: the solve's first batch is launched eagerly even when a graph
+    // is cached -- the first replayed node started ~20 us after the launch
+    // (the GPU idle after the state-init kernel) where eager launches keep
+    // the queue ahead of these long kernels from the first one
+    if (use_graph && p.max_it - i >= poll && !(g_knobs.cg_eager_first && i == 0)) {
       HIPCHECK(hipGraphLaunch(A->cg_graph, st));
       i += poll;
     } else {
