@@ -398,6 +398,106 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
   }
 }
 
+// CG mode 5's residual update on a clean one-rank 7-point layout, two lines
+// per wave (knob 68): a wave marches the columns of lines y and y + 1 (y
+// even) together, so line y's +n operand is line y + 1's own centre pair and
+// line y + 1's -n operand line y's -- per plane the two units load their +D
+// pairs, the outer lines y - 1 and y + 2, their edges and r: 8 vector loads
+// for two units instead of 10 (the residual update is vector-memory issue
+// bound: profiles/r04g_pmc_c3_iteration.txt).  Each unit sums its rows with
+// pair_sums, as spmv_pair_zm_kernel<SPMV_RUPD> does: the same bits.
+template <int JM>
+__global__ void __launch_bounds__(256) spmv_pair_zm2l_kernel(const PairLeanArgs a, const double *__restrict__ x,
+                                                             const int32_t *__restrict__ pblk,
+                                                             const PairUni *__restrict__ puni, const PairRuArgs ru) {
+  constexpr int PS = 7, NR = 5, TR = 2, LAST = 4;
+  KspState *s = ru.s;
+  if (s->top.done) {
+    if (ru.hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(ru.hw + HW_DONE, 1);
+    return;
+  }
+  const double pw = ru.ndot > 0 ? block_sum_array<16>(ru.dot_part, ru.ndot) : s->red1;
+  const CgAlpha al = cg_alpha(s, pw);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, ru.xb, false, ru.hw);
+  if (al.reason) return;
+  const double alpha = al.alpha;
+  const double *rin = (ru.r0 && al.i == 0) ? ru.r0 : ru.r;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[LAST], NL = a.anchor[3];           // plane, line
+  const int PL = NL / 128, PH = a.P / 2;                     // columns per line, column pairs per plane
+  const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
+  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
+  double nv[3] = {0.0, 0.0, 0.0};
+  const int ntask = (se - sb) * PH;
+  for (int t = w; t < ntask; t += W) {
+    const int seg = sb + t / PH, cp = t % PH;
+    const int colA = (cp / PL) * 2 * PL + cp % PL, colB = colA + PL;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cbA = colA * 128 + 2 * lane, cbB = colB * 128 + 2 * lane;
+    dbl2 zmA = bload2(xr, z0 * D + cbA - D), cA = bload2(xr, z0 * D + cbA);
+    dbl2 zmB = bload2(xr, z0 * D + cbB - D), cB = bload2(xr, z0 * D + cbB);
+    for (int z = z0; z < z1; ++z) {
+      const uint32_t bwA = (uint32_t)pblk[z * a.P + colA], bwB = (uint32_t)pblk[z * a.P + colB];
+      const int rA = z * D + cbA, rB = z * D + cbB;
+      const dbl2 zpA = bload2(xr, rA + D), zpB = bload2(xr, rB + D);
+      const dbl2 nA = bload2(xr, rA + a.anchor[1] + ((bwA & (PBLK_RUN0 << 1)) ? PAIR_OOR : 0));
+      const dbl2 nB = bload2(xr, rB + a.anchor[3] + ((bwB & (PBLK_RUN0 << 3)) ? PAIR_OOR : 0));
+      int eA = ecst, eB = ecst;
+      eA += lane == 0 ? ((bwA & PBLK_ELO) ? PAIR_OOR : 0) : ((bwA & PBLK_EHI) ? PAIR_OOR : 0);
+      eB += lane == 0 ? ((bwB & PBLK_ELO) ? PAIR_OOR : 0) : ((bwB & PBLK_EHI) ? PAIR_OOR : 0);
+      const double edA = bload1(xr, z * D + colA * 128 + eA), edB = bload1(xr, z * D + colB * 128 + eB);
+      const dbl2 rqA = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + rA));
+      const dbl2 rqB = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + rB));
+      __builtin_amdgcn_sched_barrier(0);
+      // line y's +n run is line y + 1's rows, line y + 1's -n run line y's
+      // (an empty run -- a grid edge, rare -- reads as 0.0, as its
+      // out-of-range load would)
+      const dbl2 Z{0.0, 0.0};
+      dbl2 LA[NR] = {zmA, nA, cA, (bwA & (PBLK_RUN0 << 3)) ? Z : cB, zpA};
+      dbl2 LB[NR] = {zmB, (bwB & (PBLK_RUN0 << 1)) ? Z : cA, cB, nB, zpB};
+      if (bwA & CARRY) {                         // wave-uniform, rare: an empty carried run
+        if (bwA & PBLK_RUN0) LA[0] = Z;
+        if (bwA & (PBLK_RUN0 << TR)) LA[TR] = Z;
+        if (bwA & (PBLK_RUN0 << LAST)) LA[LAST] = Z;
+      }
+      if (bwB & CARRY) {
+        if (bwB & PBLK_RUN0) LB[0] = Z;
+        if (bwB & (PBLK_RUN0 << TR)) LB[TR] = Z;
+        if (bwB & (PBLK_RUN0 << LAST)) LB[LAST] = Z;
+      }
+      const dbl2 wA = pair_sums<PS, true>(LA, edA, bwA, puni, lane);
+      const dbl2 wB = pair_sums<PS, true>(LB, edB, bwB, puni, lane);
+      auto upd = [&](dbl2 w2, dbl2 rq, int r0) __attribute__((always_inline)) {
+        const double ra = fma(-alpha, w2.x, rq.x), rb = fma(-alpha, w2.y, rq.y);
+        const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
+        nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
+        nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
+        *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+      };
+      upd(wA, rqA, rA);
+      upd(wB, rqB, rB);
+      zmA = cA; cA = zpA;
+      zmB = cB; cB = zpB;
+    }
+  }
+  block_partials<3>(nv, a.partials, gridDim.x, a.fold);
+}
+
 // 27-point z-march (Sell::puni27).  The nine runs are (dz, dy) in {-1,0,1}^2
 // at anchors -D-n, -D, -D+n, -n, 0, +n, D-n, D, D+n (each a tri run c-1, c,
 // c+1); marching a column in z, the runs of planes z-1 and z (six pairs and
@@ -1698,6 +1798,23 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
 #undef RU_J
 #undef RU_S
 #undef RU
+  // knob 68: two lines per wave (clean, one rank, 7-point, an even number of
+  // lines per plane, whole 128-row columns per line)
+  if (g_knobs.ru_2line && clean && !split && A->sd.pair_shape == 7 && a.anchor[3] > 0 && a.anchor[3] % 128 == 0 &&
+      (a.anchor[4] / a.anchor[3]) % 2 == 0 && a.anchor[4] % a.anchor[3] == 0 && a.anchor[1] == -a.anchor[3]) {
+    // tasks: column pairs per plane; the grid's segment length from the pairs
+    int L2, S2;
+    const int g2 = zm_tasks(a.P / 2, a.NZ, L2, S2, g_knobs.ru_bpc);
+    a.L = L2;
+    a.S = S2;
+    if (fold.cnt) { fold.ntotal = fold.ncount = g2; fold.base = 0; }
+    a.fold = fold;
+    note_dispatch(DSP_ZM_RUPD);
+    if (jac_mode == 2) launch_timed(&spmv_pair_zm2l_kernel<2>, g2, st, a, p, A->sd.pblk.p, A->sd.puni.p, ru);
+    else launch_timed(&spmv_pair_zm2l_kernel<0>, g2, st, a, p, A->sd.pblk.p, A->sd.puni.p, ru);
+    HIPCHECK(hipGetLastError());
+    return g2;
+  }
   // knob 66: the next step's r loaded one step ahead (clean, one rank, 2 planes per step)
   if (clean && !split && g_knobs.ru_rpf && z2 && g_knobs.ru_units != 3 && g_knobs.ru_units != 4) {
     if (A->sd.pair_shape == 5)

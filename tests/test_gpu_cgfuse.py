@@ -369,3 +369,36 @@ def test_mode5_nonsymmetric_full_rows(selfcomm, oracle_mod):
     assert (r["its"], r["reason"]) == (o["its"], o["reason"]), (r["its"], r["reason"], o["its"], o["reason"])
     assert np.allclose(r["history"], o["history"], rtol=1e-8, atol=0)
     assert np.linalg.norm(x.cpu().numpy() - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
+
+
+@pytest.mark.parametrize("dims,max_it", [((128, 128, 128), 10000), ((256, 128, 40), 10000), ((128, 128, 128), 37)])
+def test_two_line_residual_update_bitwise(selfcomm, oracle_mod, dims, max_it):
+    """Knob 68: CG mode 5's residual update with two lines per wave (line y's
+    +n operand is line y + 1's own rows) sums every row exactly as the one-line
+    z-march does: the whole solve -- its, residual history, x -- is bitwise the
+    default's; the dispatch shows the residual update ran."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    L = _lib.load()
+    A = DMat.stencil(selfcomm, "poisson3d", *dims)
+    m = A.info()["m"]
+    b = selfcomm.empty(m)
+    rhs_hash(selfcomm, 0, b)
+    outs = []
+    for k68 in (0, 1):
+        old = {k: L.mx_debug_set(k, v) for k, v in ((9, 5), (27, 1), (68, k68))}
+        try:
+            x = selfcomm.zeros(m)
+            dispatch_counts(reset=True)
+            r = A.solve(b, x, ksp="cg", pc="jacobi", rtol=1e-8, max_it=max_it, history=True)
+            dc = dispatch_counts(reset=True)
+            outs.append((r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy(), r["cg_mode"], dc))
+        finally:
+            for k, v in old.items():
+                L.mx_debug_set(k, v)
+    A.destroy()
+    a, c = outs
+    assert a[4] == c[4] == 5 and c[5]["zm_rupd"] > 0, (a[4], c[4], c[5])
+    assert a[:2] == c[:2]
+    assert np.array_equal(a[2].view(np.uint64), c[2].view(np.uint64))
+    assert np.array_equal(a[3].view(np.uint64), c[3].view(np.uint64))
