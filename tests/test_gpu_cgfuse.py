@@ -380,7 +380,11 @@ def test_two_line_residual_update_bitwise(selfcomm, oracle_mod, dims, max_it):
     from mxsolve import _lib
     from mxsolve.core import DMat, dispatch_counts, rhs_hash
     L = _lib.load()
-    A = DMat.stencil(selfcomm, "poisson3d", *dims)
+    old27 = L.mx_debug_set(27, 1)               # the row-pair layout (this module's fixture turns it off)
+    try:
+        A = DMat.stencil(selfcomm, "poisson3d", *dims)
+    finally:
+        L.mx_debug_set(27, old27)
     m = A.info()["m"]
     b = selfcomm.empty(m)
     rhs_hash(selfcomm, 0, b)
