@@ -360,8 +360,9 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         resident count at its 96 VGPRs; 0: key 45's)
  * key 57: workgroups per CU of CG mode 5's 5/7-point p.Ap pass (0, default:
  *         key 40's)
- * key 58: workgroups per CU of CG mode 5's 5/7-point residual update (0,
- *         default: key 40's)
+ * key 58: workgroups per CU of CG mode 5's 5/7-point residual update
+ *         (default 3: -1 to -2% per C2 / C3 iteration against key 40's 4; 0:
+ *         key 40's)
  * key 59: CG mode 5's p.Ap pass on a symmetric operator sums each row's
  *         forward half, p^T A p = sum_i p_i (a_ii p_i + 2 fwd_i) -- 27-point:
  *         symmetry from the column-word layout; 5/7-point: A_d checked once
@@ -388,6 +389,13 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         for the residual update; 0: the configured counts)
  * key 66: residual update with the next step's r loaded one step ahead (0/1,
  *         default 0: -0.3% per C3 iteration, within noise)
+ * key 67: the CG solve's first batch launched eagerly when its graph is
+ *         cached (0, default: within noise; 1 on)
+ * key 68: CG mode 5's 7-point residual update with two lines per wave (line
+ *         y's +n operand is line y + 1's centre pair: 8 vector loads per two
+ *         units instead of 10; the same row sums, the norm partials grouped
+ *         by other rows): 0 off, 1 on, 2 on with a 5-waves-per-SIMD register
+ *         budget, 3 (default) 2 from 2^23 rows, else off
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

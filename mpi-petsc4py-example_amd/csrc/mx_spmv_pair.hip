@@ -406,8 +406,10 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
 // for two units instead of 10 (the residual update is vector-memory issue
 // bound: profiles/r04g_pmc_c3_iteration.txt).  Each unit sums its rows with
 // pair_sums, as spmv_pair_zm_kernel<SPMV_RUPD> does: the same bits.
-template <int JM>
-__global__ void __launch_bounds__(256) spmv_pair_zm2l_kernel(const PairLeanArgs a, const double *__restrict__ x,
+// WPE: the waves-per-SIMD floor asked of the register allocator (knob 68 = 2:
+// 5, i.e. at most 96 VGPRs, against 98 -> 4 waves unconstrained).
+template <int JM, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) spmv_pair_zm2l_kernel(const PairLeanArgs a, const double *__restrict__ x,
                                                              const int32_t *__restrict__ pblk,
                                                              const PairUni *__restrict__ puni, const PairRuArgs ru) {
   constexpr int PS = 7, NR = 5, TR = 2, LAST = 4;
@@ -1799,8 +1801,12 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
 #undef RU_S
 #undef RU
   // knob 68: two lines per wave (clean, one rank, 7-point, an even number of
-  // lines per plane, whole 128-row columns per line)
-  if (g_knobs.ru_2line && clean && !split && A->sd.pair_shape == 7 && a.anchor[3] > 0 && a.anchor[3] % 128 == 0 &&
+  // lines per plane, whole 128-row columns per line); by default (3) the
+  // 5-wave form from 2^23 rows -- at 128^3 the one-line kernel measured
+  // faster (37.0 against 38.6 us per iteration), from 512 x 256 x 128 up the
+  // two-line one (-1.5 to -3%)
+  const int two = g_knobs.ru_2line == 3 ? (A->m >= (int64_t(1) << 23) ? 2 : 0) : g_knobs.ru_2line;
+  if (two && clean && !split && A->sd.pair_shape == 7 && a.anchor[3] > 0 && a.anchor[3] % 128 == 0 &&
       (a.anchor[4] / a.anchor[3]) % 2 == 0 && a.anchor[4] % a.anchor[3] == 0 && a.anchor[1] == -a.anchor[3]) {
     // tasks: column pairs per plane; the grid's segment length from the pairs
     int L2, S2;
@@ -1810,8 +1816,11 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
     if (fold.cnt) { fold.ntotal = fold.ncount = g2; fold.base = 0; }
     a.fold = fold;
     note_dispatch(DSP_ZM_RUPD);
-    if (jac_mode == 2) launch_timed(&spmv_pair_zm2l_kernel<2>, g2, st, a, p, A->sd.pblk.p, A->sd.puni.p, ru);
-    else launch_timed(&spmv_pair_zm2l_kernel<0>, g2, st, a, p, A->sd.pblk.p, A->sd.puni.p, ru);
+    const bool w5 = two == 2;
+    if (jac_mode == 2) launch_timed(w5 ? &spmv_pair_zm2l_kernel<2, 5> : &spmv_pair_zm2l_kernel<2, 1>, g2, st, a, p,
+                                    A->sd.pblk.p, A->sd.puni.p, ru);
+    else launch_timed(w5 ? &spmv_pair_zm2l_kernel<0, 5> : &spmv_pair_zm2l_kernel<0, 1>, g2, st, a, p, A->sd.pblk.p,
+                      A->sd.puni.p, ru);
     HIPCHECK(hipGetLastError());
     return g2;
   }
