@@ -396,14 +396,25 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         units instead of 10; the same row sums, the norm partials grouped
  *         by other rows): 0 off, 1 on, 2 on with a 5-waves-per-SIMD register
  *         budget, 3 (default) 2 from 2^23 rows, else off
+ * key 69: CG mode 5's direction update p = z + b p fused into its p.Ap pass
+ *         (one rank, a clean symmetric 5/7-point layout, x batches of 2 or 4):
+ *         the pass forms p_i from r_i and p_{i-1} for every operand it needs,
+ *         stores the centre rows' (the iterations between x-step batches;
+ *         the batch iterations keep the separate passes) -- the same bits as
+ *         the separate direction update + PW pass: 0 off, 1 on, 5 (default)
+ *         by size: 7-point up to 2^23 rows (128^3 -20% per iteration, 2^23
+ *         -8%; 256^3 +2%: the residual update after it slows by more than it
+ *         saves), 5-point up to 2^24 (2048^2 -14%, C2's 4096^2 -1.7%)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches
  * enqueued (or captured into a graph) since the last reset, by kind --
  * 0 general SELL, 1 SELL CG-fused (mode 1), 2 row-pair sweep, 3 / 4 7/5-point
  * z-march (split: ghost units), 5 / 6 27-point z-march, 7 / 8 fp64 row-pair
- * z-march, 9 CG mode 4, 10 halo-boundary kernel, 11 / 12 CG mode 5's p.Ap and
- * residual-update z-march passes.  Writes min(n, 16) counts; reset != 0
+ * z-march, 9 retired (round 2's CG mode 4), 10 halo-boundary kernel, 11 / 12
+ * CG mode 5's p.Ap and residual-update z-march passes, 13 / 14 coded z-march
+ * (split: ghost units), 15 CG mode 5's direction update fused into the p.Ap
+ * pass (key 69).  Writes min(n, 16) counts; reset != 0
  * zeroes them.  Not a PETSc call: it lets the parity tests show which
  * kernel ran (replayed graph launches are not counted).                     */
 int mx_debug_dispatch_counts(int64_t *out, int n, int reset);

@@ -72,6 +72,17 @@ struct KspState {
 
 __device__ __forceinline__ bool not_finite(double v) { return isnan(v) || isinf(v); }
 
+// PCApply_Jacobi by form (JM: 0 none, 1 vector d, 2 uniform scalar c)
+template <int JM> __device__ __forceinline__ double jac1(double r, double d, double c) {
+  if constexpr (JM == 1) return r * d;
+  else if constexpr (JM == 2) return r * c;
+  else return r;
+}
+// the direction update p = z + b p_{i-1} (VecAYPX_Seq; b == 0 copies z): one
+// expression for every kernel that forms p (cg_pb_kernel, the fused
+// direction + p.Ap pass), so they give the same bits
+__device__ __forceinline__ double cg_dir(double z, double b, double po) { return (b == 0.0) ? z : fma(b, po, z); }
+
 struct CgTop {
   int i;          // iteration about to run
   int reason;     // != 0: the solve stops here

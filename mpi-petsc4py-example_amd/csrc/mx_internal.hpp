@@ -260,7 +260,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int mdot_split = 7; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int box27 = 0; int box27_bpc = 0; int ru_units = 0; int zm_balance = 1; int ru_rpf = 0; int cg_eager_first = 0; int ru_2line = 3; };
+                int mdot_split = 7; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int box27 = 0; int box27_bpc = 0; int ru_units = 0; int zm_balance = 1; int ru_rpf = 0; int cg_eager_first = 0; int ru_2line = 3; int cg_pbw = 5; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -428,6 +428,7 @@ enum Dispatch {
   DSP_ZM_RUPD = 12,      // CG mode 5: the z-march residual update (product recomputed)
   DSP_PAIR_ZMC = 13,     // spmv_pair_zmc_kernel (coded z-march), one rank / no ghost units
   DSP_PAIR_ZMC_SPLIT = 14,
+  DSP_ZM_PBW = 15,       // CG mode 5: the direction update fused into the p.Ap pass (knob 69)
   DSP_COUNT = 16
 };
 void note_dispatch(int kind);
@@ -450,6 +451,13 @@ bool pair_cg5_applies(const Mat *A, int jac_mode);
 int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, double *r, const double *r0,
                          int jac_mode, double jac_c, double *partials, const Fold &fold, const double *dot_part,
                          int ndot, int xb, int *hw, hipStream_t st);
+// knob 69: CG mode 5's direction update fused into the p.Ap pass (one rank,
+// clean symmetric 5/7-point; iterations i % xb != 0): forms and stores p_i
+// (buffer i % xb) from r_i and p_{i-1}, leaves the p.Ap partials
+bool pair_cg5_pbw_applies(const Mat *A, int jac_mode, int xb);
+int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, double *const pb[4], int xb,
+                        double *hist, int jac_mode, double jac_c, double *partials, const Fold &fold,
+                        hipStream_t st);
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);

@@ -253,12 +253,6 @@ template <bool VEC> __device__ __forceinline__ void st2(double *__restrict__ v, 
   if constexpr (VEC) reinterpret_cast<dbl2 *>(v)[k] = t;
   else { v[2 * k] = t.x; v[2 * k + 1] = t.y; }
 }
-// PCApply_Jacobi by form (JM: 0 none, 1 vector d, 2 uniform scalar c)
-template <int JM> __device__ __forceinline__ double jac1(double r, double d, double c) {
-  if constexpr (JM == 1) return r * d;
-  else if constexpr (JM == 2) return r * c;
-  else return r;
-}
 constexpr int CG_VEC_BLOCKS = 4096;   // grid of the paired vector passes (grid-stride)
 constexpr int CG_MAX_VEC_GRID = 65536;  // cap on any vector-pass grid (partials buffer sizing)
 // store flavour of the row walk (knob 14): plain, or non-temporal (streamed past the caches)
@@ -382,10 +376,7 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
   // buffers picked by wave-uniform selects (pointers stay scalar; an indexed
   // pointer array went through scratch and serialised the loop)
   auto pick = [&](int k) -> double * { return k == 0 ? p0 : k == 1 ? p1 : k == 2 ? p2 : p3; };
-  auto row = [&](double rr, double dd, double po) {
-    const double z = jac1<JM>(rr, dd, dc);
-    return (b == 0.0) ? z : z + b * po;          // VecAYPX_Seq (b == 0 copies)
-  };
+  auto row = [&](double rr, double dd, double po) { return cg_dir(jac1<JM>(rr, dd, dc), b, po); };
   const int64_t stride = (int64_t)gridDim.x * 256;
   int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   // the pending steps are exactly [i - B, i) when i % B == 0 (the update pass
@@ -1664,7 +1655,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // norms pass runs on the direction update's grid (knob 34 overrides), so
   // both give the same bits, then folds in-launch and runs cg_init (one rank)
   // or leaves partials for the all-reduce.
-  const bool norms_in_pb = fused && xb > 1 && !p.guess_nonzero;
+  // knob 69: the direction update rides in mode 5's p.Ap pass (the initial
+  // norms then take their own pass over b -- the same bits, see above)
+  const bool pbw = fmode == 5 && fused && pair_cg5_pbw_applies(A, dinv.mode, xb);
+  const bool norms_in_pb = fused && xb > 1 && !p.guess_nonzero && !pbw;
   const int ngrid = g_knobs.norm_grid > 0 ? g_knobs.norm_grid : (int)cg_pb_grid(n, wide_pb);
   Fold fin;
   if (fused) { fin.cnt = s->fold_upd; fin.out = red; fin.ntotal = fin.ncount = ngrid; }
@@ -1732,15 +1726,26 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       timer.end();
     } else {
       double *pi = xb > 1 ? pbs.b[it % xb] : pv.p;
-      if (xb > 1) {
+      // knob 69: the iterations between x-step batches (it % xb != 0; the
+      // host's it is the device's i) fuse the direction update into the PW pass
+      const bool fuse_pw = pbw && it % xb != 0;
+      if (fuse_pw) {
+        timer.begin();
+        nb_spmv = pair_cg5_pbw_launch(A, s, r.p, r0, pbs.b, xb, hist_d, dinv.mode, dinv.c, part.p,
+                                      fdot_p ? *fdot_p : Fold{}, st);
+        timer.end();
+        if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG without its direction + p.Ap pass");
+      } else if (xb > 1) {
         ptimer.begin();
         cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb, wide_pb);
         ptimer.end();
       } else cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
-      timer.begin();
-      nb_spmv = matmult_overlap(A, pi, w.p, fmode == 5 ? SPMV_PW : SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
-      timer.end();
-      if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG without its MatMult");
+      if (!fuse_pw) {
+        timer.begin();
+        nb_spmv = matmult_overlap(A, pi, w.p, fmode == 5 ? SPMV_PW : SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
+        timer.end();
+        if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG without its MatMult");
+      }
     }
     // one rank: the update pass folds the MatMult's partials itself (knob 10
     // = 3; mode 5's residual update by default, knob 46)

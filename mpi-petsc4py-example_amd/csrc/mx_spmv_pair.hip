@@ -500,6 +500,144 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
   block_partials<3>(nv, a.partials, gridDim.x, a.fold);
 }
 
+// CG mode 5's direction update fused into its p.Ap pass (knob 69; one rank,
+// a clean symmetric 5/7-point layout, batched x steps): the pass forms
+// p_i = z_i + b p_{i-1} (cg_dir, the expression cg_pb_kernel uses) for the
+// operands its forward-half rows need -- the centre pair, +n, +D and the
+// line's +1 edge -- from r_i and p_{i-1}, stores the centre rows' p_i and sums
+// p.Ap as the symmetric PW pass does (pair_fwd, the same units in the same
+// order on the same grid: the same partials).  Per row: r and p_{i-1} read,
+// p_i written -- against the separate direction update (r, p_{i-1} read, p_i
+// written) plus the PW pass (p_i read again).  Operands of neighbouring rows
+// are formed by every unit that needs them from the same loads: the same bits
+// as the owner's stored p_i.  Launched only for iterations i % B != 0 (the
+// host's iteration index is the device's: a captured batch starts on a
+// multiple of B): the x-step batch iterations keep cg_pb_kernel + the PW pass
+// (their extra streams in one z-march measured 205 us against 162).
+struct PairPbArgs {
+  KspState *s;
+  const double *r;             // r_i
+  const double *r0;            // iteration 0 of a zero-guess solve: r_0 = b (not copied into r)
+  double *pb0, *pb1, *pb2, *pb3;   // p_j in buffer j % B
+  double *hist;
+  double c;                    // JM 2: the uniform Jacobi scalar
+};
+
+template <int PS, int JM, int B, int ZU>
+__global__ void __launch_bounds__(256) spmv_pair_pbw_kernel(const PairLeanArgs a, const int32_t *__restrict__ pblk,
+                                                            const PairUni *__restrict__ puni, const PairPbArgs pa) {
+  KspState *s = pa.s;
+  const CgTopIn top = s->top;
+  if (top.done) return;
+  const CgTop t = cg_top(top);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(s, t, pa.hist);
+  if (t.reason) return;
+  const int i = t.i;
+  const double b = t.b;
+  using SH = PairShape<PS>;
+  constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1, C = SH::CENTER_RUN;
+  auto pick = [&](int k) -> double * { return k == 0 ? pa.pb0 : k == 1 ? pa.pb1 : k == 2 ? pa.pb2 : pa.pb3; };
+  double *pout = pick(i % B);
+  const double *pprev = pick((i + B - 1) % B);
+  const double *rs = (pa.r0 && i == 0) ? pa.r0 : pa.r;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t rr = vec_rsrc(rs, a.n), pr = vec_rsrc(pprev, a.n);
+  const int D = a.anchor[LAST];
+  // the tri run's +1 edge: lane 63's x[ub + 128] (the backward edge is not
+  // needed by the forward half); the other lanes load the same line
+  const int eoff = 128 + a.anchor[TR];
+  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
+  const int ntask = (se - sb) * a.P;
+  double dot = 0.0;
+  // NP: b == 0 (iteration 0, a restart), p_{i-1} not read
+  auto march = [&](auto npc) __attribute__((always_inline)) {
+    constexpr bool NP = decltype(npc)::value;
+    auto dir = [&](dbl2 r2, dbl2 p2) __attribute__((always_inline)) {
+      return dbl2{cg_dir(jac1<JM>(r2.x, 0.0, pa.c), b, NP ? 0.0 : p2.x),
+                  cg_dir(jac1<JM>(r2.y, 0.0, pa.c), b, NP ? 0.0 : p2.y)};
+    };
+    for (int tk = w; tk < ntask; tk += W) {
+      const int seg = sb + tk / a.P, col = tk % a.P;
+      const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+      const int cb = col * 128 + 2 * lane;
+      dbl2 pc = dir(bload2(rr, z0 * D + cb), NP ? dbl2{0.0, 0.0} : bload2(pr, z0 * D + cb));   // p_i, centre
+      uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
+      auto step = [&](int z, auto nq) __attribute__((always_inline)) {
+        constexpr int NQ = decltype(nq)::value;
+        dbl2 zr[NQ], zpp[NQ], nr[NQ], npp[NQ];
+        double er[NQ], epp[NQ];
+        uint32_t bw[NQ];
+        bw[0] = bwn;
+#pragma unroll
+        for (int q = 1; q < NQ; ++q) bw[q] = (uint32_t)pblk[(z + q) * a.P + col];
+        if (z + NQ < z1) bwn = (uint32_t)pblk[(z + NQ) * a.P + col];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
+          zr[q] = bload2(rr, r0 + D);
+          zpp[q] = NP ? dbl2{0.0, 0.0} : bload2(pr, r0 + D);
+          if constexpr (PS == 7) {
+            const int no = r0 + a.anchor[3] + ((bw[q] & (PBLK_RUN0 << 3)) ? PAIR_OOR : 0);
+            nr[q] = bload2(rr, no);
+            npp[q] = NP ? dbl2{0.0, 0.0} : bload2(pr, no);
+          }
+          // a line's last unit has no +1 edge (wave-uniform: no loads)
+          er[q] = 0.0;
+          epp[q] = 0.0;
+          if (!(bw[q] & PBLK_EHI)) {
+            er[q] = bload1(rr, ub + eoff);
+            if constexpr (!NP) epp[q] = bload1(pr, ub + eoff);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int r0 = (z + q) * D + cb;
+          const dbl2 pz = dir(zr[q], zpp[q]);
+          const double pe = cg_dir(jac1<JM>(er[q], 0.0, pa.c), b, NP ? 0.0 : epp[q]);
+          *reinterpret_cast<dbl2 *>(pout + r0) = pc;
+          dbl2 L[NR];
+          L[0] = dbl2{0.0, 0.0};                   // -D: not in the forward half
+          if constexpr (PS == 7) { L[1] = dbl2{0.0, 0.0}; L[3] = dir(nr[q], npp[q]); }
+          L[TR] = pc;
+          L[LAST] = pz;
+          if (bw[q] & CARRY) {                     // wave-uniform, rare: an empty carried run
+            if (bw[q] & (PBLK_RUN0 << TR)) L[TR] = dbl2{0.0, 0.0};
+            if (bw[q] & (PBLK_RUN0 << LAST)) L[LAST] = dbl2{0.0, 0.0};
+          }
+          const dbl2 tq = pair_fwd<PS>(L, pe, bw[q], puni);
+          dot += L[C].x * tq.x;
+          dot += L[C].y * tq.y;
+          pc = pz;
+        }
+      };
+      int z = z0;
+      for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
+      for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
+    }
+  };
+  const std::true_type T{};
+  const std::false_type F{};
+  if (b == 0.0) march(T);
+  else march(F);
+  double v[1] = {dot};
+  block_partials<1>(v, a.partials, gridDim.x, a.fold);
+}
+
 // 27-point z-march (Sell::puni27).  The nine runs are (dz, dy) in {-1,0,1}^2
 // at anchors -D-n, -D, -D+n, -n, 0, +n, D-n, D, D+n (each a tri run c-1, c,
 // c+1); marching a column in z, the runs of planes z-1 and z (six pairs and
@@ -1771,6 +1909,63 @@ static int cg5_args(const Mat *A, PairLeanArgs &a, int bpc = 0) {
   a.P = D / 128;
   a.NZ = (int)(A->m / D);
   return zm_tasks(a.P, a.NZ, a.L, a.S, bpc);
+}
+
+// knob 69: the fused direction update + p.Ap pass applies (one rank, a clean
+// symmetric 5/7-point z-march layout with the forward-half PW pass, no or a
+// uniform Jacobi, x batches of 2 or 4).  Default (5): by size -- 7-point up
+// to 2^23 rows, 5-point up to 2^24.  Per iteration, off -> on (tools/cg_ab.py,
+// gpurun_out/r4z, r4aa): 3D 128^3 37.3 -> 29.8 us, 256 x 128 x 128 57.2 ->
+// 48.7, 256 x 256 x 128 97.9 -> 90.1, 256 x 256 x 192 130.4 -> 131.9, 256^3
+// 173.4 -> 176.9; 2D 2048^2 55.6 -> 47.8, 4096 x 2048 97.4 -> 89.9, 4096^2
+// 170.2 -> 167.3, 8192 x 4096 353.3 -> 353.1.  While the vectors fit the
+// memory-side cache the saved pass is pure gain; at 256^3 the fused pass
+// saves 4.6 us (79.4 against 62.4 + 21.6) but the residual update after it
+// loses 5.2 (72.2 against 67.0: less of p_i left in that cache); reading the
+// +D streams non-temporally made it worse (176.5 / 181.0, r4y)
+bool pair_cg5_pbw_applies(const Mat *A, int jac_mode, int xb) {
+  const int on = g_knobs.cg_pbw != 5 ? g_knobs.cg_pbw
+                                     : A->m <= (int64_t(1) << (A->sd.pair_shape == 5 ? 24 : 23));
+  return on && (xb == 2 || xb == 4) && (jac_mode == 0 || jac_mode == 2) && pair_cg5_applies(A, jac_mode) &&
+         A->sd.pair_shape != 27 && pair_lean_kind(A) == 2 && A->nghost == 0 && !A->sd.pair_ghosts && A->sym == 1 &&
+         g_knobs.pw_sym27 && pair_zm_applies(A);
+}
+
+int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, double *const pb[4], int xb,
+                        double *hist, int jac_mode, double jac_c, double *partials, const Fold &fold_in,
+                        hipStream_t st) {
+  if (!pair_cg5_pbw_applies(A, jac_mode, xb)) return 0;
+  const Sell &S = A->sd;
+  PairLeanArgs a{};
+  a.m = (int)A->m;
+  a.n = (int)A->n;
+  a.nunits = (int)S.nunits;
+  pair_anchors(S, a.anchor);
+  a.partials = partials;
+  const int NR = S.pair_shape == 5 ? 3 : 5, D = a.anchor[NR - 1];
+  a.P = D / 128;
+  a.NZ = (int)(A->m / D);
+  // the PW pass's grid (the same tasks, so the same p.Ap partials)
+  const int grid = zm_tasks(a.P, a.NZ, a.L, a.S, g_knobs.pw_bpc > 0 ? g_knobs.pw_bpc : g_knobs.pair_zm_bpc);
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
+  a.fold = fold;
+  const PairPbArgs pa{s, r, r0, pb[0], pb[1], pb[2], pb[3], hist, jac_c};
+  using PbwFn = void (*)(const PairLeanArgs, const int32_t *, const PairUni *, const PairPbArgs);
+  PbwFn f;
+  const bool z2 = g_knobs.pair_zm_units == 2;
+#define PBW(PS, JM, B) f = z2 ? &spmv_pair_pbw_kernel<PS, JM, B, 2> : &spmv_pair_pbw_kernel<PS, JM, B, 1>
+#define PBW_B(PS, JM) do { if (xb == 4) PBW(PS, JM, 4); else PBW(PS, JM, 2); } while (0)
+#define PBW_J(PS) do { if (jac_mode == 2) PBW_B(PS, 2); else PBW_B(PS, 0); } while (0)
+  if (S.pair_shape == 5) PBW_J(5);
+  else PBW_J(7);
+#undef PBW_J
+#undef PBW_B
+#undef PBW
+  note_dispatch(DSP_ZM_PBW);
+  launch_timed(f, grid, st, a, S.pblk.p, S.puni.p, pa);
+  HIPCHECK(hipGetLastError());
+  return grid;
 }
 
 int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, double *r, const double *r0,

@@ -22,7 +22,7 @@ LIB = os.path.join(ROOT, "mpi-petsc4py-example_amd", "lib", "libmxsolve.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 HOT = re.compile(r"spmv_sell_kernel|spmv_pair_lean|spmv_pair_zm|cg_|mdot|maxpy|fold_kernel")
-NOSPILL = re.compile(r"spmv_pair_zm|spmv_pair_lean|mdot|maxpy|cg_pb|"
+NOSPILL = re.compile(r"spmv_pair_zm|spmv_pair_lean|spmv_pair_pbw|mdot|maxpy|cg_pb|"
                      r"cg_update|cg_norms|cg_finish|gm_|fold_kernel|finish_many")
 
 

@@ -408,3 +408,56 @@ def test_two_line_residual_update(selfcomm, oracle_mod, dims, max_it):
     assert a[:2] == c[:2]
     assert np.allclose(a[2], c[2], rtol=1e-10, atol=0)
     assert np.linalg.norm(a[3] - c[3]) <= 1e-12 * np.linalg.norm(a[3])
+
+
+@pytest.mark.parametrize("kind,dims,pc,guess,max_it", [
+    ("poisson3d", (128, 128, 128), "jacobi", False, 10000),
+    ("poisson3d", (256, 128, 40), "none", False, 10000),
+    ("poisson3d", (128, 128, 64), "jacobi", True, 10000),
+    ("poisson3d", (128, 128, 128), "jacobi", False, 37),
+    ("poisson2d", (1024, 1024, 1), "jacobi", False, 10000),
+])
+def test_fused_direction_pw_bitwise(selfcomm, kind, dims, pc, guess, max_it):
+    """Knob 69: CG mode 5's direction update fused into the p.Ap pass forms
+    every p_i operand from r_i and p_{i-1} with the direction update's own
+    expression and sums p.Ap over the PW pass's units on its grid (the x-step
+    batch iterations keep the separate passes): the whole solve -- its,
+    reason, residual history, x -- is bitwise the separate passes' (the
+    initial norms then take their own pass over b: the same bits); the
+    dispatch shows the fused pass ran in place of some PW passes."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    L = _lib.load()
+    old27 = L.mx_debug_set(27, 1)
+    try:
+        A = DMat.stencil(selfcomm, kind, *dims)
+    finally:
+        L.mx_debug_set(27, old27)
+    m = A.info()["m"]
+    b = selfcomm.empty(m)
+    rhs_hash(selfcomm, 0, b)
+    x0 = None
+    if guess:
+        x0 = selfcomm.empty(m)
+        rhs_hash(selfcomm, 5, x0)
+        x0.mul_(1e-3)
+    outs = []
+    for k69 in (0, 1):
+        old = {k: L.mx_debug_set(k, v) for k, v in ((9, 5), (27, 1), (69, k69))}
+        try:
+            x = x0.clone() if guess else selfcomm.zeros(m)
+            dispatch_counts(reset=True)
+            r = A.solve(b, x, ksp="cg", pc=pc, rtol=1e-8, max_it=max_it, history=True, guess_nonzero=guess)
+            dc = dispatch_counts(reset=True)
+            outs.append((r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy(), r["cg_mode"], dc))
+        finally:
+            for k, v in old.items():
+                L.mx_debug_set(k, v)
+    A.destroy()
+    a, c = outs
+    assert a[4] == c[4] == 5, (a[4], c[4])
+    assert a[5]["zm_pbw"] == 0 and a[5]["zm_pw"] > 0, a[5]
+    assert c[5]["zm_pbw"] > 0 and 0 < c[5]["zm_pw"] < a[5]["zm_pw"], c[5]
+    assert a[:2] == c[:2]
+    assert np.array_equal(a[2].view(np.uint64), c[2].view(np.uint64))
+    assert np.array_equal(a[3].view(np.uint64), c[3].view(np.uint64))
