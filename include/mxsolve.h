@@ -405,6 +405,11 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         by size: 7-point up to 2^23 rows (128^3 -20% per iteration, 2^23
  *         -8%; 256^3 +2%: the residual update after it slows by more than it
  *         saves), 5-point up to 2^24 (2048^2 -14%, C2's 4096^2 -1.7%)
+ * key 70: the 27-point plane-pipelined z-march with two lines per wave (the
+ *         column words pair up by lines: line y's dy = +1 run is line y + 1's
+ *         centre run, 8 loads per plane for two units instead of 12; the same
+ *         row sums) for the MatMult and CG mode 5's residual update (1,
+ *         default: C5's share -3.7% per CG iteration, its MatMult -5%; 0 off)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

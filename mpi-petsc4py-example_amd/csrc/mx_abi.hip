@@ -549,6 +549,7 @@ int mx_debug_set(int key, int value) {
     case 53: old = g_knobs.pair_unitv; g_knobs.pair_unitv = value; break;
     case 55: old = g_knobs.cg5_27; g_knobs.cg5_27 = value; break;
     case 60: old = g_knobs.pair_zm27p; g_knobs.pair_zm27p = value; break;
+    case 70: old = g_knobs.zm27_2line; g_knobs.zm27_2line = value; break;
     case 69: old = g_knobs.cg_pbw; g_knobs.cg_pbw = value; break;
     case 68: old = g_knobs.ru_2line; g_knobs.ru_2line = value; break;
     case 67: old = g_knobs.cg_eager_first; g_knobs.cg_eager_first = value; break;

@@ -80,8 +80,9 @@ template <int JM> __device__ __forceinline__ double jac1(double r, double d, dou
 }
 // the direction update p = z + b p_{i-1} (VecAYPX_Seq; b == 0 copies z): one
 // expression for every kernel that forms p (cg_pb_kernel, the fused
-// direction + p.Ap pass), so they give the same bits
-__device__ __forceinline__ double cg_dir(double z, double b, double po) { return (b == 0.0) ? z : fma(b, po, z); }
+// direction + p.Ap pass), so they give the same bits; a multiply and an add
+// (the library builds with -ffp-contract=off), as VecAYPX_Seq's loop
+__device__ __forceinline__ double cg_dir(double z, double b, double po) { return (b == 0.0) ? z : z + b * po; }
 
 struct CgTop {
   int i;          // iteration about to run

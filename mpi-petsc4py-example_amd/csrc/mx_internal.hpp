@@ -213,6 +213,12 @@ struct Sell {
   // separable sums (mx_spmv_pair.hip spmv_pair_zm27b_kernel, knob 62)
   bool pair_box27 = false;
   double box_v = 0.0, box_c = 0.0;
+  // the column words pair up by lines (knob 70, mx_spmv_pair.hip
+  // spmv_pair_zm27p2l_kernel): whole 128-row columns per line, an even number
+  // of lines per plane, and each even line's column and the next line's column
+  // at the same x have equal edge words, no dy = +1 boundary on the first and
+  // no dy = -1 boundary on the second
+  bool pair_2l27 = false;
   // 27-point column words (one per 128-row column of a plane): when every
   // unit's empty runs are exactly its plane's z-boundary runs (plane 0: dz =
   // -1, the last plane: dz = +1 -- read out of range anyway) plus its column's
@@ -260,7 +266,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int mdot_split = 7; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int box27 = 0; int box27_bpc = 0; int ru_units = 0; int zm_balance = 1; int ru_rpf = 0; int cg_eager_first = 0; int ru_2line = 3; int cg_pbw = 5; };
+                int mdot_split = 7; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int box27 = 0; int box27_bpc = 0; int ru_units = 0; int zm_balance = 1; int ru_rpf = 0; int cg_eager_first = 0; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

@@ -1063,6 +1063,172 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p_kernel(const PairLean27Ar
   }
 }
 
+// The plane-pipelined 27-point z-march with two lines per wave (knob 70,
+// Sell::pair_2l27): a task is the columns of lines y and y + 1 (y even) at
+// one x, marched together; line y's dy = +1 run is line y + 1's centre run
+// and line y + 1's dy = -1 run line y's, so per plane the pair loads four
+// lines (y - 1 .. y + 2) and their edges -- 8 loads for two units instead of
+// 12 -- and shifts them once.  Each unit sums its rows exactly as
+// spmv_pair_zm27p_kernel does (plane27_add, the same groups in the same
+// order): the same row sums.  DOT / PW / RUPD partials then group other rows
+// per wave (to rounding).
+template <int MODE, bool UV, int JM = 0>
+__global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27Args a, const double *__restrict__ x,
+                                                                double *__restrict__ y, const int32_t *__restrict__ pblk,
+                                                                const PairUni27 *__restrict__ puni,
+                                                                const int32_t *__restrict__ pcol, const PairRuArgs ru) {
+  constexpr bool RU = MODE == SPMV_RUPD;
+  double alpha = 0.0;
+  const double *rin = nullptr;
+  if constexpr (RU) {
+    KspState *s = ru.s;
+    if (s->top.done) {
+      if (ru.hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(ru.hw + HW_DONE, 1);
+      return;
+    }
+    const double pw = ru.ndot > 0 ? block_sum_array<16>(ru.dot_part, ru.ndot) : s->red1;
+    const CgAlpha al = cg_alpha(s, pw);
+    if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, ru.xb, false, ru.hw);
+    if (al.reason) return;
+    alpha = al.alpha;
+    rin = (ru.r0 && al.i == 0) ? ru.r0 : ru.r;
+  } else {
+    if (a.done && *a.done) return;   // wave-uniform: solver finished
+  }
+  // alpha and the Jacobi scalar held in VGPRs (an empty asm pins them there):
+  // the SGPRs they would keep live across the march spilled
+  double alv = alpha, cjv = ru.c;
+  if constexpr (RU) asm volatile("" : "+v"(alv), "+v"(cjv));
+  double nv[3] = {0.0, 0.0, 0.0};   // RU: [z.z, z.r, r.r]
+  double dot = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[7], NL = a.anchor[5];           // plane, line
+  const int PL = NL / 128, PH = a.P / 2;
+  const int eb = lane == 0 ? -1 : 128;
+  // task t = (segment, line pair lp, x column xx), cp = lp PL + xx: advanced
+  // by W without divisions in the loop (their reciprocals spilled SGPRs)
+  const int NLP = PH / PL;
+  int seg = sb + w / PH, lp = (w % PH) / PL, xx = w % PL;
+  const int dseg = W / PH, dlp = (W % PH) / PL, dx = W % PL;
+  for (; seg < se;) {
+    const int colA = lp * 2 * PL + xx, colB = colA + PL;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cbA = colA * 128 + 2 * lane;               // line y's rows; line y + 1's are + NL
+    const uint32_t cwA = (uint32_t)pcol[colA], cwB = (uint32_t)pcol[colB];
+    // the four lines y - 1 .. y + 2: the outer two read out of range at a y
+    // boundary (per lane: the task's rows and edge offsets in VGPRs)
+    const int oA = cbA - NL + ((cwA & U27C_YLO) ? PAIR_OOR : 0), oB = cbA + 2 * NL + ((cwB & U27C_YHI) ? PAIR_OOR : 0);
+    const int eA = colA * 128 + eb + ((lane == 0 ? (cwA & U27_ELO) : (cwA & U27_EHI)) ? PAIR_OOR_EDGE : 0);
+    const int eo[4] = {eA - NL + ((cwA & U27C_YLO) ? PAIR_OOR : 0), eA, eA + NL, eA + 2 * NL + ((cwB & U27C_YHI) ? PAIR_OOR : 0)};
+    const int lo4[4] = {oA, cbA, cbA + NL, oB};
+    dbl2 Lq[4];
+    double lo[4], hi[4];
+    auto load = [&](int q) __attribute__((always_inline)) {
+      double e[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        Lq[k] = bload2(xr, q * D + lo4[k]);
+        e[k] = bload1(xr, q * D + eo[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lo[k] = wave_shift<true>(Lq[k].y, e[k]);
+        hi[k] = wave_shift<false>(Lq[k].x, e[k]);
+      }
+    };
+    auto plane = [&](int k0) __attribute__((always_inline)) {   // lines k0 .. k0 + 2 as one unit's plane
+      Plane27 P;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        P.L[k] = Lq[k0 + k];
+        P.lo[k] = lo[k0 + k];
+        P.hi[k] = hi[k0 + k];
+      }
+      return P;
+    };
+    auto blkA = [&](int z) -> uint32_t { return (uint32_t)pblk[min(z, a.NZ - 1) * a.P + colA]; };
+    auto blkB = [&](int z) -> uint32_t { return (uint32_t)pblk[min(z, a.NZ - 1) * a.P + colB]; };
+    uint32_t az = blkA(z0), az1 = blkA(z0 + 1), bz = blkB(z0), bz1 = blkB(z0 + 1);
+    load(z0 - 1);
+    dbl2 m1A = plane27_add<UV>(dbl2{0.0, 0.0}, puni[az & PBLK_ID], 0, plane(0));
+    dbl2 m1B = plane27_add<UV>(dbl2{0.0, 0.0}, puni[bz & PBLK_ID], 0, plane(1));
+    load(z0);
+    m1A = plane27_add<UV>(m1A, puni[az & PBLK_ID], 1, plane(0));
+    m1B = plane27_add<UV>(m1B, puni[bz & PBLK_ID], 1, plane(1));
+    dbl2 m0A = plane27_add<UV>(dbl2{0.0, 0.0}, puni[az1 & PBLK_ID], 0, plane(0));
+    dbl2 m0B = plane27_add<UV>(dbl2{0.0, 0.0}, puni[bz1 & PBLK_ID], 0, plane(1));
+    dbl2 czA = Lq[1], czB = Lq[2];
+    for (int z = z0; z < z1; ++z) {
+      const uint32_t az2 = blkA(z + 2), bz2 = blkB(z + 2);
+      const int rA = z * D + cbA, rB = rA + NL;
+      dbl2 rqA, rqB;
+      load(z + 1);
+      if constexpr (RU) {
+        rqA = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + rA));
+        rqB = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + rB));
+      }
+      const dbl2 outA = plane27_add<UV>(m1A, puni[az & PBLK_ID], 2, plane(0));
+      __builtin_amdgcn_sched_barrier(0);
+      const dbl2 outB = plane27_add<UV>(m1B, puni[bz & PBLK_ID], 2, plane(1));
+      __builtin_amdgcn_sched_barrier(0);
+      m1A = plane27_add<UV>(m0A, puni[az1 & PBLK_ID], 1, plane(0));
+      __builtin_amdgcn_sched_barrier(0);
+      m1B = plane27_add<UV>(m0B, puni[bz1 & PBLK_ID], 1, plane(1));
+      __builtin_amdgcn_sched_barrier(0);
+      m0A = plane27_add<UV>(dbl2{0.0, 0.0}, puni[az2 & PBLK_ID], 0, plane(0));
+      __builtin_amdgcn_sched_barrier(0);
+      m0B = plane27_add<UV>(dbl2{0.0, 0.0}, puni[bz2 & PBLK_ID], 0, plane(1));
+      auto emit = [&](dbl2 out, dbl2 cz, dbl2 rq, int r0) __attribute__((always_inline)) {
+        if constexpr (RU) {
+          const double ra = fma(-alv, out.x, rq.x), rb = fma(-alv, out.y, rq.y);
+          const double za = JM == 2 ? ra * cjv : ra, zb = JM == 2 ? rb * cjv : rb;
+          nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
+          nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
+          *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
+        } else {
+          if constexpr (MODE != SPMV_PW) *reinterpret_cast<dbl2 *>(y + r0) = out;
+          if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
+            dot += cz.x * out.x;
+            dot += cz.y * out.y;
+          }
+        }
+      };
+      emit(outA, czA, rqA, rA);
+      emit(outB, czB, rqB, rB);
+      czA = Lq[1];
+      czB = Lq[2];
+      az = az1; az1 = az2;
+      bz = bz1; bz1 = bz2;
+    }
+    xx += dx;
+    if (xx >= PL) { xx -= PL; ++lp; }
+    lp += dlp;
+    if (lp >= NLP) { lp -= NLP; ++seg; }
+    seg += dseg;
+  }
+  if constexpr (MODE == SPMV_DOT || MODE == SPMV_PW) {
+    double v[1] = {dot};
+    block_partials<1>(v, a.partials, gridDim.x, a.fold);
+  } else if constexpr (RU) {
+    block_partials<3>(nv, a.partials, gridDim.x, a.fold);
+  }
+}
+
 // CG mode 5's two passes on a 27-point "box" operator (Sell::pair_box27: the
 // column-word layout, every present off-diagonal slot holding one value v and
 // every diagonal one value c -- C5's 26 / -1 stencil).  Then
@@ -1665,7 +1831,21 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
     HIPCHECK(hipGetLastError());
     return grid;
   }
-  if (form == 2 && g_knobs.pair_zm27p && !(mode == SPMV_PW && sym)) {
+  // knob 70: two lines per wave (the column words pair up by lines, no ghost units)
+  if (form == 2 && g_knobs.zm27_2line && S.pair_2l27 && !split &&
+      (mode == SPMV_RUPD || mode == SPMV_DOT || mode == SPMV_PLAIN)) {
+    const bool uvp = S.pair_unit27 && g_knobs.pair_unitv;
+    grid = zm_tasks(b.P / 2, b.NZ, b.L, b.S, bpc);
+    if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
+#define P2L(MODE, JM) f = uvp ? &spmv_pair_zm27p2l_kernel<MODE, true, JM> : &spmv_pair_zm27p2l_kernel<MODE, false, JM>
+    switch (mode) {
+      case SPMV_PLAIN: P2L(SPMV_PLAIN, 0); break;
+      case SPMV_DOT: P2L(SPMV_DOT, 0); break;
+      default: if (jm == 2) P2L(SPMV_RUPD, 2); else P2L(SPMV_RUPD, 0);
+    }
+#undef P2L
+    note_dispatch(mode == SPMV_RUPD ? DSP_ZM_RUPD : DSP_PAIR_ZM27);
+  } else if (form == 2 && g_knobs.pair_zm27p && !(mode == SPMV_PW && sym)) {
     const bool uvp = S.pair_unit27 && g_knobs.pair_unitv;
     switch (mode) {
       case SPMV_PLAIN:

@@ -461,3 +461,57 @@ def test_fused_direction_pw_bitwise(selfcomm, kind, dims, pc, guess, max_it):
     assert a[:2] == c[:2]
     assert np.array_equal(a[2].view(np.uint64), c[2].view(np.uint64))
     assert np.array_equal(a[3].view(np.uint64), c[3].view(np.uint64))
+
+
+@pytest.mark.parametrize("dims,max_it", [((128, 128, 16), 10000), ((256, 128, 24), 10000), ((512, 256, 16), 10000),
+                                         ((128, 128, 16), 23), ((128, 3, 40), 10000)])
+def test_two_line_27point(selfcomm, dims, max_it):
+    """Knob 70: the 27-point plane-pipelined z-march with two lines per wave
+    (line y's dy = +1 run is line y + 1's centre run, loaded once) sums every
+    row exactly as the one-line kernel: the MatMult y = A x is bitwise the
+    default's; CG mode 5's residual update then groups its norm partials by
+    other rows, so the solve equals the default's to rounding (its and reason
+    equal, history within 1e-10, x within 1e-12).  128 x 3 x 40 has an odd
+    number of lines per plane: the layout does not pair and the solve is the
+    default's bit for bit."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    L = _lib.load()
+    old27 = L.mx_debug_set(27, 1)
+    try:
+        A = DMat.stencil(selfcomm, "poisson3d27", *dims)
+    finally:
+        L.mx_debug_set(27, old27)
+    m = A.info()["m"]
+    b = selfcomm.empty(m)
+    rhs_hash(selfcomm, 0, b)
+    xin = selfcomm.empty(m)
+    rhs_hash(selfcomm, 3, xin)
+    pairs = dims[1] % 2 == 0
+    outs = []
+    for k70 in (0, 1):
+        old = {k: L.mx_debug_set(k, v) for k, v in ((9, 5), (27, 1), (70, k70))}
+        try:
+            y = selfcomm.zeros(m)
+            A.mult(xin, y)
+            x = selfcomm.zeros(m)
+            dispatch_counts(reset=True)
+            r = A.solve(b, x, ksp="cg", pc="jacobi", rtol=1e-8, max_it=max_it, history=True)
+            dc = dispatch_counts(reset=True)
+            outs.append((r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy(), r["cg_mode"], dc,
+                         y.cpu().numpy().copy()))
+        finally:
+            for k, v in old.items():
+                L.mx_debug_set(k, v)
+    A.destroy()
+    a, c = outs
+    assert np.array_equal(a[6].view(np.uint64), c[6].view(np.uint64))
+    assert a[:2] == c[:2]
+    if not pairs:                               # (not the column-word layout: mode 2 here)
+        assert a[4] == c[4] and a[5] == c[5]
+        assert np.array_equal(a[2].view(np.uint64), c[2].view(np.uint64))
+        assert np.array_equal(a[3].view(np.uint64), c[3].view(np.uint64))
+        return
+    assert a[4] == c[4] == 5 and c[5]["zm_rupd"] > 0, (a[4], c[4], c[5])
+    assert np.allclose(a[2], c[2], rtol=1e-10, atol=0)
+    assert np.linalg.norm(a[3] - c[3]) <= 1e-12 * np.linalg.norm(a[3])
