@@ -408,8 +408,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 70: the 27-point plane-pipelined z-march with two lines per wave (the
  *         column words pair up by lines: line y's dy = +1 run is line y + 1's
  *         centre run, 8 loads per plane for two units instead of 12; the same
- *         row sums) for the MatMult and CG mode 5's residual update (1,
- *         default: C5's share -3.7% per CG iteration, its MatMult -5%; 0 off)
+ *         row sums) for the MatMult, CG mode 5's residual update and its
+ *         forward-half p.Ap pass (1, default: C5's share 199.7 -> 185.9 us per
+ *         CG iteration, residual update 86 -> 78 us, p.Ap pass 37 -> 30 us,
+ *         MatMult -5%; 0 off)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -1229,6 +1229,105 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27
   }
 }
 
+// CG mode 5's p.Ap pass on a symmetric 27-point operator (pair_fwd27, the
+// forward half) with two lines per wave (knob 70): a row's forward slots read
+// its own plane's lines y and y + 1 and the next plane's y - 1 .. y + 1, so
+// for lines y and y + 1 together a plane step loads the next plane's four
+// lines y - 1 .. y + 2 and their edges (8 loads for two units instead of 12)
+// and carries three.  Each row's t_i is pair_fwd27's, bit for bit; the p.Ap
+// partials group other rows per wave (to rounding).
+template <bool UV>
+__global__ void __launch_bounds__(256) spmv_pair_zm27s2l_kernel(const PairLean27Args a, const double *__restrict__ x,
+                                                                const int32_t *__restrict__ pblk,
+                                                                const PairUni27 *__restrict__ puni,
+                                                                const int32_t *__restrict__ pcol) {
+  if (a.done && *a.done) return;   // wave-uniform: solver finished
+  double dot = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[7], NL = a.anchor[5];
+  const int PL = NL / 128, PH = a.P / 2, NLP = PH / PL;
+  const int eb = lane == 0 ? -1 : 128;
+  int seg = sb + w / PH, lp = (w % PH) / PL, xx = w % PL;
+  const int dseg = W / PH, dlp = (W % PH) / PL, dx = W % PL;
+  for (; seg < se;) {
+    const int colA = lp * 2 * PL + xx, colB = colA + PL;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cbA = colA * 128 + 2 * lane;
+    const uint32_t cwA = (uint32_t)pcol[colA], cwB = (uint32_t)pcol[colB];
+    const int eA = colA * 128 + eb + ((lane == 0 ? (cwA & U27_ELO) : (cwA & U27_EHI)) ? PAIR_OOR_EDGE : 0);
+    const int oM = (cwA & U27C_YLO) ? PAIR_OOR : 0, oP = (cwB & U27C_YHI) ? PAIR_OOR : 0;
+    const int lo4[4] = {cbA - NL + oM, cbA, cbA + NL, cbA + 2 * NL + oP};
+    const int eo4[4] = {eA - NL + oM, eA, eA + NL, eA + 2 * NL + oP};
+    // plane z's lines y, y + 1, y + 2 (carried)
+    dbl2 C[3];
+    double Ce[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      C[k] = bload2(xr, z0 * D + lo4[k + 1]);
+      Ce[k] = bload1(xr, z0 * D + eo4[k + 1]);
+    }
+    uint32_t an = (uint32_t)pblk[z0 * a.P + colA], bn = (uint32_t)pblk[z0 * a.P + colB];
+    for (int z = z0; z < z1; ++z) {
+      const uint32_t az = an, bz = bn;
+      if (z + 1 < z1) {
+        an = (uint32_t)pblk[(z + 1) * a.P + colA];
+        bn = (uint32_t)pblk[(z + 1) * a.P + colB];
+      }
+      dbl2 N[4];
+      double Ne[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        N[k] = bload2(xr, (z + 1) * D + lo4[k]);
+        Ne[k] = bload1(xr, (z + 1) * D + eo4[k]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        dbl2 L[9];
+        double e[9];
+        L[4] = C[0]; e[4] = Ce[0]; L[5] = C[1]; e[5] = Ce[1];
+        L[6] = N[0]; e[6] = Ne[0]; L[7] = N[1]; e[7] = Ne[1]; L[8] = N[2]; e[8] = Ne[2];
+        const dbl2 t = pair_fwd27<UV>(L, e, az, puni);
+        dot += L[4].x * t.x;
+        dot += L[4].y * t.y;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      {
+        dbl2 L[9];
+        double e[9];
+        L[4] = C[1]; e[4] = Ce[1]; L[5] = C[2]; e[5] = Ce[2];
+        L[6] = N[1]; e[6] = Ne[1]; L[7] = N[2]; e[7] = Ne[2]; L[8] = N[3]; e[8] = Ne[3];
+        const dbl2 t = pair_fwd27<UV>(L, e, bz, puni);
+        dot += L[4].x * t.x;
+        dot += L[4].y * t.y;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { C[k] = N[k + 1]; Ce[k] = Ne[k + 1]; }
+    }
+    xx += dx;
+    if (xx >= PL) { xx -= PL; ++lp; }
+    lp += dlp;
+    if (lp >= NLP) { lp -= NLP; ++seg; }
+    seg += dseg;
+  }
+  double v[1] = {dot};
+  block_partials<1>(v, a.partials, gridDim.x, a.fold);
+}
+
 // CG mode 5's two passes on a 27-point "box" operator (Sell::pair_box27: the
 // column-word layout, every present off-diagonal slot holding one value v and
 // every diagonal one value c -- C5's 26 / -1 stencil).  Then
@@ -1832,6 +1931,17 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
     return grid;
   }
   // knob 70: two lines per wave (the column words pair up by lines, no ghost units)
+  if (form == 2 && g_knobs.zm27_2line && S.pair_2l27 && !split && mode == SPMV_PW && sym) {
+    const bool uv2 = S.pair_unit27 && g_knobs.pair_unitv;
+    grid = zm_tasks(b.P / 2, b.NZ, b.L, b.S, bpc);
+    if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
+    using FS = void (*)(PairLean27Args, const double *, const int32_t *, const PairUni27 *, const int32_t *);
+    FS fs = uv2 ? &spmv_pair_zm27s2l_kernel<true> : &spmv_pair_zm27s2l_kernel<false>;
+    note_dispatch(DSP_ZM_PW);
+    launch_timed(fs, grid, st, b, x, S.pblk.p, S.puni27.p, S.pcol27.p);
+    HIPCHECK(hipGetLastError());
+    return grid;
+  }
   if (form == 2 && g_knobs.zm27_2line && S.pair_2l27 && !split &&
       (mode == SPMV_RUPD || mode == SPMV_DOT || mode == SPMV_PLAIN)) {
     const bool uvp = S.pair_unit27 && g_knobs.pair_unitv;
