@@ -411,7 +411,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         row sums) for the MatMult, CG mode 5's residual update and its
  *         forward-half p.Ap pass (1, default: C5's share 199.7 -> 185.9 us per
  *         CG iteration, residual update 86 -> 78 us, p.Ap pass 37 -> 30 us,
- *         MatMult -5%; 0 off)
+ *         MatMult -5%; 0 off; 2: the p.Ap pass by groups of four lines,
+ *         27.5 us, the iteration unchanged)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

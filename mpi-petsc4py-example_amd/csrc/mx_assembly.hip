@@ -1427,6 +1427,7 @@ static void build_pair_uniform27(Sell &S, const std::vector<double> &vt, hipStre
 static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
   S.pcol27.reset();
   S.pair_2l27 = false;
+  S.pair_4l27 = false;
   S.pair_sym27 = false;
   S.pair_box27 = false;
   if (!S.puni27.p || !S.pair_clean27 || !S.pair_all || S.pat_star_off.size() < 27) return;
@@ -1452,18 +1453,22 @@ static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
     if (cw[(size_t)c] >= 0 && (uint32_t)cw[(size_t)c] != w) return;   // the column disagrees with itself
     cw[(size_t)c] = (int32_t)w;
   }
-  // line pairs for the two-line z-march (Sell::pair_2l27)
-  {
+  // line groups for the G-line z-march (Sell::pair_2l27 / pair_4l27): in each
+  // group of G lines the columns at one x share their edge words, and only
+  // the first line may have a dy = -1 boundary, only the last a dy = +1 one
+  auto groups = [&](int64_t G) {
     const int64_t nl = S.pat_star_off[16];               // run 5's centre: +n
-    bool ok = nl > 0 && nl % 128 == 0 && D % nl == 0 && (D / nl) % 2 == 0;
+    bool ok = nl > 0 && nl % 128 == 0 && D % nl == 0 && (D / nl) % G == 0;
     const int64_t PL = ok ? nl / 128 : 1;
     for (int64_t c = 0; ok && c < P; ++c) {
-      if ((c / PL) % 2) continue;                          // odd lines: the second of a pair
-      const uint32_t wa = (uint32_t)cw[(size_t)c], wb = (uint32_t)cw[(size_t)(c + PL)];
-      if ((wa & EDGES) != (wb & EDGES) || (wa & U27C_YHI) || (wb & U27C_YLO)) ok = false;
+      const int64_t k = (c / PL) % G, c0 = c - k * PL;   // line k of its group; the group's first column
+      const uint32_t wa = (uint32_t)cw[(size_t)c], w0 = (uint32_t)cw[(size_t)c0];
+      if ((wa & EDGES) != (w0 & EDGES) || (k > 0 && (wa & U27C_YLO)) || (k < G - 1 && (wa & U27C_YHI))) ok = false;
     }
-    S.pair_2l27 = ok;
-  }
+    return ok;
+  };
+  S.pair_2l27 = groups(2);
+  S.pair_4l27 = groups(4);
   S.pcol27.alloc((size_t)P);
   HIPCHECK(hipMemcpyAsync(S.pcol27.p, cw.data(), sizeof(int32_t) * P, hipMemcpyHostToDevice, st));
   HIPCHECK(hipStreamSynchronize(st));

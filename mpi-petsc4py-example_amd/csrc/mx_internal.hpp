@@ -219,6 +219,7 @@ struct Sell {
   // at the same x have equal edge words, no dy = +1 boundary on the first and
   // no dy = -1 boundary on the second
   bool pair_2l27 = false;
+  bool pair_4l27 = false;   // the same by groups of four lines (knob 70 = 2)
   // 27-point column words (one per 128-row column of a plane): when every
   // unit's empty runs are exactly its plane's z-boundary runs (plane 0: dz =
   // -1, the last plane: dz = +1 -- read out of range anyway) plus its column's

@@ -1236,7 +1236,9 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27
 // lines y - 1 .. y + 2 and their edges (8 loads for two units instead of 12)
 // and carries three.  Each row's t_i is pair_fwd27's, bit for bit; the p.Ap
 // partials group other rows per wave (to rounding).
-template <bool UV>
+// G lines per wave (knob 70 = 2: G = 4, Sell::pair_4l27): the next plane's
+// G + 2 lines per step, G + 1 carried.
+template <bool UV, int G = 2>
 __global__ void __launch_bounds__(256) spmv_pair_zm27s2l_kernel(const PairLean27Args a, const double *__restrict__ x,
                                                                 const int32_t *__restrict__ pblk,
                                                                 const PairUni27 *__restrict__ puni,
@@ -1260,63 +1262,53 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27s2l_kernel(const PairLean27
   }
   const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
   const int D = a.anchor[7], NL = a.anchor[5];
-  const int PL = NL / 128, PH = a.P / 2, NLP = PH / PL;
+  const int PL = NL / 128, PH = a.P / G, NLP = PH / PL;
   const int eb = lane == 0 ? -1 : 128;
   int seg = sb + w / PH, lp = (w % PH) / PL, xx = w % PL;
   const int dseg = W / PH, dlp = (W % PH) / PL, dx = W % PL;
   for (; seg < se;) {
-    const int colA = lp * 2 * PL + xx, colB = colA + PL;
+    const int colA = lp * G * PL + xx;                     // line y's column; line y + k's is + k PL
     const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
     const int cbA = colA * 128 + 2 * lane;
-    const uint32_t cwA = (uint32_t)pcol[colA], cwB = (uint32_t)pcol[colB];
+    const uint32_t cwA = (uint32_t)pcol[colA], cwZ = (uint32_t)pcol[colA + (G - 1) * PL];
     const int eA = colA * 128 + eb + ((lane == 0 ? (cwA & U27_ELO) : (cwA & U27_EHI)) ? PAIR_OOR_EDGE : 0);
-    const int oM = (cwA & U27C_YLO) ? PAIR_OOR : 0, oP = (cwB & U27C_YHI) ? PAIR_OOR : 0;
-    const int lo4[4] = {cbA - NL + oM, cbA, cbA + NL, cbA + 2 * NL + oP};
-    const int eo4[4] = {eA - NL + oM, eA, eA + NL, eA + 2 * NL + oP};
-    // plane z's lines y, y + 1, y + 2 (carried)
-    dbl2 C[3];
-    double Ce[3];
+    const int oM = (cwA & U27C_YLO) ? PAIR_OOR : 0, oP = (cwZ & U27C_YHI) ? PAIR_OOR : 0;
+    // line y - 1 + k, k = 0 .. G + 1
+    auto lof = [&](int k) { return cbA + (k - 1) * NL + (k == 0 ? oM : k == G + 1 ? oP : 0); };
+    auto eof = [&](int k) { return eA + (k - 1) * NL + (k == 0 ? oM : k == G + 1 ? oP : 0); };
+    // plane z's lines y .. y + G (carried)
+    dbl2 C[G + 1];
+    double Ce[G + 1];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      C[k] = bload2(xr, z0 * D + lo4[k + 1]);
-      Ce[k] = bload1(xr, z0 * D + eo4[k + 1]);
+    for (int k = 0; k <= G; ++k) {
+      C[k] = bload2(xr, z0 * D + lof(k + 1));
+      Ce[k] = bload1(xr, z0 * D + eof(k + 1));
     }
-    uint32_t an = (uint32_t)pblk[z0 * a.P + colA], bn = (uint32_t)pblk[z0 * a.P + colB];
     for (int z = z0; z < z1; ++z) {
-      const uint32_t az = an, bz = bn;
-      if (z + 1 < z1) {
-        an = (uint32_t)pblk[(z + 1) * a.P + colA];
-        bn = (uint32_t)pblk[(z + 1) * a.P + colB];
-      }
-      dbl2 N[4];
-      double Ne[4];
+      uint32_t bw[G];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        N[k] = bload2(xr, (z + 1) * D + lo4[k]);
-        Ne[k] = bload1(xr, (z + 1) * D + eo4[k]);
+      for (int u = 0; u < G; ++u) bw[u] = (uint32_t)pblk[z * a.P + colA + u * PL];
+      dbl2 N[G + 2];
+      double Ne[G + 2];
+#pragma unroll
+      for (int k = 0; k < G + 2; ++k) {
+        N[k] = bload2(xr, (z + 1) * D + lof(k));
+        Ne[k] = bload1(xr, (z + 1) * D + eof(k));
       }
       __builtin_amdgcn_sched_barrier(0);
-      {
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
         dbl2 L[9];
         double e[9];
-        L[4] = C[0]; e[4] = Ce[0]; L[5] = C[1]; e[5] = Ce[1];
-        L[6] = N[0]; e[6] = Ne[0]; L[7] = N[1]; e[7] = Ne[1]; L[8] = N[2]; e[8] = Ne[2];
-        const dbl2 t = pair_fwd27<UV>(L, e, az, puni);
+        L[4] = C[u]; e[4] = Ce[u]; L[5] = C[u + 1]; e[5] = Ce[u + 1];
+        L[6] = N[u]; e[6] = Ne[u]; L[7] = N[u + 1]; e[7] = Ne[u + 1]; L[8] = N[u + 2]; e[8] = Ne[u + 2];
+        const dbl2 t = pair_fwd27<UV>(L, e, bw[u], puni);
         dot += L[4].x * t.x;
         dot += L[4].y * t.y;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      {
-        dbl2 L[9];
-        double e[9];
-        L[4] = C[1]; e[4] = Ce[1]; L[5] = C[2]; e[5] = Ce[2];
-        L[6] = N[1]; e[6] = Ne[1]; L[7] = N[2]; e[7] = Ne[2]; L[8] = N[3]; e[8] = Ne[3];
-        const dbl2 t = pair_fwd27<UV>(L, e, bz, puni);
-        dot += L[4].x * t.x;
-        dot += L[4].y * t.y;
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { C[k] = N[k + 1]; Ce[k] = Ne[k + 1]; }
+      for (int k = 0; k <= G; ++k) { C[k] = N[k + 1]; Ce[k] = Ne[k + 1]; }
     }
     xx += dx;
     if (xx >= PL) { xx -= PL; ++lp; }
@@ -1933,10 +1925,12 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // knob 70: two lines per wave (the column words pair up by lines, no ghost units)
   if (form == 2 && g_knobs.zm27_2line && S.pair_2l27 && !split && mode == SPMV_PW && sym) {
     const bool uv2 = S.pair_unit27 && g_knobs.pair_unitv;
-    grid = zm_tasks(b.P / 2, b.NZ, b.L, b.S, bpc);
+    const bool g4 = g_knobs.zm27_2line == 2 && S.pair_4l27;
+    grid = zm_tasks(b.P / (g4 ? 4 : 2), b.NZ, b.L, b.S, bpc);
     if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
     using FS = void (*)(PairLean27Args, const double *, const int32_t *, const PairUni27 *, const int32_t *);
-    FS fs = uv2 ? &spmv_pair_zm27s2l_kernel<true> : &spmv_pair_zm27s2l_kernel<false>;
+    FS fs = g4 ? (uv2 ? &spmv_pair_zm27s2l_kernel<true, 4> : &spmv_pair_zm27s2l_kernel<false, 4>)
+               : (uv2 ? &spmv_pair_zm27s2l_kernel<true, 2> : &spmv_pair_zm27s2l_kernel<false, 2>);
     note_dispatch(DSP_ZM_PW);
     launch_timed(fs, grid, st, b, x, S.pblk.p, S.puni27.p, S.pcol27.p);
     HIPCHECK(hipGetLastError());
