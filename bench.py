@@ -772,6 +772,9 @@ def main():
         general = spmv_general_leg(comm, n)
 
     iter_bytes = cg_iter_bytes_design(info, m, nnz_loc, ng, mode, xb)
+    # the library's default residual update at this size (mx_spmv_pair.hip
+    # pair_cg5_rupd_launch, knob 68 = 3: two lines per wave from 2^23 rows)
+    two_line = world == 1 and mode == 5 and m >= (1 << 23) and info.get("pair_shape") == 7
     iter_gbps = iter_bytes * value / 1e9
     if rank == 0:
         traffic = load_traffic(n, world, mode)
@@ -795,7 +798,9 @@ def main():
                                             "WRITE_SIZE, gfx950 correction) of the same kernel on a builder box, "
                                             "not counters of this run") if traffic else None,
                          "traffic_detail": traffic,
-                         "kernel": ("spmv_pair_zm_kernel<SPMV_RUPD> (CG mode 5 residual update only: r -= alpha A p "
+                         "kernel": (("spmv_pair_zm2l_kernel<JM, 5> (two lines per wave, knob 68; " if two_line else
+                                     "spmv_pair_zm_kernel<SPMV_RUPD> (") +
+                                    "CG mode 5 residual update only: r -= alpha A p "
                                     "with A p recomputed, [z.z, z.r, r.r] folded" if mode == 5 else
                                     "spmv_sell_kernel<SPMV_CG> (CG-fused MatMult" if mode == 1 else
                                     ("spmv_pair_zm_kernel<SPMV_DOT> (CG MatMult, lean row-pair z-march" if info.get("pair_zmarch") else

@@ -93,8 +93,10 @@ def main():
     # the general kernel or the lean row-pair / z-march kernels)
     # (CG mode 5: the residual update spmv_pair_zm_kernel<7,...> -- SPMV_RUPD --
     # is the roofline kernel, keyed "/mode5")
+    # (from 2^23 rows: its two-lines-per-wave form spmv_pair_zm2l_kernel)
     cands = [k for k in fetch if k.startswith(("spmv_sell_kernel<3,", "spmv_sell_kernel<2,", "spmv_pair_zm_kernel<7,",
-                                               "spmv_pair_zm_kernel<2,", "spmv_pair_lean_kernel<2,"))]
+                                               "spmv_pair_zm2l_kernel<", "spmv_pair_zm_kernel<2,",
+                                               "spmv_pair_lean_kernel<2,"))]
     sp = max(cands, key=lambda k: sum(durs.get(k, [0.0]))) if cands else None
     if sp and not sp.startswith("spmv_sell_kernel<3,"):
         alg = spmv_alg
@@ -113,7 +115,8 @@ def main():
         wr = statistics.median(write[sp]) * 1024
         corr = f16 if f16 else 2.0
         traffic = fr * corr + wr
-        out[f"{grid}^3/N{ngpu}" + ("/mode5" if sp.startswith("spmv_pair_zm_kernel<7,") else "")] = {
+        out[f"{grid}^3/N{ngpu}" + ("/mode5" if sp.startswith(("spmv_pair_zm_kernel<7,", "spmv_pair_zm2l_kernel<"))
+                                   else "")] = {
             "bytes_per_launch": round(traffic), "fetch_bytes_raw": round(fr), "write_bytes": round(wr),
             "fetch_correction": round(corr, 4), "calib_8B_per_lane": f8 and round(f8, 4),
             "calib_16B_per_lane": f16 and round(f16, 4), "algorithmic_bytes": alg,
