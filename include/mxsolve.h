@@ -302,8 +302,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         at launch; 0/1, default 1)
  * key 28: resident workgroups per CU for the row-pair SpMV grid (default 4)
  * key 29: CG modes 2/5 apply the deferred x steps every B iterations from B
- *         rotating direction buffers (1, 2 or 4; default 0 = auto: 4 in mode
- *         5, else 2)
+ *         rotating direction buffers (1, 2, 4 or 8; default 0 = auto: 4 in
+ *         mode 5, else 2; 8 -- the same bits -- measured within +-1% of 4 per
+ *         256^3 iteration: the batch launch's eleven streams give back what
+ *         the rarer x pass saves)
  * key 33: no-progress deadline in ms of the KSP poller's wait on an RCCL
  *         communicator (re-armed whenever the device's count of iterations
  *         begun moves); past it the communicator is aborted and the call fails

@@ -43,7 +43,7 @@ struct CgTopIn {
   double xa, xpend;         // deferred x step (CG modes 1/2): x += xa p_{xi} while xpend != 0
   // mode 2 with batched x steps (knob 29 = B > 1): the steps of directions
   // [xlo, xhi) are pending, alpha_j in xal[j % B], p_j in buffer j % B
-  double xal[4];
+  double xal[8];
   int xlo, xhi;
 };
 

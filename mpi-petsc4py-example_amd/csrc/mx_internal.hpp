@@ -462,7 +462,7 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
 // clean symmetric 5/7-point; iterations i % xb != 0): forms and stores p_i
 // (buffer i % xb) from r_i and p_{i-1}, leaves the p.Ap partials
 bool pair_cg5_pbw_applies(const Mat *A, int jac_mode, int xb);
-int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, double *const pb[4], int xb,
+int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, double *const pb[8], int xb,
                         double *hist, int jac_mode, double jac_c, double *partials, const Fold &fold,
                         hipStream_t st);
 // true when matmult_overlap splits the product: interior launch || halo, then

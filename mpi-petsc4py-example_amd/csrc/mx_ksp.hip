@@ -357,12 +357,11 @@ __global__ void __launch_bounds__(256) cg_p_kernel(int64_t n, KspState *__restri
 #ifndef CG_X_NTS
 #define CG_X_NTS 1   // batched x steps: x stored non-temporally (with knob 32 bit 0)
 #endif
-struct PBufs { double *b[4]; };
+struct PBufs { double *b[8]; };
 template <int JM, int B>
 __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restrict__ s, const double *__restrict__ r,
                                                     const double *__restrict__ dv, const double dc,
-                                                    double *__restrict__ p0, double *__restrict__ p1,
-                                                    double *__restrict__ p2, double *__restrict__ p3,
+                                                    double *pb, const int64_t ps,
                                                     double *__restrict__ x, double *__restrict__ hist, const int unr,
                                                     const double *__restrict__ r0, double *__restrict__ npart,
                                                     const Fold fin) {
@@ -373,9 +372,11 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
   if (t.reason) return;
   const int i = t.i;
   const double b = t.b;
-  // buffers picked by wave-uniform selects (pointers stay scalar; an indexed
-  // pointer array went through scratch and serialised the loop)
-  auto pick = [&](int k) -> double * { return k == 0 ? p0 : k == 1 ? p1 : k == 2 ? p2 : p3; };
+  // the B direction buffers lie ps doubles apart from pb (one carve): p_j in
+  // buffer j % B at pb + (j % B) ps -- scalar arithmetic (an indexed pointer
+  // array went through scratch and serialised the loop; eight pointer
+  // arguments spilled SGPRs)
+  auto pick = [&](int k) -> double * { return pb + k * ps; };
   auto row = [&](double rr, double dd, double po) { return cg_dir(jac1<JM>(rr, dd, dc), b, po); };
   const int64_t stride = (int64_t)gridDim.x * 256;
   int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -387,12 +388,20 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
     double al[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) al[q] = top.xal[q];
+    // B = 8: the eight step lengths held in VGPRs (an empty asm pins them;
+    // as SGPRs beside the eight buffer pointers they spilled)
+    if constexpr (B == 8) {
+#pragma unroll
+      for (int q = 0; q < B; ++q) asm volatile("" : "+v"(al[q]));
+    }
     // the first batch ([0, B)) of a zero-guess solve is x's first write: x
     // is the +0.0 the solve started from, so it is not read (nor zeroed at
     // the start); fma(a, p, +0.0) is what the read would have given
     const bool xz = top.xlo == 0 && s->guess_zero;
-    double *__restrict__ pout = p0;
-    const double *__restrict__ pprev = B == 4 ? p3 : p1;
+    double *__restrict__ pout = pb;
+    const double *__restrict__ pprev = pick(B - 1);
+    const double *__restrict__ p1 = pick(1), *__restrict__ p2 = pick(2), *__restrict__ p3 = pick(3);
+    const double *__restrict__ p4 = pick(4), *__restrict__ p5 = pick(5), *__restrict__ p6 = pick(6);
     auto batch = [&](auto ntc) __attribute__((always_inline)) {   // non-temporal reads: see walk below
       constexpr bool NTL = decltype(ntc)::value;
       auto ldv = [&](const double *q) __attribute__((always_inline)) -> double {
@@ -402,9 +411,15 @@ __global__ void __launch_bounds__(256) cg_pb_kernel(int64_t n, KspState *__restr
       for (; k < n; k += stride) {
         const double po = ldv(pprev + k);
         double xx = fma(al[0], ldv(pout + k), xz ? 0.0 : ldv(x + k));   // x += a_{i-B} p_{i-B}, oldest first
-        if constexpr (B == 4) {
+        if constexpr (B >= 4) {
           xx = fma(al[1], ldv(p1 + k), xx);
           xx = fma(al[2], ldv(p2 + k), xx);
+        }
+        if constexpr (B == 8) {
+          xx = fma(al[3], ldv(p3 + k), xx);
+          xx = fma(al[4], ldv(p4 + k), xx);
+          xx = fma(al[5], ldv(p5 + k), xx);
+          xx = fma(al[6], ldv(p6 + k), xx);
         }
         // ... x += a_{i-1} p_{i-1}; x is next read B iterations on, so with
         // CG_X_NTS its store bypasses the memory-side cache (p_i keeps it)
@@ -649,19 +664,21 @@ __global__ void cg_finish_xb_kernel(int64_t n, const KspState *__restrict__ s, c
       for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = 0.0;
     return;
   }
-  // at most B - 1 + 1 pending steps; their buffers and scalars picked once
-  const double *p[4];
-  double a[4];
+  // at most B pending steps; their buffers and scalars picked once
+  const double *p[8];
+  double a[8];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < 8; ++q) {
     const int j = (j0 + (q < np ? q : 0)) % B;
-    p[q] = j == 0 ? pb.b[0] : j == 1 ? pb.b[1] : j == 2 ? pb.b[2] : pb.b[3];
+    p[q] = pb.b[0];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) p[q] = j == c ? pb.b[c] : p[q];
     a[q] = s->top.xal[j];
   }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     double xx = xz ? 0.0 : x[i];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 8; ++q)
       if (q < np) xx = fma(a[q], p[q][i], xx);
     x[i] = xx;
   }
@@ -1547,9 +1564,10 @@ static void cg_pb_launch(hipStream_t st, int64_t n, KspState *s, const double *r
   Fold fin = fin_in;
   fin.ntotal = fin.ncount = (int)g;
   const int unr = (cg_unroll(n) ? 1 : 0) | ((g_knobs.cg_ntl & 1) ? 2 : 0);
-#define CGPB(JM, BB) launch_timed(&cg_pb_kernel<JM, BB>, (int)g, st, n, s, r, j.d, j.c, pb.b[0], pb.b[1], pb.b[2], \
-                                     pb.b[3], x, hist, unr, r0, npart, fin)
-#define CGPB_J(JM) do { if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
+  const int64_t ps = pb.b[1] - pb.b[0];   // (the buffers are carved consecutively, cg_solve)
+#define CGPB(JM, BB) launch_timed(&cg_pb_kernel<JM, BB>, (int)g, st, n, s, r, j.d, j.c, pb.b[0], ps, x, hist, unr, r0, \
+                                     npart, fin)
+#define CGPB_J(JM) do { if (B == 8) CGPB(JM, 8); else if (B == 4) CGPB(JM, 4); else CGPB(JM, 2); } while (0)
   switch (j.mode) { case 1: CGPB(1, 2); break; case 2: CGPB_J(2); break; default: CGPB_J(0); }
 #undef CGPB_J
 #undef CGPB
@@ -1619,16 +1637,20 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // (batches of 4 only with no or a uniform Jacobi: the vector-Jacobi
   // direction update with four p buffers spilled SGPRs and is not on any
   // default path -- mode 5, the only one batching by 4, needs a uniform one)
-  const int xbk = g_knobs.cg_xbatch == 0 ? (fmode == 5 ? 4 : 2) : (g_knobs.cg_xbatch == 4 && dinv.mode == 1) ? 2
-                                                                                                           : g_knobs.cg_xbatch;
-  const int xb = ((fmode == 2 || fmode == 5) && (xbk == 2 || xbk == 4) && poll % xbk == 0) ? xbk : 1;
+  const int xbk = g_knobs.cg_xbatch == 0 ? (fmode == 5 ? 4 : 2)
+                  : ((g_knobs.cg_xbatch == 4 || g_knobs.cg_xbatch == 8) && dinv.mode == 1) ? 2 : g_knobs.cg_xbatch;
+  const int xb = ((fmode == 2 || fmode == 5) && (xbk == 2 || xbk == 4 || xbk == 8) && poll % xbk == 0) ? xbk : 1;
   const bool wide_pb = fmode == 5;
-  Carve cv(workspace(A, carve_size({nv, nv, nv, nv, npart, nhist, xb == 4 ? nv : 0, xb == 4 ? nv : 0})));
-  struct { double *p; } r{cv.take(nv)}, pv{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)};
+  const size_t nx = xb >= 4 ? nv : 0, nx8 = xb == 8 ? nv : 0;
+  Carve cv(workspace(A, carve_size({nv, nv, npart, nhist, nv, nv, nx, nx, nx8, nx8, nx8, nx8})));
+  struct { double *p; } r{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)}, pv{cv.take(nv)};
   double *pv2 = cv.take(nv);   // fused CG: p_i alternates between pv (i even) and pv2
-  double *pv3 = xb == 4 ? cv.take(nv) : pv.p;
-  double *pv4 = xb == 4 ? cv.take(nv) : pv2;
-  const PBufs pbs{{pv.p, pv2, pv3, pv4}};
+  // x batches of B: p_j in buffer j % B, the B buffers carved consecutively
+  // (equally spaced: the kernels address them from pv; unused slots repeat
+  // the first two)
+  PBufs pbs{{pv.p, pv2, pv.p, pv2, pv.p, pv2, pv.p, pv2}};
+  for (int q = 2; q < xb; ++q) pbs.b[q] = cv.take(nv);
+  double *pv3 = pbs.b[2], *pv4 = pbs.b[3];
   struct { KspState *p; } sd{state_buf(A)};
   const KspInit kin{p.rtol, p.atol, p.dtol, p.haptol, p.breakdowntol, p.max_it, normtype, !p.guess_nonzero, p.restart};
   ksp_state_init_kernel<<<1, 256, 0, st>>>(sd.p, kin);
@@ -1782,7 +1804,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     // could have baked in (template choice, launch geometry, argument) counts
     key = {(uintptr_t)x, (uintptr_t)r.p, (uintptr_t)r0, (uintptr_t)poller.hw, (uintptr_t)hist_d, (uintptr_t)dinv.mode, (uintptr_t)dinv.d, 0,
            (uintptr_t)poll, (uintptr_t)fmode, (uintptr_t)fold_at, (uintptr_t)pv.p, (uintptr_t)w.p, (uintptr_t)pv2,
-           (uintptr_t)part.p, (uintptr_t)xb, (uintptr_t)pv3, (uintptr_t)pv4};
+           (uintptr_t)part.p, (uintptr_t)xb, (uintptr_t)pv3, (uintptr_t)pv4, (uintptr_t)pbs.b[4],
+           (uintptr_t)pbs.b[5], (uintptr_t)pbs.b[6], (uintptr_t)pbs.b[7]};
     const int *kw = reinterpret_cast<const int *>(&g_knobs);
     for (size_t q = 0; q < sizeof(Knobs) / sizeof(int); ++q) key.push_back((uintptr_t)(uint32_t)kw[q]);
     std::memcpy(&key[7], &dinv.c, sizeof(double));

@@ -518,7 +518,8 @@ struct PairPbArgs {
   KspState *s;
   const double *r;             // r_i
   const double *r0;            // iteration 0 of a zero-guess solve: r_0 = b (not copied into r)
-  double *pb0, *pb1, *pb2, *pb3;   // p_j in buffer j % B
+  double *pb;                  // p_j in buffer j % B, at pb + (j % B) ps
+  int64_t ps;
   double *hist;
   double c;                    // JM 2: the uniform Jacobi scalar
 };
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(256) spmv_pair_pbw_kernel(const PairLeanArgs a
   const double b = t.b;
   using SH = PairShape<PS>;
   constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1, C = SH::CENTER_RUN;
-  auto pick = [&](int k) -> double * { return k == 0 ? pa.pb0 : k == 1 ? pa.pb1 : k == 2 ? pa.pb2 : pa.pb3; };
+  auto pick = [&](int k) -> double * { return pa.pb + k * pa.ps; };
   double *pout = pick(i % B);
   const double *pprev = pick((i + B - 1) % B);
   const double *rs = (pa.r0 && i == 0) ? pa.r0 : pa.r;
@@ -2210,12 +2211,12 @@ static int cg5_args(const Mat *A, PairLeanArgs &a, int bpc = 0) {
 bool pair_cg5_pbw_applies(const Mat *A, int jac_mode, int xb) {
   const int on = g_knobs.cg_pbw != 5 ? g_knobs.cg_pbw
                                      : A->m <= (int64_t(1) << (A->sd.pair_shape == 5 ? 24 : 23));
-  return on && (xb == 2 || xb == 4) && (jac_mode == 0 || jac_mode == 2) && pair_cg5_applies(A, jac_mode) &&
+  return on && (xb == 2 || xb == 4 || xb == 8) && (jac_mode == 0 || jac_mode == 2) && pair_cg5_applies(A, jac_mode) &&
          A->sd.pair_shape != 27 && pair_lean_kind(A) == 2 && A->nghost == 0 && !A->sd.pair_ghosts && A->sym == 1 &&
          g_knobs.pw_sym27 && pair_zm_applies(A);
 }
 
-int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, double *const pb[4], int xb,
+int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, double *const pb[8], int xb,
                         double *hist, int jac_mode, double jac_c, double *partials, const Fold &fold_in,
                         hipStream_t st) {
   if (!pair_cg5_pbw_applies(A, jac_mode, xb)) return 0;
@@ -2234,12 +2235,12 @@ int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, 
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = grid; fold.base = 0; }
   a.fold = fold;
-  const PairPbArgs pa{s, r, r0, pb[0], pb[1], pb[2], pb[3], hist, jac_c};
+  const PairPbArgs pa{s, r, r0, pb[0], pb[1] - pb[0], hist, jac_c};   // (consecutive carves, cg_solve)
   using PbwFn = void (*)(const PairLeanArgs, const int32_t *, const PairUni *, const PairPbArgs);
   PbwFn f;
   const bool z2 = g_knobs.pair_zm_units == 2;
 #define PBW(PS, JM, B) f = z2 ? &spmv_pair_pbw_kernel<PS, JM, B, 2> : &spmv_pair_pbw_kernel<PS, JM, B, 1>
-#define PBW_B(PS, JM) do { if (xb == 4) PBW(PS, JM, 4); else PBW(PS, JM, 2); } while (0)
+#define PBW_B(PS, JM) do { if (xb == 8) PBW(PS, JM, 8); else if (xb == 4) PBW(PS, JM, 4); else PBW(PS, JM, 2); } while (0)
 #define PBW_J(PS) do { if (jac_mode == 2) PBW_B(PS, 2); else PBW_B(PS, 0); } while (0)
   if (S.pair_shape == 5) PBW_J(5);
   else PBW_J(7);

@@ -515,3 +515,44 @@ def test_two_line_27point(selfcomm, dims, max_it):
     assert a[4] == c[4] == 5 and c[5]["zm_rupd"] > 0, (a[4], c[4], c[5])
     assert np.allclose(a[2], c[2], rtol=1e-10, atol=0)
     assert np.linalg.norm(a[3] - c[3]) <= 1e-12 * np.linalg.norm(a[3])
+
+
+@pytest.mark.parametrize("kind,dims,mode,max_it", [
+    ("poisson3d", (256, 128, 40), 5, 10000), ("poisson3d", (256, 128, 40), 5, 37), ("poisson3d", (256, 128, 40), 5, 20),
+    ("poisson3d", (128, 128, 128), 5, 10000), ("poisson3d", (256, 128, 40), 2, 10000), ("poisson3d", (256, 128, 40), 2, 29),
+    ("poisson3d27", (128, 128, 16), 5, 10000), ("poisson2d", (1024, 1024, 1), 5, 10000),
+])
+def test_xbatch8_bitwise(selfcomm, kind, dims, mode, max_it):
+    """Knob 29 = 8: x steps batched by eight (eight direction buffers) apply
+    the same fma(a_j, p_j, x) chain oldest first as batches of four -- x never
+    feeds back into the iteration -- so the whole solve (its, reason, history,
+    x) is bitwise the same; max_it 37 / 20 / 29 stop with 5 / 4 / 5 steps
+    pending for the finish pass."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, rhs_hash
+    L = _lib.load()
+    old27 = L.mx_debug_set(27, 1)
+    try:
+        A = DMat.stencil(selfcomm, kind, *dims)
+    finally:
+        L.mx_debug_set(27, old27)
+    m = A.info()["m"]
+    b = selfcomm.empty(m)
+    rhs_hash(selfcomm, 0, b)
+    outs = []
+    for xb in (4, 8):
+        old = {k: L.mx_debug_set(k, v) for k, v in ((9, mode), (27, 1), (29, xb))}
+        try:
+            x = selfcomm.zeros(m)
+            r = A.solve(b, x, ksp="cg", pc="jacobi", rtol=1e-8, max_it=max_it, history=True)
+            outs.append((r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy(), r["cg_mode"],
+                         r["cg_xbatch"]))
+        finally:
+            for k, v in old.items():
+                L.mx_debug_set(k, v)
+    A.destroy()
+    a, c = outs
+    assert a[4] == c[4] == mode and (a[5], c[5]) == (4, 8), (a[4:], c[4:])
+    assert a[:2] == c[:2]
+    assert np.array_equal(a[2].view(np.uint64), c[2].view(np.uint64))
+    assert np.array_equal(a[3].view(np.uint64), c[3].view(np.uint64))
