@@ -556,3 +556,30 @@ def test_xbatch8_bitwise(selfcomm, kind, dims, mode, max_it):
     assert a[:2] == c[:2]
     assert np.array_equal(a[2].view(np.uint64), c[2].view(np.uint64))
     assert np.array_equal(a[3].view(np.uint64), c[3].view(np.uint64))
+
+
+@pytest.mark.parametrize("max_it", [20, 37, 10000])
+def test_finish_unaligned_x(selfcomm, max_it):
+    """The batched x steps' finish pass takes 16-byte row pairs when the
+    caller's x is 16-byte aligned and one row per step otherwise (an x that
+    is a view one element into a larger buffer): the same bits either way."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, rhs_hash
+    L = _lib.load()
+    old27 = L.mx_debug_set(27, 1)
+    try:
+        A = DMat.stencil(selfcomm, "poisson3d", 128, 128, 40)
+    finally:
+        L.mx_debug_set(27, old27)
+    m = A.info()["m"]
+    b = selfcomm.empty(m)
+    rhs_hash(selfcomm, 0, b)
+    xa = selfcomm.zeros(m)
+    big = selfcomm.zeros(m + 1)
+    xu = big[1:]
+    assert xu.data_ptr() % 16 == 8
+    ra = A.solve(b, xa, ksp="cg", pc="jacobi", rtol=1e-8, max_it=max_it)
+    ru = A.solve(b, xu, ksp="cg", pc="jacobi", rtol=1e-8, max_it=max_it)
+    A.destroy()
+    assert (ra["its"], ra["reason"]) == (ru["its"], ru["reason"])
+    assert torch.equal(xa.view(torch.int64), xu.contiguous().view(torch.int64))
