@@ -296,6 +296,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 23: value codes -- one byte per slot into a table of <= 255 distinct
  *         values -- for the diagonal block (read at assembly and at launch;
  *         0/1, default 1)
+ * key 24: retired (round 1's SpMV unroll switch; no effect)
  * key 25: non-temporal y stores in the SpMV (0/1, default 0)
  * key 26: resident workgroups per CU for the single-row SpMV grid (default 6)
  * key 27: row-pair SpMV layout for 5/7/27-point patterns (read at assembly and
@@ -306,6 +307,13 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         mode 5, else 2; 8 -- the same bits -- measured within +-1% of 4 per
  *         256^3 iteration: the batch launch's eleven streams give back what
  *         the rarer x pass saves)
+ * key 30: the row-pair block dictionary (read at assembly: 1, default, when
+ *         repeats pay for the indirection; 2 always; 0 one block per unit)
+ * key 31: the general SELL sweep runs its items from the last down (0/1,
+ *         default 0; 1 also turns the lean row-pair kernels off)
+ * key 32: non-temporal loads in the CG vector passes: bit 0 the direction
+ *         update's r / p_{i-1} reads, bit 1 the update pass's w / r reads
+ *         (default 3)
  * key 33: no-progress deadline in ms of the KSP poller's wait on an RCCL
  *         communicator (re-armed whenever the device's count of iterations
  *         begun moves); past it the communicator is aborted and the call fails

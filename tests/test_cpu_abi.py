@@ -57,3 +57,15 @@ def test_built_for_gfx950():
     assert b"amdgcn-amd-amdhsa--gfx950" in data
     for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
         assert other not in data
+
+
+def test_every_debug_key_documented():
+    """Every measurement knob mx_debug_set accepts (csrc/mx_abi.hip) has its
+    "key N:" entry in include/mxsolve.h, so an A/B setting named in DESIGN.md
+    or a profile can be looked up."""
+    import re
+    abi = open(os.path.join(ROOT, "mpi-petsc4py-example_amd", "csrc", "mx_abi.hip")).read()
+    keys = sorted({int(k) for k in re.findall(r"case (\d+): old = g_knobs", abi)})
+    hdr = open(os.path.join(ROOT, "include", "mxsolve.h")).read()
+    doc = {int(k) for k in re.findall(r"key (\d+):", hdr)}
+    assert keys and not [k for k in keys if k not in doc]
