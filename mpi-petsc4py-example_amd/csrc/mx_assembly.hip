@@ -262,19 +262,32 @@ __global__ void __launch_bounds__(256) canon_rows_wave_kernel(
       v = val[start + l];
     }
   }
+  // Already canonical (every kept column above the previous kept column of
+  // its row, in input order -- scipy's canonical CSR, the stencil generator):
+  // the sort would only move the dropped lanes to the end, which the ballot
+  // compaction below does anyway, and there is nothing to dedupe.  Decided per
+  // wave, so most waves of such inputs skip the bitonic network.
+  const int gbase0 = lane - l;
+  const unsigned long long vb = __ballot(c != KEY_DROP);
+  const unsigned long long below_v = vb & ((l == 0) ? 0ULL : (((1ULL << l) - 1ULL) << gbase0));
+  const int pl = below_v ? 63 - __clzll(below_v) : lane;
+  const int64_t cprev = __shfl(c, pl, 64);
+  const bool sorted = !__any(c != KEY_DROP && below_v != 0 && cprev >= c);
   // bitonic sort of (c, p) ascending inside each W-lane segment
+  if (!sorted) {
 #pragma unroll
-  for (int k = 2; k <= W; k <<= 1) {
+    for (int k = 2; k <= W; k <<= 1) {
 #pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      int64_t c2 = __shfl_xor(c, j, 64);
-      int64_t p2 = __shfl_xor(p, j, 64);
-      double v2 = __shfl_xor(v, j, 64);
-      const bool up = (l & k) == 0;
-      const bool lower = (l & j) == 0;
-      const bool mine_less = (c < c2) || (c == c2 && p < p2);
-      const bool keep = (lower == up) ? mine_less : !mine_less;
-      if (!keep) { c = c2; p = p2; v = v2; }
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        int64_t c2 = __shfl_xor(c, j, 64);
+        int64_t p2 = __shfl_xor(p, j, 64);
+        double v2 = __shfl_xor(v, j, 64);
+        const bool up = (l & k) == 0;
+        const bool lower = (l & j) == 0;
+        const bool mine_less = (c < c2) || (c == c2 && p < p2);
+        const bool keep = (lower == up) ? mine_less : !mine_less;
+        if (!keep) { c = c2; p = p2; v = v2; }
+      }
     }
   }
   const bool valid = c != KEY_DROP;
@@ -484,21 +497,83 @@ static void canon_huge_rows(const std::vector<int64_t> &rows, const int64_t *row
 }
 
 // ---------------------------------------------------------------- split
-__global__ void split_count_kernel(int64_t m, const int64_t *__restrict__ rowptr,
-                                   const int64_t *__restrict__ cnt, const int64_t *__restrict__ ccol,
-                                   int64_t cstart, int64_t cend, int64_t *__restrict__ cnt_d,
-                                   int64_t *__restrict__ cnt_o, unsigned *__restrict__ bitmap) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const int64_t s = rowptr[i], n = cnt[i];
+// W-lane segment per row (the canonicalisation's width): lane l reads entry
+// base + l of its row, chunks of W entries, so a wave's loads are contiguous
+// runs of the canonical arrays instead of 64 row walks ~W entries apart (the
+// thread-per-row kernels they replace took 33 ms of a 27-point share's
+// 100 ms assembly, round 5).  A row's diagonal / ghost
+// entries keep their order: each lane's destination is its segment's running
+// count plus the ballot prefix below it.
+template <int W>
+__device__ __forceinline__ unsigned long long seg_bits(unsigned long long ball, int gbase) {
+  return W == 64 ? ball : ((ball >> gbase) & ((1ULL << (W == 64 ? 0 : W)) - 1ULL));
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) split_count_seg_kernel(int64_t m, const int64_t *__restrict__ rowptr,
+                                                              const int64_t *__restrict__ cnt,
+                                                              const int64_t *__restrict__ ccol, int64_t cstart,
+                                                              int64_t cend, int64_t *__restrict__ cnt_d,
+                                                              int64_t *__restrict__ cnt_o, unsigned *__restrict__ bitmap) {
+  const int lane = threadIdx.x & 63, l = lane % W, gbase = lane - l;
+  const int64_t row = (int64_t)blockIdx.x * (256 / W) + threadIdx.x / W;
+  const bool rv = row < m;
+  const int64_t s = rv ? rowptr[row] : 0, n = rv ? cnt[row] : 0;
   int64_t d = 0;
-  for (int64_t j = 0; j < n; ++j) {
-    const int64_t c = ccol[s + j];
-    if (c >= cstart && c < cend) d++;
-    else atomicOr(&bitmap[c >> 5], 1u << (c & 31));
+  int64_t nmax = n;   // wave-uniform trip count
+  for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, (int64_t)__shfl_xor(nmax, o, 64));
+  for (int64_t b = 0; b < nmax; b += W) {
+    const bool in = b + l < n;
+    const int64_t c = in ? ccol[s + b + l] : 0;
+    const bool isd = in && c >= cstart && c < cend;
+    if (in && !isd) atomicOr(&bitmap[c >> 5], 1u << (c & 31));
+    d += __popcll(seg_bits<W>(__ballot(isd), gbase));
   }
-  cnt_d[i] = d;
-  cnt_o[i] = n - d;
+  if (rv && l == 0) { cnt_d[row] = d; cnt_o[row] = n - d; }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) fill_split_seg_kernel(
+    int64_t m, const int64_t *__restrict__ rowptr, const int64_t *__restrict__ cnt, const int64_t *__restrict__ ccol,
+    const double *__restrict__ cval, int64_t cstart, int64_t cend, int64_t rstart, const int64_t *__restrict__ dptr,
+    const int64_t *__restrict__ optr, int32_t *__restrict__ dcol, double *__restrict__ dval, int32_t *__restrict__ ocol,
+    double *__restrict__ oval, double *__restrict__ diag, const unsigned *__restrict__ bitmap,
+    const int64_t *__restrict__ wbase) {
+  const int lane = threadIdx.x & 63, l = lane % W, gbase = lane - l;
+  const int64_t row = (int64_t)blockIdx.x * (256 / W) + threadIdx.x / W;
+  const bool rv = row < m;
+  const int64_t s = rv ? rowptr[row] : 0, n = rv ? cnt[row] : 0;
+  int64_t pd = rv ? dptr[row] : 0, po = rv ? optr[row] : 0;
+  const int64_t grow = rstart + row;
+  const unsigned long long below = l == 0 ? 0ULL : ((1ULL << l) - 1ULL);
+  int64_t nmax = n;
+  for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, (int64_t)__shfl_xor(nmax, o, 64));
+  bool have_diag = false;
+  for (int64_t b = 0; b < nmax; b += W) {
+    const bool in = b + l < n;
+    const int64_t c = in ? ccol[s + b + l] : 0;
+    const double v = in ? cval[s + b + l] : 0.0;
+    const bool isd = in && c >= cstart && c < cend;
+    const bool iso = in && !isd;
+    const unsigned long long bd = seg_bits<W>(__ballot(isd), gbase), bo = seg_bits<W>(__ballot(iso), gbase);
+    const unsigned long long bg = seg_bits<W>(__ballot(isd && c == grow), gbase);
+    if (isd) {
+      const int64_t t = pd + __popcll(bd & below);
+      dcol[t] = (int32_t)(c - cstart);
+      dval[t] = v;
+      if (c == grow) diag[row] = v;
+    } else if (iso) {
+      const int64_t w = c >> 5;
+      const unsigned bit = (unsigned)(c & 31);
+      const int64_t t = po + __popcll(bo & below);
+      ocol[t] = (int32_t)(wbase[w] + __popc(bitmap[w] & ((1u << bit) - 1u)));
+      oval[t] = v;
+    }
+    pd += __popcll(bd);
+    po += __popcll(bo);
+    have_diag = have_diag || bg != 0;
+  }
+  if (rv && l == 0 && !have_diag) diag[row] = 0.0;
 }
 
 __global__ void popc_kernel(int64_t nw, const unsigned *__restrict__ bitmap, int64_t *__restrict__ out) {
@@ -518,37 +593,6 @@ __global__ void garray_kernel(int64_t nw, const unsigned *__restrict__ bitmap,
       b &= b - 1;
     }
   }
-}
-
-__global__ void fill_split_kernel(int64_t m, const int64_t *__restrict__ rowptr,
-                                  const int64_t *__restrict__ cnt, const int64_t *__restrict__ ccol,
-                                  const double *__restrict__ cval, int64_t cstart, int64_t cend,
-                                  int64_t rstart, const int64_t *__restrict__ dptr,
-                                  const int64_t *__restrict__ optr, int32_t *__restrict__ dcol,
-                                  double *__restrict__ dval, int32_t *__restrict__ ocol,
-                                  double *__restrict__ oval, double *__restrict__ diag,
-                                  const unsigned *__restrict__ bitmap,
-                                  const int64_t *__restrict__ wbase) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const int64_t s = rowptr[i], n = cnt[i];
-  int64_t pd = dptr[i], po = optr[i];
-  double dg = 0.0;
-  const int64_t grow = rstart + i;
-  for (int64_t j = 0; j < n; ++j) {
-    const int64_t c = ccol[s + j];
-    const double v = cval[s + j];
-    if (c >= cstart && c < cend) {
-      dcol[pd] = (int32_t)(c - cstart); dval[pd++] = v;
-      if (c == grow) dg = v;
-    } else {
-      const int64_t w = c >> 5;
-      const unsigned b = (unsigned)(c & 31);
-      ocol[po] = (int32_t)(wbase[w] + __popc(bitmap[w] & ((1u << b) - 1u)));
-      oval[po++] = v;
-    }
-  }
-  diag[i] = dg;
 }
 
 // ---------------------------------------------------------------- SELL-64
@@ -596,29 +640,50 @@ __device__ __forceinline__ int64_t sell_slot(int64_t base, int j, int w, int lan
                                      : (int64_t)(w >> 1) * 2 * SLICE + lane);
 }
 
+// SELL fill, one wave per slice, with the slice's canonical entries staged in LDS: a
+// slice's 64 rows are one contiguous range of the CSR arrays, so the wave
+// reads it with contiguous loads and each lane then walks its row in LDS
+// (the global row walks touched 64 lines per load, lanes ~K entries apart:
+// 8.1 ms for a 27-point share, round 5).  One wave per block; a slice with
+// more entries than the staging buffer takes the global walk.
+constexpr int SELL_STAGE = 2048;
+
 template <bool PAIRED>
-__global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
-                                 const int32_t *__restrict__ ccol, const double *__restrict__ cval,
-                                 int64_t nslices, const int64_t *__restrict__ sptr,
-                                 const int32_t *__restrict__ width, const int32_t *__restrict__ doff,
-                                 int32_t *__restrict__ scol, double *__restrict__ sval,
-                                 uint32_t *__restrict__ mask, uint8_t *__restrict__ mask8) {
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ void __launch_bounds__(64) sell_fill_lds_kernel(int64_t m, const int64_t *__restrict__ ptr,
+                                                           const int32_t *__restrict__ ccol,
+                                                           const double *__restrict__ cval, int64_t nslices,
+                                                           const int64_t *__restrict__ sptr,
+                                                           const int32_t *__restrict__ width,
+                                                           const int32_t *__restrict__ doff, int32_t *__restrict__ scol,
+                                                           double *__restrict__ sval, uint32_t *__restrict__ mask,
+                                                           uint8_t *__restrict__ mask8) {
+  __shared__ int32_t lc[SELL_STAGE];
+  __shared__ double lv[SELL_STAGE];
+  const int64_t s = blockIdx.x;
   if (s >= nslices) return;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x;
   const int64_t row = s * SLICE + lane;
+  const int64_t r0 = s * SLICE, r1 = min(m, r0 + SLICE);
+  const int64_t a0 = ptr[r0], cnt = ptr[r1] - a0;
   const int wr = width[s];
   const int64_t base = sptr[s];
-  const int64_t rs = row < m ? ptr[row] : 0;
+  const int64_t rs = row < m ? ptr[row] : a0;
   const int len = row < m ? (int)(ptr[row + 1] - rs) : 0;
+  const bool staged = cnt <= SELL_STAGE;   // block-uniform
+  if (staged) {
+    for (int64_t e = lane; e < cnt; e += 64) { lc[e] = ccol[a0 + e]; lv[e] = cval[a0 + e]; }
+    __syncthreads();
+  }
+  const int32_t *__restrict__ rc = staged ? lc + (rs - a0) : ccol + rs;
+  const double *__restrict__ rvv = staged ? lv + (rs - a0) : cval + rs;
   if (wr < 0) {                       // aligned-offset slice
     const int k = -wr;
     uint32_t mk = 0;
     int cur = 0;
     for (int j = 0; j < k; ++j) {
       const int off = doff[s * DIA_MAX + j];
-      const bool hit = cur < len && (int64_t)ccol[rs + cur] - row == off;
-      sval[sell_slot(base, j, k, lane, PAIRED)] = hit ? cval[rs + cur] : 0.0;
+      const bool hit = cur < len && (int64_t)rc[cur] - row == off;
+      sval[sell_slot(base, j, k, lane, PAIRED)] = hit ? rvv[cur] : 0.0;
       if (hit) { mk |= 1u << j; ++cur; }
     }
     if (mask8) mask8[row] = (uint8_t)mk;
@@ -629,8 +694,8 @@ __global__ void sell_fill_kernel(int64_t m, const int64_t *__restrict__ ptr,
   for (int j = 0; j < w; ++j) {
     const bool in = j < len;
     const int64_t t = sell_slot(base, j, w, lane, PAIRED);
-    scol[t] = in ? ccol[rs + j] : -1;
-    sval[t] = in ? cval[rs + j] : 0.0;
+    scol[t] = in ? rc[j] : -1;
+    sval[t] = in ? rvv[j] : 0.0;
   }
 }
 
@@ -740,6 +805,11 @@ static void share_offset_patterns(Sell &S, const std::vector<int32_t> &wh, int64
                                   hipMemcpyDeviceToHost, st));
           HIPCHECK(hipStreamSynchronize(st));
         }
+        S.pat_len.resize((size_t)npat);
+        for (int q = 0; q < npat; ++q) S.pat_len[(size_t)q] = -wh[(size_t)rep[(size_t)q]];
+        S.pat_host.resize((size_t)npat * DIA_MAX);
+        HIPCHECK(hipMemcpyAsync(S.pat_host.data(), ptab.p, sizeof(int32_t) * S.pat_host.size(), hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
         S.doff = std::move(ptab);
         S.npat = npat;
         dia_inb_kernel<<<(unsigned)cdiv(ns, 256), 256, 0, st>>>(ns, ncols, S.width.p, S.doff.p, S.dpat.p);
@@ -902,57 +972,45 @@ static int pair_shape_of(const std::vector<int32_t> &o) {
 
 constexpr int pair_bytes(int k) { return (2 * k + 15) / 16 * 16; }
 
-// one wave per unit; sets DPAT_PAIR on slice 2u and writes the unit's codes
-__global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, int32_t star, const int64_t *__restrict__ sptr,
-                                 const int32_t *__restrict__ width, int32_t *__restrict__ dpat,
-                                 const int32_t *__restrict__ doff, const double *__restrict__ sval,
-                                 const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8,
-                                 const unsigned long long *__restrict__ tab, const uint8_t *__restrict__ slot_code,
-                                 uint8_t *__restrict__ pcode) {
+// one wave per unit; sets DPAT_PAIR on slice 2u and writes the unit's codes.
+// The slot mapping (dominant slot j -> slot of the slice's own pattern, and
+// whether a pattern's offsets all belong to the dominant one) is a per-pattern
+// table built on the host, and each code is read from the slice's code block
+// (code_fill_kernel's bytes, VCODE_ABSENT where the row lacks the slot) rather
+// than looked up again by value; the lane's 2K codes go out as 8-byte words.
+// (Round 4's form scanned the patterns and probed the value table per slot and
+// stored single bytes: 16.3 ms for a 27-point share.)
+__global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, const int32_t *__restrict__ width,
+                                 int32_t *__restrict__ dpat, const int8_t *__restrict__ pmap,
+                                 const uint8_t *__restrict__ pok, const int64_t *__restrict__ cptr,
+                                 const uint8_t *__restrict__ code, uint8_t *__restrict__ pcode) {
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (u >= nunits) return;
   const int lane = threadIdx.x & 63;
   const int64_t s0 = 2 * u, s1 = s0 + 1;
-  const int32_t *__restrict__ so = doff + (int64_t)star * DIA_MAX;
-  // slot j of the dominant pattern -> slot of slice sl's own pattern, or -1
-  auto slot_of = [&](int64_t sl, int j) -> int {
-    const int32_t *__restrict__ po = doff + (int64_t)(dpat[sl] & DPAT_ID) * DIA_MAX;
-    for (int q = 0; q < -width[sl]; ++q)
-      if (po[q] == so[j]) return q;
-    return -1;
-  };
-  // every offset of the slice's pattern is one of the dominant pattern's
-  auto ok = [&](int64_t sl) {
-    if (width[sl] >= 0) return false;
-    const int32_t *__restrict__ po = doff + (int64_t)(dpat[sl] & DPAT_ID) * DIA_MAX;
-    for (int q = 0; q < -width[sl]; ++q) {
-      bool in = false;
-      for (int j = 0; j < k; ++j) in = in || po[q] == so[j];
-      if (!in) return false;
-    }
-    return true;
-  };
-  if (u * 128 + 127 >= m || !ok(s0) || !ok(s1)) return;   // wave-uniform
+  if (u * 128 + 127 >= m || width[s0] >= 0 || width[s1] >= 0) return;   // wave-uniform
+  const int p0 = dpat[s0] & DPAT_ID, p1 = dpat[s1] & DPAT_ID;
+  if (!pok[p0] || !pok[p1]) return;
+  const int64_t sl = lane < 32 ? s0 : s1;
+  const int8_t *__restrict__ mp = pmap + (int64_t)(lane < 32 ? p0 : p1) * DIA_MAX;
+  const uint8_t *__restrict__ cb = code + cptr[sl];
   const int pb = pair_bytes(k);
-  uint8_t *dst = pcode + (u * 64 + lane) * pb;
-  for (int h = 0; h < 2; ++h) {
-    const int64_t row = u * 128 + 2 * lane + h;
-    const int64_t sl = row >> 6;
-    const int li = (int)(row & 63);
-    const int kw = -width[sl];
-    const uint32_t mk = mask8 ? (uint32_t)mask8[row] : mask[row];
-    for (int j = 0; j < k; ++j) {
-      int c = VCODE_ABSENT;
-      const int q = slot_of(sl, j);
-      if (q >= 0 && ((mk >> q) & 1u)) {
-        const double v = sval[sell_slot(sptr[sl], q, kw, li, true)];
-        const int hh = vdict_find(tab, (unsigned long long)__double_as_longlong(v));
-        c = hh >= 0 ? slot_code[hh] : 0;
+  unsigned long long *dst = reinterpret_cast<unsigned long long *>(pcode + (u * 64 + lane) * pb);
+  for (int w = 0; w < pb / 8; ++w) {
+    unsigned long long word = 0;
+    for (int t = 0; t < 8; ++t) {
+      const int idx = 8 * w + t;
+      unsigned long long c = VCODE_ABSENT;
+      if (idx < 2 * k) {
+        const int h = idx >= k ? 1 : 0;
+        const int q = mp[idx - h * k];
+        const int li = (2 * lane + h) & 63;
+        if (q >= 0) c = cb[(int64_t)(q >> 3) * CODE_BATCH + 8 * li + (q & 7)];
       }
-      dst[h * k + j] = (uint8_t)c;
+      word |= c << (8 * t);
     }
+    dst[w] = word;
   }
-  for (int j = 2 * k; j < pb; ++j) dst[j] = (uint8_t)VCODE_ABSENT;
   if (lane == 0) dpat[s0] |= DPAT_PAIR;
 }
 
@@ -1563,10 +1621,36 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
   if (S.pair_shape) {
     S.nunits = ns / 2;
     S.pcode.alloc((size_t)std::max<int64_t>(S.nunits, 1) * 64 * pair_bytes(S.dia_k));
-    if (S.nunits)
-      pair_fill_kernel<<<(unsigned)cdiv(S.nunits, 4), 256, 0, st>>>(m, S.nunits, S.dia_k, S.pat_star, S.sptr.p,
-                                                                   S.width.p, S.dpat.p, S.doff.p, S.val.p, S.mask.p,
-                                                                   S.mask8.p, tab.p, sc.p, S.pcode.p);
+    if (S.nunits) {
+      // per pattern: where each dominant slot sits in it, and whether its
+      // offsets are all dominant ones (pair_fill_kernel)
+      const int64_t np = S.npat;
+      if ((int64_t)S.pat_len.size() != np) fail(MX_ERR_INTERNAL, "row pairs without shared offset patterns");
+      std::vector<int8_t> pm((size_t)np * DIA_MAX, -1);
+      std::vector<uint8_t> pk((size_t)np, 0);
+      const int32_t *so = S.pat_host.data() + (size_t)S.pat_star * DIA_MAX;
+      for (int64_t p = 0; p < np; ++p) {
+        const int32_t *po = S.pat_host.data() + (size_t)p * DIA_MAX;
+        const int len = S.pat_len[(size_t)p];
+        bool ok = true;
+        for (int q = 0; q < len; ++q) {
+          int at = -1;
+          for (int j = 0; j < S.dia_k; ++j)
+            if (so[j] == po[q]) at = j;
+          if (at < 0) ok = false;
+          else pm[(size_t)p * DIA_MAX + at] = (int8_t)q;
+        }
+        pk[(size_t)p] = ok ? 1 : 0;
+      }
+      DBuf<int8_t> pmd(pm.size());
+      DBuf<uint8_t> pkd(pk.size());
+      HIPCHECK(hipMemcpyAsync(pmd.p, pm.data(), pm.size(), hipMemcpyHostToDevice, st));
+      HIPCHECK(hipMemcpyAsync(pkd.p, pk.data(), pk.size(), hipMemcpyHostToDevice, st));
+      pair_fill_kernel<<<(unsigned)cdiv(S.nunits, 4), 256, 0, st>>>(m, S.nunits, S.dia_k, S.width.p, S.dpat.p, pmd.p,
+                                                                   pkd.p, S.cptr.p, S.code.p, S.pcode.p);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipStreamSynchronize(st));   // pmd / pkd are freed on return
+    }
     HIPCHECK(hipGetLastError());
     {
       DBuf<unsigned long long> cnt(1);
@@ -1636,8 +1720,8 @@ static void build_sell(Sell &S, int64_t m, int64_t ncols, const int64_t *ptr, co
   exclusive_scan_i64(S.sptr.p, S.sptr.p, ns, st, &S.slots);
   S.col.alloc((size_t)std::max<int64_t>(S.slots, 1));
   S.val.alloc((size_t)std::max<int64_t>(S.slots, 1));
-  sell_fill_kernel<true><<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p,
-                                                                S.doff.p, S.col.p, S.val.p, S.mask.p, S.mask8.p);
+  sell_fill_lds_kernel<true><<<(unsigned)ns, 64, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p, S.doff.p, S.col.p,
+                                                          S.val.p, S.mask.p, S.mask8.p);
   HIPCHECK(hipGetLastError());
   if (S.dia_slices) share_offset_patterns(S, wh, ncols, st);
   else S.dpat.alloc(1);
@@ -1844,9 +1928,13 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   A->optr.alloc((size_t)m + 1);
   HIPCHECK(hipMemsetAsync(A->dptr.p, 0, sizeof(int64_t) * (m + 1), st));
   HIPCHECK(hipMemsetAsync(A->optr.p, 0, sizeof(int64_t) * (m + 1), st));
+  // segment width for the split passes (canonical rows are no longer than the input's)
+  const int SW = Lh <= 8 ? 8 : Lh <= 16 ? 16 : Lh <= 32 ? 32 : 64;
   if (m) {
-    split_count_kernel<<<(unsigned)cdiv(m, 256), 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, A->cstart, A->cend,
-                                                                A->dptr.p, A->optr.p, bitmap.p);
+    const unsigned g = (unsigned)cdiv(m, 256 / SW);
+#define SPLITC(WW) split_count_seg_kernel<WW><<<g, 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p)
+    switch (SW) { case 8: SPLITC(8); break; case 16: SPLITC(16); break; case 32: SPLITC(32); break; default: SPLITC(64); }
+#undef SPLITC
     HIPCHECK(hipGetLastError());
   }
   exclusive_scan_i64(A->dptr.p, A->dptr.p, m + 1, st, &A->nnz_d);
@@ -1869,9 +1957,10 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   A->oval.alloc((size_t)std::max<int64_t>(A->nnz_o, 1));
   A->diag.alloc((size_t)std::max<int64_t>(m, 1));
   if (m) {
-    fill_split_kernel<<<(unsigned)cdiv(m, 256), 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, cval.p, A->cstart, A->cend,
-                                                               A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p,
-                                                               A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p);
+    const unsigned g = (unsigned)cdiv(m, 256 / SW);
+#define SPLITF(WW) fill_split_seg_kernel<WW><<<g, 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, cval.p, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
+    switch (SW) { case 8: SPLITF(8); break; case 16: SPLITF(16); break; case 32: SPLITF(32); break; default: SPLITF(64); }
+#undef SPLITF
     HIPCHECK(hipGetLastError());
   }
   A->garray_h.resize((size_t)A->nghost);
@@ -1918,52 +2007,62 @@ __device__ __forceinline__ double kappa_d(int64_t a, int64_t b, int64_t c) {
   return 1.0 + (double)t * 0.25;
 }
 
-__global__ void stencil_kernel(int kind, int64_t nx, int64_t ny, int64_t nz, int64_t row0, int64_t m,
-                               int S, int64_t *__restrict__ cols, double *__restrict__ vals) {
+// One thread per (row, slot), so a wave's stores are contiguous runs of the
+// fixed-stride arrays (a thread per row wrote 27 strided doubles: 13.9 ms for
+// a 27-point share, round 5).  Grid coordinates in 32-bit arithmetic when the
+// global row count allows (I32), 64-bit otherwise; the values and the order of
+// the diagonal's sum are the row kernel's.
+template <int KIND, bool I32>
+__global__ void stencil_kernel(int64_t nx, int64_t ny, int64_t nz, int64_t row0, int64_t m,
+                               int64_t *__restrict__ cols, double *__restrict__ vals) {
+  constexpr int S = KIND == 0 ? 5 : (KIND == 2 ? 27 : 7);
+  const int64_t total = m * S;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < m; li += stride) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t li = t / S;
+    const int q = (int)(t - li * S);
     const int64_t row = row0 + li;
-    const int64_t i = row % nx, j = (row / nx) % ny, k = (kind == 0) ? 0 : row / (nx * ny);
-    int64_t *cp = cols + li * S;
-    double *vp = vals + li * S;
-    int t = 0;
-    if (kind == 0) {
-      const int di[5] = {0, -1, 0, 1, 0}, dj[5] = {-1, 0, 0, 0, 1};
-      for (int q = 0; q < 5; ++q, ++t) {
-        const int64_t ii = i + di[q], jj = j + dj[q];
-        const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny;
-        cp[t] = in ? ii + nx * jj : -1;
-        vp[t] = (q == 2) ? 4.0 : -1.0;
-      }
-    } else if (kind == 1 || kind == 3) {
-      const int di[7] = {0, 0, -1, 0, 1, 0, 0}, dj[7] = {0, -1, 0, 0, 0, 1, 0}, dk[7] = {-1, 0, 0, 0, 0, 0, 1};
-      double diag = 6.0;
-      if (kind == 3)
-        diag = kappa_d(i - 1, j, k) + kappa_d(i, j, k) + kappa_d(i, j - 1, k) + kappa_d(i, j, k) +
-               kappa_d(i, j, k - 1) + kappa_d(i, j, k) + 0.5;
-      for (int q = 0; q < 7; ++q, ++t) {
-        const int64_t ii = i + di[q], jj = j + dj[q], kk = k + dk[q];
-        const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny && kk >= 0 && kk < nz;
-        cp[t] = in ? ii + nx * (jj + ny * kk) : -1;
-        double v;
-        if (q == 3) v = diag;
-        else if (kind == 1) v = -1.0;
-        else {
-          v = -kappa_d(i < ii ? i : ii, j < jj ? j : jj, k < kk ? k : kk);
-          if (q == 2) v = v - 0.5;
-        }
-        vp[t] = v;
-      }
+    int64_t i, j, k;
+    if (I32) {
+      const uint32_t r = (uint32_t)row, nx32 = (uint32_t)nx, ny32 = (uint32_t)ny;
+      const uint32_t rest = r / nx32;
+      i = r - rest * nx32;
+      j = KIND == 0 ? rest : rest % ny32;
+      k = KIND == 0 ? 0 : rest / ny32;
     } else {
-      for (int dk = -1; dk <= 1; ++dk)
-        for (int dj = -1; dj <= 1; ++dj)
-          for (int di = -1; di <= 1; ++di, ++t) {
-            const int64_t ii = i + di, jj = j + dj, kk = k + dk;
-            const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny && kk >= 0 && kk < nz;
-            cp[t] = in ? ii + nx * (jj + ny * kk) : -1;
-            vp[t] = (di == 0 && dj == 0 && dk == 0) ? 26.0 : -1.0;
-          }
+      i = row % nx;
+      j = (row / nx) % ny;
+      k = KIND == 0 ? 0 : row / (nx * ny);
     }
+    int di, dj, dk;
+    if (KIND == 0) {
+      di = q == 1 ? -1 : q == 3 ? 1 : 0;
+      dj = q == 0 ? -1 : q == 4 ? 1 : 0;
+      dk = 0;
+    } else if (KIND == 2) {
+      dk = q / 9 - 1;
+      dj = (q / 3) % 3 - 1;
+      di = q % 3 - 1;
+    } else {
+      di = q == 2 ? -1 : q == 4 ? 1 : 0;
+      dj = q == 1 ? -1 : q == 5 ? 1 : 0;
+      dk = q == 0 ? -1 : q == 6 ? 1 : 0;
+    }
+    const int64_t ii = i + di, jj = j + dj, kk = k + dk;
+    const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny && kk >= 0 && kk < nz;
+    cols[t] = in ? ii + nx * (jj + ny * kk) : -1;
+    double v;
+    if (KIND == 0) v = q == 2 ? 4.0 : -1.0;
+    else if (KIND == 1) v = q == 3 ? 6.0 : -1.0;
+    else if (KIND == 2) v = q == 13 ? 26.0 : -1.0;
+    else if (q == 3)
+      v = kappa_d(i - 1, j, k) + kappa_d(i, j, k) + kappa_d(i, j - 1, k) + kappa_d(i, j, k) +
+          kappa_d(i, j, k - 1) + kappa_d(i, j, k) + 0.5;
+    else {
+      v = -kappa_d(i < ii ? i : ii, j < jj ? j : jj, k < kk ? k : kk);
+      if (q == 2) v = v - 0.5;
+    }
+    vals[t] = v;
   }
 }
 
@@ -1981,7 +2080,12 @@ void stencil_coo(Comm *c, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t 
   stride_rowptr_kernel<<<grid_for(m + 1, 256, 8192), 256, 0, c->stream>>>(m, S, rowptr.p);
   HIPCHECK(hipGetLastError());
   if (m) {
-    stencil_kernel<<<grid_for(m, 256, 8192), 256, 0, c->stream>>>(kind, nx, ny, nz, row0, m, S, cols.p, vals.p);
+    const bool i32 = (kind == 0 ? nx * ny : nx * ny * nz) < ((int64_t)1 << 31);
+    const unsigned g = grid_for(m * S, 256, 65536);
+#define STK(K) if (i32) stencil_kernel<K, true><<<g, 256, 0, c->stream>>>(nx, ny, nz, row0, m, cols.p, vals.p); \
+               else stencil_kernel<K, false><<<g, 256, 0, c->stream>>>(nx, ny, nz, row0, m, cols.p, vals.p)
+    switch (kind) { case 0: STK(0); break; case 1: STK(1); break; case 2: STK(2); break; default: STK(3); }
+#undef STK
     HIPCHECK(hipGetLastError());
   }
 }

@@ -170,6 +170,8 @@ struct Sell {
   // row-pair copy of the codes (mx_assembly.hip, pair_fill_kernel)
   int32_t pat_star = -1;              // the dominant pattern of width dia_k
   std::vector<int32_t> pat_star_off;
+  std::vector<int32_t> pat_len;       // [npat] offsets per shared pattern (host copy; empty: per-slice lists)
+  std::vector<int32_t> pat_host;      // [npat * DIA_MAX] the shared patterns (host copy)
   int pair_shape = 0;                 // 0, 5, 7, 27
   int64_t nunits = 0;
   DBuf<uint8_t> pcode;    // unit code blocks (64 * pair_bytes per unit), or the distinct ones
