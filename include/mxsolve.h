@@ -62,10 +62,13 @@ typedef struct {
   double haptol;       /* GMRES happy breakdown, 1e-30                                */
   double breakdowntol; /* GMRES restart consistency check, 0.1                        */
   int poll_every;      /* host polls the device convergence flag every k its (0: 16) */
-  int profile;         /* bit 0: time every SpMV launch with HIP events; bit 1: every
-                          CG mode-5 residual-update launch; bit 2: every CG direction-
-                          update launch with batched x steps (cg_pb_kernel; one rank:
-                          events attached to the kernel's dispatch)                  */
+  int profile;         /* bit 0: time every SpMV launch with HIP events (CG mode 5:
+                          the plain p.Ap passes; GMRES: the MatMult); bit 1: every CG
+                          mode-5 residual-update launch / GMRES MDot; bit 2: every CG
+                          direction-update launch with batched x steps (cg_pb_kernel)
+                          / GMRES MAXPY + norm; bit 3: every CG fused direction +
+                          p.Ap pass (one rank: events attached to the kernel's
+                          dispatch)                                                  */
 } mx_ksp_params;
 
 typedef struct {
@@ -82,6 +85,12 @@ typedef struct {
   int cg_xbatch;       /* CG: deferred x steps applied every this many iterations    */
   double pb_ms;        /* sum of profiled direction-update launch times (profile bit 2) */
   int pb_count;        /* direction-update launches profiled                        */
+  double pbw_ms;       /* sum of profiled fused direction + p.Ap pass times (bit 3)  */
+  int pbw_count;       /* fused direction + p.Ap launches profiled                  */
+  double mdot_ms;      /* GMRES: sum of profiled MDot launch times (profile bit 1)   */
+  int mdot_count;
+  double maxpy_ms;     /* GMRES: sum of profiled MAXPY + norm launch times (bit 2)   */
+  int maxpy_count;
 } mx_ksp_result;
 
 typedef struct {
@@ -282,10 +291,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         vector is aligned (0/1, default 0: one row per thread per step)
  * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
  * key 15: grid cap of the halo-boundary SpMV launch (0 = default 2048)
- * key 16: GMRES VecMDot vectors per pass over w with key 50 = 0 (4 or 8;
- *         default 8: measured 1.4% faster per GMRES(30) step than 32 at 256^3;
- *         the 16/32-wide kernels were dropped in round 4 -- they spilled 30 / 142
- *         SGPRs)
  * key 18: library buffers >= 64 MiB physically contiguous when the driver can
  *         provide them (hipDeviceMallocContiguous, else hipMalloc; 0/1, default 1)
  * key 19: one-byte row masks for aligned-offset slices when every slice has
@@ -296,7 +301,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 23: value codes -- one byte per slot into a table of <= 255 distinct
  *         values -- for the diagonal block (read at assembly and at launch;
  *         0/1, default 1)
- * key 24: retired (round 1's SpMV unroll switch; no effect)
  * key 25: non-temporal y stores in the SpMV (0/1, default 0)
  * key 26: resident workgroups per CU for the single-row SpMV grid (default 6)
  * key 27: row-pair SpMV layout for 5/7/27-point patterns (read at assembly and
@@ -309,8 +313,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         the rarer x pass saves)
  * key 30: the row-pair block dictionary (read at assembly: 1, default, when
  *         repeats pay for the indirection; 2 always; 0 one block per unit)
- * key 31: the general SELL sweep runs its items from the last down (0/1,
- *         default 0; 1 also turns the lean row-pair kernels off)
  * key 32: non-temporal loads in the CG vector passes: bit 0 the direction
  *         update's r / p_{i-1} reads, bit 1 the update pass's w / r reads
  *         (default 3)
@@ -323,7 +325,7 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         whose fused iteration-0 norms it must match bit for bit)
  * key 35: row-pair SpMV reads uniform-slot dictionary blocks as slot values +
  *         lane masks when the matrix has them (0/1, default 1)
- * key 36: grid of the GMRES MDot pass (0 = default: 3 per CU for key 50 = 7, else 1024)
+ * key 36: grid of the GMRES MDot pass (0 = default: 3 workgroups per CU)
  * key 37: the Jacobi-fused row-pair MatMult (GMRES) takes dinv from a table
  *         indexed by the rows' diagonal code instead of reading the dinv
  *         vector (0/1, default 1; the same bits)
@@ -350,18 +352,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         27-point z-march zeroes empty runs and x-line edges where it loads
  *         them (no per-run branches, no selects; the same bits)
  * key 49: 27-point z-march planes per step (1, default, or 2)
- * key 50: GMRES MDot in one pass over w for <= 32 basis vectors (7, default:
- *         a workgroup holds 4096 rows of w in registers and walks the basis
- *         one vector at a time, the next vector's loads issued before the
- *         current one's sums, four lane partials reduced together -- -2 to
- *         -3% per GMRES(30) step against 2; 6: the same with 2048 rows; 2: 2048
- *         rows, four vectors' loads at once; 4 / 5: 2 with the next four's
- *         loads first (4096 / 1024 rows); 1: the four waves of a workgroup
- *         split the vectors; 0: groups of key 16)
- * key 51: GMRES MAXPY + norm pass in chunks (2 / 3: one vector at a time with
- *         the next in flight, 2048 / 4096 rows -- measured 3% slower; 1: 2048 rows per workgroup
- *         step, 16-byte pairs; 0, default: one row per thread -- measured
- *         0.5% faster per GMRES(30) step beside the chunk MDot)
  * key 54: GMRES basis stride padding in rows (multiple of 32; default 256:
  *         2 KB between the vectors' rows, -1.8% per GMRES(30) step at 256^3)
  * key 55: CG mode 5 (p.Ap pass + residual update recomputing A p) also for
@@ -386,21 +376,12 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         exact product: the same bits; 1, default; 0: multiply and add)
  * key 61: testing: a device stall of this many us before each GMRES restart
  *         read-back (default 0), so the no-progress deadline can be driven
- * key 62: CG mode 5's 27-point passes by separable box sums on a "box"
- *         operator (one off-diagonal value, one diagonal value; A p =
- *         (c - v) p + v box(p), reassociated: A p to rounding, not the
- *         MatMult's bits) -- 1 on, 0 (default: measured 1-2% slower per C5
- *         iteration than the slot-order passes, which are not VALU-bound)
- * key 63: workgroups per CU of the key-62 kernels (0: the 27-point defaults)
- * key 64: residual update planes per z-march step, 3 or 4 (0, default: key 42's)
+ * (keys 16, 24, 31, 50, 51, 62-64, 66, 67 -- variants measured and not kept --
+ *  were retired in round 5; setting them has no effect)
  * key 65: z-march grids that fill whole task rounds (1, default: the
  *         workgroups per CU, at most the configured, whose tasks per XCD are
  *         a whole number of rounds of its waves -- C5's share: 4 instead of 5
  *         for the residual update; 0: the configured counts)
- * key 66: residual update with the next step's r loaded one step ahead (0/1,
- *         default 0: -0.3% per C3 iteration, within noise)
- * key 67: the CG solve's first batch launched eagerly when its graph is
- *         cached (0, default: within noise; 1 on)
  * key 68: CG mode 5's 7-point residual update with two lines per wave (line
  *         y's +n operand is line y + 1's centre pair: 8 vector loads per two
  *         units instead of 10; the same row sums, the norm partials grouped

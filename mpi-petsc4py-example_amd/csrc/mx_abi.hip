@@ -511,20 +511,17 @@ int mx_debug_set(int key, int value) {
     case 13: old = g_knobs.cg_vec; g_knobs.cg_vec = value; break;
     case 14: old = g_knobs.cg_nts; g_knobs.cg_nts = value; break;
     case 15: old = g_knobs.bnd_grid; g_knobs.bnd_grid = value; break;
-    case 16: old = g_knobs.mdot_group; g_knobs.mdot_group = value; break;
     case 18: old = g_knobs.contig; g_knobs.contig = value; break;
     case 19: old = g_knobs.mask8; g_knobs.mask8 = value; break;
     case 21: old = g_knobs.cg_unroll; g_knobs.cg_unroll = value; break;
     case 22: old = g_knobs.cg_upd_grid; g_knobs.cg_upd_grid = std::min(value, 65536); break;
     case 23: old = g_knobs.vcodes; g_knobs.vcodes = value; break;
-    case 24: old = g_knobs.spmv_unroll; g_knobs.spmv_unroll = value; break;
     case 25: old = g_knobs.spmv_ynt; g_knobs.spmv_ynt = value; break;
     case 26: old = g_knobs.spmv_bpc; g_knobs.spmv_bpc = value; break;
     case 27: old = g_knobs.spmv_pairs; g_knobs.spmv_pairs = value; break;
     case 28: old = g_knobs.spmv_pair_bpc; g_knobs.spmv_pair_bpc = value; break;
     case 29: old = g_knobs.cg_xbatch; g_knobs.cg_xbatch = value; break;
     case 30: old = g_knobs.pdict; g_knobs.pdict = value; break;
-    case 31: old = g_knobs.spmv_rev; g_knobs.spmv_rev = value; break;
     case 32: old = g_knobs.cg_ntl; g_knobs.cg_ntl = value; break;
     case 33: old = g_knobs.comm_timeout_ms; if (value > 0) g_knobs.comm_timeout_ms = value; break;
     case 34: old = g_knobs.norm_grid; g_knobs.norm_grid = std::min(std::max(value, 0), 16384); break;
@@ -543,8 +540,6 @@ int mx_debug_set(int key, int value) {
     case 47: old = g_knobs.comm_wait_ms; g_knobs.comm_wait_ms = std::max(value, 0); break;
     case 48: old = g_knobs.pair_col27; g_knobs.pair_col27 = value; break;
     case 49: old = g_knobs.pair_zm27_units; g_knobs.pair_zm27_units = value == 2 ? 2 : 1; break;
-    case 50: old = g_knobs.mdot_split; g_knobs.mdot_split = value; break;
-    case 51: old = g_knobs.maxpy_pairs; g_knobs.maxpy_pairs = value; break;
     case 52: old = g_knobs.pair_zmc; g_knobs.pair_zmc = value; break;
     case 53: old = g_knobs.pair_unitv; g_knobs.pair_unitv = value; break;
     case 55: old = g_knobs.cg5_27; g_knobs.cg5_27 = value; break;
@@ -552,12 +547,7 @@ int mx_debug_set(int key, int value) {
     case 70: old = g_knobs.zm27_2line; g_knobs.zm27_2line = value; break;
     case 69: old = g_knobs.cg_pbw; g_knobs.cg_pbw = value; break;
     case 68: old = g_knobs.ru_2line; g_knobs.ru_2line = value; break;
-    case 67: old = g_knobs.cg_eager_first; g_knobs.cg_eager_first = value; break;
-    case 66: old = g_knobs.ru_rpf; g_knobs.ru_rpf = value; break;
     case 65: old = g_knobs.zm_balance; g_knobs.zm_balance = value; break;
-    case 64: old = g_knobs.ru_units; g_knobs.ru_units = value; break;
-    case 62: old = g_knobs.box27; g_knobs.box27 = value; break;
-    case 63: old = g_knobs.box27_bpc; g_knobs.box27_bpc = std::min(std::max(value, 0), 8); break;
     case 61: old = g_knobs.gm_stall_us; g_knobs.gm_stall_us = std::min(std::max(value, 0), 2000000); break;
     case 59: old = g_knobs.pw_sym27; g_knobs.pw_sym27 = value; break;
     case 57: old = g_knobs.pw_bpc; g_knobs.pw_bpc = std::min(std::max(value, 0), 8); break;

@@ -1487,7 +1487,6 @@ static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
   S.pair_2l27 = false;
   S.pair_4l27 = false;
   S.pair_sym27 = false;
-  S.pair_box27 = false;
   if (!S.puni27.p || !S.pair_clean27 || !S.pair_all || S.pat_star_off.size() < 27) return;
   const int64_t D = S.pat_star_off[22];                   // run 7's centre: +D
   if (D <= 0 || D % 128 != 0 || m % D != 0 || m > (int64_t(1) << 27)) return;
@@ -1546,25 +1545,6 @@ static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
     if (j != 13 && have[j] != have[26 - j]) sym = false;
     else if (j != 13 && have[j] && std::memcmp(&V[j], &V[26 - j], sizeof(double)) != 0) sym = false;
   S.pair_sym27 = sym;
-  // the box operator (Sell::pair_box27): one value over every block's present
-  // off-diagonal slots and one over their diagonals
-  S.pair_box27 = false;
-  bool box = true, hv = false, hc = false;
-  double bv = 0.0, bc = 0.0;
-  for (int64_t b = 0; b < nb && box; ++b)
-    for (int j = 0; j < 27 && box; ++j) {
-      if (!(blk[(size_t)b].pm[j] | blk[(size_t)b].pm[27 + j])) continue;
-      const double v = blk[(size_t)b].v[j];
-      double &ref = j == 13 ? bc : bv;
-      bool &have = j == 13 ? hc : hv;
-      if (!have) { ref = v; have = true; }
-      else if (std::memcmp(&ref, &v, sizeof(double)) != 0) box = false;
-    }
-  if (box && hv && hc && std::isfinite(bv) && std::isfinite(bc)) {
-    S.pair_box27 = true;
-    S.box_v = bv;
-    S.box_c = bc;
-  }
 }
 
 static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st) {

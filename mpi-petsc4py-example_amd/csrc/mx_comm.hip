@@ -36,7 +36,8 @@ namespace mx {
 
 Comm::~Comm() {}
 
-void Comm::wait_until(const std::function<bool()> &ready, hipStream_t s, const std::function<long long()> &) {
+void Comm::wait_until(const std::function<bool()> &ready, hipStream_t s, const std::function<long long()> &,
+                      long long) {
   hipStream_t q = s ? s : stream;
   for (int spins = 0; !ready(); ++spins) {
     if ((spins & 63) == 63) {
@@ -152,10 +153,16 @@ struct RcclComm : Comm {
   // asynchronous error does not hang the rank forever; 0 = no deadline).
   // GMRES's restart read-back observes progress (gm_step_kernel stores a step
   // count into the host word), so it runs under knob 33 like the CG poller.
-  template <class Q> void watch(Q query, const char *what, const std::function<long long()> &progress = {}) {
-    const int limit = progress ? g_knobs.comm_timeout_ms : g_knobs.comm_wait_ms;
+  // A progress wait is armed (knob 33) only once the count has moved off the
+  // caller's baseline -- the device has begun the waited-for work, so every
+  // rank has entered it; before that a rank whose peers enter the solve late
+  // (host work between solves) waits under knob 47 like any other wait.
+  template <class Q> void watch(Q query, const char *what, const std::function<long long()> &progress = {},
+                                long long baseline = 0) {
+    int limit = g_knobs.comm_wait_ms;
     auto t0 = std::chrono::steady_clock::now();
-    long long seen = progress ? progress() : 0;
+    long long seen = baseline;
+    bool armed = false;
     for (int spins = 0;; ++spins) {
       const hipError_t e = query();
       if (e == hipSuccess) return;
@@ -165,12 +172,16 @@ struct RcclComm : Comm {
         abort_comm();
         fail(MX_ERR_COMM, std::string(what) + ": RCCL asynchronous error: " + ncclGetErrorString(ar));
       }
-      if (limit > 0) {
-        const auto now = std::chrono::steady_clock::now();
-        if (progress) {
-          const long long p = progress();
-          if (p != seen) { seen = p; t0 = now; }
+      const auto now = std::chrono::steady_clock::now();
+      if (progress) {
+        const long long p = progress();
+        if (p != seen) {
+          seen = p;
+          t0 = now;
+          if (!armed) { armed = true; limit = g_knobs.comm_timeout_ms; }
         }
+      }
+      if (limit > 0) {
         if (now - t0 > std::chrono::milliseconds(limit)) {
           abort_comm();
           fail(MX_ERR_COMM, std::string(what) + ": no progress for " + std::to_string(limit) +
@@ -196,10 +207,10 @@ struct RcclComm : Comm {
     watch([&] { return hipEventQuery(ev); }, "event wait");
   }
   void wait_until(const std::function<bool()> &ready, hipStream_t s,
-                  const std::function<long long()> &progress) override {
+                  const std::function<long long()> &progress, long long baseline) override {
     if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     hipStream_t q = s ? s : stream;
-    watch([&] { return ready() ? hipSuccess : hipStreamQuery(q); }, "progress wait", progress);
+    watch([&] { return ready() ? hipSuccess : hipStreamQuery(q); }, "progress wait", progress, baseline);
   }
 };
 

@@ -84,9 +84,12 @@ struct Comm {
   // Host spins until ready() (a word the device writes into pinned host
   // memory) or until stream s has drained (then the caller re-reads the word);
   // a device error on s raises.  progress (optional): a count the device
-  // advances -- RCCL communicators re-arm their no-progress deadline on it.
+  // advances -- RCCL communicators re-arm their no-progress deadline on it,
+  // once it has moved off `baseline` (the count before the waited-for work
+  // was enqueued): until then a peer may simply not have arrived yet, and the
+  // plain wait deadline (knob 47) applies.
   virtual void wait_until(const std::function<bool()> &ready, hipStream_t s,
-                          const std::function<long long()> &progress = {});
+                          const std::function<long long()> &progress = {}, long long baseline = 0);
 };
 
 Comm *make_self_comm(int device);
@@ -209,12 +212,6 @@ struct Sell {
   // (with the box-boundary presence of the column words, a_ij == a_ji): CG
   // mode 5's p.Ap pass sums each row's forward half (mx_spmv_pair.hip pair_fwd27)
   bool pair_sym27 = false;
-  // the column-word 27-point layout is a "box" operator: every block's present
-  // off-diagonal slots hold one value box_v and its diagonal one value box_c,
-  // so A p = (box_c - box_v) p + box_v (box sum of p): CG mode 5's passes use
-  // separable sums (mx_spmv_pair.hip spmv_pair_zm27b_kernel, knob 62)
-  bool pair_box27 = false;
-  double box_v = 0.0, box_c = 0.0;
   // the column words pair up by lines (knob 70, mx_spmv_pair.hip
   // spmv_pair_zm27p2l_kernel): whole 128-row columns per line, an even number
   // of lines per plane, and each even line's column and the next line's column
@@ -261,15 +258,15 @@ struct VCodes { const uint8_t *code; const int64_t *cptr; const double *tab; int
 // runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
 struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
-                int bnd_grid = 0; int mdot_group = 8;
+                int bnd_grid = 0;
                 int contig = 1; int mask8 = 1; int cg_unroll = 2;
-                int cg_upd_grid = 0; int vcodes = 1; int spmv_unroll = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
-                int cg_xbatch = 0; int pdict = 1; int spmv_rev = 0; int cg_ntl = 3;
+                int cg_upd_grid = 0; int vcodes = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
+                int cg_xbatch = 0; int pdict = 1; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int mdot_split = 7; int maxpy_pairs = 0; int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int box27 = 0; int box27_bpc = 0; int ru_units = 0; int zm_balance = 1; int ru_rpf = 0; int cg_eager_first = 0; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; };
+                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

@@ -815,76 +815,6 @@ __global__ void __launch_bounds__(256) mdot_kernel(int64_t n, const double *__re
   block_sum_to_partials<NV>(acc, partials + (size_t)j0 * gridDim.x, gridDim.x);
 }
 
-// VecMDot in one pass over w for nv <= 4 * 8 basis vectors: the four waves of
-// a workgroup walk the same rows and split the vectors between them (wave g:
-// vectors [g q, g q + q), q = ceil(nv / 4) = NQ).  w is read from HBM once per
-// step -- the other three waves' reads of a line hit the XCD's L2 -- where
-// mdot_kernel's groups of 8 re-read it per group (ceil(nv / 8) passes), and
-// every load is a 16-byte pair per lane.  Each vector's partial is one wave's
-// sum (no block fold): partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
-template <int NQ>
-__global__ void __launch_bounds__(256) mdot_split_kernel(int64_t n, const double *__restrict__ w,
-                                                         const double *__restrict__ V, int64_t ldv, int nv,
-                                                         const double *__restrict__ vscale,
-                                                         double *__restrict__ partials,
-                                                         const int *__restrict__ stop_flag) {
-  if (*stop_flag) return;
-  const int lane = threadIdx.x & 63;
-  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int j0 = g * NQ, cnt = min(NQ, nv - j0);
-  if (cnt <= 0) return;   // wave-uniform: no vectors for this wave (nv < 4 NQ)
-  constexpr int U = NQ <= 3 ? 2 : 1;   // row pairs per lane per step: >= 6 loads in flight
-  double acc[NQ], sc[NQ];
-  const dbl2 *__restrict__ vk[NQ];
-#pragma unroll
-  for (int k = 0; k < NQ; ++k) {
-    const int j = j0 + (k < cnt ? k : cnt - 1);   // past cnt: the last vector again (cached lines, dropped)
-    acc[k] = 0.0;
-    sc[k] = vscale[j];
-    vk[k] = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
-  }
-  const dbl2 *__restrict__ w2 = reinterpret_cast<const dbl2 *>(w);
-  const int64_t n2 = n >> 1, stride = (int64_t)gridDim.x * 64;
-  int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  for (; i + (U - 1) * stride < n2; i += U * stride) {
-    dbl2 wi[U], v[U][NQ];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      wi[u] = w2[i + u * stride];
-#pragma unroll
-      for (int k = 0; k < NQ; ++k) v[u][k] = __builtin_nontemporal_load(vk[k] + i + u * stride);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < NQ; ++k) {
-        acc[k] += wi[u].x * (sc[k] * v[u][k].x);
-        acc[k] += wi[u].y * (sc[k] * v[u][k].y);
-      }
-  }
-  if constexpr (U > 1) {
-    if (i < n2) {
-      const dbl2 wi = w2[i];
-#pragma unroll
-      for (int k = 0; k < NQ; ++k) {
-        const dbl2 v = __builtin_nontemporal_load(vk[k] + i);
-        acc[k] += wi.x * (sc[k] * v.x);
-        acc[k] += wi.y * (sc[k] * v.y);
-      }
-    }
-  }
-  if ((n & 1) && blockIdx.x == 0 && lane == 0) {   // odd length: the last row
-    const double wl = w[n - 1];
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) acc[k] += wl * (sc[k] * V[(int64_t)(j0 + (k < cnt ? k : cnt - 1)) * ldv + n - 1]);
-  }
-#pragma unroll
-  for (int k = 0; k < NQ; ++k) {
-    const double s = wave_sum(acc[k]);
-    if (lane == 0 && k < cnt) partials[(size_t)(j0 + k) * gridDim.x + blockIdx.x] = s;
-  }
-}
-
 // Four lane-distributed partials a0..a3 summed over the wave together: the
 // xor-32 step exchanges two values, the xor-16 step one, then four plain
 // steps -- lanes 16 q .. 16 q + 15 end with value q = 2 (l >> 5 & 1) + (l >> 4 & 1)'s total
@@ -898,22 +828,23 @@ __device__ __forceinline__ double red4(double a0, double a1, double a2, double a
   return c;
 }
 
-// VecMDot in one pass over w, chunk form (knob 50 = 2, the default; nv <= 32):
-// a workgroup holds 2048 rows of w in registers (WP = 4 16-byte pairs per
-// thread) and walks the basis vectors four at a time, reading 16 KB of each
-// contiguously per step.  Each vector's chunk sum is reduced across the wave
-// at once and added to one lane's running total (one accumulator register
-// instead of nv).  On 2^24 rows this streams at 7.0-7.1 TB/s, the
-// plain read ceiling, where the split form (several vectors' 1 KB pieces
-// interleaved per wave step) makes 6.0-6.4 (tools/mdot_probe.hip chunk4r).
+// VecMDot in one pass over w, chunk form (nv <= 32): a workgroup holds 4096
+// rows of w in registers (WP = 8 16-byte pairs per thread) and walks the basis
+// vectors one at a time, reading a 32 KB piece of each contiguously (few DRAM
+// streams at once), the next vector's loads issued before the current one's
+// sums; the four lane partials of a group of four vectors are reduced
+// together (red4) and vector j's chunk total is added to one lane's running
+// total (one accumulator register instead of nv).  Measured in round 4
+// against four vectors in flight per wave (0.8316 -> 0.803 ms per GMRES(30)
+// step at 256^3) and round 3's groups of four (126 SGPR spills);
+// tools/mdot_probe.hip rates the walk at the plain read ceiling.
 // partials[j * gridDim.x + blockIdx.x] as mdot_kernel.
-template <int WP, int FORM = 0>
 __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
                                                          const double *__restrict__ vscale,
                                                          double *__restrict__ partials,
                                                          const int *__restrict__ stop_flag) {
-  constexpr int NVX = 32;
+  constexpr int NVX = 32, WP = 8;
   if (*stop_flag) return;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   double acc = 0.0;                                // lane j: vector j's running total
@@ -927,97 +858,35 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
       const int64_t i = c0 + k * 256 + threadIdx.x;
       wr[k] = (FULL || i < n2) ? w2[i] : dbl2{0.0, 0.0};
     }
-    // vectors four at a time: their 16 loads in flight together (clamped to
-    // the last vector, so branch-free), then the four lane partials reduced
-    // together by a transposed butterfly (red4: 7 fp64 shuffles instead of 4
-    // wave sums of 6); vector j's chunk total lands in lanes 16 (j & 3) ..
-    // 16 (j & 3) + 15 and is kept in lane 16 (j & 3) + (j >> 2).  Round 3's
-    // fully unrolled walk over 32 guarded vectors kept every vector's address
-    // and scale in SGPRs (126 spills); tools/mdot_probe.hip chunk4grp4.
-    auto group = [&](int j, dbl2 (&t)[4][WP], double (&sq)[4]) __attribute__((always_inline)) {
+    auto vload = [&](int j, dbl2 (&t)[WP]) __attribute__((always_inline)) {
+      const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int jq = min(j + q, nv - 1);
-        sq[q] = j + q < nv ? vscale[jq] : 0.0;
-        const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)jq * ldv);
-#pragma unroll
-        for (int k = 0; k < WP; ++k) {
-          const int64_t i = c0 + k * 256 + threadIdx.x;
-          t[q][k] = (FULL || i < n2) ? __builtin_nontemporal_load(vq + i) : dbl2{0.0, 0.0};
-        }
+      for (int k = 0; k < WP; ++k) {
+        const int64_t i = c0 + k * 256 + threadIdx.x;
+        t[k] = (FULL || i < n2) ? __builtin_nontemporal_load(vq + i) : dbl2{0.0, 0.0};
       }
     };
-    auto finish = [&](int j, const dbl2 (&t)[4][WP], const double (&sq)[4]) __attribute__((always_inline)) {
+    dbl2 ta[WP], tb[WP];
+    vload(0, ta);
+    for (int j = 0; j < nv; j += 4) {            // wave-uniform
       double a[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        dbl2 (&cur)[WP] = (q & 1) ? tb : ta;
+        dbl2 (&nxt)[WP] = (q & 1) ? ta : tb;
+        if (j + q + 1 < nv) vload(j + q + 1, nxt);
         a[q] = 0.0;
+        if (j + q < nv) {
+          const double sj = vscale[j + q];
 #pragma unroll
-        for (int k = 0; k < WP; ++k) {
-          a[q] += wr[k].x * (sq[q] * t[q][k].x);
-          a[q] += wr[k].y * (sq[q] * t[q][k].y);
+          for (int k = 0; k < WP; ++k) {
+            a[q] += wr[k].x * (sj * cur[k].x);
+            a[q] += wr[k].y * (sj * cur[k].y);
+          }
         }
       }
       const double r = red4(a[0], a[1], a[2], a[3], lane);
       if ((lane & 15) == (j >> 2)) acc += r;
-    };
-    if constexpr (FORM == 2) {
-      // knob 50 = 6: one vector at a time (the workgroup streams one 16 KB
-      // piece of one vector, as round 3's walk did: few DRAM streams at once),
-      // the next vector's loads issued before this one's sums; the four lane
-      // partials of a group reduced together (red4)
-      auto vload = [&](int j, dbl2 (&t)[WP]) __attribute__((always_inline)) {
-        const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
-#pragma unroll
-        for (int k = 0; k < WP; ++k) {
-          const int64_t i = c0 + k * 256 + threadIdx.x;
-          t[k] = (FULL || i < n2) ? __builtin_nontemporal_load(vq + i) : dbl2{0.0, 0.0};
-        }
-      };
-      dbl2 ta[WP], tb[WP];
-      vload(0, ta);
-      for (int j = 0; j < nv; j += 4) {            // wave-uniform
-        double a[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          dbl2 (&cur)[WP] = (q & 1) ? tb : ta;
-          dbl2 (&nxt)[WP] = (q & 1) ? ta : tb;
-          if (j + q + 1 < nv) vload(j + q + 1, nxt);
-          a[q] = 0.0;
-          if (j + q < nv) {
-            const double sj = vscale[j + q];
-#pragma unroll
-            for (int k = 0; k < WP; ++k) {
-              a[q] += wr[k].x * (sj * cur[k].x);
-              a[q] += wr[k].y * (sj * cur[k].y);
-            }
-          }
-        }
-        const double r = red4(a[0], a[1], a[2], a[3], lane);
-        if ((lane & 15) == (j >> 2)) acc += r;
-      }
-    } else if constexpr (FORM == 1) {
-      // knob 50 = 4: the next group's 16 loads issued before this group's sums
-      dbl2 t[4][WP], tn[4][WP];
-      double sq[4], sqn[4];
-      group(0, t, sq);
-      for (int j = 0; j < nv; j += 4) {            // wave-uniform
-        if (j + 4 < nv) group(j + 4, tn, sqn);
-        finish(j, t, sq);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          sq[q] = sqn[q];
-#pragma unroll
-          for (int k = 0; k < WP; ++k) t[q][k] = tn[q][k];
-        }
-      }
-    } else {
-      for (int j = 0; j < nv; j += 4) {            // wave-uniform
-        dbl2 t[4][WP];
-        double sq[4];
-        group(j, t, sq);
-        finish(j, t, sq);
-      }
     }
   };
   for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
@@ -1041,7 +910,6 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
 // workgroup (workgroup 0 commits), then VecMAXPY_Seq's grouping (first nv%4
 // vectors, then groups of four) and ||w||^2, folded in-launch (fold.cnt) or
 // as plain partials
-template <bool CHUNK>
 __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
                                                          KspState *__restrict__ s, const double *__restrict__ red_k,
@@ -1068,73 +936,9 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
     for (int j = threadIdx.x; j < nv; j += 256) hh[(size_t)(nv - 1) * ld + j] = 0.0 - a[j];
   const int rem = nv & 3;
   double v[1] = {0.0};
-  if (CHUNK) {
-    // chunk form (knob 51 = 1, the default): a workgroup updates 2048 rows per
-    // step, 4 16-byte pairs of w per thread, and reads each group of four
-    // basis vectors' 16 KB pieces contiguously -- 5.9-6.2 TB/s against
-    // 5.5-6.0 for one row per thread (tools/mdot_probe.hip).  Every row's
-    // expression is the row form's below (VecMAXPY_Seq's grouping), so the
-    // same bits.
-    constexpr int WP = 4;
-    const int64_t n2 = n >> 1, csz = 256 * WP, nfull = n2 / csz;
-    dbl2 *__restrict__ w2 = reinterpret_cast<dbl2 *>(w);
-    auto chunk = [&](int64_t c0, auto fullc) __attribute__((always_inline)) {
-      constexpr bool FULL = decltype(fullc)::value;
-      auto in = [&](int k) { return FULL || c0 + k * 256 + threadIdx.x < n2; };
-      auto ld = [&](int j, int k) -> dbl2 {
-        if (!in(k)) return dbl2{0.0, 0.0};
-        const dbl2 t = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv) + c0 +
-                                                  k * 256 + threadIdx.x);
-        return dbl2{sc[j] * t.x, sc[j] * t.y};
-      };
-      dbl2 u[WP];
-#pragma unroll
-      for (int k = 0; k < WP; ++k) u[k] = in(k) ? w2[c0 + k * 256 + threadIdx.x] : dbl2{0.0, 0.0};
-      int j = 0;
-      if (rem) {                                   // the first nv % 4 vectors
-        dbl2 t[3][WP];
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-#pragma unroll
-          for (int k = 0; k < WP; ++k) t[q][k] = q < rem ? ld(q, k) : dbl2{0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < WP; ++k) {
-          if (rem == 1) {
-            u[k] = dbl2{a[0] * t[0][k].x + u[k].x, a[0] * t[0][k].y + u[k].y};
-          } else if (rem == 2) {
-            u[k] = u[k] + dbl2{a[0] * t[0][k].x + a[1] * t[1][k].x, a[0] * t[0][k].y + a[1] * t[1][k].y};
-          } else {
-            u[k] = u[k] + dbl2{(a[0] * t[0][k].x + a[1] * t[1][k].x) + a[2] * t[2][k].x,
-                               (a[0] * t[0][k].y + a[1] * t[1][k].y) + a[2] * t[2][k].y};
-          }
-        }
-        j = rem;
-      }
-      for (; j < nv; j += 4) {                     // groups of four
-        dbl2 t[4][WP];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int k = 0; k < WP; ++k) t[q][k] = ld(j + q, k);
-#pragma unroll
-        for (int k = 0; k < WP; ++k)
-          u[k] = u[k] + dbl2{((a[j] * t[0][k].x + a[j + 1] * t[1][k].x) + a[j + 2] * t[2][k].x) + a[j + 3] * t[3][k].x,
-                             ((a[j] * t[0][k].y + a[j + 1] * t[1][k].y) + a[j + 2] * t[2][k].y) + a[j + 3] * t[3][k].y};
-      }
-#pragma unroll
-      for (int k = 0; k < WP; ++k) {
-        if (!in(k)) continue;
-        w2[c0 + k * 256 + threadIdx.x] = u[k];
-        v[0] += u[k].x * u[k].x;
-        v[0] += u[k].y * u[k].y;
-      }
-    };
-    for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
-    if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
-  }
   {
-    const int64_t i0 = CHUNK ? (n & ~(int64_t)1) : 0, stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = i0 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
       double u = w[i];
       int j = 0;
       auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
@@ -1146,98 +950,6 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
       w[i] = u;
       v[0] += u * u;
     }
-  }
-  block_partials<1>(v, partials, gridDim.x, fold);
-}
-
-// The MAXPY + norm pass one vector at a time (knob 51 = 2 / 3: WP = 4 / 8
-// pairs per thread): a workgroup holds 512 WP rows of w in registers and
-// walks the basis in order, loading the next vector's piece before adding the
-// current one (few DRAM streams at once, the next one in flight: the MDot's
-// mdot_chunk_kernel<WP, 2> form).  VecMAXPY_Seq's grouping is kept exactly:
-// a group's products are summed in order, g = a_j0 v_j0, g = g + a_j v_j,
-// then u = u + g at the group's end (the first nv % 4 vectors, then fours),
-// fl(s_j v) applied on read -- every row's bits are maxpy_norm_kernel's.
-template <int WP>
-__global__ void __launch_bounds__(256) maxpy_seq_kernel(int64_t n, double *__restrict__ w,
-                                                        const double *__restrict__ V, int64_t ldv, int nv,
-                                                        KspState *__restrict__ s, const double *__restrict__ red_k,
-                                                        const double *__restrict__ vscale,
-                                                        double *__restrict__ hh, int ld,
-                                                        double *__restrict__ partials, const Fold fold) {
-  if (s->inner_stop) return;
-  __shared__ double a[MAX_RESTART + 1], sc[MAX_RESTART + 1];
-  __shared__ int bad;
-  if (threadIdx.x == 0) bad = 0;
-  __syncthreads();
-  for (int j = threadIdx.x; j < nv; j += 256) {
-    const double h = red_k[j];
-    if (not_finite(h)) bad = 1;
-    a[j] = -h;                                   // lhh[j] = -h_j
-    sc[j] = vscale[j];
-  }
-  __syncthreads();
-  if (bad) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) stop(s, R_DIVERGED_NANORINF);
-    return;
-  }
-  if (blockIdx.x == 0)
-    for (int j = threadIdx.x; j < nv; j += 256) hh[(size_t)(nv - 1) * ld + j] = 0.0 - a[j];
-  const int rem = nv & 3;
-  double v[1] = {0.0};
-  const int64_t n2 = n >> 1, csz = 256 * WP, nfull = n2 / csz;
-  dbl2 *__restrict__ w2 = reinterpret_cast<dbl2 *>(w);
-  auto chunk = [&](int64_t c0, auto fullc) __attribute__((always_inline)) {
-    constexpr bool FULL = decltype(fullc)::value;
-    auto in = [&](int k) { return FULL || c0 + k * 256 + threadIdx.x < n2; };
-    auto vload = [&](int j, dbl2 (&t)[WP]) __attribute__((always_inline)) {
-      const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V + (int64_t)j * ldv);
-#pragma unroll
-      for (int k = 0; k < WP; ++k)
-        t[k] = in(k) ? __builtin_nontemporal_load(vq + c0 + k * 256 + threadIdx.x) : dbl2{0.0, 0.0};
-    };
-    dbl2 u[WP], g[WP], ta[WP], tb[WP];
-#pragma unroll
-    for (int k = 0; k < WP; ++k) u[k] = in(k) ? w2[c0 + k * 256 + threadIdx.x] : dbl2{0.0, 0.0};
-    vload(0, ta);
-    auto step = [&](int j, dbl2 (&cur)[WP], dbl2 (&nxt)[WP]) __attribute__((always_inline)) {
-      if (j + 1 < nv) vload(j + 1, nxt);         // wave-uniform
-      const bool first = j == 0 || (j >= rem && (j - rem) % 4 == 0);
-      const bool last = (j < rem) ? j == rem - 1 : (j - rem) % 4 == 3;
-      const double aj = a[j], sj = sc[j];
-#pragma unroll
-      for (int k = 0; k < WP; ++k) {
-        const dbl2 p = dbl2{aj * (sj * cur[k].x), aj * (sj * cur[k].y)};
-        g[k] = first ? p : dbl2{g[k].x + p.x, g[k].y + p.y};
-        if (last) u[k] = dbl2{u[k].x + g[k].x, u[k].y + g[k].y};
-      }
-    };
-    for (int j = 0; j < nv; j += 2) {
-      step(j, ta, tb);
-      if (j + 1 < nv) step(j + 1, tb, ta);
-    }
-#pragma unroll
-    for (int k = 0; k < WP; ++k) {
-      if (!in(k)) continue;
-      w2[c0 + k * 256 + threadIdx.x] = u[k];
-      v[0] += u[k].x * u[k].x;
-      v[0] += u[k].y * u[k].y;
-    }
-  };
-  for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
-  if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // odd length: the last row (row form)
-    const int64_t i = n - 1;
-    double uu = w[i];
-    int j = 0;
-    auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
-    if (rem == 1) { uu = a[0] * vj(0) + uu; j = 1; }
-    else if (rem == 2) { uu = uu + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
-    else if (rem == 3) { uu = uu + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
-    for (; j < nv; j += 4)
-      uu = uu + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
-    w[i] = uu;
-    v[0] += uu * uu;
   }
   block_partials<1>(v, partials, gridDim.x, fold);
 }
@@ -1438,7 +1150,7 @@ struct Poller {
     prev_end = end;
     if (++pending < 2) return false;
     c->wait_until([&] { return word(HW_DONE) != 0 || word(HW_PROGRESS) >= target; }, st,
-                  [&] { return (long long)word(HW_PROGRESS); });
+                  [&] { return (long long)word(HW_PROGRESS); }, 0);   // the words are zeroed per solve
     return word(HW_DONE) != 0;
   }
 };
@@ -1535,7 +1247,9 @@ void Mat::release_ksp() {
 // Consecutive vectors are skewed by g_knobs.ws_skew doubles so that equal
 // indices of different vectors do not sit at the same offset modulo the
 // large powers of two the HBM channel interleave repeats on.
-static size_t carve_step(size_t n) { return (n + 31) / 32 * 32 + (size_t)std::max(g_knobs.ws_skew, 0); }
+// The skew is rounded up to an even count: the direction buffers are read and
+// written as 16-byte pairs (cg_pb_kernel's batch carve, spmv_pair_pbw_kernel).
+static size_t carve_step(size_t n) { return (n + 31) / 32 * 32 + ((size_t)std::max(g_knobs.ws_skew, 0) + 1) / 2 * 2; }
 struct Carve {
   double *base;
   size_t off = 0;
@@ -1699,6 +1413,8 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   utimer.ext = c->size == 1;
   SpmvTimer ptimer((p.profile & 4) != 0, st, std::min(p.max_it, 4096));   // the batched direction update
   ptimer.ext = c->size == 1;
+  SpmvTimer wtimer((p.profile & 8) != 0, st, std::min(p.max_it, 4096));   // the fused direction + p.Ap pass
+  wtimer.ext = c->size == 1;
 
   // r = b - A x  (or b)
   if (p.guess_nonzero) {
@@ -1790,10 +1506,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       // host's it is the device's i) fuse the direction update into the PW pass
       const bool fuse_pw = pbw && it % xb != 0;
       if (fuse_pw) {
-        timer.begin();
+        wtimer.begin();
         nb_spmv = pair_cg5_pbw_launch(A, s, r.p, r0, pbs.b, xb, hist_d, dinv.mode, dinv.c, part.p,
                                       fdot_p ? *fdot_p : Fold{}, st);
-        timer.end();
+        wtimer.end();
         if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG without its direction + p.Ap pass");
       } else if (xb > 1) {
         ptimer.begin();
@@ -1890,7 +1606,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
     // is cached -- the first replayed node started ~20 us after the launch
     // (the GPU idle after the state-init kernel) where eager launches keep
     // the queue ahead of these long kernels from the first one
-    if (use_graph && p.max_it - i >= poll && !(g_knobs.cg_eager_first && i == 0)) {
+    if (use_graph && p.max_it - i >= poll) {
       HIPCHECK(hipGraphLaunch(A->cg_graph, st));
       i += poll;
     } else {
@@ -1922,6 +1638,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   timer.collect(res.spmv_ms, res.spmv_count);
   utimer.collect(res.upd_ms, res.upd_count);
   ptimer.collect(res.pb_ms, res.pb_count);
+  wtimer.collect(res.pbw_ms, res.pbw_count);
   res.cg_mode = fmode;
   res.cg_xbatch = xb;
   if (hist_host)
@@ -1929,15 +1646,12 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
 }
 
 // Grid of every MDot launch of a solve (one partial row stride for the
-// finish): knob 36, default RED_BLOCKS.  mdot_kernel<32> holds 139 VGPRs (3
-// waves per SIMD, 768 resident workgroups), yet its resident grid measured
-// 1.1% slower per GMRES(30) step than 1024 and 512 0.8% (tools/gmres_ab.py)
-// (knob 50 = 7, the default chunk form, holds 153 VGPRs: three workgroups per
-// CU are resident, so its grid is one generation of them -- 768 on 256 CUs --
-// instead of 1024 in two uneven generations)
+// finish): knob 36, default one resident generation of the chunk kernel (153
+// VGPRs: three workgroups per CU -- 768 on 256 CUs -- instead of 1024 in two
+// uneven generations)
 static int mdot_grid() {
   if (g_knobs.mdot_grid > 0) return g_knobs.mdot_grid;
-  return g_knobs.mdot_split == 7 ? std::min(RED_BLOCKS, 3 * device_cu_count()) : RED_BLOCKS;
+  return std::min(RED_BLOCKS, 3 * device_cu_count());
 }
 
 template <int NV>
@@ -1946,31 +1660,19 @@ static void launch_mdot(hipStream_t st, int64_t n, const double *w, const double
   mdot_kernel<NV><<<grid, 256, 0, st>>>(n, w, V, ldv, j0, k, vscale, partials, stop_flag);
 }
 
-// partials rows [j0, j0 + NV) are written (rows >= nv with zeros): the
-// buffer holds max_k + 2 rows rounded up to 32; groups are gw wide (knob 16)
+// VecMDot of nv vectors: one pass over w (chunk form) up to 32 vectors (every
+// GMRES(30) step), groups of 8 vectors per pass beyond (restart > 31).
+// Partials rows [j0, j0 + NV) are written (rows >= nv with zeros): the
+// buffer holds max_k + 2 rows rounded up to 32
 static void mdot(hipStream_t st, int64_t n, const double *w, const double *V, int64_t ldv, int nv,
                  const double *vscale, double *partials, const int *stop_flag, int grid) {
-  if ((g_knobs.mdot_split == 2 || (g_knobs.mdot_split >= 4 && g_knobs.mdot_split <= 7)) && nv <= 32) {   // one pass over w, chunk form (knob 50)
-    if (g_knobs.mdot_split == 4) mdot_chunk_kernel<4, 1><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
-    else if (g_knobs.mdot_split == 5) mdot_chunk_kernel<2, 1><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
-    else if (g_knobs.mdot_split == 6) mdot_chunk_kernel<4, 2><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
-    else if (g_knobs.mdot_split == 7) mdot_chunk_kernel<8, 2><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
-    else mdot_chunk_kernel<4><<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
+  if (nv <= 32) {
+    launch_timed(&mdot_chunk_kernel, grid, st, n, w, V, ldv, nv, vscale, partials, stop_flag);
     HIPCHECK(hipGetLastError());
     return;
   }
-  if (g_knobs.mdot_split == 1 && nv <= 32) {   // one pass over w, split form (knob 50)
-    using F = void (*)(int64_t, const double *, const double *, int64_t, int, const double *, double *, const int *);
-    static constexpr F tab[8] = {&mdot_split_kernel<1>, &mdot_split_kernel<2>, &mdot_split_kernel<3>,
-                                 &mdot_split_kernel<4>, &mdot_split_kernel<5>, &mdot_split_kernel<6>,
-                                 &mdot_split_kernel<7>, &mdot_split_kernel<8>};
-    tab[(nv + 3) / 4 - 1]<<<grid, 256, 0, st>>>(n, w, V, ldv, nv, vscale, partials, stop_flag);
-    HIPCHECK(hipGetLastError());
-    return;
-  }
-  const int gw = g_knobs.mdot_group == 4 ? 4 : 8;
-  for (int j0 = 0; j0 < nv; j0 += gw) {
-    const int k = std::min(gw, nv - j0);
+  for (int j0 = 0; j0 < nv; j0 += 8) {
+    const int k = std::min(8, nv - j0);
     if (k <= 2) launch_mdot<2>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
     else if (k <= 4) launch_mdot<4>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
     else launch_mdot<8>(st, n, w, V, ldv, j0, k, vscale, partials, stop_flag, grid);
@@ -2022,8 +1724,12 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   const bool fused = c->size == 1;
   double *hist_d = hist_host ? hist.p : nullptr;
   Events ev(A);
-  SpmvTimer timer(p.profile != 0, st, std::min(p.max_it, 4096));
+  SpmvTimer timer((p.profile & 1) != 0, st, std::min(p.max_it, 4096));
   timer.ext = c->size == 1;
+  SpmvTimer dtimer((p.profile & 2) != 0, st, std::min(p.max_it, 4096));   // MDot
+  dtimer.ext = c->size == 1;
+  SpmvTimer xtimer((p.profile & 4) != 0, st, std::min(p.max_it, 4096));   // MAXPY + norm
+  xtimer.ext = c->size == 1;
   HIPCHECK(hipEventRecord(ev.a, st));
   const unsigned egrid = grid_for(n, 256, 8192);
   if (!p.guess_nonzero) vec_set(st, n, 0.0, x);
@@ -2056,20 +1762,23 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
     gm_start_kernel<<<1, 256, 0, st>>>(s, part.p, RED_BLOCKS, fused, grs.p, hist_d, first ? snorm : 0.0, vsc.p);
     HIPCHECK(hipGetLastError());
     first = 0;
+    const long long cycle_base = launched;   // the progress word before this cycle's steps
     for (int k = 0; k < max_k; ++k) {
       double *vk = V.p + (int64_t)k * ldv, *vk1 = V.p + (int64_t)(k + 1) * ldv;
       timer.begin();
       matmult_overlap(A, vk, vk1, dinv.mode ? SPMV_JACOBI_S : SPMV_PLAIN_S, dinv, nullptr, istop, nullptr,
                       nullptr, vsc.p + k);
       timer.end();
+      dtimer.begin();
       mdot(st, n, vk1, V.p, ldv, k + 1, vsc.p, part.p, istop, mgrid);
+      dtimer.end();
       finish_many_kernel<<<k + 1, 256, 0, st>>>(part.p, mgrid, red.p, istop);
       c->allreduce_sum(red.p, k + 1);
       // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
-      if (g_knobs.maxpy_pairs == 2 || g_knobs.maxpy_pairs == 3)   // one vector at a time (knob 51)
-        (g_knobs.maxpy_pairs == 3 ? &maxpy_seq_kernel<8> : &maxpy_seq_kernel<4>)<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
-      else
-        (g_knobs.maxpy_pairs ? &maxpy_norm_kernel<true> : &maxpy_norm_kernel<false>)<<<RED_BLOCKS, 256, 0, st>>>(n, vk1, V.p, ldv, k + 1, s, red.p, vsc.p, hh.p, ld, part.p, fnorm);
+      xtimer.begin();
+      launch_timed(&maxpy_norm_kernel, RED_BLOCKS, st, n, vk1, (const double *)V.p, ldv, k + 1, s,
+                   (const double *)red.p, (const double *)vsc.p, hh.p, ld, part.p, fnorm);
+      xtimer.end();
       c->allreduce_sum(sred, 1);
       ++launched;
       gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p,
@@ -2083,7 +1792,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
     if (g_knobs.gm_stall_us > 0) debug_stall(st, g_knobs.gm_stall_us);   // knob 61: the deadline tests
     // the cycle's state read-back: a wait that observes the step count
     HIPCHECK(hipMemcpyAsync(A->state_pinned, s, sizeof(KspState), hipMemcpyDeviceToHost, st));
-    c->wait_until([] { return false; }, st, [&] { return (long long)poller.word(HW_PROGRESS); });
+    c->wait_until([] { return false; }, st, [&] { return (long long)poller.word(HW_PROGRESS); }, cycle_base);
     std::memcpy(&hs, A->state_pinned, sizeof(KspState));
     if (hs.top.done) break;
   }
@@ -2097,6 +1806,8 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   res.solve_ms = ms;
   res.launched_its = launched;
   timer.collect(res.spmv_ms, res.spmv_count);
+  dtimer.collect(res.mdot_ms, res.mdot_count);
+  xtimer.collect(res.maxpy_ms, res.maxpy_count);
   if (hist_host) HIPCHECK(hipMemcpy(hist_host, hist.p, sizeof(double) * ((size_t)hs.its + 1), hipMemcpyDeviceToHost));
 }
 

@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     double *__restrict__ partials, const int *__restrict__ done, const CgFuse cg, const Fold fold,
     const double *__restrict__ xscale, const uint8_t *__restrict__ vcode, const int64_t *__restrict__ vcptr,
     const double *__restrict__ vtab_g, int ntab, int ynt, const uint8_t *__restrict__ pcode, int pat_star,
-    const int32_t *__restrict__ pblk, int pdict, int rev, const PairUni *__restrict__ puni,
+    const int32_t *__restrict__ pblk, int pdict, const PairUni *__restrict__ puni,
     const double *__restrict__ dtab_g) {
   static_assert(PS == 0 || VC, "row pairs: coded values");
   static_assert(!UNI || PS == 5 || PS == 7, "uniform-slot blocks: 5/7-point row pairs");
@@ -510,10 +510,7 @@ __global__ void __launch_bounds__(256) spmv_sell_kernel(
     }
     finish(s, sum, o, xc, hc);
   };
-  // rev: the sweep runs from the last item down (each XCD's range stays
-  // contiguous), so the rows the previous kernel wrote last -- still in the
-  // memory-side cache -- are read first
-  auto item = [&](int i) -> int { return rev ? (int)(nitems - 1) - i : i; };
+  auto item = [&](int i) -> int { return i; };
   if constexpr (PS == 0) {
     for (int s = s0; s < send; s += sstep) one_slice(item(s));
   } else {
@@ -874,7 +871,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   A->m, A->n, A->sd.nslices, A->sd.sptr.p, A->sd.width.p, A->sd.col.p, A->sd.val.p, A->sd.doff.p, A->sd.dpat.p, \
       A->sd.mask.p, A->sd.mask8.p, A->so.sptr.p, A->so.width.p, A->so.col.p, A->so.val.p, x, lvec, y, jac, \
       partials, done_flag, cg, fold, xscale, vc.code, vc.cptr, vc.tab, vc.ntab, g_knobs.spmv_ynt, \
-      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, pair_flags(A), g_knobs.spmv_rev, A->sd.puni.p, dtab
+      A->sd.pcode.p, A->sd.pat_star, A->sd.pblk.p, pair_flags(A), A->sd.puni.p, dtab
   using KFn = decltype(&spmv_sell_kernel<SPMV_PLAIN, true, 0, false, 0, false>);
   KFn kf = nullptr;
 #define SPMV_KDU(MODE, NT, SP, JM, VC, K) kf = &spmv_sell_kernel<MODE, NT, K, SP, JM, VC>

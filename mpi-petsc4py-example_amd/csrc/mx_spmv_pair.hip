@@ -246,11 +246,7 @@ struct PairRuArgs {
   int *hw;                     // the host's pinned words (Poller)
 };
 
-// RPF (knob 66, residual update only): the next step's r pairs are loaded
-// one step ahead, so every wave keeps its own HBM stream (r is read from
-// memory: the direction update read it non-temporally) in flight while it
-// sums the current planes
-template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0, bool SYM = false, bool RPF = false>
+template <int MODE, int PS, bool SPLIT, bool CLEAN, int ZU, int JM = 0, bool SYM = false>
 __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a, const double *__restrict__ x,
                                                            double *__restrict__ y, const int32_t *__restrict__ pblk,
                                                            const PairUni *__restrict__ puni, const PairRuArgs ru) {
@@ -302,20 +298,9 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
     const int cb = col * 128 + 2 * lane;       // the lane's rows within a plane
     dbl2 zm = bload2(xr, z0 * D + cb - D), c = bload2(xr, z0 * D + cb);
     uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
-    constexpr bool PF = RPF && RU;
-    dbl2 rn[ZU];                                // PF: the next full step's r, loaded ahead
-    bool have = false;
-    if constexpr (PF) {
-      if (z0 + ZU <= z1) {
-#pragma unroll
-        for (int q = 0; q < ZU; ++q) rn[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + (z0 + q) * D + cb));
-        have = true;
-      }
-    }
     // NQ units (planes z .. z + NQ - 1) with all their loads in flight
     auto step = [&](int z, auto nq) __attribute__((always_inline)) {
       constexpr int NQ = decltype(nq)::value;
-      constexpr bool PFS = PF && NQ == ZU;      // a full step: its r came with the previous one
       dbl2 L[NQ][NR], zp[NQ], rq[NQ];
       double e[NQ];
       uint32_t bw[NQ];
@@ -334,18 +319,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm_kernel(const PairLeanArgs a,
         int eo = ecst;
         if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
         e[q] = bload1(xr, ub + eo);
-        if constexpr (RU) {
-          if constexpr (PFS) rq[q] = have ? rn[q % ZU] : __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
-          else rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
-        }
-      }
-      if constexpr (PFS) {                         // the next full step's r
-        have = z + 2 * ZU <= z1;
-        if (have) {
-#pragma unroll
-          for (int q = 0; q < ZU; ++q)
-            rn[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + (z + ZU + q) * D + cb));
-        }
+        if constexpr (RU) rq[q] = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0));
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1321,143 +1295,6 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27s2l_kernel(const PairLean27
   block_partials<1>(v, a.partials, gridDim.x, a.fold);
 }
 
-// CG mode 5's two passes on a 27-point "box" operator (Sell::pair_box27: the
-// column-word layout, every present off-diagonal slot holding one value v and
-// every diagonal one value c -- C5's 26 / -1 stencil).  Then
-//   (A p)_i = (c - v) p_i + v B_i,   B_i = sum of p over the 3 x 3 x 3 box
-// (absent neighbours read as 0.0, as the column words already arrange), and
-// the box sum is separable: per loaded plane, each of its three lines' x
-// triples (lo + p_x + p_x+1 and p_x + p_x+1 + hi: three adds for the lane's
-// two rows), the plane's y sum of those, and the z sum of three consecutive
-// planes' sums -- 17 adds for the lane's two rows where the slot-order sum
-// takes 54 multiply-adds.  The round-3 kernels were VALU-issue-bound on those
-// (217 VALU instructions per unit, 36% of wave cycles issue-stalled); this
-// form is an HBM stream.  The sums are reassociated, so A p is not the
-// MatMult's bits (mx_mat_mult keeps PETSc's slot order): it equals them to
-// rounding, and the CG iterates equal the oracle's within the north-star bar
-// (its and reason equal, x within rel-L2 1e-10; tests/test_gpu_cgfuse.py).
-// What crosses a step: the two previous planes' sums and the centre pair.
-// PW: the p.Ap partials (full rows, nothing stored); RUPD: alpha from the PW
-// partials, r = r - alpha A p (daxpy's fma), z = c_J r, [z.z, z.r, r.r].
-template <int MODE, int JM = 0>
-__global__ void __launch_bounds__(256) spmv_pair_zm27b_kernel(const PairLean27Args a, const double *__restrict__ x,
-                                                              const int32_t *__restrict__ pcol, const double cmv,
-                                                              const double bv, const PairRuArgs ru) {
-  static_assert(MODE == SPMV_PW || MODE == SPMV_RUPD, "CG mode 5's passes");
-  constexpr bool RU = MODE == SPMV_RUPD;
-  double alpha = 0.0;
-  const double *rin = nullptr;
-  if constexpr (RU) {
-    KspState *s = ru.s;
-    if (s->top.done) {
-      if (ru.hw && blockIdx.x == 0 && threadIdx.x == 0) host_store(ru.hw + HW_DONE, 1);
-      return;
-    }
-    const double pw = ru.ndot > 0 ? block_sum_array<16>(ru.dot_part, ru.ndot) : s->red1;
-    const CgAlpha al = cg_alpha(s, pw);
-    if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_alpha(s, al, pw, ru.xb, false, ru.hw);
-    if (al.reason) return;
-    alpha = al.alpha;
-    rin = (ru.r0 && al.i == 0) ? ru.r0 : ru.r;
-  } else {
-    if (a.done && *a.done) return;   // wave-uniform: solver finished
-  }
-  double nv[3] = {0.0, 0.0, 0.0};   // RU: [z.z, z.r, r.r]
-  double dot = 0.0;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int sb, se, W, w;
-  if ((gridDim.x & 7) == 0) {
-    const int xcd = blockIdx.x & 7;
-    W = (gridDim.x >> 3) * LEAN_WAVES;
-    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
-    sb = a.S * xcd / 8;
-    se = a.S * (xcd + 1) / 8;
-  } else {
-    W = gridDim.x * LEAN_WAVES;
-    w = blockIdx.x * LEAN_WAVES + wid;
-    sb = 0;
-    se = a.S;
-  }
-  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
-  const int D = a.anchor[7];
-  const int eb = lane == 0 ? -1 : 128;                   // edge: lane 0 x[ub + c - 1], others x[ub + 128 + c]
-  const int ntask = (se - sb) * a.P;
-  for (int t = w; t < ntask; t += W) {
-    const int seg = sb + t / a.P, col = t % a.P;
-    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
-    const int cb = col * 128 + 2 * lane;
-    const uint32_t cw = (uint32_t)pcol[col];
-    const int oor[3] = {(cw & U27C_YLO) ? PAIR_OOR : 0, 0, (cw & U27C_YHI) ? PAIR_OOR : 0};
-    const int ebe = eb + ((lane == 0 ? (cw & U27_ELO) : (cw & U27_EHI)) ? PAIR_OOR_EDGE : 0);
-    // plane q's three lines (dy = -1, 0, +1) and their edge values
-    auto load = [&](int q, dbl2 (&L)[3], double (&e)[3]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        L[k] = bload2(xr, q * D + cb + a.anchor[3 + k] + oor[k]);
-        e[k] = bload1(xr, q * D + col * 128 + ebe + a.anchor[3 + k] + oor[k]);
-      }
-    };
-    // the plane's box-row sums for the lane's two rows
-    auto psum = [&](const dbl2 (&L)[3], const double (&e)[3]) __attribute__((always_inline)) -> dbl2 {
-      dbl2 t[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double lo = wave_shift<true>(L[k].y, e[k]);   // x[r0 + c - 1]
-        const double hi = wave_shift<false>(L[k].x, e[k]);  // x[r0 + c + 2]
-        const double u = L[k].x + L[k].y;
-        t[k] = dbl2{lo + u, u + hi};
-      }
-      return dbl2{(t[0].x + t[1].x) + t[2].x, (t[0].y + t[1].y) + t[2].y};
-    };
-    // software-pipelined by one plane: plane z + 2's loads (and row z + 1's
-    // r) are issued before plane z + 1 is summed, so every wave keeps a
-    // plane's reads in flight while it computes (the slot-order kernels, at
-    // 73-98 VGPRs, could not afford the second set)
-    dbl2 L[3], Ln[3];
-    double e[3], en[3];
-    dbl2 rq, rqn;
-    load(z0 - 1, L, e);                                  // (plane -1: out of range, 0.0)
-    load(z0, Ln, en);
-    dbl2 sm = psum(L, e);
-    dbl2 s0 = psum(Ln, en);
-    dbl2 cz = Ln[1];                                     // unit z0's own rows
-    load(z0 + 1, L, e);                                  // (past the last plane: 0.0)
-    if constexpr (RU) rq = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + z0 * D + cb));
-    for (int z = z0; z < z1; ++z) {
-      const int r0 = z * D + cb;
-      if (z + 1 < z1) {                                  // wave-uniform: the next step's reads
-        load(z + 2, Ln, en);
-        if constexpr (RU) rqn = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + r0 + D));
-      }
-      const dbl2 sp = psum(L, e);
-      const dbl2 bx = dbl2{(sm.x + s0.x) + sp.x, (sm.y + s0.y) + sp.y};
-      const dbl2 ap = dbl2{fma(cmv, cz.x, bv * bx.x), fma(cmv, cz.y, bv * bx.y)};
-      if constexpr (RU) {
-        const double ra = fma(-alpha, ap.x, rq.x), rb = fma(-alpha, ap.y, rq.y);
-        const double za = JM == 2 ? ra * ru.c : ra, zb = JM == 2 ? rb * ru.c : rb;
-        nv[0] += za * za; nv[1] += za * ra; nv[2] += ra * ra;
-        nv[0] += zb * zb; nv[1] += zb * rb; nv[2] += rb * rb;
-        *reinterpret_cast<dbl2 *>(ru.r + r0) = dbl2{ra, rb};
-      } else {
-        dot += cz.x * ap.x;
-        dot += cz.y * ap.y;
-      }
-      sm = s0;
-      s0 = sp;
-      cz = L[1];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) { L[k] = Ln[k]; e[k] = en[k]; }
-      if constexpr (RU) rq = rqn;
-    }
-  }
-  if constexpr (RU) block_partials<3>(nv, a.partials, gridDim.x, a.fold);
-  else {
-    double v[1] = {dot};
-    block_partials<1>(v, a.partials, gridDim.x, a.fold);
-  }
-}
-
 // fp64 row pairs (Sell::pval, uncoded 5/7-point layouts whose every unit is
 // select-free): the z-march with the unit's values streamed (K 16-byte pairs
 // per lane, non-temporal) instead of a dictionary block's uniform values.
@@ -1739,8 +1576,7 @@ using ZmFn = void (*)(PairLeanArgs, const double *, double *, const int32_t *, c
 // the layout side of the choice (mode and split aside): 0 none, 1 lean, 2 lean select-free
 int pair_lean_kind(const Mat *A) {
   const Sell &S = A->sd;
-  if (!g_knobs.pair_lean || !g_knobs.vcodes || !g_knobs.spmv_pairs || !g_knobs.pair_uni || g_knobs.spmv_ynt ||
-      g_knobs.spmv_rev)
+  if (!g_knobs.pair_lean || !g_knobs.vcodes || !g_knobs.spmv_pairs || !g_knobs.pair_uni || g_knobs.spmv_ynt)
     return 0;
   if (S.pair_shape == 27) {    // the 27-point form exists as a z-march only
     if (S.ntab <= 0 || !S.puni27.p || S.pair_blocks <= 0 || !S.pair_all || !g_knobs.pair_zm) return 0;
@@ -1909,20 +1745,6 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // the plane-pipelined form (knob 60): column words; the symmetric p.Ap pass
   // keeps the carried-operand kernel
   const bool sym = S.pair_sym27 && g_knobs.pw_sym27;
-  if ((mode == SPMV_PW || mode == SPMV_RUPD) && form == 2 && !split && S.pair_box27 && g_knobs.box27) {
-    // the box operator's separable sums (knob 62), on knob 63 workgroups per CU
-    if (g_knobs.box27_bpc > 0) {
-      grid = zm_tasks(b.P, b.NZ, b.L, b.S, g_knobs.box27_bpc);
-      if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
-    }
-    using FB = void (*)(PairLean27Args, const double *, const int32_t *, double, double, PairRuArgs);
-    FB fb = mode == SPMV_PW ? &spmv_pair_zm27b_kernel<SPMV_PW> : jm == 2 ? &spmv_pair_zm27b_kernel<SPMV_RUPD, 2>
-                                                                         : &spmv_pair_zm27b_kernel<SPMV_RUPD, 0>;
-    note_dispatch(mode == SPMV_PW ? DSP_ZM_PW : DSP_ZM_RUPD);
-    launch_timed(fb, grid, st, b, x, S.pcol27.p, S.box_c - S.box_v, S.box_v, ru);
-    HIPCHECK(hipGetLastError());
-    return grid;
-  }
   // knob 70: two lines per wave (the column words pair up by lines, no ghost units)
   if (form == 2 && g_knobs.zm27_2line && S.pair_2l27 && !split && mode == SPMV_PW && sym) {
     const bool uv2 = S.pair_unit27 && g_knobs.pair_unitv;
@@ -2052,7 +1874,7 @@ void pair_sym_prepare(Mat *A) {
 bool pair_code_applies(const Mat *A) {
   const Sell &S = A->sd;
   if (!g_knobs.pair_zmc || !g_knobs.pair_zm || !g_knobs.vcodes || !g_knobs.spmv_pairs || g_knobs.spmv_ynt ||
-      g_knobs.spmv_rev || !S.pair_code_clean || S.ntab <= 0 || S.puni.p || S.pair_blocks <= 0 || !S.pair_all ||
+      !S.pair_code_clean || S.ntab <= 0 || S.puni.p || S.pair_blocks <= 0 || !S.pair_all ||
       (S.pair_shape != 5 && S.pair_shape != 7) || !S.pcode.p || !S.vtab.p)
     return false;
   if (A->m % 128 != 0 || A->m > PAIR_CLEAN_MAX_ROWS || A->n > PAIR_CLEAN_MAX_ROWS || S.nunits * 128 != A->m) return false;
@@ -2303,26 +2125,6 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
                       A->sd.puni.p, ru);
     HIPCHECK(hipGetLastError());
     return g2;
-  }
-  // knob 66: the next step's r loaded one step ahead (clean, one rank, 2 planes per step)
-  if (clean && !split && g_knobs.ru_rpf && z2 && g_knobs.ru_units != 3 && g_knobs.ru_units != 4) {
-    if (A->sd.pair_shape == 5)
-      f = jac_mode == 2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 2, 2, false, true>
-                        : &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 2, 0, false, true>;
-    else
-      f = jac_mode == 2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 2, 2, false, true>
-                        : &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 2, 0, false, true>;
-  }
-  // knob 64: 3 or 4 planes per step for the clean one-rank residual update
-  // (more of its HBM reads in flight per wave)
-  if (clean && !split && (g_knobs.ru_units == 3 || g_knobs.ru_units == 4)) {
-    const bool u4 = g_knobs.ru_units == 4, j2 = jac_mode == 2;
-    if (A->sd.pair_shape == 5)
-      f = u4 ? (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 4, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 4, 0>)
-             : (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 3, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 5, false, true, 3, 0>);
-    else
-      f = u4 ? (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 4, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 4, 0>)
-             : (j2 ? &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 3, 2> : &spmv_pair_zm_kernel<SPMV_RUPD, 7, false, true, 3, 0>);
   }
   note_dispatch(DSP_ZM_RUPD);
   launch_timed(f, grid, st, a, p, nullptr, A->sd.pblk.p, A->sd.puni.p, ru);

@@ -12,6 +12,7 @@ and reductions run over RCCL inside libmxsolve.so.
 from __future__ import annotations
 
 import atexit
+import sys
 import os
 import pickle
 
@@ -64,19 +65,37 @@ def _buf(spec):
     return spec, []
 
 
+_EXIT_ON_EXCEPTION = []
+
+
+def _note_uncaught(prev):
+    """sys.excepthook wrapper: remember that the interpreter is exiting on an
+    unhandled exception, so _finalize skips its long barrier."""
+    def hook(tp, val, tb):
+        _EXIT_ON_EXCEPTION.append(tp)
+        prev(tp, val, tb)
+    return hook
+
+
 def _finalize(dist):
     """MPI_Finalize at interpreter exit (mpi4py registers the same): a last
     barrier, then the process group torn down while every rank is still
     there.  Without it a rank could exit while a peer's gloo threads were
     still live, and that peer's teardown died in std::terminate ('terminate
-    called without an active exception', about one run in ten)."""
+    called without an active exception', about one run in ten).  A rank
+    exiting on an unhandled exception skips the barrier (its peers are not
+    coming, or are blocked elsewhere): it closes its connections at once so
+    the failure reaches them.  MXSOLVE_FINALIZE_TIMEOUT_S bounds the barrier
+    (default 300 s)."""
     if not dist.is_initialized():
         return
     try:
         # bounded: a rank that died (or is stuck in another collective) must
         # not hold its peers' exit forever
         import datetime
-        dist.monitored_barrier(timeout=datetime.timedelta(seconds=300))
+        if not _EXIT_ON_EXCEPTION:
+            t = float(os.environ.get("MXSOLVE_FINALIZE_TIMEOUT_S", "300"))
+            dist.monitored_barrier(timeout=datetime.timedelta(seconds=t))
     except Exception:  # noqa: BLE001 -- a peer already gone: tear down anyway
         pass
     try:
@@ -96,6 +115,7 @@ class Comm:
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 dist.init_process_group("gloo")
+                sys.excepthook = _note_uncaught(sys.excepthook)
                 atexit.register(_finalize, dist)
             self._dist = dist
             self._rank, self._size = dist.get_rank(), dist.get_world_size()

@@ -39,7 +39,9 @@ class KSPResult(C.Structure):
     _fields_ = [("its", C.c_int), ("reason", C.c_int), ("rnorm", C.c_double),
                 ("solve_ms", C.c_double), ("spmv_ms", C.c_double), ("spmv_count", C.c_int),
                 ("launched_its", C.c_int), ("cg_mode", C.c_int), ("upd_ms", C.c_double), ("upd_count", C.c_int),
-                ("cg_xbatch", C.c_int), ("pb_ms", C.c_double), ("pb_count", C.c_int)]
+                ("cg_xbatch", C.c_int), ("pb_ms", C.c_double), ("pb_count", C.c_int),
+                ("pbw_ms", C.c_double), ("pbw_count", C.c_int), ("mdot_ms", C.c_double), ("mdot_count", C.c_int),
+                ("maxpy_ms", C.c_double), ("maxpy_count", C.c_int)]
 
 
 class MatInfo(C.Structure):

@@ -244,11 +244,6 @@ def test_batched_x_steps_equal_separate(selfcomm, oracle_mod, kind, kw, B):
                                                  ("poisson3d", 128, "jacobi", 41, {"xb": 1}),
                                                  ("poisson3d27", 128, "jacobi", 10000, {"poll": 6}),
                                                  ("poisson2d", 256, "jacobi", 10000, {"xb": 1, "guess": True}),
-                                                 # knob 62: the 27-point box operator's separable sums
-                                                 ("poisson3d27", 128, "jacobi", 10000, {"box": 1}),
-                                                 ("poisson3d27", 128, "jacobi", 37, {"box": 1}),
-                                                 ("poisson3d27", 128, "none", 10000, {"box": 1, "guess": True}),
-                                                 ("poisson3d27", 128, "jacobi", 10000, {"box": 1, "poll": 6}),
                                                  ])
 def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw):
     """CG mode 5 (knob 9 = 5): the MatMult stores no product -- a p.Ap pass
@@ -279,7 +274,6 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
         old29 = L.mx_debug_set(29, kw.get("xb", 0) if mode == 5 else 0)   # mode 5: x batches of 4 by default
         old59 = L.mx_debug_set(59, kw.get("sym", 1))   # 27-point: the symmetric forward-half p.Ap pass
         old60 = L.mx_debug_set(60, kw.get("k60", 1))   # 27-point: the plane-pipelined z-march
-        old62 = L.mx_debug_set(62, kw.get("box", 0))   # 27-point: the box operator's separable sums
         try:
             A = DMat.stencil(selfcomm, kind, n)
             m = A.info()["m"]
@@ -310,7 +304,6 @@ def test_mode5_recomputed_product(selfcomm, oracle_mod, kind, n, pc, max_it, kw)
             L.mx_debug_set(29, old29)
             L.mx_debug_set(59, old59)
             L.mx_debug_set(60, old60)
-            L.mx_debug_set(62, old62)
 
     m5, dc5, bh, x0 = run(5)
     m2, dc2, _, _ = run(2)

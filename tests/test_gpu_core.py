@@ -266,3 +266,29 @@ def test_ksp_destroy_then_solve(selfcomm, oracle_mod):
     r2 = A.solve(b, x2, ksp="cg", pc="jacobi")
     assert r1["its"] == r2["its"] and torch.equal(x1, x2)
     A.destroy()
+
+
+def test_destroy_current_comm_then_torch(selfcomm):
+    """A communicator whose stream is torch's current stream is destroyed,
+    then torch allocates and computes at once -- no fixture in between (the
+    autouse _selfcomm_stream fixture would re-activate the session stream and
+    hide a regression of DeviceComm.destroy's stream hand-back, round 4's
+    `HIP error: invalid argument`)."""
+    from mxsolve.core import DeviceComm, DMat, rhs_hash
+    c = DeviceComm.self_comm(0)
+    sp = c.stream_ptr
+    assert torch.cuda.current_stream(0).cuda_stream == sp          # creation made it current
+    A = DMat.stencil(c, "poisson3d", 16)
+    b = c.empty(A.info()["m"])
+    rhs_hash(c, 0, b)
+    x = c.zeros(A.info()["m"])
+    r = A.solve(b, x, ksp="cg")
+    assert r["reason"] == 2
+    A.destroy()
+    c.destroy()
+    assert torch.cuda.current_stream(0).cuda_stream != sp
+    v = torch.arange(1 << 20, dtype=torch.float64, device="cuda:0")
+    w = torch.empty_like(v).copy_(v).mul_(2.0)
+    s = float(w.sum())
+    torch.cuda.synchronize()
+    assert s == float((1 << 20) * ((1 << 20) - 1))

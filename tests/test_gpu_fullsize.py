@@ -20,6 +20,10 @@ from _hostinfo import host_threads
 
 pytestmark = pytest.mark.gpu
 
+# the converged counts (its, CONVERGED_RTOL) the oracle gives for each
+# configuration; bench.py's configuration legs check the GPU solve against these
+FULL_COUNTS = {"C2": (7723, 2), "C3": (560, 2), "C4": (530, 2), "C5share": (245, 2)}
+
 
 def true_prec_residual(A, b, x, dinv_scalar=None):
     from mxsolve.core import vnorm
@@ -59,7 +63,7 @@ def oracle_parity(comm, oracle_mod, kind, dims, ksp, **kw):
 def test_c4_full_parity(selfcomm, oracle_mod):
     """C4: conv-diff 256^3, GMRES(30)+Jacobi, the 8-block code dictionary layout."""
     r, xr, o = oracle_parity(selfcomm, oracle_mod, "convdiff3d", (256, 256, 256), "gmres")
-    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) and r["reason"] == 2, (r["its"], o["its"])
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) == FULL_COUNTS["C4"], (r["its"], o["its"])
     assert np.linalg.norm(xr - o["x"]) / np.linalg.norm(o["x"]) <= 1e-10
     assert np.allclose(r["history"], o["history"], rtol=1e-8, atol=0)
 
@@ -68,7 +72,7 @@ def test_c4_full_parity(selfcomm, oracle_mod):
 def test_c5_share_full_parity(selfcomm, oracle_mod):
     """C5's one-GPU share: 27-point 512x512x64, CG+Jacobi, 27-point row pairs."""
     r, xr, o = oracle_parity(selfcomm, oracle_mod, "poisson3d27", (512, 512, 64), "cg")
-    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) and r["reason"] == 2, (r["its"], o["its"])
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) == FULL_COUNTS["C5share"], (r["its"], o["its"])
     assert np.linalg.norm(xr - o["x"]) / np.linalg.norm(o["x"]) <= 1e-10
     assert np.allclose(r["history"], o["history"], rtol=1e-8, atol=0)
 
@@ -79,7 +83,7 @@ def test_c2_full_parity(selfcomm, oracle_mod):
     iterations, where an iteration-count drift would show first): its and
     reason equal, residual history within 1e-8, x within rel-L2 1e-10."""
     r, xr, o = oracle_parity(selfcomm, oracle_mod, "poisson2d", (4096, 4096, 1), "cg")
-    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) and r["reason"] == 2, (r["its"], o["its"])
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) == FULL_COUNTS["C2"], (r["its"], o["its"])
     assert np.allclose(r["history"], o["history"], rtol=1e-8, atol=0)
     assert np.linalg.norm(xr - o["x"]) / np.linalg.norm(o["x"]) <= 1e-10
 
@@ -100,7 +104,7 @@ def test_c3_full_parity(selfcomm, oracle_mod):
     O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
     del ip, c, v
     o = O.solve(b.cpu().numpy(), ksp="cg", nthreads=host_threads())
-    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) == (560, 2)
+    assert (r["its"], r["reason"]) == (o["its"], o["reason"]) == FULL_COUNTS["C3"]
     xr = x.cpu().numpy()
     assert np.linalg.norm(xr - o["x"]) / np.linalg.norm(o["x"]) <= 1e-10
 
