@@ -404,6 +404,11 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         CG iteration, residual update 86 -> 78 us, p.Ap pass 37 -> 30 us,
  *         MatMult -5%; 0 off; 2: the p.Ap pass by groups of four lines,
  *         27.5 us, the iteration unchanged)
+ * key 72: assembly canonicalises and splits rows in two register passes
+ *         (count, then fill after the row-pointer scans) when every row has
+ *         at most 64 entries (1, default; 0: the canonical copy in HBM, then
+ *         the split passes -- the path rows longer than 64 always take; the
+ *         same arrays bit for bit)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -58,15 +58,19 @@ void convert_index(const void *src, int bytes, int64_t n, int64_t *dst, hipStrea
   }
 }
 
+// grid-stride (a capped grid): one atomicMax per workgroup -- a workgroup per
+// 256 rows put 65,536 atomics on one word (0.75 ms for 2^24 rows)
 __global__ void row_len_max_kernel(int64_t m, const int64_t *__restrict__ rowptr,
                                    unsigned long long *__restrict__ out, int *__restrict__ err) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long mx = 0;
-  if (i < m) {
-    int64_t len = rowptr[i + 1] - rowptr[i];
-    if (len < 0) atomicOr(err, 4);
-    else mx = (unsigned long long)len;
+  bool bad = false;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    const int64_t len = rowptr[i + 1] - rowptr[i];
+    if (len < 0) bad = true;
+    else mx = (unsigned long long)len > mx ? (unsigned long long)len : mx;
   }
+  if (bad) atomicOr(err, 4);
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long t = __shfl_xor(mx, o, 64);
     mx = t > mx ? t : mx;
@@ -235,6 +239,78 @@ static int64_t coo_redistribute(Comm *c, const std::vector<int64_t> &rr, int64_t
 // ---------------------------------------------------------------- row canonicalisation
 // One W-lane segment per row (W | 64).  Keys (col, pos) are unique per row
 // except the dropped/padding lanes, which all carry (KEY_DROP, KEY_DROP).
+// canon_seg: the row's entries (lane l: entry l) sorted and deduplicated in
+// registers; returns keep (this lane holds a canonical entry: column c and,
+// with VALS, its value -- INSERT: the last of its run, ADD: the run folded in
+// input order).  The kept lanes are in ascending column order.
+template <int W, bool VALS>
+__device__ __forceinline__ bool canon_seg(int lane, int l, bool active, int64_t start, int64_t len,
+                                          const int64_t *__restrict__ col, const double *__restrict__ val,
+                                          const int64_t *__restrict__ pos, int64_t N, int add, int *__restrict__ err,
+                                          int64_t &c, double &out) {
+  int64_t p = KEY_DROP;
+  double v = 0.0;
+  c = KEY_DROP;
+  if (active && l < len) {
+    int64_t cc = col[start + l];
+    if (cc >= 0) {
+      if (err && cc >= N) atomicOr(err, 1);
+      c = cc;
+      p = pos ? pos[start + l] : (int64_t)l;
+      if (VALS) v = val[start + l];
+    }
+  }
+  // Already canonical (every kept column above the previous kept column of
+  // its row, in input order -- scipy's canonical CSR, the stencil generator):
+  // the sort would only move the dropped lanes to the end, which the ballot
+  // compaction of the callers does anyway, and there is nothing to dedupe.
+  // Decided per wave, so most waves of such inputs skip the bitonic network.
+  const int gbase0 = lane - l;
+  const unsigned long long vb = __ballot(c != KEY_DROP);
+  const unsigned long long below_v = vb & ((l == 0) ? 0ULL : (((1ULL << l) - 1ULL) << gbase0));
+  const int pl = below_v ? 63 - __clzll(below_v) : lane;
+  const int64_t cprev = __shfl(c, pl, 64);
+  const bool sorted = !__any(c != KEY_DROP && below_v != 0 && cprev >= c);
+  // bitonic sort of (c, p) ascending inside each W-lane segment
+  if (!sorted) {
+#pragma unroll
+    for (int k = 2; k <= W; k <<= 1) {
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        int64_t c2 = __shfl_xor(c, j, 64);
+        int64_t p2 = __shfl_xor(p, j, 64);
+        double v2 = VALS ? __shfl_xor(v, j, 64) : 0.0;
+        const bool up = (l & k) == 0;
+        const bool lower = (l & j) == 0;
+        const bool mine_less = (c < c2) || (c == c2 && p < p2);
+        const bool keep = (lower == up) ? mine_less : !mine_less;
+        if (!keep) { c = c2; p = p2; if (VALS) v = v2; }
+      }
+    }
+  }
+  const bool valid = c != KEY_DROP;
+  const int64_t c_next = __shfl(c, (lane + 1) & 63, 64);
+  const int64_t c_prev = __shfl(c, (lane + 63) & 63, 64);
+  bool keep;
+  out = v;
+  if (!add) {
+    keep = valid && (l == W - 1 || c_next != c);       // INSERT: last occurrence wins
+  } else {
+    keep = valid && (l == 0 || c_prev != c);           // ADD: run head folds its run in order
+    if (VALS) {
+      bool run = true;
+#pragma unroll
+      for (int t = 1; t < W; ++t) {
+        const double vt = __shfl(v, (lane + t) & 63, 64);
+        const int64_t ct = __shfl(c, (lane + t) & 63, 64);
+        run = run && (l + t < W) && (ct == c);
+        if (run) out = out + vt;
+      }
+    }
+  }
+  return keep;
+}
+
 template <int W>
 __global__ void __launch_bounds__(256) canon_rows_wave_kernel(
     int64_t m, const int64_t *__restrict__ rowptr, const int64_t *__restrict__ col,
@@ -250,64 +326,9 @@ __global__ void __launch_bounds__(256) canon_rows_wave_kernel(
   const bool too_long = len > W;
   if (rvalid && too_long && l == 0) long_rows[atomicAdd(nlong, 1ULL)] = row;
   const bool active = rvalid && !too_long;
-
-  int64_t c = KEY_DROP, p = KEY_DROP;
-  double v = 0.0;
-  if (active && l < len) {
-    int64_t cc = col[start + l];
-    if (cc >= 0) {
-      if (cc >= N) atomicOr(err, 1);
-      c = cc;
-      p = pos ? pos[start + l] : (int64_t)l;
-      v = val[start + l];
-    }
-  }
-  // Already canonical (every kept column above the previous kept column of
-  // its row, in input order -- scipy's canonical CSR, the stencil generator):
-  // the sort would only move the dropped lanes to the end, which the ballot
-  // compaction below does anyway, and there is nothing to dedupe.  Decided per
-  // wave, so most waves of such inputs skip the bitonic network.
-  const int gbase0 = lane - l;
-  const unsigned long long vb = __ballot(c != KEY_DROP);
-  const unsigned long long below_v = vb & ((l == 0) ? 0ULL : (((1ULL << l) - 1ULL) << gbase0));
-  const int pl = below_v ? 63 - __clzll(below_v) : lane;
-  const int64_t cprev = __shfl(c, pl, 64);
-  const bool sorted = !__any(c != KEY_DROP && below_v != 0 && cprev >= c);
-  // bitonic sort of (c, p) ascending inside each W-lane segment
-  if (!sorted) {
-#pragma unroll
-    for (int k = 2; k <= W; k <<= 1) {
-#pragma unroll
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        int64_t c2 = __shfl_xor(c, j, 64);
-        int64_t p2 = __shfl_xor(p, j, 64);
-        double v2 = __shfl_xor(v, j, 64);
-        const bool up = (l & k) == 0;
-        const bool lower = (l & j) == 0;
-        const bool mine_less = (c < c2) || (c == c2 && p < p2);
-        const bool keep = (lower == up) ? mine_less : !mine_less;
-        if (!keep) { c = c2; p = p2; v = v2; }
-      }
-    }
-  }
-  const bool valid = c != KEY_DROP;
-  const int64_t c_next = __shfl(c, (lane + 1) & 63, 64);
-  const int64_t c_prev = __shfl(c, (lane + 63) & 63, 64);
-  bool keep;
-  double out = v;
-  if (!add) {
-    keep = valid && (l == W - 1 || c_next != c);       // INSERT: last occurrence wins
-  } else {
-    keep = valid && (l == 0 || c_prev != c);           // ADD: run head folds its run in order
-    bool run = true;
-#pragma unroll
-    for (int t = 1; t < W; ++t) {
-      const double vt = __shfl(v, (lane + t) & 63, 64);
-      const int64_t ct = __shfl(c, (lane + t) & 63, 64);
-      run = run && (l + t < W) && (ct == c);
-      if (run) out = out + vt;
-    }
-  }
+  int64_t c;
+  double out;
+  const bool keep = canon_seg<W, true>(lane, l, active, start, len, col, val, pos, N, add, err, c, out);
   const unsigned long long ball = __ballot(keep);
   const int gbase = lane - l;
   const unsigned long long gmask =
@@ -317,6 +338,75 @@ __global__ void __launch_bounds__(256) canon_rows_wave_kernel(
     if (keep) { ccol[start + idx] = c; cval[start + idx] = out; }
     if (l == 0) cnt_out[row] = __popcll(gmask);
   }
+}
+
+// Canonicalisation fused with the MPIAIJ split, for inputs whose rows are all
+// at most 64 entries (every configuration; longer rows take the separate
+// passes above and below): a count pass sorts / deduplicates each row in
+// registers and writes its A_d / A_o counts (and the ghost bitmap) straight
+// into the split's row pointers, then -- after the scans -- a fill pass
+// repeats the same register canonicalisation with the values and stores the
+// split arrays.  No canonical copy of the input goes through HBM (round 4:
+// canonicalise 14.4 GB + split count 3.6 + split fill 12.6 for a 27-point
+// share; fused: 3.6 + 12.6).
+template <int W>
+__device__ __forceinline__ unsigned long long seg_bits_w(unsigned long long ball, int gbase) {
+  return W == 64 ? ball : ((ball >> gbase) & ((1ULL << (W == 64 ? 0 : W)) - 1ULL));
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) canon_count_kernel(int64_t m, const int64_t *__restrict__ rowptr,
+                                                          const int64_t *__restrict__ col,
+                                                          const int64_t *__restrict__ pos, int64_t N, int add,
+                                                          int64_t cstart, int64_t cend, int64_t *__restrict__ cnt_d,
+                                                          int64_t *__restrict__ cnt_o, unsigned *__restrict__ bitmap,
+                                                          int *__restrict__ err) {
+  const int lane = threadIdx.x & 63, l = lane % W, gbase = lane - l;
+  const int64_t row = (int64_t)blockIdx.x * (256 / W) + threadIdx.x / W;
+  const bool rv = row < m;
+  const int64_t start = rv ? rowptr[row] : 0;
+  const int64_t len = rv ? rowptr[row + 1] - start : 0;
+  int64_t c;
+  double out;
+  const bool keep = canon_seg<W, false>(lane, l, rv, start, len, col, nullptr, pos, N, add, err, c, out);
+  const bool isd = keep && c >= cstart && c < cend, iso = keep && !isd;
+  if (iso) atomicOr(&bitmap[c >> 5], 1u << (c & 31));
+  const int nd = __popcll(seg_bits_w<W>(__ballot(isd), gbase)), no = __popcll(seg_bits_w<W>(__ballot(iso), gbase));
+  if (rv && l == 0) { cnt_d[row] = nd; cnt_o[row] = no; }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) canon_fill_kernel(
+    int64_t m, const int64_t *__restrict__ rowptr, const int64_t *__restrict__ col, const double *__restrict__ val,
+    const int64_t *__restrict__ pos, int64_t N, int add, int64_t cstart, int64_t cend, int64_t rstart,
+    const int64_t *__restrict__ dptr, const int64_t *__restrict__ optr, int32_t *__restrict__ dcol,
+    double *__restrict__ dval, int32_t *__restrict__ ocol, double *__restrict__ oval, double *__restrict__ diag,
+    const unsigned *__restrict__ bitmap, const int64_t *__restrict__ wbase) {
+  const int lane = threadIdx.x & 63, l = lane % W, gbase = lane - l;
+  const int64_t row = (int64_t)blockIdx.x * (256 / W) + threadIdx.x / W;
+  const bool rv = row < m;
+  const int64_t start = rv ? rowptr[row] : 0;
+  const int64_t len = rv ? rowptr[row + 1] - start : 0;
+  int64_t c;
+  double out;
+  const bool keep = canon_seg<W, true>(lane, l, rv, start, len, col, val, pos, N, add, nullptr, c, out);
+  const bool isd = keep && c >= cstart && c < cend, iso = keep && !isd;
+  const unsigned long long below = l == 0 ? 0ULL : ((1ULL << l) - 1ULL);
+  const unsigned long long bd = seg_bits_w<W>(__ballot(isd), gbase), bo = seg_bits_w<W>(__ballot(iso), gbase);
+  const unsigned long long bg = seg_bits_w<W>(__ballot(isd && c == rstart + row), gbase);
+  if (isd) {
+    const int64_t t = dptr[row] + __popcll(bd & below);
+    dcol[t] = (int32_t)(c - cstart);
+    dval[t] = out;
+    if (c == rstart + row) diag[row] = out;
+  } else if (iso) {
+    const int64_t w = c >> 5;
+    const unsigned bit = (unsigned)(c & 31);
+    const int64_t t = optr[row] + __popcll(bo & below);
+    ocol[t] = (int32_t)(wbase[w] + __popc(bitmap[w] & ((1u << bit) - 1u)));
+    oval[t] = out;
+  }
+  if (rv && l == 0 && !bg) diag[row] = 0.0;
 }
 
 // Rows longer than 64 entries: one block per row, LDS bitonic sort, then a
@@ -1846,7 +1936,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   DBuf<unsigned long long> lmax(2);
   HIPCHECK(hipMemsetAsync(lmax.p, 0, sizeof(unsigned long long) * 2, st));
   if (m) {
-    row_len_max_kernel<<<(unsigned)cdiv(m, 256), 256, 0, st>>>(m, rowptr, lmax.p, err.p);
+    row_len_max_kernel<<<grid_for(m, 256, 2048), 256, 0, st>>>(m, rowptr, lmax.p, err.p);
     HIPCHECK(hipGetLastError());
   }
   unsigned long long Lh = 0;
@@ -1855,50 +1945,6 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   int64_t tot_in = 0;
   if (m) HIPCHECK(hipMemcpy(&tot_in, rowptr + m, sizeof(int64_t), hipMemcpyDeviceToHost));
 
-  // ---- canonicalise rows
-  DBuf<int64_t> ccol((size_t)std::max<int64_t>(tot_in, 1));
-  DBuf<double> cval((size_t)std::max<int64_t>(tot_in, 1));
-  DBuf<int64_t> cnt_out((size_t)m + 1);
-  DBuf<int64_t> long_rows((size_t)m + 1);
-  if (m) {
-    const int add = in.insert_mode == MX_ADD_VALUES;
-    int W = 64;
-    if (Lh <= 8) W = 8; else if (Lh <= 16) W = 16; else if (Lh <= 32) W = 32;
-    const unsigned grid = (unsigned)cdiv(m, 256 / W);
-#define CANON(WW) canon_rows_wave_kernel<WW><<<grid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, long_rows.p, &lmax.p[1], err.p)
-    switch (W) { case 8: CANON(8); break; case 16: CANON(16); break; case 32: CANON(32); break; default: CANON(64); }
-#undef CANON
-    HIPCHECK(hipGetLastError());
-    if (Lh > 64) {
-      unsigned long long nl = 0;
-      HIPCHECK(hipMemcpyAsync(&nl, &lmax.p[1], sizeof(nl), hipMemcpyDeviceToHost, st));
-      HIPCHECK(hipStreamSynchronize(st));
-      if (nl) {
-        DBuf<int64_t> huge((size_t)nl);
-        HIPCHECK(hipMemsetAsync(&lmax.p[0], 0, sizeof(unsigned long long), st));   // reused: huge-row count
-        canon_rows_block_kernel<<<(unsigned)nl, 256, 0, st>>>(long_rows.p, rowptr, col, val, pos, N, add, ccol.p,
-                                                              cval.p, cnt_out.p, err.p, huge.p, &lmax.p[0]);
-        HIPCHECK(hipGetLastError());
-        if (Lh > LONG_ROW_MAX) {
-          unsigned long long nh = 0;
-          HIPCHECK(hipMemcpyAsync(&nh, &lmax.p[0], sizeof(nh), hipMemcpyDeviceToHost, st));
-          HIPCHECK(hipStreamSynchronize(st));
-          std::vector<int64_t> hrows((size_t)nh);
-          if (nh) HIPCHECK(hipMemcpy(hrows.data(), huge.p, sizeof(int64_t) * nh, hipMemcpyDeviceToHost));
-          std::sort(hrows.begin(), hrows.end());
-          canon_huge_rows(hrows, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, err.p, st);
-        }
-      }
-    }
-  }
-  int herr = 0;
-  HIPCHECK(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
-  HIPCHECK(hipStreamSynchronize(st));
-  if (herr & 4) fail(MX_ERR_ARG, "row pointer array is not nondecreasing");
-  if (herr & 1) fail(MX_ERR_OUTOFRANGE, "Column too large: max " + std::to_string(N - 1));
-  const double t_canon = wall_ms();
-
-  // ---- split into A_d / A_o with a ghost bitmap
   const bool multi = c->size > 1;
   const int64_t nw = multi ? cdiv(N, 32) : 0;
   DBuf<unsigned> bitmap((size_t)std::max<int64_t>(nw, 1));
@@ -1908,15 +1954,75 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   A->optr.alloc((size_t)m + 1);
   HIPCHECK(hipMemsetAsync(A->dptr.p, 0, sizeof(int64_t) * (m + 1), st));
   HIPCHECK(hipMemsetAsync(A->optr.p, 0, sizeof(int64_t) * (m + 1), st));
-  // segment width for the split passes (canonical rows are no longer than the input's)
+  const int add = in.insert_mode == MX_ADD_VALUES;
+  // segment width: the longest row's
   const int SW = Lh <= 8 ? 8 : Lh <= 16 ? 16 : Lh <= 32 ? 32 : 64;
-  if (m) {
-    const unsigned g = (unsigned)cdiv(m, 256 / SW);
-#define SPLITC(WW) split_count_seg_kernel<WW><<<g, 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p)
-    switch (SW) { case 8: SPLITC(8); break; case 16: SPLITC(16); break; case 32: SPLITC(32); break; default: SPLITC(64); }
+  const unsigned sgrid = (unsigned)cdiv(std::max<int64_t>(m, 1), 256 / SW);
+  const bool fused = Lh <= 64 && g_knobs.asm_fused;
+  auto check_err = [&] {
+    int herr = 0;
+    HIPCHECK(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (herr & 4) fail(MX_ERR_ARG, "row pointer array is not nondecreasing");
+    if (herr & 1) fail(MX_ERR_OUTOFRANGE, "Column too large: max " + std::to_string(N - 1));
+  };
+  DBuf<int64_t> ccol, cnt_out;
+  DBuf<double> cval;
+  double t_canon;
+  if (fused) {
+    // ---- canonicalise + split counts in one register pass (canon_count_kernel)
+    if (m) {
+#define CCNT(WW) canon_count_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, col, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p)
+      switch (SW) { case 8: CCNT(8); break; case 16: CCNT(16); break; case 32: CCNT(32); break; default: CCNT(64); }
+#undef CCNT
+      HIPCHECK(hipGetLastError());
+    }
+    check_err();
+    t_canon = wall_ms();
+  } else {
+    // ---- canonicalise rows
+    ccol.alloc((size_t)std::max<int64_t>(tot_in, 1));
+    cval.alloc((size_t)std::max<int64_t>(tot_in, 1));
+    cnt_out.alloc((size_t)m + 1);
+    DBuf<int64_t> long_rows((size_t)m + 1);
+    if (m) {
+#define CANON(WW) canon_rows_wave_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, long_rows.p, &lmax.p[1], err.p)
+      switch (SW) { case 8: CANON(8); break; case 16: CANON(16); break; case 32: CANON(32); break; default: CANON(64); }
+#undef CANON
+      HIPCHECK(hipGetLastError());
+      if (Lh > 64) {
+        unsigned long long nl = 0;
+        HIPCHECK(hipMemcpyAsync(&nl, &lmax.p[1], sizeof(nl), hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        if (nl) {
+          DBuf<int64_t> huge((size_t)nl);
+          HIPCHECK(hipMemsetAsync(&lmax.p[0], 0, sizeof(unsigned long long), st));   // reused: huge-row count
+          canon_rows_block_kernel<<<(unsigned)nl, 256, 0, st>>>(long_rows.p, rowptr, col, val, pos, N, add, ccol.p,
+                                                                cval.p, cnt_out.p, err.p, huge.p, &lmax.p[0]);
+          HIPCHECK(hipGetLastError());
+          if (Lh > LONG_ROW_MAX) {
+            unsigned long long nh = 0;
+            HIPCHECK(hipMemcpyAsync(&nh, &lmax.p[0], sizeof(nh), hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipStreamSynchronize(st));
+            std::vector<int64_t> hrows((size_t)nh);
+            if (nh) HIPCHECK(hipMemcpy(hrows.data(), huge.p, sizeof(int64_t) * nh, hipMemcpyDeviceToHost));
+            std::sort(hrows.begin(), hrows.end());
+            canon_huge_rows(hrows, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, err.p, st);
+          }
+        }
+      }
+    }
+    check_err();
+    t_canon = wall_ms();
+    // ---- split counts + ghost bitmap
+    if (m) {
+#define SPLITC(WW) split_count_seg_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p)
+      switch (SW) { case 8: SPLITC(8); break; case 16: SPLITC(16); break; case 32: SPLITC(32); break; default: SPLITC(64); }
 #undef SPLITC
-    HIPCHECK(hipGetLastError());
+      HIPCHECK(hipGetLastError());
+    }
   }
+  // ---- split: row pointers, garray (bitmap popcount scan), A_d / A_o
   exclusive_scan_i64(A->dptr.p, A->dptr.p, m + 1, st, &A->nnz_d);
   exclusive_scan_i64(A->optr.p, A->optr.p, m + 1, st, &A->nnz_o);
   if (!multi && A->nnz_o) fail(MX_ERR_INTERNAL, "off-diagonal entries on one rank");
@@ -1937,10 +2043,15 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   A->oval.alloc((size_t)std::max<int64_t>(A->nnz_o, 1));
   A->diag.alloc((size_t)std::max<int64_t>(m, 1));
   if (m) {
-    const unsigned g = (unsigned)cdiv(m, 256 / SW);
-#define SPLITF(WW) fill_split_seg_kernel<WW><<<g, 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, cval.p, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
-    switch (SW) { case 8: SPLITF(8); break; case 16: SPLITF(16); break; case 32: SPLITF(32); break; default: SPLITF(64); }
+    if (fused) {
+#define CFILL(WW) canon_fill_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
+      switch (SW) { case 8: CFILL(8); break; case 16: CFILL(16); break; case 32: CFILL(32); break; default: CFILL(64); }
+#undef CFILL
+    } else {
+#define SPLITF(WW) fill_split_seg_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, cval.p, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
+      switch (SW) { case 8: SPLITF(8); break; case 16: SPLITF(16); break; case 32: SPLITF(32); break; default: SPLITF(64); }
 #undef SPLITF
+    }
     HIPCHECK(hipGetLastError());
   }
   A->garray_h.resize((size_t)A->nghost);

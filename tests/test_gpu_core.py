@@ -292,3 +292,52 @@ def test_destroy_current_comm_then_torch(selfcomm):
     s = float(w.sum())
     torch.cuda.synchronize()
     assert s == float((1 << 20) * ((1 << 20) - 1))
+
+
+@pytest.mark.parametrize("case", ["dup-insert", "dup-add", "coo-add", "stencil27", "ref"])
+def test_assembly_fused_vs_separate(selfcomm, golden, case):
+    """Knob 72: the fused canonicalise+split passes (rows <= 64 entries, the
+    default) give the separate passes' arrays bit for bit -- CSR, A_d / A_o
+    split, diagonal."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat
+    L = _lib.load()
+    rng = np.random.default_rng(21)
+
+    def build():
+        if case.startswith("dup"):
+            M, N = 301, 400
+            lens = rng.integers(0, 65, M)
+            ip = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+            nnz = int(ip[-1])
+            cols = rng.integers(-2, 90, nnz).astype(np.int64)
+            vals = rng.standard_normal(nnz)
+            vals[rng.random(nnz) < 0.05] = 0.0
+            return lambda: DMat.from_csr(selfcomm, M, N, ip, cols, vals, add=case.endswith("add"))
+        if case == "coo-add":
+            n = 9000
+            r, c, v = rng.integers(-1, 700, n), rng.integers(-1, 700, n), rng.standard_normal(n)
+            return lambda: DMat.from_coo(selfcomm, 700, 700, r, c, v, add=True)
+        if case == "stencil27":
+            return lambda: DMat.stencil(selfcomm, "poisson3d27", 24, 20, 9)
+        return lambda: DMat.from_csr(selfcomm, 100, 100, golden["sys_indptr"], golden["sys_indices"],
+                                     golden["sys_data"])
+
+    make = build()
+    outs = []
+    for knob in (1, 0):
+        old = L.mx_debug_set(72, knob)
+        try:
+            A = make()
+            d = torch.zeros(A.info()["m"], dtype=torch.float64, device="cuda")
+            A.diagonal(d)
+            outs.append((A.csr(), A.split(), d.cpu().numpy()))
+            A.destroy()
+        finally:
+            L.mx_debug_set(72, old)
+    (c1, s1, d1), (c0, s0, d0) = outs
+    for a, b in zip(c1, c0):
+        assert np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+    for k in s1:
+        assert np.array_equal(np.asarray(s1[k]).view(np.uint8), np.asarray(s0[k]).view(np.uint8)), k
+    assert np.array_equal(d1.view(np.uint64), d0.view(np.uint64))
