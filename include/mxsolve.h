@@ -409,6 +409,11 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         at most 64 entries (1, default; 0: the canonical copy in HBM, then
  *         the split passes -- the path rows longer than 64 always take; the
  *         same arrays bit for bit)
+ * key 74: the 27-point two-line residual update and p.Ap pass split the
+ *         line groups of every plane across the XCDs, in segments of L
+ *         planes, instead of one slab of NZ / 8 planes per XCD, when the
+ *         segments come out longer than the slab (1, default; 0 off):
+ *         C5's share residual update 75.0 -> 72.3 us, p.Ap pass 26.0 -> 24.3
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -726,6 +726,7 @@ __device__ __forceinline__ dbl2 pair_fwd27(const dbl2 (&L)[9], const double (&e)
 
 struct PairLean27Args {
   int n, P, NZ, L, S;
+  int xcol;                    // two-line kernels: XCDs split the line groups (1) instead of the planes (0)
   int anchor[9];
   double *partials;
   const int *done;
@@ -1047,7 +1048,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p_kernel(const PairLean27Ar
 // spmv_pair_zm27p_kernel does (plane27_add, the same groups in the same
 // order): the same row sums.  DOT / PW / RUPD partials then group other rows
 // per wave (to rounding).
-template <int MODE, bool UV, int JM = 0>
+template <int MODE, bool UV, int JM = 0, bool XC = false>
 __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27Args a, const double *__restrict__ x,
                                                                 double *__restrict__ y, const int32_t *__restrict__ pblk,
                                                                 const PairUni27 *__restrict__ puni,
@@ -1079,7 +1080,25 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int sb, se, W, w;
-  if ((gridDim.x & 7) == 0) {
+  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
+  const int D = a.anchor[7], NL = a.anchor[5];           // plane, line
+  const int PL = NL / 128;
+  const int eb = lane == 0 ? -1 : 128;
+  // task t = (segment, line pair lp, x column xx), cp = lp PL + xx: advanced
+  // by W without divisions in the loop (their reciprocals spilled SGPRs).
+  // XC (knob 74, grid a multiple of 8): the XCD owns line pairs [lpb, lpb +
+  // NLP) of every plane (segments of L planes, all of them) instead of a slab
+  // of planes; lp then counts from lpb
+  int NLP = a.P / 2 / PL, lpb = 0;
+  if constexpr (XC) {
+    const int xcd = blockIdx.x & 7, nall = NLP;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    lpb = nall * xcd / 8;
+    NLP = nall * (xcd + 1) / 8 - lpb;
+    sb = 0;
+    se = a.S;
+  } else if ((gridDim.x & 7) == 0) {
     const int xcd = blockIdx.x & 7;
     W = (gridDim.x >> 3) * LEAN_WAVES;
     w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
@@ -1091,17 +1110,16 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27
     sb = 0;
     se = a.S;
   }
-  const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
-  const int D = a.anchor[7], NL = a.anchor[5];           // plane, line
-  const int PL = NL / 128, PH = a.P / 2;
-  const int eb = lane == 0 ? -1 : 128;
-  // task t = (segment, line pair lp, x column xx), cp = lp PL + xx: advanced
-  // by W without divisions in the loop (their reciprocals spilled SGPRs)
-  const int NLP = PH / PL;
+  const int PH = NLP * PL;
+  int lpbv = lpb;
+  if constexpr (XC) asm volatile("" : "+v"(lpbv));
   int seg = sb + w / PH, lp = (w % PH) / PL, xx = w % PL;
   const int dseg = W / PH, dlp = (W % PH) / PL, dx = W % PL;
   for (; seg < se;) {
-    const int colA = lp * 2 * PL + xx, colB = colA + PL;
+    // XC: lpb lives in a VGPR across the march (one SGPR fewer: the kernel
+    // sits at the SGPR bound), the task's column read back to a scalar
+    const int colA = XC ? __builtin_amdgcn_readfirstlane((lpbv + lp) * 2 * PL + xx) : lp * 2 * PL + xx;
+    const int colB = colA + PL;
     const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
     const int cbA = colA * 128 + 2 * lane;               // line y's rows; line y + 1's are + NL
     const uint32_t cwA = (uint32_t)pcol[colA], cwB = (uint32_t)pcol[colB];
@@ -1113,18 +1131,24 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27
     const int lo4[4] = {oA, cbA, cbA + NL, oB};
     dbl2 Lq[4];
     double lo[4], hi[4];
+    auto fetch = [&](int q, dbl2 (&Lr)[4], double (&er)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        Lr[k] = bload2(xr, q * D + lo4[k]);
+        er[k] = bload1(xr, q * D + eo[k]);
+      }
+    };
+    auto shift = [&](const double (&er)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lo[k] = wave_shift<true>(Lq[k].y, er[k]);
+        hi[k] = wave_shift<false>(Lq[k].x, er[k]);
+      }
+    };
     auto load = [&](int q) __attribute__((always_inline)) {
       double e[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        Lq[k] = bload2(xr, q * D + lo4[k]);
-        e[k] = bload1(xr, q * D + eo[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        lo[k] = wave_shift<true>(Lq[k].y, e[k]);
-        hi[k] = wave_shift<false>(Lq[k].x, e[k]);
-      }
+      fetch(q, Lq, e);
+      shift(e);
     };
     auto plane = [&](int k0) __attribute__((always_inline)) {   // lines k0 .. k0 + 2 as one unit's plane
       Plane27 P;
@@ -1213,7 +1237,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27
 // partials group other rows per wave (to rounding).
 // G lines per wave (knob 70 = 2: G = 4, Sell::pair_4l27): the next plane's
 // G + 2 lines per step, G + 1 carried.
-template <bool UV, int G = 2>
+template <bool UV, int G = 2, bool XC = false>
 __global__ void __launch_bounds__(256) spmv_pair_zm27s2l_kernel(const PairLean27Args a, const double *__restrict__ x,
                                                                 const int32_t *__restrict__ pblk,
                                                                 const PairUni27 *__restrict__ puni,
@@ -1237,12 +1261,21 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27s2l_kernel(const PairLean27
   }
   const __amdgpu_buffer_rsrc_t xr = vec_rsrc(x, a.n);
   const int D = a.anchor[7], NL = a.anchor[5];
-  const int PL = NL / 128, PH = a.P / G, NLP = PH / PL;
+  const int PL = NL / 128;
+  int NLP = a.P / G / PL, lpb = 0;
+  if (XC) {                                                // the XCD owns line groups, not planes (knob 74)
+    const int xcd = blockIdx.x & 7, nall = NLP;
+    lpb = nall * xcd / 8;
+    NLP = nall * (xcd + 1) / 8 - lpb;
+    sb = 0;
+    se = a.S;
+  }
+  const int PH = NLP * PL;
   const int eb = lane == 0 ? -1 : 128;
   int seg = sb + w / PH, lp = (w % PH) / PL, xx = w % PL;
   const int dseg = W / PH, dlp = (W % PH) / PL, dx = W % PL;
   for (; seg < se;) {
-    const int colA = lp * G * PL + xx;                     // line y's column; line y + k's is + k PL
+    const int colA = (XC ? lpb + lp : lp) * G * PL + xx;   // line y's column; line y + k's is + k PL
     const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
     const int cbA = colA * 128 + 2 * lane;
     const uint32_t cwA = (uint32_t)pcol[colA], cwZ = (uint32_t)pcol[colA + (G - 1) * PL];
@@ -1259,17 +1292,20 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27s2l_kernel(const PairLean27
       C[k] = bload2(xr, z0 * D + lof(k + 1));
       Ce[k] = bload1(xr, z0 * D + eof(k + 1));
     }
+    auto fetch = [&](int q, dbl2 (&Lr)[G + 2], double (&er)[G + 2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < G + 2; ++k) {
+        Lr[k] = bload2(xr, q * D + lof(k));
+        er[k] = bload1(xr, q * D + eof(k));
+      }
+    };
     for (int z = z0; z < z1; ++z) {
       uint32_t bw[G];
 #pragma unroll
       for (int u = 0; u < G; ++u) bw[u] = (uint32_t)pblk[z * a.P + colA + u * PL];
       dbl2 N[G + 2];
       double Ne[G + 2];
-#pragma unroll
-      for (int k = 0; k < G + 2; ++k) {
-        N[k] = bload2(xr, (z + 1) * D + lof(k));
-        Ne[k] = bload1(xr, (z + 1) * D + eof(k));
-      }
+      fetch(z + 1, N, Ne);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < G; ++u) {
@@ -1745,15 +1781,48 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // the plane-pipelined form (knob 60): column words; the symmetric p.Ap pass
   // keeps the carried-operand kernel
   const bool sym = S.pair_sym27 && g_knobs.pw_sym27;
+  // knob 74: the two-line kernels' XCDs split the line groups of every plane
+  // (segments of L planes) instead of taking a slab of NZ / 8 planes each,
+  // when the waves can still all be busy with segments longer than the
+  // slab: each segment re-reads its one or two leading planes, so short
+  // slabs (C5's share: 8 planes) re-read a quarter of p.  The residual update
+  // keeps zm_tasks' workgroups per CU (4 resident at its 100 VGPRs); the p.Ap
+  // pass takes the requested count (knob 45: 6, resident at 78 VGPRs) --
+  // every count fills whole rounds here.  C5's share: residual update 75.0 ->
+  // 72.3 us, p.Ap pass 26.0 -> 24.3 us (round 5, gpurun_out/r5i, r5j).
+  auto xcol_geom = [&](int G, int &L, int &Sg) -> int {
+    if (!g_knobs.zm27_xcol || b.anchor[5] % 128 != 0 || b.NZ < 16) return 0;
+    int g = zm_tasks(b.P / G, b.NZ, L, Sg, bpc);
+    if (mode == SPMV_PW) g = (bpc * device_cu_count()) & ~7;
+    if (g < 8 || (g & 7)) return 0;
+    const int PL = b.anchor[5] / 128, nlp = b.P / G / PL;
+    const int64_t wx = (int64_t)g / 8 * LEAN_WAVES, cx = (int64_t)(nlp / 8) * PL;
+    if (cx <= 0) return 0;
+    const int segs = (int)std::min<int64_t>(b.NZ, std::max<int64_t>(1, (wx + cx - 1) / cx));
+    const int Lx = (b.NZ + segs - 1) / segs, slab = (b.NZ + 7) / 8;
+    if (Lx <= slab) return 0;
+    L = Lx;
+    Sg = (b.NZ + Lx - 1) / Lx;
+    return g;
+  };
+  auto geom2l = [&](int G) -> int {
+    int L2, S2;
+    const int gx = (mode == SPMV_PW || mode == SPMV_RUPD) ? xcol_geom(G, L2, S2) : 0;
+    if (gx) { b.L = L2; b.S = S2; b.xcol = 1; return gx; }
+    b.xcol = 0;
+    return zm_tasks(b.P / G, b.NZ, b.L, b.S, bpc);
+  };
   // knob 70: two lines per wave (the column words pair up by lines, no ghost units)
   if (form == 2 && g_knobs.zm27_2line && S.pair_2l27 && !split && mode == SPMV_PW && sym) {
     const bool uv2 = S.pair_unit27 && g_knobs.pair_unitv;
     const bool g4 = g_knobs.zm27_2line == 2 && S.pair_4l27;
-    grid = zm_tasks(b.P / (g4 ? 4 : 2), b.NZ, b.L, b.S, bpc);
+    if (g4) { b.xcol = 0; grid = zm_tasks(b.P / 4, b.NZ, b.L, b.S, bpc); }
+    else grid = geom2l(2);
     if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
     using FS = void (*)(PairLean27Args, const double *, const int32_t *, const PairUni27 *, const int32_t *);
     FS fs = g4 ? (uv2 ? &spmv_pair_zm27s2l_kernel<true, 4> : &spmv_pair_zm27s2l_kernel<false, 4>)
-               : (uv2 ? &spmv_pair_zm27s2l_kernel<true, 2> : &spmv_pair_zm27s2l_kernel<false, 2>);
+               : b.xcol ? (uv2 ? &spmv_pair_zm27s2l_kernel<true, 2, true> : &spmv_pair_zm27s2l_kernel<false, 2, true>)
+                        : (uv2 ? &spmv_pair_zm27s2l_kernel<true, 2> : &spmv_pair_zm27s2l_kernel<false, 2>);
     note_dispatch(DSP_ZM_PW);
     launch_timed(fs, grid, st, b, x, S.pblk.p, S.puni27.p, S.pcol27.p);
     HIPCHECK(hipGetLastError());
@@ -1762,13 +1831,19 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   if (form == 2 && g_knobs.zm27_2line && S.pair_2l27 && !split &&
       (mode == SPMV_RUPD || mode == SPMV_DOT || mode == SPMV_PLAIN)) {
     const bool uvp = S.pair_unit27 && g_knobs.pair_unitv;
-    grid = zm_tasks(b.P / 2, b.NZ, b.L, b.S, bpc);
+    grid = geom2l(2);
     if (fold.cnt) { fold.ntotal = fold.ncount = grid; b.fold = fold; }
 #define P2L(MODE, JM) f = uvp ? &spmv_pair_zm27p2l_kernel<MODE, true, JM> : &spmv_pair_zm27p2l_kernel<MODE, false, JM>
     switch (mode) {
       case SPMV_PLAIN: P2L(SPMV_PLAIN, 0); break;
       case SPMV_DOT: P2L(SPMV_DOT, 0); break;
-      default: if (jm == 2) P2L(SPMV_RUPD, 2); else P2L(SPMV_RUPD, 0);
+      default:
+        if (b.xcol) f = jm == 2 ? (uvp ? &spmv_pair_zm27p2l_kernel<SPMV_RUPD, true, 2, true>
+                                        : &spmv_pair_zm27p2l_kernel<SPMV_RUPD, false, 2, true>)
+                                : (uvp ? &spmv_pair_zm27p2l_kernel<SPMV_RUPD, true, 0, true>
+                                       : &spmv_pair_zm27p2l_kernel<SPMV_RUPD, false, 0, true>);
+        else if (jm == 2) P2L(SPMV_RUPD, 2);
+        else P2L(SPMV_RUPD, 0);
     }
 #undef P2L
     note_dispatch(mode == SPMV_RUPD ? DSP_ZM_RUPD : DSP_PAIR_ZM27);
