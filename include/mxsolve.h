@@ -414,6 +414,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         planes, instead of one slab of NZ / 8 planes per XCD, when the
  *         segments come out longer than the slab (1, default; 0 off):
  *         C5's share residual update 75.0 -> 72.3 us, p.Ap pass 26.0 -> 24.3
+ * key 75: workgroups per CU of the key-74 residual update (default 2; 0: the
+ *         slab form's count -- 4 at C5's share: 72.5 against 69.2 us)
+ * key 76: workgroups per CU of the key-74 p.Ap pass (default 3; 0: key 45's
+ *         -- 6: 24.4 against 23.5 us at C5's share)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -547,6 +547,8 @@ int mx_debug_set(int key, int value) {
     case 70: old = g_knobs.zm27_2line; g_knobs.zm27_2line = value; break;
     case 72: old = g_knobs.asm_fused; g_knobs.asm_fused = value; break;
     case 74: old = g_knobs.zm27_xcol; g_knobs.zm27_xcol = value; break;
+    case 75: old = g_knobs.zm27_xcol_ru; g_knobs.zm27_xcol_ru = value; break;
+    case 76: old = g_knobs.zm27_xcol_pw; g_knobs.zm27_xcol_pw = value; break;
     case 69: old = g_knobs.cg_pbw; g_knobs.cg_pbw = value; break;
     case 68: old = g_knobs.ru_2line; g_knobs.ru_2line = value; break;
     case 65: old = g_knobs.zm_balance; g_knobs.zm_balance = value; break;

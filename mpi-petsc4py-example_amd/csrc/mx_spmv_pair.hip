@@ -1786,14 +1786,16 @@ static int zm27_launch(Mat *A, int mode, bool split, bool clean, const double *x
   // when the waves can still all be busy with segments longer than the
   // slab: each segment re-reads its one or two leading planes, so short
   // slabs (C5's share: 8 planes) re-read a quarter of p.  The residual update
-  // keeps zm_tasks' workgroups per CU (4 resident at its 100 VGPRs); the p.Ap
-  // pass takes the requested count (knob 45: 6, resident at 78 VGPRs) --
-  // every count fills whole rounds here.  C5's share: residual update 75.0 ->
-  // 72.3 us, p.Ap pass 26.0 -> 24.3 us (round 5, gpurun_out/r5i, r5j).
+  // runs 2 workgroups per CU (knob 75; 4 are resident at its 100 VGPRs), the
+  // p.Ap pass 3 (knob 76; 6 resident at 78 VGPRs) -- every count fills whole
+  // rounds here, and fewer waves streaming longer segments measured faster:
+  // C5's share, residual update 75.0 -> 72.3 us at 4 per CU -> 69.2 at 2,
+  // p.Ap pass 26.0 -> 24.4 at 6 -> 23.5 at 3 (round 5, gpurun_out/r5i-r5n).
   auto xcol_geom = [&](int G, int &L, int &Sg) -> int {
     if (!g_knobs.zm27_xcol || b.anchor[5] % 128 != 0 || b.NZ < 16) return 0;
     int g = zm_tasks(b.P / G, b.NZ, L, Sg, bpc);
-    if (mode == SPMV_PW) g = (bpc * device_cu_count()) & ~7;
+    const int xb = mode == SPMV_PW ? g_knobs.zm27_xcol_pw : g_knobs.zm27_xcol_ru;   // knobs 76 / 75
+    if (xb > 0) g = (xb * device_cu_count()) & ~7;
     if (g < 8 || (g & 7)) return 0;
     const int PL = b.anchor[5] / 128, nlp = b.P / G / PL;
     const int64_t wx = (int64_t)g / 8 * LEAN_WAVES, cx = (int64_t)(nlp / 8) * PL;
