@@ -418,6 +418,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         slab form's count -- 4 at C5's share: 72.5 against 69.2 us)
  * key 76: workgroups per CU of the key-74 p.Ap pass (default 3; 0: key 45's
  *         -- 6: 24.4 against 23.5 us at C5's share)
+ * key 77: grid of the GMRES MAXPY + norm pass (0, default: 1024 workgroups;
+ *         at most 16384)
+ * key 78: planes per step of the coded z-march (1, default; 2; 0: key 42's)
+ * key 79: workgroups per CU of the coded z-march (0, default: key 40's)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -266,7 +266,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; };
+                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; };
 extern Knobs g_knobs;
 
 struct Halo {

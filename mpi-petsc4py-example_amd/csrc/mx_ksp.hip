@@ -1748,7 +1748,9 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   int *istop = &s->inner_stop;
   Poller poller(A, st);            // its pinned words: the step count (HW_PROGRESS)
   Fold fnorm;                      // ||w||^2 of the MAXPY pass, folded in-launch into s->red[0]
-  fnorm.cnt = s->fold_upd; fnorm.out = sred; fnorm.ntotal = fnorm.ncount = RED_BLOCKS;
+  // MAXPY + norm grid (knob 77; one partial per workgroup, within part's rows)
+  const int xgrid = g_knobs.maxpy_grid > 0 ? std::min<int>(g_knobs.maxpy_grid, (int)std::min<size_t>(npart, 16384)) : RED_BLOCKS;
+  fnorm.cnt = s->fold_upd; fnorm.out = sred; fnorm.ntotal = fnorm.ncount = xgrid;
   while (true) {
     // KSPInitialResidual: vv0 = B (b - A x)
     if (first && !p.guess_nonzero) {
@@ -1776,12 +1778,12 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       c->allreduce_sum(red.p, k + 1);
       // orthogonalisation coefficients + MAXPY + ||w||^2 folded in-launch
       xtimer.begin();
-      launch_timed(&maxpy_norm_kernel, RED_BLOCKS, st, n, vk1, (const double *)V.p, ldv, k + 1, s,
+      launch_timed(&maxpy_norm_kernel, xgrid, st, n, vk1, (const double *)V.p, ldv, k + 1, s,
                    (const double *)red.p, (const double *)vsc.p, hh.p, ld, part.p, fnorm);
       xtimer.end();
       c->allreduce_sum(sred, 1);
       ++launched;
-      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, RED_BLOCKS, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p,
+      gm_step_kernel<<<1, 256, 0, st>>>(s, k, part.p, xgrid, 0, hh.p, ld, grs.p, cc.p, ss.p, hist_d, vsc.p,
                                         poller.hw, launched);
       HIPCHECK(hipGetLastError());
     }

@@ -1972,7 +1972,7 @@ static int pair_code_launch(Mat *A, int mode, bool split, const double *x, doubl
   const int D = zm_plane(A, S.pair_shape, a.anchor);
   a.P = D / 128;
   a.NZ = (int)(A->m / D);
-  const int grid = zm_tasks(a.P, a.NZ, a.L, a.S);
+  const int grid = zm_tasks(a.P, a.NZ, a.L, a.S, g_knobs.zmc_bpc);   // knob 79 (0: key 40's)
   a.partials = partials;
   a.done = done;
   Fold fold = fold_in;
@@ -1983,7 +1983,9 @@ static int pair_code_launch(Mat *A, int mode, bool split, const double *x, doubl
   const PairCodeArgs ca{S.pcode.p, S.vtab.p, S.dtab.p, xscale, jac};
   using F = void (*)(PairLeanArgs, const double *, double *, const int32_t *, PairCodeArgs);
   F f = nullptr;
-  const bool z2 = g_knobs.pair_zm_units == 2;
+  // planes per step (knob 78; 0: key 42's): one measured faster than two at
+  // C4 (46.1 -> 44.0 us per MatMult, round 5 gpurun_out/r5p)
+  const bool z2 = (g_knobs.zmc_units > 0 ? g_knobs.zmc_units : g_knobs.pair_zm_units) == 2;
 #define ZMC_U(MODE, PS, SP, DTV) f = z2 ? &spmv_pair_zmc_kernel<MODE, PS, SP, 2, DTV> : &spmv_pair_zmc_kernel<MODE, PS, SP, 1, DTV>
 #define ZMC_S(MODE, PS, DTV) do { if (split) ZMC_U(MODE, PS, true, DTV); else ZMC_U(MODE, PS, false, DTV); } while (0)
 #define ZMC_P(MODE, DTV) do { if (S.pair_shape == 5) ZMC_S(MODE, 5, DTV); else ZMC_S(MODE, 7, DTV); } while (0)
