@@ -703,7 +703,12 @@ def main():
         # driver's node, so if it fails there (an RCCL error, or no progress
         # for 30 s: knob 33), the eager legs are already measured and the
         # line is still printed from them
+        # mode 5 fuses the direction update into the split p.Ap pass between
+        # x-step batches (knob 80, default on); "mode5sep" keeps the separate
+        # direction update pass (the same bits), so the first 8-GPU run shows
+        # which pays on xGMI
         leg_specs = [("mode2/eager", {9: 2, 7: 1}), ("mode5/eager", {9: 5, 7: 1}),
+                     ("mode5sep/eager", {9: 5, 80: 0, 7: 1}),
                      ("mode2/graph", {9: 2, 7: 2, 33: 30000}), ("mode5/graph", {9: 5, 7: 2, 33: 30000})]
 
     def set_knobs(kn):

@@ -422,6 +422,10 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         at most 16384)
  * key 78: planes per step of the coded z-march (1, default; 2; 0: key 42's)
  * key 79: workgroups per CU of the coded z-march (0, default: key 40's)
+ * key 80: CG mode 5 on P > 1 ranks fuses the direction update into the split
+ *         p.Ap pass on the iterations between x-step batches (the halo pack
+ *         forms the ghost planes' p_i from r and p_{i-1}; the same bits as
+ *         the separate passes): 1 on (default), 0 off
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches
@@ -431,7 +435,8 @@ int mx_debug_set(int key, int value);
  * z-march, 9 retired (round 2's CG mode 4), 10 halo-boundary kernel, 11 / 12
  * CG mode 5's p.Ap and residual-update z-march passes, 13 / 14 coded z-march
  * (split: ghost units), 15 CG mode 5's direction update fused into the p.Ap
- * pass (key 69).  Writes min(n, 16) counts; reset != 0
+ * pass (key 69), 16 the same fused into the split p.Ap pass on P > 1 ranks
+ * (key 80).  Writes min(n, 17) counts; reset != 0
  * zeroes them.  Not a PETSc call: it lets the parity tests show which
  * kernel ran (replayed graph launches are not counted).                     */
 int mx_debug_dispatch_counts(int64_t *out, int n, int reset);

@@ -551,6 +551,7 @@ int mx_debug_set(int key, int value) {
     case 76: old = g_knobs.zm27_xcol_pw; g_knobs.zm27_xcol_pw = value; break;
     case 77: old = g_knobs.maxpy_grid; g_knobs.maxpy_grid = std::min(std::max(value, 0), 16384); break;
     case 78: old = g_knobs.zmc_units; g_knobs.zmc_units = value; break;
+    case 80: old = g_knobs.cg_pbws; g_knobs.cg_pbws = value; break;
     case 79: old = g_knobs.zmc_bpc; g_knobs.zmc_bpc = std::min(std::max(value, 0), 8); break;
     case 69: old = g_knobs.cg_pbw; g_knobs.cg_pbw = value; break;
     case 68: old = g_knobs.ru_2line; g_knobs.ru_2line = value; break;

@@ -266,7 +266,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; };
+                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; int cg_pbws = 1; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -435,7 +435,8 @@ enum Dispatch {
   DSP_PAIR_ZMC = 13,     // spmv_pair_zmc_kernel (coded z-march), one rank / no ghost units
   DSP_PAIR_ZMC_SPLIT = 14,
   DSP_ZM_PBW = 15,       // CG mode 5: the direction update fused into the p.Ap pass (knob 69)
-  DSP_COUNT = 16
+  DSP_ZM_PBWS = 16,      // CG mode 5 on P > 1 ranks: the same fused into the split p.Ap pass (knob 80)
+  DSP_COUNT = 17
 };
 void note_dispatch(int kind);
 extern std::atomic<long long> g_dispatch[DSP_COUNT];
@@ -464,6 +465,15 @@ bool pair_cg5_pbw_applies(const Mat *A, int jac_mode, int xb);
 int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, double *const pb[8], int xb,
                         double *hist, int jac_mode, double jac_c, double *partials, const Fold &fold,
                         hipStream_t st);
+// knob 80: the same on P > 1 ranks with the split p.Ap pass (full rows; the
+// ghost units' diagonal-block sums stored into y for the boundary kernel).
+// cg5_pbws_matmult: the halo pack forms and sends the ghost planes' p_i, the
+// fused pass runs meanwhile, the boundary kernel finishes the ghost rows
+bool pair_cg5_pbws_applies(const Mat *A, int jac_mode, int xb);
+int pair_cg5_pbws_launch(Mat *A, KspState *s, const double *r, double *const pb[8], int xb, double *hist, int jac_mode,
+                         double jac_c, double *y, double *partials, hipStream_t st);
+int cg5_pbws_matmult(Mat *A, KspState *s, const double *r, double *const pb[8], int xb, int it, double *hist,
+                     const Jac &jac, double *y, double *partials, int *done, const Fold *fold);
 // true when matmult_overlap splits the product: interior launch || halo, then
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);

@@ -1434,6 +1434,9 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // knob 69: the direction update rides in mode 5's p.Ap pass (the initial
   // norms then take their own pass over b -- the same bits, see above)
   const bool pbw = fmode == 5 && fused && pair_cg5_pbw_applies(A, dinv.mode, xb);
+  // knob 80: the same on P > 1 ranks, into the split p.Ap pass (the halo pack
+  // forms the ghost planes' p_i)
+  const bool pbws = fmode == 5 && !fused && xb > 1 && pair_cg5_pbws_applies(A, dinv.mode, xb);
   const bool norms_in_pb = fused && xb > 1 && !p.guess_nonzero && !pbw;
   const int ngrid = g_knobs.norm_grid > 0 ? g_knobs.norm_grid : (int)cg_pb_grid(n, wide_pb);
   Fold fin;
@@ -1504,8 +1507,13 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
       double *pi = xb > 1 ? pbs.b[it % xb] : pv.p;
       // knob 69: the iterations between x-step batches (it % xb != 0; the
       // host's it is the device's i) fuse the direction update into the PW pass
-      const bool fuse_pw = pbw && it % xb != 0;
-      if (fuse_pw) {
+      const bool fuse_pw = pbw && it % xb != 0, fuse_pws = pbws && it % xb != 0;
+      if (fuse_pws) {
+        wtimer.begin();
+        nb_spmv = cg5_pbws_matmult(A, s, r.p, pbs.b, xb, it, hist_d, dinv, w.p, part.p, done, fdot_p);
+        wtimer.end();
+        if (!nb_spmv) fail(MX_ERR_INTERNAL, "CG without its direction + p.Ap pass");
+      } else if (fuse_pw) {
         wtimer.begin();
         nb_spmv = pair_cg5_pbw_launch(A, s, r.p, r0, pbs.b, xb, hist_d, dinv.mode, dinv.c, part.p,
                                       fdot_p ? *fdot_p : Fold{}, st);
@@ -1516,7 +1524,7 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
         cg_pb_launch(st, n, s, r.p, dinv, pbs, xb, x, hist_d, r0, part.p, fpb, wide_pb);
         ptimer.end();
       } else cg_p_launch(st, n, s, r.p, dinv, pv.p, defer_x ? x : nullptr, hist_d);
-      if (!fuse_pw) {
+      if (!fuse_pw && !fuse_pws) {
         timer.begin();
         nb_spmv = matmult_overlap(A, pi, w.p, fmode == 5 ? SPMV_PW : SPMV_DOT, Jac{}, part.p, done, nullptr, fdot_p);
         timer.end();

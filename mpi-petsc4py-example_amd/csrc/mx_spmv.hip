@@ -962,6 +962,55 @@ bool matmult_splits(const Mat *A) {
   return A->comm->size > 1 && A->halo.nbnd > 0 && (g_knobs.overlap || pair_forces_split(A));
 }
 
+// CG mode 5 on P > 1 ranks, the iterations between x-step batches (knob 80):
+// the direction update fused into the split p.Ap pass.  The halo pack forms
+// the ghost planes' p_i = z_i + b p_{i-1} from r_i and p_{i-1} (pack_cg_kernel,
+// as CG mode 1 does) and sends it on the comm stream while the fused pass
+// (pair_cg5_pbws_launch) forms every operand the same way, stores p_i and the
+// ghost units' diagonal-block sums; the boundary kernel then continues those
+// rows over the halo from the stored p_i -- the launches, partials and bits of
+// cg_pb_kernel + matmult_overlap(SPMV_PW) without the direction update's pass.
+int cg5_pbws_matmult(Mat *A, KspState *s, const double *r, double *const pb[8], int xb, int it, double *hist,
+                     const Jac &jac, double *y, double *partials, int *done, const Fold *fold) {
+  Comm *c = A->comm;
+  Halo &H = A->halo;
+  hipStream_t st = c->stream;
+  CgFuse cg;
+  cg.r = r;
+  cg.pold = pb[(it + xb - 1) % xb];
+  cg.pnew = pb[it % xb];
+  cg.st = s;
+  cg.hist = hist;
+  cg.jac = jac;
+  int nmain;
+  if (g_knobs.overlap) {
+    hipStream_t cs = c->comm_stream;
+    if (!H.ev_x) {
+      HIPCHECK(hipEventCreateWithFlags(&H.ev_x, hipEventDisableTiming));
+      HIPCHECK(hipEventCreateWithFlags(&H.ev_done, hipEventDisableTiming));
+    }
+    HIPCHECK(hipEventRecord(H.ev_x, st));
+    HIPCHECK(hipStreamWaitEvent(cs, H.ev_x, 0));
+    halo_exchange(A, nullptr, &cg, done, cs);
+    HIPCHECK(hipEventRecord(H.ev_done, cs));
+    nmain = pair_cg5_pbws_launch(A, s, r, pb, xb, hist, jac.mode, jac.c, y, partials, st);
+    HIPCHECK(hipStreamWaitEvent(st, H.ev_done, 0));
+  } else {
+    halo_exchange(A, nullptr, &cg, done, st);
+    nmain = pair_cg5_pbws_launch(A, s, r, pb, xb, hist, jac.mode, jac.c, y, partials, st);
+  }
+  const int nb = std::min(g_knobs.bnd_grid > 0 ? g_knobs.bnd_grid : BND_BLOCKS, (H.nbnd + SPMV_WAVES - 1) / SPMV_WAVES);
+  Fold f;
+  if (fold) { f = *fold; f.ntotal = nmain + nb; f.base = nmain; f.ncount = nb; }
+  double *pbn = partials ? (fold ? partials : partials + nmain) : nullptr;
+  note_dispatch(DSP_BOUNDARY);
+  spmv_boundary_kernel<SPMV_DOT><<<nb, 256, 0, st>>>(A->m, H.bnd_slices.p, H.nbnd, A->so.sptr.p, A->so.width.p,
+                                                    A->so.col.p, A->so.val.p, cg.pnew, H.lvec.p, y, Jac{}, pbn, done,
+                                                    f, nullptr);
+  HIPCHECK(hipGetLastError());
+  return nmain + nb;
+}
+
 int matmult_overlap(Mat *A, const double *x, double *y, int mode, Jac jac, double *partials,
                     int *done_flag, const CgFuse *cg, const Fold *fold, const double *xscale) {
   Comm *c = A->comm;

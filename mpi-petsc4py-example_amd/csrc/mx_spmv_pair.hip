@@ -613,6 +613,129 @@ __global__ void __launch_bounds__(256) spmv_pair_pbw_kernel(const PairLeanArgs a
   block_partials<1>(v, a.partials, gridDim.x, a.fold);
 }
 
+// The direction update fused into CG mode 5's p.Ap pass on P > 1 ranks
+// (knob 80): the split PW pass of spmv_pair_zm_kernel
+// <SPMV_PW, PS, SPLIT = true> -- full rows, the ghost units' diagonal-block
+// sums stored for the boundary kernel -- with every operand it gathers formed
+// as p_i = z_i + b p_{i-1} from r_i and p_{i-1} (cg_dir, the direction
+// update's expression), the centre rows' p_i stored into the direction
+// buffer.  The same units in the same order on the same grid with the same
+// sums: p_i, the stored diagonal-block sums and the p.Ap partials are the
+// separate passes' bits.  The ghost planes' p_i leave through the halo pack,
+// which forms them from r and p_{i-1} too (pack_cg_kernel), before this
+// launch starts; the boundary kernel then reads the stored p_i.
+template <int PS, bool CLEAN, int ZU, int JM>
+__global__ void __launch_bounds__(256) spmv_pair_zmpbs_kernel(const PairLeanArgs a, double *__restrict__ y,
+                                                              const int32_t *__restrict__ pblk,
+                                                              const PairUni *__restrict__ puni, const PairPbArgs pa,
+                                                              int xb) {
+  KspState *s = pa.s;
+  const CgTopIn top = s->top;
+  if (top.done) return;
+  const CgTop t = cg_top(top);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cg_commit_top(s, t, pa.hist);
+  if (t.reason) return;
+  const int i = t.i;
+  const double b = t.b;
+  double *pout = pa.pb + (int64_t)(i % xb) * pa.ps;
+  const double *pprev = pa.pb + (int64_t)((i + xb - 1) % xb) * pa.ps;
+  using SH = PairShape<PS>;
+  constexpr int NR = SH::NR, TR = PS == 5 ? 1 : 2, LAST = NR - 1;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int sb, se, W, w;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    W = (gridDim.x >> 3) * LEAN_WAVES;
+    w = (blockIdx.x >> 3) * LEAN_WAVES + wid;
+    sb = a.S * xcd / 8;
+    se = a.S * (xcd + 1) / 8;
+  } else {
+    W = gridDim.x * LEAN_WAVES;
+    w = blockIdx.x * LEAN_WAVES + wid;
+    sb = 0;
+    se = a.S;
+  }
+  const __amdgpu_buffer_rsrc_t rr = vec_rsrc(pa.r, a.n), pr = vec_rsrc(pprev, a.n);
+  const int D = a.anchor[LAST];
+  const int ecst = lane == 0 ? a.anchor[TR] - 1 : 128 + a.anchor[TR];
+  constexpr uint32_t CARRY = PBLK_RUN0 | (PBLK_RUN0 << TR) | (PBLK_RUN0 << LAST);
+  auto dir1 = [&](double r1, double p1) __attribute__((always_inline)) {
+    return cg_dir(jac1<JM>(r1, 0.0, pa.c), b, p1);
+  };
+  auto dir2 = [&](dbl2 r2, dbl2 p2) __attribute__((always_inline)) { return dbl2{dir1(r2.x, p2.x), dir1(r2.y, p2.y)}; };
+  auto ld2 = [&](int off) __attribute__((always_inline)) { return dir2(bload2(rr, off), bload2(pr, off)); };
+  double dot = 0.0;
+  const int ntask = (se - sb) * a.P;
+  for (int tk = w; tk < ntask; tk += W) {
+    const int seg = sb + tk / a.P, col = tk % a.P;
+    const int z0 = seg * a.L, z1 = min(z0 + a.L, a.NZ);
+    const int cb = col * 128 + 2 * lane;
+    dbl2 zm = ld2(z0 * D + cb - D), c = ld2(z0 * D + cb);
+    uint32_t bwn = (uint32_t)pblk[z0 * a.P + col];
+    auto step = [&](int z, auto nq) __attribute__((always_inline)) {
+      constexpr int NQ = decltype(nq)::value;
+      dbl2 L[NQ][NR], zp[NQ], zr[NQ], zq[NQ], Lr[NQ][NR], Lp[NQ][NR];
+      double e[NQ], er[NQ], ep[NQ];
+      uint32_t bw[NQ];
+      bw[0] = bwn;
+#pragma unroll
+      for (int q = 1; q < NQ; ++q) bw[q] = (uint32_t)pblk[(z + q) * a.P + col];
+      if (z + NQ < z1) bwn = (uint32_t)pblk[(z + NQ) * a.P + col];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r0 = (z + q) * D + cb, ub = (z + q) * D + col * 128;
+        zr[q] = bload2(rr, r0 + D);
+        zq[q] = bload2(pr, r0 + D);
+#pragma unroll
+        for (int r = 1; r < LAST; ++r)
+          if (r != TR) {
+            const int off = r0 + a.anchor[r] + (CLEAN && (bw[q] & (PBLK_RUN0 << r)) ? PAIR_OOR : 0);
+            Lr[q][r] = bload2(rr, off);
+            Lp[q][r] = bload2(pr, off);
+          }
+        int eo = ecst;
+        if constexpr (CLEAN) eo += lane == 0 ? ((bw[q] & PBLK_ELO) ? PAIR_OOR : 0) : ((bw[q] & PBLK_EHI) ? PAIR_OOR : 0);
+        er[q] = bload1(rr, ub + eo);
+        ep[q] = bload1(pr, ub + eo);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        zp[q] = dir2(zr[q], zq[q]);
+#pragma unroll
+        for (int r = 1; r < LAST; ++r)
+          if (r != TR) L[q][r] = dir2(Lr[q][r], Lp[q][r]);
+        e[q] = dir1(er[q], ep[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        L[q][0] = q == 0 ? zm : q == 1 ? c : zp[q - 2];
+        L[q][TR] = q == 0 ? c : zp[q - 1];
+        L[q][LAST] = zp[q];
+        const int r0 = (z + q) * D + cb;
+        *reinterpret_cast<dbl2 *>(pout + r0) = L[q][TR];        // the unit's own p_i
+        if constexpr (CLEAN) {
+          if (bw[q] & CARRY) {                     // wave-uniform, rare: an empty carried run
+            if (bw[q] & PBLK_RUN0) L[q][0] = dbl2{0.0, 0.0};
+            if (bw[q] & (PBLK_RUN0 << TR)) L[q][TR] = dbl2{0.0, 0.0};
+            if (bw[q] & (PBLK_RUN0 << LAST)) L[q][LAST] = dbl2{0.0, 0.0};
+          }
+        }
+        pair_unit<SPMV_PW, PS, true, CLEAN>(L[q], e[q], bw[q], puni, y, r0, lane, dot);
+      }
+      if constexpr (NQ == 1) zm = c;
+      else zm = zp[NQ - 2];
+      c = zp[NQ - 1];
+    };
+    int z = z0;
+    for (; z + ZU <= z1; z += ZU) step(z, std::integral_constant<int, ZU>{});
+    for (; z < z1; ++z) step(z, std::integral_constant<int, 1>{});
+  }
+  double v[1] = {dot};
+  block_partials<1>(v, a.partials, gridDim.x, a.fold);
+}
+
 // 27-point z-march (Sell::puni27).  The nine runs are (dz, dy) in {-1,0,1}^2
 // at anchors -D-n, -D, -D+n, -n, 0, +n, D-n, D, D+n (each a tri run c-1, c,
 // c+1); marching a column in z, the runs of planes z-1 and z (six pairs and
@@ -2150,6 +2273,49 @@ int pair_cg5_pbw_launch(Mat *A, KspState *s, const double *r, const double *r0, 
 #undef PBW
   note_dispatch(DSP_ZM_PBW);
   launch_timed(f, grid, st, a, S.pblk.p, S.puni.p, pa);
+  HIPCHECK(hipGetLastError());
+  return grid;
+}
+
+// knob 80: the P > 1 fused direction update + split p.Ap pass applies (CG
+// mode 5 on a rank whose product splits, a lean 5/7-point z-march layout, no
+// or a uniform Jacobi, x batches of 2 / 4 / 8): 0 off, 1 on (default)
+bool pair_cg5_pbws_applies(const Mat *A, int jac_mode, int xb) {
+  return g_knobs.cg_pbws && A->comm->size > 1 && (xb == 2 || xb == 4 || xb == 8) &&
+         (jac_mode == 0 || jac_mode == 2) && A->sd.pair_shape != 27 && pair_cg5_applies(A, jac_mode) &&
+         matmult_splits(A) && pair_lean_kind(A) > 0 && pair_zm_applies(A);
+}
+
+// the main launch of that pass (the halo and the boundary kernel around it:
+// mx_spmv.hip cg5_pbws_matmult); the PW split pass's grid and tasks
+int pair_cg5_pbws_launch(Mat *A, KspState *s, const double *r, double *const pb[8], int xb, double *hist, int jac_mode,
+                         double jac_c, double *y, double *partials, hipStream_t st) {
+  const Sell &S = A->sd;
+  PairLeanArgs a{};
+  a.m = (int)A->m;
+  a.n = (int)A->n;
+  a.nunits = (int)S.nunits;
+  pair_anchors(S, a.anchor);
+  a.partials = partials;
+  const int NR = S.pair_shape == 5 ? 3 : 5, D = a.anchor[NR - 1];
+  a.P = D / 128;
+  a.NZ = (int)(A->m / D);
+  const int grid = zm_tasks(a.P, a.NZ, a.L, a.S, g_knobs.pw_bpc > 0 ? g_knobs.pw_bpc : g_knobs.pair_zm_bpc);
+  a.fold = Fold{};
+  const PairPbArgs pa{s, r, nullptr, pb[0], pb[1] - pb[0], hist, jac_c};   // (consecutive carves, cg_solve)
+  using Fn = void (*)(const PairLeanArgs, double *, const int32_t *, const PairUni *, const PairPbArgs, int);
+  Fn f;
+  const bool clean = pair_lean_kind(A) == 2, z2 = g_knobs.pair_zm_units == 2;
+#define PBS(PS, CL, JM) f = z2 ? &spmv_pair_zmpbs_kernel<PS, CL, 2, JM> : &spmv_pair_zmpbs_kernel<PS, CL, 1, JM>
+#define PBS_J(PS, CL) do { if (jac_mode == 2) PBS(PS, CL, 2); else PBS(PS, CL, 0); } while (0)
+#define PBS_C(PS) do { if (clean) PBS_J(PS, true); else PBS_J(PS, false); } while (0)
+  if (S.pair_shape == 5) PBS_C(5);
+  else PBS_C(7);
+#undef PBS_C
+#undef PBS_J
+#undef PBS
+  note_dispatch(DSP_ZM_PBWS);
+  launch_timed(f, grid, st, a, y, S.pblk.p, S.puni.p, pa, xb);
   HIPCHECK(hipGetLastError());
   return grid;
 }

@@ -400,14 +400,14 @@ def vmaxpy(comm: DeviceComm, y, alphas, xs):
 
 DISPATCH_KINDS = ("sell", "sell_cg", "pair_lean", "pair_zm", "pair_zm_split", "pair_zm27", "pair_zm27_split",
                   "pair_zmf64", "pair_zmf64_split", "pair_zmcg", "boundary", "zm_pw", "zm_rupd", "pair_zmc",
-                  "pair_zmc_split", "zm_pbw")
+                  "pair_zmc_split", "zm_pbw", "zm_pbws")
 
 
 def dispatch_counts(reset: bool = False) -> dict:
     """Host-side counts of the MatMult-family launches by kernel kind since the
     last reset (mx_debug_dispatch_counts; replayed graph launches not counted)."""
-    out = (C.c_int64 * 16)()
-    call("mx_debug_dispatch_counts", out, 16, int(reset))
+    out = (C.c_int64 * len(DISPATCH_KINDS))()
+    call("mx_debug_dispatch_counts", out, len(DISPATCH_KINDS), int(reset))
     return {k: int(out[i]) for i, k in enumerate(DISPATCH_KINDS)}
 
 

@@ -545,7 +545,7 @@ def _north_star_oracle(oracle_mod, n, P=8):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("n,fuse", [(128, 3), (128, 1), (256, 3), (256, 1)])
+@pytest.mark.parametrize("n,fuse", [(128, 3), (128, 1), (256, 3), (256, 1), (256, 5)])
 def test_north_star_partition_p8(oracle_mod, n, fuse):
     """BASELINE C3's target partition: 3D 7-point n^3 over P = 8 row blocks
     (test.py:68-74's PetscSplitOwnership: n/8 planes per rank, one ghost plane
@@ -602,6 +602,8 @@ def test_north_star_partition_p8(oracle_mod, n, fuse):
     assert dc["pair_zm_split"] >= P and dc["boundary"] >= P
     if fuse == 1:
         assert dc["sell_cg"] >= P * its and dc["pair_zm_split"] == P, dc
+    elif fuse == 5:   # mode 5 with the direction update fused into the split p.Ap pass (knob 80)
+        assert dc["zm_pbws"] >= P * (its // 2) and dc["zm_rupd"] >= P * its and dc["sell_cg"] == 0, dc
     else:             # auto on P > 1 ranks with the z-march: mode 2
         assert dc["sell_cg"] == 0 and dc["pair_zm_split"] >= P * (its + 1), dc
     assert dc["boundary"] >= P * (its + 1)
@@ -665,7 +667,8 @@ def test_c5_p8_weak_scaling_properties():
 @pytest.mark.parametrize("P,kind,n,applies", [(2, "poisson3d", 128, True), (8, "poisson3d", 128, True),
                                               (4, "poisson2d", 512, True), (3, "poisson3d", 64, False)])
 def test_distributed_mode5(oracle_mod, P, kind, n, applies):
-    """CG mode 5 (knob 9 = 5) on P ranks: the p.Ap pass stores only the ghost
+    """CG mode 5 (knob 9 = 5) on P ranks (with the direction update fused into
+    the p.Ap pass between x-step batches, knob 80): the p.Ap pass stores only the ghost
     units' diagonal-block sums, the boundary kernel finishes those rows (A_o
     over the halo) and adds their p.w terms, and the residual update
     recomputes A p on the other units and reads w on the ghost units.  Its and
@@ -705,7 +708,9 @@ def test_distributed_mode5(oracle_mod, P, kind, n, applies):
     its = o["its"]
     if applies:
         assert all(r[3] == 5 for r in res)
-        assert dc["zm_pw"] >= P * its and dc["zm_rupd"] >= P * its and dc["boundary"] >= P * its, dc
+        # (the p.Ap pass, or on the iterations between x-step batches the
+        # direction update fused into it: knob 80)
+        assert dc["zm_pw"] + dc["zm_pbws"] >= P * its and dc["zm_rupd"] >= P * its and dc["boundary"] >= P * its, dc
         assert dc["pair_zm_split"] == 0 and dc["sell"] == 0, dc
     else:
         assert all(r[3] == 2 for r in res) and dc["zm_pw"] == 0 and dc["zm_rupd"] == 0, dc
@@ -815,3 +820,57 @@ def test_c4_p8_partition(oracle_mod, n):
     xs = np.concatenate([r[4] for r in res])
     assert np.linalg.norm(xs - o["x"]) <= REL_TOL * np.linalg.norm(o["x"])
     assert dc["pair_zmc_split"] >= P * o["its"] and dc["boundary"] >= P * o["its"], dc
+
+
+@pytest.mark.parametrize("P,kind,n", [(2, "poisson3d", 128), (4, "poisson2d", 512), (8, "poisson3d", 128),
+                                      (8, "poisson3d", 64)])
+def test_distributed_mode5_fused_direction(oracle_mod, P, kind, n):
+    """CG mode 5 on P ranks with the direction update fused into the split
+    p.Ap pass (knob 80, the iterations between x-step batches: the halo pack
+    forms the ghost planes' p_i from r and p_{i-1}, the fused pass forms every
+    operand and stores p_i and the ghost units' diagonal-block sums, the
+    boundary kernel finishes those rows): every rank's x, its and reason and
+    the residual history bit for bit those of the separate passes (knob 80 =
+    0: cg_pb_kernel + the split p.Ap pass), and its / reason equal to the
+    oracle's P-rank model; the dispatch counts show the fused pass ran."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat, dispatch_counts, rhs_hash
+    ip, c, v = oracle_mod.stencil(kind, n)
+    M = ip.size - 1
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+    o = O.solve(oracle_mod.rhs_hash(0, M), ksp="cg")
+
+    def body(comm):
+        A = DMat.stencil(comm, kind, n)
+        info = A.info()
+        b = comm.empty(info["m"])
+        rhs_hash(comm, info["rstart"], b)
+        x = comm.zeros(info["m"])
+        r = A.solve(b, x, ksp="cg", history=True)
+        out = (r["its"], r["reason"], x.cpu().numpy(), r["cg_mode"], r["history"].copy(), r["cg_xbatch"])
+        A.destroy()
+        return out
+
+    L = _lib.load()
+    outs, dcs = [], []
+    for k80 in (1, 0):
+        old = {k: L.mx_debug_set(k, v) for k, v in ((9, 5), (80, k80))}
+        dispatch_counts(reset=True)
+        try:
+            outs.append(run_ranks(P, body))
+        finally:
+            for k, v in old.items():
+                L.mx_debug_set(k, v)
+        dcs.append(dispatch_counts(reset=True))
+    fused, sep = outs
+    its = o["its"]
+    assert all(r[0] == its and r[1] == o["reason"] for r in fused), ([r[:2] for r in fused], its)
+    for a, b in zip(fused, sep):
+        assert a[0] == b[0] and a[1] == b[1] and a[3] == b[3] == 5 and a[5] == b[5] > 1
+        assert np.array_equal(a[2].view(np.uint64), b[2].view(np.uint64))
+        assert np.array_equal(a[4].view(np.uint64), b[4].view(np.uint64))
+    xs = np.concatenate([r[2] for r in fused])
+    assert np.linalg.norm(xs - o["x"]) / np.linalg.norm(o["x"]) <= REL_TOL
+    xb = fused[0][5]
+    assert dcs[0]["zm_pbws"] >= P * (its - its // xb - 1) and dcs[1]["zm_pbws"] == 0, dcs
+    assert dcs[0]["zm_pw"] < dcs[1]["zm_pw"], dcs
