@@ -828,8 +828,10 @@ def main():
                   "frac": round(bytes_pw / (spmv_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                   # the direction update fused into the p.Ap pass (knob 69; off at 256^3):
                   # r and p_(i-1) in, p_i out
-                  "fused_direction_pass": kernel_frac("spmv_pair_pbw_kernel", rp["pbw_ms"], rp["pbw_count"],
-                                                      24 * m + meta)}
+                  "fused_direction_pass": kernel_frac("spmv_pair_pbw_kernel" if world == 1 else
+                                                      "cg5_pbws_matmult (halo pack + fused split p.Ap pass + "
+                                                      "boundary kernel, HIP events around them)",
+                                                      rp["pbw_ms"], rp["pbw_count"], 24 * m + meta)}
         else:
             bytes_launch = bytes_spmv + (32 * m if mode == 1 else 0)   # SPMV_CG: + r, x r/w, p_i
             avg_ms = spmv_avg_ms
