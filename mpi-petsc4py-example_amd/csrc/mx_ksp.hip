@@ -1371,7 +1371,12 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   // otherwise (the general SELL kernel) 1 up to CG_FUSE_MAX_ROWS local rows, else 2
   int fmode = g_knobs.cg_fuse;
   if (fmode == 3) {
-    if (fused && pair_cg5_applies(A, dinv.mode)) fmode = 5;
+    // mode 5 on one rank; on P > 1 ranks where the direction update fuses
+    // into the split p.Ap pass (knob 80): the N = 2 rehearsal ran 1659 it/s
+    // against mode 2's 1573 (profiles/r05x_shm2_n2.json), the interior-rank
+    // proxy's kernels 63.4 us per iteration against mode 5's separate passes'
+    // 67.2 (round 5, gpurun_out/r5w)
+    if (pair_cg5_applies(A, dinv.mode) && (fused || pair_cg5_pbws_applies(A, dinv.mode, 4))) fmode = 5;
     else if (pair_lean_kind(A) > 0 && pair_zm_applies(A)) fmode = 2;
     else fmode = n <= CG_FUSE_MAX_ROWS ? 1 : 2;
   }

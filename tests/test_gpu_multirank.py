@@ -551,8 +551,10 @@ def test_north_star_partition_p8(oracle_mod, n, fuse):
     (test.py:68-74's PetscSplitOwnership: n/8 planes per rank, one ghost plane
     from each neighbour -- 2 n^2 ghosts on the interior ranks), solved by
     test.py:50's CG + Jacobi with the fusion mode the 8-GPU node runs:
-    fuse 3 = auto (mode 2 with the z-march MatMult: the SPLIT kernel with the
-    ghost units flagged, the boundary kernel finishing them) and mode 1 (the
+    fuse 3 = auto (round 5: mode 5 -- the split p.Ap pass with the direction
+    update fused in between x-step batches, the boundary kernel finishing the
+    ghost units, the residual update recomputing A p), 5 (the same, explicit)
+    and mode 1 (the
     CG-fused general SELL MatMult, halo packed from r / p_{i-1}, the boundary
     kernel; auto before round 3).  MatMult bit-exact, its and reason equal to the
     oracle's P = 8 model, x within rel-L2 1e-10; the dispatch counts show
@@ -602,10 +604,9 @@ def test_north_star_partition_p8(oracle_mod, n, fuse):
     assert dc["pair_zm_split"] >= P and dc["boundary"] >= P
     if fuse == 1:
         assert dc["sell_cg"] >= P * its and dc["pair_zm_split"] == P, dc
-    elif fuse == 5:   # mode 5 with the direction update fused into the split p.Ap pass (knob 80)
+    else:             # mode 5 (auto on P > 1 ranks, round 5) with the direction update
+                      # fused into the split p.Ap pass (knob 80)
         assert dc["zm_pbws"] >= P * (its // 2) and dc["zm_rupd"] >= P * its and dc["sell_cg"] == 0, dc
-    else:             # auto on P > 1 ranks with the z-march: mode 2
-        assert dc["sell_cg"] == 0 and dc["pair_zm_split"] >= P * (its + 1), dc
     assert dc["boundary"] >= P * (its + 1)
 
 
