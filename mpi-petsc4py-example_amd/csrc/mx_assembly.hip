@@ -243,13 +243,16 @@ static int64_t coo_redistribute(Comm *c, const std::vector<int64_t> &rr, int64_t
 // registers; returns keep (this lane holds a canonical entry: column c and,
 // with VALS, its value -- INSERT: the last of its run, ADD: the run folded in
 // input order).  The kept lanes are in ascending column order.
-template <int W, bool VALS>
-__device__ __forceinline__ bool canon_seg(int lane, int l, bool active, int64_t start, int64_t len,
-                                          const int64_t *__restrict__ col, const double *__restrict__ val,
-                                          const int64_t *__restrict__ pos, int64_t N, int add, int *__restrict__ err,
-                                          int64_t &c, double &out) {
-  int64_t p = KEY_DROP;
-  double v = 0.0;
+// canon_load: lane l's input entry (column, input position, value), or the
+// drop key; canon_sorted: canon_seg on loaded entries (the fused count / fill
+// passes load several rows' entries first, then sort each).
+template <bool VALS>
+__device__ __forceinline__ void canon_load(int l, bool active, int64_t start, int64_t len,
+                                           const int64_t *__restrict__ col, const double *__restrict__ val,
+                                           const int64_t *__restrict__ pos, int64_t N, int *__restrict__ err,
+                                           int64_t &c, int64_t &p, double &v) {
+  p = KEY_DROP;
+  v = 0.0;
   c = KEY_DROP;
   if (active && l < len) {
     int64_t cc = col[start + l];
@@ -260,6 +263,24 @@ __device__ __forceinline__ bool canon_seg(int lane, int l, bool active, int64_t 
       if (VALS) v = val[start + l];
     }
   }
+}
+
+template <int W, bool VALS>
+__device__ __forceinline__ bool canon_sorted(int lane, int l, int add, int64_t &c, int64_t p, double v, double &out);
+
+template <int W, bool VALS>
+__device__ __forceinline__ bool canon_seg(int lane, int l, bool active, int64_t start, int64_t len,
+                                          const int64_t *__restrict__ col, const double *__restrict__ val,
+                                          const int64_t *__restrict__ pos, int64_t N, int add, int *__restrict__ err,
+                                          int64_t &c, double &out) {
+  int64_t p;
+  double v;
+  canon_load<VALS>(l, active, start, len, col, val, pos, N, err, c, p, v);
+  return canon_sorted<W, VALS>(lane, l, add, c, p, v, out);
+}
+
+template <int W, bool VALS>
+__device__ __forceinline__ bool canon_sorted(int lane, int l, int add, int64_t &c, int64_t p, double v, double &out) {
   // Already canonical (every kept column above the previous kept column of
   // its row, in input order -- scipy's canonical CSR, the stencil generator):
   // the sort would only move the dropped lanes to the end, which the ballot
@@ -349,6 +370,8 @@ __global__ void __launch_bounds__(256) canon_rows_wave_kernel(
 // split arrays.  No canonical copy of the input goes through HBM (round 4:
 // canonicalise 14.4 GB + split count 3.6 + split fill 12.6 for a 27-point
 // share; fused: 3.6 + 12.6).
+constexpr int CANON_R = 4, CANON_FR = 1;
+
 template <int W>
 __device__ __forceinline__ unsigned long long seg_bits_w(unsigned long long ball, int gbase) {
   return W == 64 ? ball : ((ball >> gbase) & ((1ULL << (W == 64 ? 0 : W)) - 1ULL));
@@ -361,20 +384,36 @@ __global__ void __launch_bounds__(256) canon_count_kernel(int64_t m, const int64
                                                           int64_t cstart, int64_t cend, int64_t *__restrict__ cnt_d,
                                                           int64_t *__restrict__ cnt_o, unsigned *__restrict__ bitmap,
                                                           int *__restrict__ err) {
+  // CANON_R rows per W-lane segment, every row's loads issued before the
+  // first row is sorted (one row per segment left each wave waiting on two
+  // dependent loads at a time: 2.35 ms for a 27-point share, round 5)
   const int lane = threadIdx.x & 63, l = lane % W, gbase = lane - l;
-  const int64_t row = (int64_t)blockIdx.x * (256 / W) + threadIdx.x / W;
-  const bool rv = row < m;
-  const int64_t start = rv ? rowptr[row] : 0;
-  const int64_t len = rv ? rowptr[row + 1] - start : 0;
-  int64_t c;
-  double out;
-  const bool keep = canon_seg<W, false>(lane, l, rv, start, len, col, nullptr, pos, N, add, err, c, out);
-  const bool isd = keep && c >= cstart && c < cend, iso = keep && !isd;
-  if (iso) atomicOr(&bitmap[c >> 5], 1u << (c & 31));
-  const int nd = __popcll(seg_bits_w<W>(__ballot(isd), gbase)), no = __popcll(seg_bits_w<W>(__ballot(iso), gbase));
-  if (rv && l == 0) { cnt_d[row] = nd; cnt_o[row] = no; }
+  const int64_t row0 = (int64_t)blockIdx.x * (256 / W) * CANON_R + threadIdx.x / W;
+  int64_t start[CANON_R], len[CANON_R], c[CANON_R], p[CANON_R];
+  double v[CANON_R];
+#pragma unroll
+  for (int r = 0; r < CANON_R; ++r) {
+    const int64_t row = row0 + (int64_t)r * (256 / W);
+    start[r] = row < m ? rowptr[row] : 0;
+    len[r] = row < m ? rowptr[row + 1] - start[r] : 0;
+  }
+#pragma unroll
+  for (int r = 0; r < CANON_R; ++r)
+    canon_load<false>(l, row0 + (int64_t)r * (256 / W) < m, start[r], len[r], col, nullptr, pos, N, err, c[r], p[r], v[r]);
+#pragma unroll
+  for (int r = 0; r < CANON_R; ++r) {
+    const int64_t row = row0 + (int64_t)r * (256 / W);
+    double out;
+    const bool keep = canon_sorted<W, false>(lane, l, add, c[r], p[r], v[r], out);
+    const bool isd = keep && c[r] >= cstart && c[r] < cend, iso = keep && !isd;
+    if (iso) atomicOr(&bitmap[c[r] >> 5], 1u << (c[r] & 31));
+    const int nd = __popcll(seg_bits_w<W>(__ballot(isd), gbase)), no = __popcll(seg_bits_w<W>(__ballot(iso), gbase));
+    if (row < m && l == 0) { cnt_d[row] = nd; cnt_o[row] = no; }
+  }
 }
 
+// (one row per segment: four, as in the count pass, measured 5.65 ms against
+// 4.4 for a 27-point share -- 99 VGPRs, half the waves)
 template <int W>
 __global__ void __launch_bounds__(256) canon_fill_kernel(
     int64_t m, const int64_t *__restrict__ rowptr, const int64_t *__restrict__ col, const double *__restrict__ val,
@@ -383,30 +422,43 @@ __global__ void __launch_bounds__(256) canon_fill_kernel(
     double *__restrict__ dval, int32_t *__restrict__ ocol, double *__restrict__ oval, double *__restrict__ diag,
     const unsigned *__restrict__ bitmap, const int64_t *__restrict__ wbase) {
   const int lane = threadIdx.x & 63, l = lane % W, gbase = lane - l;
-  const int64_t row = (int64_t)blockIdx.x * (256 / W) + threadIdx.x / W;
-  const bool rv = row < m;
-  const int64_t start = rv ? rowptr[row] : 0;
-  const int64_t len = rv ? rowptr[row + 1] - start : 0;
-  int64_t c;
-  double out;
-  const bool keep = canon_seg<W, true>(lane, l, rv, start, len, col, val, pos, N, add, nullptr, c, out);
-  const bool isd = keep && c >= cstart && c < cend, iso = keep && !isd;
-  const unsigned long long below = l == 0 ? 0ULL : ((1ULL << l) - 1ULL);
-  const unsigned long long bd = seg_bits_w<W>(__ballot(isd), gbase), bo = seg_bits_w<W>(__ballot(iso), gbase);
-  const unsigned long long bg = seg_bits_w<W>(__ballot(isd && c == rstart + row), gbase);
-  if (isd) {
-    const int64_t t = dptr[row] + __popcll(bd & below);
-    dcol[t] = (int32_t)(c - cstart);
-    dval[t] = out;
-    if (c == rstart + row) diag[row] = out;
-  } else if (iso) {
-    const int64_t w = c >> 5;
-    const unsigned bit = (unsigned)(c & 31);
-    const int64_t t = optr[row] + __popcll(bo & below);
-    ocol[t] = (int32_t)(wbase[w] + __popc(bitmap[w] & ((1u << bit) - 1u)));
-    oval[t] = out;
+  const int64_t row0 = (int64_t)blockIdx.x * (256 / W) * CANON_FR + threadIdx.x / W;
+  int64_t start[CANON_FR], len[CANON_FR], c[CANON_FR], p[CANON_FR];
+  double v[CANON_FR];
+#pragma unroll
+  for (int r = 0; r < CANON_FR; ++r) {
+    const int64_t row = row0 + (int64_t)r * (256 / W);
+    start[r] = row < m ? rowptr[row] : 0;
+    len[r] = row < m ? rowptr[row + 1] - start[r] : 0;
   }
-  if (rv && l == 0 && !bg) diag[row] = 0.0;
+#pragma unroll
+  for (int r = 0; r < CANON_FR; ++r)
+    canon_load<true>(l, row0 + (int64_t)r * (256 / W) < m, start[r], len[r], col, val, pos, N, nullptr, c[r], p[r], v[r]);
+#pragma unroll
+  for (int r = 0; r < CANON_FR; ++r) {
+    const int64_t row = row0 + (int64_t)r * (256 / W);
+    const bool rv = row < m;
+    double out;
+    const bool keep = canon_sorted<W, true>(lane, l, add, c[r], p[r], v[r], out);
+    const int64_t cr = c[r];
+    const bool isd = keep && cr >= cstart && cr < cend, iso = keep && !isd;
+    const unsigned long long below = l == 0 ? 0ULL : ((1ULL << l) - 1ULL);
+    const unsigned long long bd = seg_bits_w<W>(__ballot(isd), gbase), bo = seg_bits_w<W>(__ballot(iso), gbase);
+    const unsigned long long bg = seg_bits_w<W>(__ballot(isd && cr == rstart + row), gbase);
+    if (isd) {
+      const int64_t t = dptr[row] + __popcll(bd & below);
+      dcol[t] = (int32_t)(cr - cstart);
+      dval[t] = out;
+      if (cr == rstart + row) diag[row] = out;
+    } else if (iso) {
+      const int64_t w = cr >> 5;
+      const unsigned bit = (unsigned)(cr & 31);
+      const int64_t t = optr[row] + __popcll(bo & below);
+      ocol[t] = (int32_t)(wbase[w] + __popc(bitmap[w] & ((1u << bit) - 1u)));
+      oval[t] = out;
+    }
+    if (rv && l == 0 && !bg) diag[row] = 0.0;
+  }
 }
 
 // Rows longer than 64 entries: one block per row, LDS bitonic sort, then a
@@ -689,14 +741,21 @@ __global__ void garray_kernel(int64_t nw, const unsigned *__restrict__ bitmap,
 // One wave per slice: longest row (SELL width) and, for the diagonal block,
 // the distinct column offsets d = col - row in ascending order (enumerated by
 // repeated wave-min over each lane's sorted row).  Picks the aligned-offset
-// format when 8 k + 4 < 12 w bytes per row.
-__global__ void slice_format_kernel(int64_t m, const int64_t *__restrict__ ptr,
-                                    const int32_t *__restrict__ col, int64_t nslices, int allow_dia,
-                                    int32_t *__restrict__ width, int64_t *__restrict__ slots,
-                                    int32_t *__restrict__ doff) {
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (s >= nslices) return;   // wave-uniform
-  const int lane = threadIdx.x & 63;
+// format when 8 k + 4 < 12 w bytes per row.  The slice's columns are staged
+// in LDS by contiguous loads first: the walk's k dependent steps then wait on
+// LDS, not on a global load each (3.25 ms for a 27-point share when every
+// step went to memory, round 5).  A slice with more entries than the stage
+// walks global memory.
+constexpr int SELL_STAGE = 2048;
+
+__global__ void __launch_bounds__(64) slice_format_kernel(int64_t m, const int64_t *__restrict__ ptr,
+                                                          const int32_t *__restrict__ col, int64_t nslices,
+                                                          int allow_dia, int32_t *__restrict__ width,
+                                                          int64_t *__restrict__ slots, int32_t *__restrict__ doff) {
+  __shared__ int32_t lc[SELL_STAGE];
+  const int64_t s = blockIdx.x;
+  if (s >= nslices) return;   // block-uniform
+  const int lane = threadIdx.x;
   const int64_t row = s * SLICE + lane;
   int64_t a = 0, b = 0;
   if (row < m) { a = ptr[row]; b = ptr[row + 1]; }
@@ -705,9 +764,17 @@ __global__ void slice_format_kernel(int64_t m, const int64_t *__restrict__ ptr,
   for (int o = 32; o > 0; o >>= 1) w = max(w, __shfl_xor(w, o, 64));
   int k = 0;
   if (allow_dia && w > 0) {
+    const int64_t r0 = s * SLICE, r1 = min(m, r0 + SLICE);
+    const int64_t a0 = ptr[r0], cnt = ptr[r1] - a0;
+    const bool staged = cnt <= SELL_STAGE;   // block-uniform
+    if (staged) {
+      for (int64_t e = lane; e < cnt; e += 64) lc[e] = col[a0 + e];
+      __syncthreads();
+    }
     int64_t cur = a;
     while (true) {
-      int my = cur < b ? (int)(col[cur] - row) : INT_MAX;
+      int my = INT_MAX;
+      if (cur < b) my = (int)((staged ? lc[cur - a0] : col[cur]) - row);
       int mn = my;
       for (int o = 32; o > 0; o >>= 1) mn = min(mn, __shfl_xor(mn, o, 64));
       if (mn == INT_MAX) break;
@@ -735,8 +802,8 @@ __device__ __forceinline__ int64_t sell_slot(int64_t base, int j, int w, int lan
 // reads it with contiguous loads and each lane then walks its row in LDS
 // (the global row walks touched 64 lines per load, lanes ~K entries apart:
 // 8.1 ms for a 27-point share, round 5).  One wave per block; a slice with
-// more entries than the staging buffer takes the global walk.
-constexpr int SELL_STAGE = 2048;
+// more entries than the staging buffer takes the global walk.  Aligned-offset
+// slices are filled by sell_fill_dia_kernel (they return at once here).
 
 template <bool PAIRED>
 __global__ void __launch_bounds__(64) sell_fill_lds_kernel(int64_t m, const int64_t *__restrict__ ptr,
@@ -751,11 +818,12 @@ __global__ void __launch_bounds__(64) sell_fill_lds_kernel(int64_t m, const int6
   __shared__ double lv[SELL_STAGE];
   const int64_t s = blockIdx.x;
   if (s >= nslices) return;
+  const int wr = width[s];
+  if (wr < 0) return;                 // aligned-offset slice: sell_fill_dia_kernel
   const int lane = threadIdx.x;
   const int64_t row = s * SLICE + lane;
   const int64_t r0 = s * SLICE, r1 = min(m, r0 + SLICE);
   const int64_t a0 = ptr[r0], cnt = ptr[r1] - a0;
-  const int wr = width[s];
   const int64_t base = sptr[s];
   const int64_t rs = row < m ? ptr[row] : a0;
   const int len = row < m ? (int)(ptr[row + 1] - rs) : 0;
@@ -766,20 +834,6 @@ __global__ void __launch_bounds__(64) sell_fill_lds_kernel(int64_t m, const int6
   }
   const int32_t *__restrict__ rc = staged ? lc + (rs - a0) : ccol + rs;
   const double *__restrict__ rvv = staged ? lv + (rs - a0) : cval + rs;
-  if (wr < 0) {                       // aligned-offset slice
-    const int k = -wr;
-    uint32_t mk = 0;
-    int cur = 0;
-    for (int j = 0; j < k; ++j) {
-      const int off = doff[s * DIA_MAX + j];
-      const bool hit = cur < len && (int64_t)rc[cur] - row == off;
-      sval[sell_slot(base, j, k, lane, PAIRED)] = hit ? rvv[cur] : 0.0;
-      if (hit) { mk |= 1u << j; ++cur; }
-    }
-    if (mask8) mask8[row] = (uint8_t)mk;
-    else mask[row] = mk;
-    return;
-  }
   const int w = wr;
   for (int j = 0; j < w; ++j) {
     const bool in = j < len;
@@ -927,17 +981,6 @@ __device__ __forceinline__ unsigned vdict_hash(unsigned long long k) {
   return (unsigned)((k * 0x9E3779B97F4A7C15ULL) >> 52);   // 12 bits
 }
 
-__device__ __forceinline__ int vdict_find(const unsigned long long *__restrict__ tab, unsigned long long k) {
-  unsigned h = vdict_hash(k);
-  for (int probe = 0; probe < VDICT_SLOTS; ++probe) {
-    const unsigned long long c = tab[h];
-    if (c == k) return (int)h;
-    if (c == VDICT_EMPTY) return -1;
-    h = (h + 1) & (VDICT_SLOTS - 1);
-  }
-  return -1;
-}
-
 // one wave per slice, the slots a row stores (absent aligned-offset slots
 // and padding skipped).  st[0] = distinct values inserted, st[1] = overflow
 // (too many, or a value with the empty pattern).  A plain read that sees
@@ -962,14 +1005,112 @@ __device__ __forceinline__ bool slot_stored(int wr, uint32_t mk, const int32_t *
   return wr < 0 ? ((mk >> j) & 1u) != 0 : col[t] >= 0;
 }
 
+// The aligned-offset slices' fill (paired slot order), one slice per 256-thread
+// block: the slice's CSR entries are read in order by contiguous loads, each
+// placed in an LDS image of the slice's k x 64 slots by its row (a search of
+// the slice's row starts) and its offset's rank in the slice's ascending list
+// (a search of doff), with the row's presence bit; then the image is written
+// out as 16-byte slot pairs, absent slots 0.0.  The same slots and masks as a
+// per-row walk (every entry's offset is in the list, which slice_format_kernel
+// enumerated from these rows), without a wave walking 64 rows ~k entries apart
+// (6.4 ms for a 27-point share at 6 waves per CU, round 5).  With tab set it
+// also collects the value dictionary (vdict_insert_kernel's table, which then
+// skips these slices): the slice's stored values go through an LDS set first,
+// a plain read before any CAS, so a value the slice repeats costs one LDS
+// read, and only the slice's distinct values reach the global table.
+__global__ void __launch_bounds__(256) sell_fill_dia_kernel(int64_t m, const int64_t *__restrict__ ptr,
+                                                            const int32_t *__restrict__ ccol,
+                                                            const double *__restrict__ cval, int64_t nslices,
+                                                            const int64_t *__restrict__ sptr,
+                                                            const int32_t *__restrict__ width,
+                                                            const int32_t *__restrict__ doff, double *__restrict__ sval,
+                                                            uint32_t *__restrict__ mask, uint8_t *__restrict__ mask8,
+                                                            unsigned long long *tab, int *vst) {
+  constexpr int VS_N = 64;
+  __shared__ double img[DIA_MAX * SLICE];
+  __shared__ unsigned long long vs[VS_N];
+  __shared__ int32_t rs[SLICE + 1], dl[DIA_MAX];
+  __shared__ uint32_t mk[SLICE];
+  const int64_t s = blockIdx.x;
+  if (s >= nslices) return;
+  const int wr = width[s];
+  if (wr >= 0) return;                // block-uniform: a SELL slice
+  const int k = -wr, t = threadIdx.x;
+  const int64_t r0 = s * SLICE, r1 = min(m, r0 + SLICE);
+  const int nr = (int)(r1 - r0);
+  const int64_t a0 = ptr[r0];
+  if (t <= SLICE) rs[t] = (int32_t)(ptr[r0 + min(t, nr)] - a0);
+  if (t < SLICE) mk[t] = 0u;
+  if (t < k) dl[t] = doff[s * DIA_MAX + t];
+  if (t < VS_N) vs[t] = VDICT_EMPTY;
+  __syncthreads();
+  const int cnt = rs[SLICE];
+  for (int e = t; e < cnt; e += 256) {
+    const int32_t c = ccol[a0 + e];
+    const double v = cval[a0 + e];
+    int lo = 0, hi = nr - 1;                      // the last row starting at or before e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (rs[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const int off = (int)((int64_t)c - (r0 + lo));
+    int jl = 0, jh = k - 1;                       // off's rank in the ascending list
+    while (jl < jh) {
+      const int mid = (jl + jh) >> 1;
+      if (dl[mid] < off) jl = mid + 1; else jh = mid;
+    }
+    img[jl * SLICE + lo] = v;
+    atomicOr(&mk[lo], 1u << jl);
+  }
+  __syncthreads();
+  if (tab && !*(volatile int *)(vst + 1)) {       // block-uniform
+    for (int q = t; q < k * SLICE; q += 256) {
+      const int j = q / SLICE, l = q % SLICE;
+      if (!((mk[l] >> j) & 1u)) continue;
+      const unsigned long long key = (unsigned long long)__double_as_longlong(img[q]);
+      if (key == VDICT_EMPTY) { vst[1] = 1; continue; }
+      unsigned h = vdict_hash(key) & (VS_N - 1);
+      bool done = false;
+      for (int probe = 0; probe < VS_N && !done; ++probe) {
+        unsigned long long c = vs[h];
+        if (c == VDICT_EMPTY) c = atomicCAS(&vs[h], VDICT_EMPTY, key);
+        done = c == VDICT_EMPTY || c == key;
+        h = (h + 1) & (VS_N - 1);
+      }
+      if (!done && !vdict_insert(tab, vst, key)) vst[1] = 1;   // the LDS set full: straight to the table
+    }
+    __syncthreads();
+    if (t < VS_N && vs[t] != VDICT_EMPTY && !vdict_insert(tab, vst, vs[t])) vst[1] = 1;
+  }
+  const int64_t base = sptr[s];
+  const int np = k >> 1;
+  for (int q = t; q < np * SLICE; q += 256) {     // slot pairs (2 jp, 2 jp + 1) of row l
+    const int jp = q / SLICE, l = q % SLICE, j = 2 * jp;
+    const uint32_t b = mk[l];
+    const double v0 = (b >> j) & 1u ? img[j * SLICE + l] : 0.0;
+    const double v1 = (b >> (j + 1)) & 1u ? img[(j + 1) * SLICE + l] : 0.0;
+    *reinterpret_cast<double2 *>(sval + base + (int64_t)jp * 2 * SLICE + 2 * l) = make_double2(v0, v1);
+  }
+  if (k & 1) {                                    // the odd last slot, one per row
+    const int j = k - 1;
+    for (int l = t; l < SLICE; l += 256) sval[base + (int64_t)np * 2 * SLICE + l] = (mk[l] >> j) & 1u ? img[j * SLICE + l] : 0.0;
+  }
+  if (t < SLICE) {                                // rows past m: 0, as their slots
+    if (mask8) mask8[r0 + t] = (uint8_t)mk[t];
+    else mask[r0 + t] = mk[t];
+  }
+}
+
+// (skip_dia: the aligned-offset slices' values were collected by sell_fill_dia_kernel)
 __global__ void vdict_insert_kernel(int64_t ns, const int64_t *__restrict__ sptr, const int32_t *__restrict__ width,
                                     const int32_t *__restrict__ col, const double *__restrict__ sval,
                                     const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8,
-                                    unsigned long long *tab, int *st) {
+                                    unsigned long long *tab, int *st, int skip_dia) {
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= ns || *(volatile int *)(st + 1)) return;
   const int lane = threadIdx.x & 63;
   const int wr = width[s];
+  if (skip_dia && wr < 0) return;
   const int w = wr < 0 ? -wr : wr;
   const int64_t row = s * SLICE + lane;
   const uint32_t mk = wr >= 0 ? 0u : (mask8 ? (uint32_t)mask8[row] : mask[row]);
@@ -992,40 +1133,6 @@ __global__ void code_bytes_kernel(int64_t ns, const int32_t *__restrict__ width,
   if (s >= ns) return;
   const int w = width[s] < 0 ? -width[s] : width[s];
   cb[s] = (int64_t)((w + 7) / 8) * CODE_BATCH;
-}
-
-// one wave per slice: lane = row, 8 slots per 8-byte word; absent slots of
-// aligned-offset rows and slots past the width get VCODE_ABSENT (the table
-// holds 0.0 there)
-__global__ void code_fill_kernel(int64_t ns, const int64_t *__restrict__ sptr, const int32_t *__restrict__ width,
-                                 const int32_t *__restrict__ col,
-                                 const double *__restrict__ sval, const int64_t *__restrict__ cptr,
-                                 const unsigned long long *__restrict__ tab, const uint8_t *__restrict__ slot_code,
-                                 const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8,
-                                 uint8_t *__restrict__ code) {
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (s >= ns) return;
-  const int lane = threadIdx.x & 63;
-  const int wr = width[s];
-  const int w = wr < 0 ? -wr : wr;
-  const int64_t base = sptr[s];
-  const int64_t row = s * SLICE + lane;
-  const uint32_t mk = wr >= 0 ? 0u : (mask8 ? (uint32_t)mask8[row] : mask[row]);
-  for (int b = 0; b < (w + 7) / 8; ++b) {
-    unsigned long long word = 0;
-    for (int q = 0; q < 8; ++q) {
-      const int j = 8 * b + q;
-      unsigned long long c = VCODE_ABSENT;
-      const int64_t t = j < w ? sell_slot(base, j, w, lane, true) : 0;
-      if (j < w && slot_stored(wr, mk, col, t, j)) {
-        const double v = sval[t];
-        const int h = vdict_find(tab, (unsigned long long)__double_as_longlong(v));
-        c = h >= 0 ? slot_code[h] : 0;
-      }
-      word |= c << (8 * q);
-    }
-    reinterpret_cast<unsigned long long *>(code + cptr[s] + (int64_t)b * CODE_BATCH)[lane] = word;
-  }
 }
 
 // ---------------------------------------------------------------- row pairs
@@ -1062,31 +1169,80 @@ static int pair_shape_of(const std::vector<int32_t> &o) {
 
 constexpr int pair_bytes(int k) { return (2 * k + 15) / 16 * 16; }
 
-// one wave per unit; sets DPAT_PAIR on slice 2u and writes the unit's codes.
-// The slot mapping (dominant slot j -> slot of the slice's own pattern, and
-// whether a pattern's offsets all belong to the dominant one) is a per-pattern
-// table built on the host, and each code is read from the slice's code block
-// (code_fill_kernel's bytes, VCODE_ABSENT where the row lacks the slot) rather
-// than looked up again by value; the lane's 2K codes go out as 8-byte words.
-// (Round 4's form scanned the patterns and probed the value table per slot and
-// stored single bytes: 16.3 ms for a 27-point share.)
-__global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, const int32_t *__restrict__ width,
-                                 int32_t *__restrict__ dpat, const int8_t *__restrict__ pmap,
-                                 const uint8_t *__restrict__ pok, const int64_t *__restrict__ cptr,
-                                 const uint8_t *__restrict__ code, uint8_t *__restrict__ pcode) {
-  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (u >= nunits) return;
-  const int lane = threadIdx.x & 63;
+// Value codes and row-pair codes in one pass, one 128-thread block per unit
+// (slices 2u and 2u + 1, a wave each).  Each wave writes its slice's code
+// words (lane = row, 8 slots per 8-byte word; absent slots of aligned-offset
+// rows and slots past the width get VCODE_ABSENT, whose table entry is 0.0)
+// and keeps an aligned-offset slice's codes in LDS.  A pair unit then gathers
+// its lanes' 2K codes from there by a per-pattern slot map built on the host
+// (dominant slot j -> the slot of the slice's own pattern, and whether the
+// pattern's offsets all belong to the dominant one), writes them as 8-byte
+// words and sets DPAT_PAIR on slice 2u.  Round 4's pair fill scanned the
+// patterns and probed the value table per slot with single-byte stores
+// (16.3 ms for a 27-point share); round 5's separate pass read each code
+// back with a byte load (1.7 ms).  pcode = nullptr: code words only.
+__global__ void __launch_bounds__(128) code_pair_fill_kernel(
+    int64_t m, int64_t ns, const int64_t *__restrict__ sptr, const int32_t *__restrict__ width,
+    const int32_t *__restrict__ col, const double *__restrict__ sval, const int64_t *__restrict__ cptr,
+    const unsigned long long *__restrict__ keys, int ntab, const uint32_t *__restrict__ mask, const uint8_t *__restrict__ mask8, uint8_t *__restrict__ code,
+    int64_t nunits, int k, int32_t *__restrict__ dpat, const int8_t *__restrict__ pmap,
+    const uint8_t *__restrict__ pok, uint8_t *__restrict__ pcode) {
+  __shared__ uint8_t lcode[2][DIA_MAX][SLICE];
+  __shared__ unsigned long long kl[VCODE_MAX];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t u = blockIdx.x, s = 2 * u + wv;
+  for (int i = threadIdx.x; i < ntab; i += 128) kl[i] = keys[i];
+  __syncthreads();
+  // a value's code: its rank among the sorted keys (S.vtab's order), 0 if absent
+  auto code_of = [&](double v) -> unsigned long long {
+    const unsigned long long key = (unsigned long long)__double_as_longlong(v);
+    int lo = 0, hi = ntab;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (kl[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo < ntab && kl[lo] == key ? (unsigned long long)lo : 0ULL;
+  };
+  if (s < ns) {
+    const int wr = width[s];
+    const int w = wr < 0 ? -wr : wr;
+    const int64_t base = sptr[s];
+    const int64_t row = s * SLICE + lane;
+    const uint32_t mk = wr >= 0 ? 0u : (mask8 ? (uint32_t)mask8[row] : mask[row]);
+    for (int b = 0; b < (w + 7) / 8; ++b) {
+      unsigned long long word = 0;
+      for (int q = 0; q < 8; q += 2) {
+        const int j = 8 * b + q;
+        unsigned long long c[2] = {VCODE_ABSENT, VCODE_ABSENT};
+        if (wr < 0 && j + 1 < w) {                 // an aligned-offset slot pair: one 16-byte load
+          const double2 v2 = *reinterpret_cast<const double2 *>(sval + sell_slot(base, j, w, lane, true));
+          if ((mk >> j) & 1u) c[0] = code_of(v2.x);
+          if ((mk >> (j + 1)) & 1u) c[1] = code_of(v2.y);
+        } else {
+          for (int h = 0; h < 2; ++h) {
+            const int64_t t = j + h < w ? sell_slot(base, j + h, w, lane, true) : 0;
+            if (j + h < w && slot_stored(wr, mk, col, t, j + h)) c[h] = code_of(sval[t]);
+          }
+        }
+        for (int h = 0; h < 2; ++h) {
+          if (wr < 0 && j + h < w) lcode[wv][j + h][lane] = (uint8_t)c[h];
+          word |= c[h] << (8 * (q + h));
+        }
+      }
+      reinterpret_cast<unsigned long long *>(code + cptr[s] + (int64_t)b * CODE_BATCH)[lane] = word;
+    }
+  }
+  if (!pcode || u >= nunits) return;   // block-uniform
+  __syncthreads();
   const int64_t s0 = 2 * u, s1 = s0 + 1;
-  if (u * 128 + 127 >= m || width[s0] >= 0 || width[s1] >= 0) return;   // wave-uniform
+  if (u * 128 + 127 >= m || width[s0] >= 0 || width[s1] >= 0) return;   // block-uniform
   const int p0 = dpat[s0] & DPAT_ID, p1 = dpat[s1] & DPAT_ID;
   if (!pok[p0] || !pok[p1]) return;
-  const int64_t sl = lane < 32 ? s0 : s1;
-  const int8_t *__restrict__ mp = pmap + (int64_t)(lane < 32 ? p0 : p1) * DIA_MAX;
-  const uint8_t *__restrict__ cb = code + cptr[sl];
+  const int hs = lane < 32 ? 0 : 1;
+  const int8_t *__restrict__ mp = pmap + (int64_t)(hs ? p1 : p0) * DIA_MAX;
   const int pb = pair_bytes(k);
   unsigned long long *dst = reinterpret_cast<unsigned long long *>(pcode + (u * 64 + lane) * pb);
-  for (int w = 0; w < pb / 8; ++w) {
+  for (int w = wv; w < pb / 8; w += 2) {
     unsigned long long word = 0;
     for (int t = 0; t < 8; ++t) {
       const int idx = 8 * w + t;
@@ -1094,14 +1250,13 @@ __global__ void pair_fill_kernel(int64_t m, int64_t nunits, int k, const int32_t
       if (idx < 2 * k) {
         const int h = idx >= k ? 1 : 0;
         const int q = mp[idx - h * k];
-        const int li = (2 * lane + h) & 63;
-        if (q >= 0) c = cb[(int64_t)(q >> 3) * CODE_BATCH + 8 * li + (q & 7)];
+        if (q >= 0) c = lcode[hs][q][(2 * lane + h) & 63];
       }
       word |= c << (8 * t);
     }
     dst[w] = word;
   }
-  if (lane == 0) dpat[s0] |= DPAT_PAIR;
+  if (threadIdx.x == 0) dpat[s0] |= DPAT_PAIR;
 }
 
 // fp64 row pairs (Sell::pval / pflag): one wave per unit, the pair_fill_kernel
@@ -1637,16 +1792,31 @@ static void build_pair_col27(Sell &S, int64_t m, hipStream_t st) {
   S.pair_sym27 = sym;
 }
 
-static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st) {
+// The value dictionary's open-addressing table, set up before the diagonal
+// block's SELL fill, which collects the aligned-offset slices' values into it
+struct VDict {
+  DBuf<unsigned long long> tab;
+  DBuf<int> stat;
+  bool dia_done = false;   // sell_fill_dia_kernel inserted the aligned-offset slices' values
+  void init(hipStream_t st) {
+    tab.alloc(VDICT_SLOTS);
+    stat.alloc(2);
+    const std::vector<unsigned long long> th(VDICT_SLOTS, VDICT_EMPTY);
+    HIPCHECK(hipMemcpyAsync(tab.p, th.data(), sizeof(unsigned long long) * VDICT_SLOTS, hipMemcpyHostToDevice, st));
+    HIPCHECK(hipMemsetAsync(stat.p, 0, 2 * sizeof(int), st));
+    HIPCHECK(hipStreamSynchronize(st));   // th is freed on return
+  }
+};
+
+static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t ncols, hipStream_t st, VDict &vd) {
   S.ntab = 0;
-  if (S.slots == 0 || !g_knobs.vcodes) return;
-  DBuf<unsigned long long> tab(VDICT_SLOTS);
-  DBuf<int> stat(2);
+  if (S.slots == 0 || !g_knobs.vcodes || !vd.tab.p) return;
+  DBuf<unsigned long long> &tab = vd.tab;
+  DBuf<int> &stat = vd.stat;
   std::vector<unsigned long long> th(VDICT_SLOTS, VDICT_EMPTY);
-  HIPCHECK(hipMemcpyAsync(tab.p, th.data(), sizeof(unsigned long long) * VDICT_SLOTS, hipMemcpyHostToDevice, st));
-  HIPCHECK(hipMemsetAsync(stat.p, 0, 2 * sizeof(int), st));
-  vdict_insert_kernel<<<(unsigned)cdiv(S.nslices, 4), 256, 0, st>>>(S.nslices, S.sptr.p, S.width.p, S.col.p, S.val.p,
-                                                                  S.mask.p, S.mask8.p, tab.p, stat.p);
+  if (!vd.dia_done || S.dia_slices < S.nslices)
+    vdict_insert_kernel<<<(unsigned)cdiv(S.nslices, 4), 256, 0, st>>>(S.nslices, S.sptr.p, S.width.p, S.col.p, S.val.p,
+                                                                    S.mask.p, S.mask8.p, tab.p, stat.p, vd.dia_done ? 1 : 0);
   HIPCHECK(hipGetLastError());
   int sh[2];
   HIPCHECK(hipMemcpyAsync(sh, stat.p, sizeof(sh), hipMemcpyDeviceToHost, st));
@@ -1658,10 +1828,6 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
   for (unsigned long long k : th)
     if (k != VDICT_EMPTY) keys.push_back(k);
   std::sort(keys.begin(), keys.end());
-  std::vector<uint8_t> slot_code(VDICT_SLOTS, 0);
-  for (int h = 0; h < VDICT_SLOTS; ++h)
-    if (th[h] != VDICT_EMPTY)
-      slot_code[h] = (uint8_t)(std::lower_bound(keys.begin(), keys.end(), th[h]) - keys.begin());
   std::vector<double> vt(VCODE_MAX, 0.0);
   for (size_t i = 0; i < keys.size(); ++i) std::memcpy(&vt[i], &keys[i], sizeof(double));
   const int64_t ns = S.nslices;
@@ -1671,8 +1837,6 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
   exclusive_scan_i64(S.cptr.p, S.cptr.p, ns, st, &S.code_bytes);
   S.code.alloc((size_t)std::max<int64_t>(S.code_bytes, 8));
   S.vtab.alloc(VCODE_MAX);
-  DBuf<uint8_t> sc(VDICT_SLOTS);
-  HIPCHECK(hipMemcpyAsync(sc.p, slot_code.data(), VDICT_SLOTS, hipMemcpyHostToDevice, st));
   HIPCHECK(hipMemcpyAsync(S.vtab.p, vt.data(), sizeof(double) * vt.size(), hipMemcpyHostToDevice, st));
   {
     // jacobi_setup_kernel's dinv = d == 0 ? 1 : 1 / d, per code (IEEE division,
@@ -1682,18 +1846,17 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
     S.dtab.alloc(VCODE_MAX);
     HIPCHECK(hipMemcpyAsync(S.dtab.p, dt.data(), sizeof(double) * dt.size(), hipMemcpyHostToDevice, st));
   }
-  code_fill_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(ns, S.sptr.p, S.width.p, S.col.p, S.val.p, S.cptr.p, tab.p, sc.p,
-                                                          S.mask.p, S.mask8.p, S.code.p);
-  HIPCHECK(hipGetLastError());
   // row pairs read the operand through buffer loads with 32-bit byte offsets
   S.pair_shape = g_knobs.spmv_pairs && S.pat_star >= 0 && m < PAIR_MAX_ROWS && ncols < PAIR_MAX_ROWS
                      ? pair_shape_of(S.pat_star_off) : 0;
+  DBuf<int8_t> pmd;
+  DBuf<uint8_t> pkd;
   if (S.pair_shape) {
     S.nunits = ns / 2;
     S.pcode.alloc((size_t)std::max<int64_t>(S.nunits, 1) * 64 * pair_bytes(S.dia_k));
     if (S.nunits) {
       // per pattern: where each dominant slot sits in it, and whether its
-      // offsets are all dominant ones (pair_fill_kernel)
+      // offsets are all dominant ones (code_pair_fill_kernel)
       const int64_t np = S.npat;
       if ((int64_t)S.pat_len.size() != np) fail(MX_ERR_INTERNAL, "row pairs without shared offset patterns");
       std::vector<int8_t> pm((size_t)np * DIA_MAX, -1);
@@ -1712,15 +1875,19 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
         }
         pk[(size_t)p] = ok ? 1 : 0;
       }
-      DBuf<int8_t> pmd(pm.size());
-      DBuf<uint8_t> pkd(pk.size());
+      pmd.alloc(pm.size());
+      pkd.alloc(pk.size());
       HIPCHECK(hipMemcpyAsync(pmd.p, pm.data(), pm.size(), hipMemcpyHostToDevice, st));
       HIPCHECK(hipMemcpyAsync(pkd.p, pk.data(), pk.size(), hipMemcpyHostToDevice, st));
-      pair_fill_kernel<<<(unsigned)cdiv(S.nunits, 4), 256, 0, st>>>(m, S.nunits, S.dia_k, S.width.p, S.dpat.p, pmd.p,
-                                                                   pkd.p, S.cptr.p, S.code.p, S.pcode.p);
-      HIPCHECK(hipGetLastError());
-      HIPCHECK(hipStreamSynchronize(st));   // pmd / pkd are freed on return
+      HIPCHECK(hipStreamSynchronize(st));   // pm / pk are freed at the end of this block
     }
+  }
+  code_pair_fill_kernel<<<(unsigned)cdiv(ns, 2), 128, 0, st>>>(
+      m, ns, S.sptr.p, S.width.p, S.col.p, S.val.p, S.cptr.p,
+      reinterpret_cast<const unsigned long long *>(S.vtab.p), (int)keys.size(), S.mask.p, S.mask8.p, S.code.p,
+      S.pair_shape ? S.nunits : 0, S.dia_k, S.dpat.p, pmd.p, pkd.p, S.pair_shape && S.nunits ? S.pcode.p : nullptr);
+  HIPCHECK(hipGetLastError());
+  if (S.pair_shape) {
     HIPCHECK(hipGetLastError());
     {
       DBuf<unsigned long long> cnt(1);
@@ -1752,19 +1919,34 @@ static void build_value_codes(Sell &S, const int32_t *wid_o, int64_t m, int64_t 
     S.pair_all = S.pair_used == m / 128;
     if (g_knobs.pair_col27) build_pair_col27(S, m, st);
   }
-  HIPCHECK(hipStreamSynchronize(st));   // tab / sc are freed on return
+  HIPCHECK(hipStreamSynchronize(st));   // the host tables are freed on return
   S.ntab = (int)keys.size();
 }
 
 static void build_sell(Sell &S, int64_t m, int64_t ncols, const int64_t *ptr, const int32_t *col,
-                       const double *val, hipStream_t st, bool allow_dia) {
+                       const double *val, hipStream_t st, bool allow_dia, VDict *vd = nullptr) {
   S.nslices = cdiv(m, SLICE);
   const int64_t ns = S.nslices;
   S.width.alloc((size_t)std::max<int64_t>(ns, 1));
   S.sptr.alloc((size_t)std::max<int64_t>(ns, 1));
   S.doff.alloc((size_t)std::max<int64_t>(allow_dia ? ns * DIA_MAX : 1, 1));
   if (ns == 0) { S.slots = 0; S.mask.alloc(1); return; }
-  slice_format_kernel<<<(unsigned)cdiv(ns, 4), 256, 0, st>>>(m, ptr, col, ns, allow_dia ? 1 : 0, S.width.p,
+  if (!allow_dia) {   // an off-diagonal block with no entries (one rank): every width 0, nothing to fill
+    int64_t nnz = 0;
+    HIPCHECK(hipMemcpyAsync(&nnz, ptr + m, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (nnz == 0) {
+      HIPCHECK(hipMemsetAsync(S.width.p, 0, sizeof(int32_t) * ns, st));
+      HIPCHECK(hipMemsetAsync(S.sptr.p, 0, sizeof(int64_t) * ns, st));
+      S.slots = 0;
+      S.mask.alloc(1);
+      S.col.alloc(1);
+      S.val.alloc(1);
+      S.dpat.alloc(1);
+      return;
+    }
+  }
+  slice_format_kernel<<<(unsigned)ns, 64, 0, st>>>(m, ptr, col, ns, allow_dia ? 1 : 0, S.width.p,
                                                               S.sptr.p, S.doff.p);
   HIPCHECK(hipGetLastError());
   std::vector<int32_t> wh;
@@ -1788,10 +1970,18 @@ static void build_sell(Sell &S, int64_t m, int64_t ncols, const int64_t *ptr, co
   }
   if (!S.mask.p) S.mask.alloc(1);
   exclusive_scan_i64(S.sptr.p, S.sptr.p, ns, st, &S.slots);
-  S.col.alloc((size_t)std::max<int64_t>(S.slots, 1));
+  // aligned-offset slices keep no columns (their offsets are in doff): a
+  // diagonal block made only of such slices needs no column array
+  S.col.alloc((size_t)std::max<int64_t>(S.dia_slices < ns ? S.slots : 0, 1));
   S.val.alloc((size_t)std::max<int64_t>(S.slots, 1));
-  sell_fill_lds_kernel<true><<<(unsigned)ns, 64, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p, S.doff.p, S.col.p,
-                                                          S.val.p, S.mask.p, S.mask8.p);
+  if (S.dia_slices < ns)
+    sell_fill_lds_kernel<true><<<(unsigned)ns, 64, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p, S.doff.p, S.col.p,
+                                                            S.val.p, S.mask.p, S.mask8.p);
+  if (S.dia_slices)
+    sell_fill_dia_kernel<<<(unsigned)ns, 256, 0, st>>>(m, ptr, col, val, ns, S.sptr.p, S.width.p, S.doff.p, S.val.p,
+                                                       S.mask.p, S.mask8.p, vd ? vd->tab.p : nullptr,
+                                                       vd ? vd->stat.p : nullptr);
+  if (vd && S.dia_slices) vd->dia_done = true;
   HIPCHECK(hipGetLastError());
   if (S.dia_slices) share_offset_patterns(S, wh, ncols, st);
   else S.dpat.alloc(1);
@@ -1958,6 +2148,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   // segment width: the longest row's
   const int SW = Lh <= 8 ? 8 : Lh <= 16 ? 16 : Lh <= 32 ? 32 : 64;
   const unsigned sgrid = (unsigned)cdiv(std::max<int64_t>(m, 1), 256 / SW);
+  const unsigned cgrid = (unsigned)cdiv(std::max<int64_t>(m, 1), 256 / SW * CANON_R);    // the fused count pass
+  const unsigned fgrid = (unsigned)cdiv(std::max<int64_t>(m, 1), 256 / SW * CANON_FR);   // the fused fill pass
   const bool fused = Lh <= 64 && g_knobs.asm_fused;
   auto check_err = [&] {
     int herr = 0;
@@ -1972,7 +2164,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   if (fused) {
     // ---- canonicalise + split counts in one register pass (canon_count_kernel)
     if (m) {
-#define CCNT(WW) canon_count_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, col, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p)
+#define CCNT(WW) canon_count_kernel<WW><<<cgrid, 256, 0, st>>>(m, rowptr, col, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p)
       switch (SW) { case 8: CCNT(8); break; case 16: CCNT(16); break; case 32: CCNT(32); break; default: CCNT(64); }
 #undef CCNT
       HIPCHECK(hipGetLastError());
@@ -2044,7 +2236,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   A->diag.alloc((size_t)std::max<int64_t>(m, 1));
   if (m) {
     if (fused) {
-#define CFILL(WW) canon_fill_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
+#define CFILL(WW) canon_fill_kernel<WW><<<fgrid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
       switch (SW) { case 8: CFILL(8); break; case 16: CFILL(16); break; case 32: CFILL(32); break; default: CFILL(64); }
 #undef CFILL
     } else {
@@ -2060,9 +2252,11 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   const double t_split = wall_ms();
 
   // ---- SpMV layouts
-  build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0);
+  VDict vd;
+  if (g_knobs.vcodes && m) vd.init(st);
+  build_sell(A->sd, m, A->n, A->dptr.p, A->dcol.p, A->dval.p, st, g_knobs.dia != 0, vd.tab.p ? &vd : nullptr);
   build_sell(A->so, m, A->nghost, A->optr.p, A->ocol.p, A->oval.p, st, false);
-  build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, A->n, st);
+  build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, A->n, st, vd);
   build_pair_f64(A->sd, m, A->n, A->so.nslices ? A->so.width.p : nullptr, st);
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
