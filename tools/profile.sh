@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/prof
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--steps ${STEPS:-50} --warmup 5 --no-cpu --no-solve --no-asm --grid ${GRID:-256}"
+ARGS="--steps ${STEPS:-50} --warmup 5 --no-cpu --no-solve --no-asm --no-configs --grid ${GRID:-256}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $R/bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv --kernel-include-regex 'spmv|cg_|fold|stream_read' -d $OUT/fetch -o run -- python3 $R/bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv --kernel-include-regex 'spmv|cg_|fold|stream_read' -d $OUT/write -o run -- python3 $R/bench.py $ARGS > $OUT/write.log 2>&1
