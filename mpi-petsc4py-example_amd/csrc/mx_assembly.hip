@@ -423,13 +423,15 @@ __global__ void __launch_bounds__(256) canon_fill_kernel(
     const unsigned *__restrict__ bitmap, const int64_t *__restrict__ wbase) {
   const int lane = threadIdx.x & 63, l = lane % W, gbase = lane - l;
   const int64_t row0 = (int64_t)blockIdx.x * (256 / W) * CANON_FR + threadIdx.x / W;
-  int64_t start[CANON_FR], len[CANON_FR], c[CANON_FR], p[CANON_FR];
+  int64_t start[CANON_FR], len[CANON_FR], c[CANON_FR], p[CANON_FR], dp[CANON_FR], op[CANON_FR];
   double v[CANON_FR];
 #pragma unroll
-  for (int r = 0; r < CANON_FR; ++r) {
+  for (int r = 0; r < CANON_FR; ++r) {   // the row's split offsets too: no load after the sort
     const int64_t row = row0 + (int64_t)r * (256 / W);
     start[r] = row < m ? rowptr[row] : 0;
     len[r] = row < m ? rowptr[row + 1] - start[r] : 0;
+    dp[r] = row < m ? dptr[row] : 0;
+    op[r] = row < m ? optr[row] : 0;
   }
 #pragma unroll
   for (int r = 0; r < CANON_FR; ++r)
@@ -446,14 +448,14 @@ __global__ void __launch_bounds__(256) canon_fill_kernel(
     const unsigned long long bd = seg_bits_w<W>(__ballot(isd), gbase), bo = seg_bits_w<W>(__ballot(iso), gbase);
     const unsigned long long bg = seg_bits_w<W>(__ballot(isd && cr == rstart + row), gbase);
     if (isd) {
-      const int64_t t = dptr[row] + __popcll(bd & below);
+      const int64_t t = dp[r] + __popcll(bd & below);
       dcol[t] = (int32_t)(cr - cstart);
       dval[t] = out;
       if (cr == rstart + row) diag[row] = out;
     } else if (iso) {
       const int64_t w = cr >> 5;
       const unsigned bit = (unsigned)(cr & 31);
-      const int64_t t = optr[row] + __popcll(bo & below);
+      const int64_t t = op[r] + __popcll(bo & below);
       ocol[t] = (int32_t)(wbase[w] + __popc(bitmap[w] & ((1u << bit) - 1u)));
       oval[t] = out;
     }

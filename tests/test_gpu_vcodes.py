@@ -55,6 +55,8 @@ def test_stencils_use_codes(selfcomm, oracle_mod, kind, n):
     (-2, -1, 0, 1, 2, 5),                           # k = 6 (runtime body, one batch)
     tuple(range(-6, 7)),                            # k = 13: two batches, odd
     tuple(range(-8, 9)),                            # k = 17: three batches
+    tuple(range(-16, 16)),                          # k = 32 = DIA_MAX: every mask bit, a full LDS image
+    tuple(range(-16, 17)),                          # k = 33: past DIA_MAX, general slices
 ])
 @pytest.mark.parametrize("nvals", [1, 3, 255])
 def test_aligned_offset_slices(selfcomm, oracle_mod, offsets, nvals):
