@@ -70,10 +70,12 @@ int mx_last_error(char *buf, size_t len) {
 
 int mx_get_unique_id(void *out, size_t len) { return guard([&] { get_unique_id(out, len); }); }
 
+
 int mx_comm_create_rccl(int rank, int size, int device, const void *uid, size_t uid_len, mx_comm *out) {
   return guard([&] {
     if (size < 1 || rank < 0 || rank >= size) fail(MX_ERR_ARG, "bad rank/size");
     *out = new mx_comm_s{make_rccl_comm(rank, size, device, uid, uid_len)};
+    load_code_objects();
   });
 }
 
@@ -82,19 +84,26 @@ int mx_comm_create_shm(int rank, int size, int device, const char *name, int64_t
     if (size < 1 || rank < 0 || rank >= size) fail(MX_ERR_ARG, "bad rank/size");
     if (!name || name[0] != '/') fail(MX_ERR_ARG, "shared-memory name must start with '/'");
     *out = new mx_comm_s{make_shm_comm(rank, size, device, name, slot_kib)};
+    load_code_objects();
   });
 }
 
 int mx_comm_abort(mx_comm c) { return guard([&] { if (c && c->c) abort_shm_comm(c->c); }); }
 
 int mx_comm_create_self(int device, mx_comm *out) {
-  return guard([&] { *out = new mx_comm_s{make_self_comm(device)}; });
+  return guard([&] {
+    *out = new mx_comm_s{make_self_comm(device)};
+    load_code_objects();
+  });
 }
 
 int mx_world_create_local(int size, void **world) { return guard([&] { *world = make_local_world(size); }); }
 
 int mx_comm_create_local(void *world, int rank, int device, mx_comm *out) {
-  return guard([&] { *out = new mx_comm_s{make_local_comm(world, rank, device)}; });
+  return guard([&] {
+    *out = new mx_comm_s{make_local_comm(world, rank, device)};
+    load_code_objects();
+  });
 }
 
 int mx_world_destroy(void *world) { return guard([&] { destroy_local_world(world); }); }

@@ -2377,4 +2377,12 @@ void stencil_coo(Comm *c, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t 
   }
 }
 
+// this translation unit's code object, loaded now rather than at the first
+// launch of one of its kernels (load_code_objects)
+void load_code_assembly() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&row_len_max_kernel));
+  (void)hipGetLastError();
+}
+
 }  // namespace mx

@@ -536,4 +536,22 @@ Comm *make_local_comm(void *world, int rank, int device) {
 void destroy_local_world(void *world) { delete static_cast<LocalWorld *>(world); }
 void abort_local_world(void *world) { static_cast<LocalWorld *>(world)->abort_all(); }
 
+// this translation unit's code object, loaded now rather than at the first
+// launch of one of its kernels (load_code_objects)
+void load_code_comm() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&local_sum_kernel));
+  (void)hipGetLastError();
+}
+
+void load_code_objects() {
+  load_code_comm();
+  load_code_vec();
+  load_code_assembly();
+  load_code_spmv();
+  load_code_spmv_pair();
+  load_code_ksp();
+  load_code_direct();
+}
+
 }  // namespace mx

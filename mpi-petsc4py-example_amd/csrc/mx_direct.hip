@@ -130,4 +130,12 @@ void dense_lu_solve(Comm *c, int64_t n, const int64_t *ip_h, const int64_t *cj_h
   if (herr) fail(MX_ERR_INTERNAL, "Zero pivot in LU factorization");
 }
 
+// this translation unit's code object, loaded now rather than at the first
+// launch of one of its kernels (load_code_objects)
+void load_code_direct() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&densify_kernel));
+  (void)hipGetLastError();
+}
+
 }  // namespace mx

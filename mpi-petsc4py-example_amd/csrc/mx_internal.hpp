@@ -516,4 +516,18 @@ inline unsigned grid_for(int64_t n, int block, int64_t cap = 1 << 16) {
   return (unsigned)g;
 }
 
+// HIP loads a translation unit's code object at the first launch of one of
+// its kernels (1-25 ms each for this library, 11 ms for the row-pair SpMV's
+// alone): load_code_objects (mx_abi.hip) loads every unit's when a
+// communicator is created, so that cost is paid at initialisation, not inside
+// the first assembly or solve that needs a new kernel family.
+void load_code_comm();
+void load_code_vec();
+void load_code_assembly();
+void load_code_spmv();
+void load_code_spmv_pair();
+void load_code_ksp();
+void load_code_direct();
+void load_code_objects();
+
 }  // namespace mx

@@ -1876,4 +1876,12 @@ void ksp_solve(Mat *A, const mx_ksp_params &p, const double *b, double *x, mx_ks
   HIPCHECK(hipStreamSynchronize(st));
 }
 
+// this translation unit's code object, loaded now rather than at the first
+// launch of one of its kernels (load_code_objects)
+void load_code_ksp() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&jacobi_setup_kernel));
+  (void)hipGetLastError();
+}
+
 }  // namespace mx

@@ -1067,4 +1067,12 @@ void mat_mult(Mat *A, const double *x, double *y) {
   matmult_overlap(A, x, y, SPMV_PLAIN, Jac{}, nullptr, nullptr);
 }
 
+// this translation unit's code object, loaded now rather than at the first
+// launch of one of its kernels (load_code_objects)
+void load_code_spmv() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&pack_kernel));
+  (void)hipGetLastError();
+}
+
 }  // namespace mx

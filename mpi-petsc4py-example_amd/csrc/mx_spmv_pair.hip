@@ -1298,7 +1298,7 @@ __global__ void __launch_bounds__(256) spmv_pair_zm27p2l_kernel(const PairLean27
     for (int z = z0; z < z1; ++z) {
       const uint32_t az2 = blkA(z + 2), bz2 = blkB(z + 2);
       const int rA = z * D + cbA, rB = rA + NL;
-      dbl2 rqA, rqB;
+      dbl2 rqA{0.0, 0.0}, rqB{0.0, 0.0};   // read only by the residual update
       load(z + 1);
       if constexpr (RU) {
         rqA = __builtin_nontemporal_load(reinterpret_cast<const dbl2 *>(rin + rA));
@@ -2375,6 +2375,14 @@ int pair_cg5_rupd_launch(Mat *A, KspState *s, const double *p, const double *w, 
   launch_timed(f, grid, st, a, p, nullptr, A->sd.pblk.p, A->sd.puni.p, ru);
   HIPCHECK(hipGetLastError());
   return grid;
+}
+
+// this translation unit's code object, loaded now rather than at the first
+// launch of one of its kernels (load_code_objects)
+void load_code_spmv_pair() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&sym_check_kernel));
+  (void)hipGetLastError();
 }
 
 }  // namespace mx

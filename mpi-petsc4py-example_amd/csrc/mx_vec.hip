@@ -359,4 +359,12 @@ void debug_stall(hipStream_t s, int stall_us) {
   HIPCHECK(hipGetLastError());
 }
 
+// this translation unit's code object, loaded now rather than at the first
+// launch of one of its kernels (load_code_objects)
+void load_code_vec() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&finish_kernel));
+  (void)hipGetLastError();
+}
+
 }  // namespace mx
