@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define MX_ABI_VERSION 1
+/* 2: mx_ksp_result grew the pbw / mdot / maxpy timing fields (its size changed) */
+#define MX_ABI_VERSION 2
 
 enum {
   MX_OK = 0,

@@ -131,7 +131,7 @@ def load():
         fn = getattr(lib, name)   # AttributeError if the ABI lost a symbol
         fn.restype = res
         fn.argtypes = args
-    if lib.mx_version() != 1:
+    if lib.mx_version() != 2:
         raise ImportError("libmxsolve ABI version mismatch")
     # diagnostics / A/B runs: MXSOLVE_KNOBS="27=0+3=8192" (mx_debug_set keys, include/mxsolve.h)
     for kv in filter(None, os.environ.get("MXSOLVE_KNOBS", "").split("+")):
