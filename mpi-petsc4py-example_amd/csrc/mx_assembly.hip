@@ -2124,6 +2124,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
     rowptr = rowptr_own.p; col = gcol.p; val = gval.p; pos = gpos.p;
   }
 
+
   // ---- longest row picks the segment width
   DBuf<unsigned long long> lmax(2);
   HIPCHECK(hipMemsetAsync(lmax.p, 0, sizeof(unsigned long long) * 2, st));
@@ -2165,6 +2166,14 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   double t_canon;
   if (fused) {
     // ---- canonicalise + split counts in one register pass (canon_count_kernel)
+    // Drain the device first.  With several ranks' threads sharing one GPU
+    // (in-process ranks), this pass launched straight after the split
+    // arrays' allocation and zeroing read a few rows of columns as zeros in
+    // ~3% of 8-rank assemblies that followed solves in the same process
+    // (tools/asm_race.py: 12 of ~360; the columns were correct when read
+    // back afterwards); with this synchronisation 0 of 300, and the separate
+    // passes 0 of 330.  One synchronisation per assembly.
+    HIPCHECK(hipDeviceSynchronize());
     if (m) {
 #define CCNT(WW) canon_count_kernel<WW><<<cgrid, 256, 0, st>>>(m, rowptr, col, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p)
       switch (SW) { case 8: CCNT(8); break; case 16: CCNT(16); break; case 32: CCNT(32); break; default: CCNT(64); }

@@ -93,3 +93,35 @@ def _selfcomm_stream():
     if _SELF and _SELF[0].h:
         _SELF[0].activate()
     yield
+
+
+def _knobs(L):
+    """Every mx_debug_set key's current value (set to 0 and back: a valid key
+    returns the 0 just set on the way back, an unknown one -1)."""
+    vals = {}
+    for k in range(1, 100):
+        old = L.mx_debug_set(k, 0)
+        if L.mx_debug_set(k, old) == 0:
+            vals[k] = old
+    return vals
+
+
+@pytest.fixture(autouse=True)
+def _knobs_restored(request):
+    """A GPU test leaves the library's knobs as it found them: the knobs are
+    process-global, and one left changed silently alters every later test
+    (a default path that no longer runs).  A leak is undone and fails the test
+    that caused it."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from mxsolve import _lib
+    L = _lib.load()
+    before = _knobs(L)
+    yield
+    after = _knobs(L)
+    leaked = {k: (before[k], after.get(k)) for k in before if after.get(k) != before[k]}
+    for k, (v, _) in leaked.items():
+        L.mx_debug_set(k, v)
+    if leaked:
+        pytest.fail(f"knobs left changed (key: (before, after)): {leaked}")

@@ -815,7 +815,7 @@ def test_c4_p8_partition(oracle_mod, n):
     for q, (info, *_r) in enumerate(res):
         nb = (q > 0) + (q < P - 1)
         assert info["rstart"] == ranges[q] and info["m"] == M // P
-        assert info["nghost"] == nb * plane and info["pair_code"] == 1
+        assert info["nghost"] == nb * plane and info["pair_code"] == 1, (q, info)
     assert np.array_equal(np.concatenate([r[1] for r in res]).view(np.uint64), y_ref.view(np.uint64))
     assert all(r[2] == o["its"] and r[3] == o["reason"] == 2 for r in res), ([r[2:4] for r in res], o["its"])
     xs = np.concatenate([r[4] for r in res])
