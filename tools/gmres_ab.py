@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Interleaved A/B of GMRES(30) variants (knob sets) on conv-diff n^3, one operator.
-    python tools/gmres_ab.py [n] [rounds] variant ...   (variant: "16=8+..." knob=value)"""
+    python tools/gmres_ab.py [n] [rounds] variant ...   (variant: "77=512+..." knob=value)"""
 import json, os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-petsc4py-example_amd"))
 import numpy as np, torch  # noqa: E401,E402
@@ -10,7 +10,7 @@ from mxsolve.core import DeviceComm, DMat, rhs_hash  # noqa: E402
 L = _lib.load()
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-variants = sys.argv[3:] or ["16=8", "16=16"]
+variants = sys.argv[3:] or ["", "77=512"]
 comm = DeviceComm.self_comm(0)
 A = DMat.stencil(comm, "convdiff3d", n)
 m = A.info()["m"]

@@ -6,7 +6,7 @@ OUT=$R/gpurun_out/pmc${TAG:-}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-ARGS="${SPMV_ARGS:-poisson3d 256 20 ${SPMV_KNOBS:-24=1}}"
+ARGS="${SPMV_ARGS:-poisson3d 256 20 ${SPMV_KNOBS:-}}"
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 i=0
 for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_SMEM" \
