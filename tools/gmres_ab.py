@@ -19,7 +19,7 @@ b = comm.empty(m); rhs_hash(comm, 0, b); x = comm.zeros(m)
 
 def setv(v):
     old = []
-    for kv in v.split("+"):
+    for kv in filter(None, v.split("+")):   # "" = the defaults
         k, val = kv.split("=")
         old.append(f"{k}={L.mx_debug_set(int(k), int(val))}")
     return "+".join(old)
