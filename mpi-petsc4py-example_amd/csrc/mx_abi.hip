@@ -153,8 +153,14 @@ int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
     int64_t m = m_local;
     if (m < 0) { const int64_t q = Mg / k->size, r = Mg % k->size; m = q + (k->rank < r ? 1 : 0); }
     hipStream_t st = k->stream;
-    DBuf<int64_t> ip((size_t)m + 1), cl((size_t)(nnz > 0 ? nnz : 1));
-    DBuf<double> vl((size_t)(nnz > 0 ? nnz : 1));
+    // 32-bit columns (scipy's default index type) are read as is by the
+    // fused assembly passes: a device array directly, a host array after its
+    // copy; 64-bit ones are copied / taken as is too
+    const bool c32 = col_bytes == 4;
+    DBuf<int64_t> ip((size_t)m + 1), cl;
+    DBuf<int32_t> cl32;
+    if (!src_is_device) { if (c32) cl32.alloc((size_t)(nnz > 0 ? nnz : 1)); else cl.alloc((size_t)(nnz > 0 ? nnz : 1)); }
+    DBuf<double> vl((size_t)(src_is_device && nnz > 0 ? 0 : (nnz > 0 ? nnz : 1)));
     // host-side copies of the two scalars petsc4py checks
     int64_t first = 0, last = 0;
     if (src_is_device) {
@@ -172,24 +178,28 @@ int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
     if (first != 0) fail(MX_ERR_ARG, "I[0] is " + std::to_string(first) + ", expected 0");
     if (last != nnz) fail(MX_ERR_ARG, "size(J) is " + std::to_string(nnz) + ", expected " + std::to_string(last));
     if (!src_is_device) {
-      DBuf<char> stage((size_t)std::max<int64_t>((m + 1) * indptr_bytes, nnz * col_bytes) + 8);
+      DBuf<char> stage((size_t)(m + 1) * indptr_bytes + 8);
       HIPCHECK(hipMemcpyAsync(stage.p, indptr, (size_t)(m + 1) * indptr_bytes, hipMemcpyHostToDevice, st));
       convert_index(stage.p, indptr_bytes, m + 1, ip.p, st);
       HIPCHECK(hipStreamSynchronize(st));
       if (nnz) {
-        HIPCHECK(hipMemcpyAsync(stage.p, cols, (size_t)nnz * col_bytes, hipMemcpyHostToDevice, st));
-        convert_index(stage.p, col_bytes, nnz, cl.p, st);
+        void *cdst = c32 ? (void *)cl32.p : (void *)cl.p;
+        HIPCHECK(hipMemcpyAsync(cdst, cols, (size_t)nnz * col_bytes, hipMemcpyHostToDevice, st));
         HIPCHECK(hipMemcpyAsync(vl.p, vals, sizeof(double) * nnz, hipMemcpyHostToDevice, st));
       }
       HIPCHECK(hipStreamSynchronize(st));
-    } else if (nnz) {
-      convert_index(cols, col_bytes, nnz, cl.p, st);
-      HIPCHECK(hipMemcpyAsync(vl.p, vals, sizeof(double) * nnz, hipMemcpyDeviceToDevice, st));
     }
     HIPCHECK(hipStreamSynchronize(st));
     const double t_h2d = wall_ms();
     AssemblyInput in;
-    in.rowptr = ip.p; in.cols = cl.p; in.vals = vl.p; in.nnz = nnz;
+    if (src_is_device) {
+      if (c32) in.cols32 = static_cast<const int32_t *>(cols);
+      else in.cols = static_cast<const int64_t *>(cols);
+    } else {
+      in.cols = cl.p; in.cols32 = cl32.p;
+    }
+    if (!in.cols && !in.cols32) { cl.alloc(1); in.cols = cl.p; }   // nnz == 0 from device
+    in.rowptr = ip.p; in.vals = src_is_device && nnz ? vals : vl.p; in.nnz = nnz;
     in.insert_mode = insert_mode;
     *A = new mx_mat_s{assemble(k, Mg, Ng, m_local, n_local, in)};
     g_asm_times.h2d_ms = t_h2d - t0;
@@ -229,10 +239,11 @@ int mx_mat_create_stencil(mx_comm c, int kind, int64_t nx, int64_t ny, int64_t n
     for (int i = 0; i < k->rank; ++i) row0 += q + (i < r ? 1 : 0);
     const int64_t m = q + (k->rank < r ? 1 : 0);
     DBuf<int64_t> rp, cl;
+    DBuf<int32_t> cl32;
     DBuf<double> vl;
-    stencil_coo(k, kind, nx, ny, nz, row0, m, rp, cl, vl);
+    stencil_coo(k, kind, nx, ny, nz, row0, m, rp, cl, cl32, vl);
     AssemblyInput in;
-    in.rowptr = rp.p; in.cols = cl.p; in.vals = vl.p;
+    in.rowptr = rp.p; in.cols = cl.p; in.cols32 = cl32.p; in.vals = vl.p;
     in.nnz = m * (kind == 0 ? 5 : (kind == 2 ? 27 : 7));
     in.insert_mode = MX_INSERT_VALUES;
     *A = new mx_mat_s{assemble(k, Mg, Mg, -1, -1, in)};

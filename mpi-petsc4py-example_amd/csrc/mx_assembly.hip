@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <unordered_map>
 
 #include "mx_internal.hpp"
@@ -246,16 +247,16 @@ static int64_t coo_redistribute(Comm *c, const std::vector<int64_t> &rr, int64_t
 // canon_load: lane l's input entry (column, input position, value), or the
 // drop key; canon_sorted: canon_seg on loaded entries (the fused count / fill
 // passes load several rows' entries first, then sort each).
-template <bool VALS>
+template <bool VALS, typename CT = int64_t>
 __device__ __forceinline__ void canon_load(int l, bool active, int64_t start, int64_t len,
-                                           const int64_t *__restrict__ col, const double *__restrict__ val,
+                                           const CT *__restrict__ col, const double *__restrict__ val,
                                            const int64_t *__restrict__ pos, int64_t N, int *__restrict__ err,
                                            int64_t &c, int64_t &p, double &v) {
   p = KEY_DROP;
   v = 0.0;
   c = KEY_DROP;
   if (active && l < len) {
-    int64_t cc = col[start + l];
+    const int64_t cc = (int64_t)col[start + l];   // int32 columns sign-extend: -1 stays a drop
     if (cc >= 0) {
       if (err && cc >= N) atomicOr(err, 1);
       c = cc;
@@ -377,9 +378,9 @@ __device__ __forceinline__ unsigned long long seg_bits_w(unsigned long long ball
   return W == 64 ? ball : ((ball >> gbase) & ((1ULL << (W == 64 ? 0 : W)) - 1ULL));
 }
 
-template <int W>
+template <int W, typename CT>
 __global__ void __launch_bounds__(256) canon_count_kernel(int64_t m, const int64_t *__restrict__ rowptr,
-                                                          const int64_t *__restrict__ col,
+                                                          const CT *__restrict__ col,
                                                           const int64_t *__restrict__ pos, int64_t N, int add,
                                                           int64_t cstart, int64_t cend, int64_t *__restrict__ cnt_d,
                                                           int64_t *__restrict__ cnt_o, unsigned *__restrict__ bitmap,
@@ -399,7 +400,7 @@ __global__ void __launch_bounds__(256) canon_count_kernel(int64_t m, const int64
   }
 #pragma unroll
   for (int r = 0; r < CANON_R; ++r)
-    canon_load<false>(l, row0 + (int64_t)r * (256 / W) < m, start[r], len[r], col, nullptr, pos, N, err, c[r], p[r], v[r]);
+    canon_load<false, CT>(l, row0 + (int64_t)r * (256 / W) < m, start[r], len[r], col, nullptr, pos, N, err, c[r], p[r], v[r]);
 #pragma unroll
   for (int r = 0; r < CANON_R; ++r) {
     const int64_t row = row0 + (int64_t)r * (256 / W);
@@ -414,9 +415,9 @@ __global__ void __launch_bounds__(256) canon_count_kernel(int64_t m, const int64
 
 // (one row per segment: four, as in the count pass, measured 5.65 ms against
 // 4.4 for a 27-point share -- 99 VGPRs, half the waves)
-template <int W>
+template <int W, typename CT>
 __global__ void __launch_bounds__(256) canon_fill_kernel(
-    int64_t m, const int64_t *__restrict__ rowptr, const int64_t *__restrict__ col, const double *__restrict__ val,
+    int64_t m, const int64_t *__restrict__ rowptr, const CT *__restrict__ col, const double *__restrict__ val,
     const int64_t *__restrict__ pos, int64_t N, int add, int64_t cstart, int64_t cend, int64_t rstart,
     const int64_t *__restrict__ dptr, const int64_t *__restrict__ optr, int32_t *__restrict__ dcol,
     double *__restrict__ dval, int32_t *__restrict__ ocol, double *__restrict__ oval, double *__restrict__ diag,
@@ -435,7 +436,7 @@ __global__ void __launch_bounds__(256) canon_fill_kernel(
   }
 #pragma unroll
   for (int r = 0; r < CANON_FR; ++r)
-    canon_load<true>(l, row0 + (int64_t)r * (256 / W) < m, start[r], len[r], col, val, pos, N, nullptr, c[r], p[r], v[r]);
+    canon_load<true, CT>(l, row0 + (int64_t)r * (256 / W) < m, start[r], len[r], col, val, pos, N, nullptr, c[r], p[r], v[r]);
 #pragma unroll
   for (int r = 0; r < CANON_FR; ++r) {
     const int64_t row = row0 + (int64_t)r * (256 / W);
@@ -2088,6 +2089,9 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   DBuf<double> gval;
   const int64_t *rowptr = in.rowptr;
   const int64_t *col = in.cols;
+  const int32_t *col32 = in.cols ? nullptr : in.cols32;   // read as is by the fused passes
+  DBuf<int64_t> col_wide;
+  if (col32 && in.coo_rows) fail(MX_ERR_INTERNAL, "32-bit columns with COO input");
   const double *val = in.vals;
   const int64_t *pos = nullptr;
   DBuf<int64_t> rd_rows, rd_cols;
@@ -2154,6 +2158,12 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   const unsigned cgrid = (unsigned)cdiv(std::max<int64_t>(m, 1), 256 / SW * CANON_R);    // the fused count pass
   const unsigned fgrid = (unsigned)cdiv(std::max<int64_t>(m, 1), 256 / SW * CANON_FR);   // the fused fill pass
   const bool fused = Lh <= 64 && g_knobs.asm_fused;
+  if (col32 && !fused) {   // the separate passes (and long rows) take 64-bit columns
+    col_wide.alloc((size_t)std::max<int64_t>(tot_in, 1));
+    if (tot_in) convert_index(col32, 4, tot_in, col_wide.p, st);
+    col = col_wide.p;
+    col32 = nullptr;
+  }
   auto check_err = [&] {
     int herr = 0;
     HIPCHECK(hipMemcpyAsync(&herr, err.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -2175,7 +2185,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
     // passes 0 of 330.  One synchronisation per assembly.
     HIPCHECK(hipDeviceSynchronize());
     if (m) {
-#define CCNT(WW) canon_count_kernel<WW><<<cgrid, 256, 0, st>>>(m, rowptr, col, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p)
+#define CCNT(WW) if (col32) canon_count_kernel<WW, int32_t><<<cgrid, 256, 0, st>>>(m, rowptr, col32, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p); \
+                 else canon_count_kernel<WW, int64_t><<<cgrid, 256, 0, st>>>(m, rowptr, col, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p)
       switch (SW) { case 8: CCNT(8); break; case 16: CCNT(16); break; case 32: CCNT(32); break; default: CCNT(64); }
 #undef CCNT
       HIPCHECK(hipGetLastError());
@@ -2247,9 +2258,11 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   A->diag.alloc((size_t)std::max<int64_t>(m, 1));
   if (m) {
     if (fused) {
-#define CFILL(WW) canon_fill_kernel<WW><<<fgrid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
+#define CFILL_T(WW, T, CP) canon_fill_kernel<WW, T><<<fgrid, 256, 0, st>>>(m, rowptr, CP, val, pos, N, add, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
+#define CFILL(WW) if (col32) CFILL_T(WW, int32_t, col32); else CFILL_T(WW, int64_t, col)
       switch (SW) { case 8: CFILL(8); break; case 16: CFILL(16); break; case 32: CFILL(32); break; default: CFILL(64); }
 #undef CFILL
+#undef CFILL_T
     } else {
 #define SPLITF(WW) fill_split_seg_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, cnt_out.p, ccol.p, cval.p, A->cstart, A->cend, A->rstart, A->dptr.p, A->optr.p, A->dcol.p, A->dval.p, A->ocol.p, A->oval.p, A->diag.p, bitmap.p, wbase.p)
       switch (SW) { case 8: SPLITF(8); break; case 16: SPLITF(16); break; case 32: SPLITF(32); break; default: SPLITF(64); }
@@ -2310,7 +2323,8 @@ __device__ __forceinline__ double kappa_d(int64_t a, int64_t b, int64_t c) {
 // the diagonal's sum are the row kernel's.
 template <int KIND, bool I32>
 __global__ void stencil_kernel(int64_t nx, int64_t ny, int64_t nz, int64_t row0, int64_t m,
-                               int64_t *__restrict__ cols, double *__restrict__ vals) {
+                               typename std::conditional<I32, int32_t, int64_t>::type *__restrict__ cols,
+                               double *__restrict__ vals) {
   constexpr int S = KIND == 0 ? 5 : (KIND == 2 ? 27 : 7);
   const int64_t total = m * S;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -2346,7 +2360,7 @@ __global__ void stencil_kernel(int64_t nx, int64_t ny, int64_t nz, int64_t row0,
     }
     const int64_t ii = i + di, jj = j + dj, kk = k + dk;
     const bool in = ii >= 0 && ii < nx && jj >= 0 && jj < ny && kk >= 0 && kk < nz;
-    cols[t] = in ? ii + nx * (jj + ny * kk) : -1;
+    cols[t] = in ? ii + nx * (jj + ny * kk) : -1;   // 32-bit columns when the row count allows
     double v;
     if (KIND == 0) v = q == 2 ? 4.0 : -1.0;
     else if (KIND == 1) v = q == 3 ? 6.0 : -1.0;
@@ -2367,18 +2381,21 @@ __global__ void stride_rowptr_kernel(int64_t m, int S, int64_t *__restrict__ row
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= m; i += stride) rowptr[i] = i * S;
 }
 
+// Columns go to `cols32` (4 B an entry, read as is by the fused assembly
+// passes) when the global row count fits 31 bits, else to `cols`.
 void stencil_coo(Comm *c, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t row0, int64_t m,
-                 DBuf<int64_t> &rowptr, DBuf<int64_t> &cols, DBuf<double> &vals) {
+                 DBuf<int64_t> &rowptr, DBuf<int64_t> &cols, DBuf<int32_t> &cols32, DBuf<double> &vals) {
   const int S = kind == 0 ? 5 : (kind == 2 ? 27 : 7);
+  const bool i32 = (kind == 0 ? nx * ny : nx * ny * nz) < ((int64_t)1 << 31);
   rowptr.alloc((size_t)m + 1);
-  cols.alloc((size_t)std::max<int64_t>(m * S, 1));
+  if (i32) cols32.alloc((size_t)std::max<int64_t>(m * S, 1));
+  else cols.alloc((size_t)std::max<int64_t>(m * S, 1));
   vals.alloc((size_t)std::max<int64_t>(m * S, 1));
   stride_rowptr_kernel<<<grid_for(m + 1, 256, 8192), 256, 0, c->stream>>>(m, S, rowptr.p);
   HIPCHECK(hipGetLastError());
   if (m) {
-    const bool i32 = (kind == 0 ? nx * ny : nx * ny * nz) < ((int64_t)1 << 31);
     const unsigned g = grid_for(m * S, 256, 65536);
-#define STK(K) if (i32) stencil_kernel<K, true><<<g, 256, 0, c->stream>>>(nx, ny, nz, row0, m, cols.p, vals.p); \
+#define STK(K) if (i32) stencil_kernel<K, true><<<g, 256, 0, c->stream>>>(nx, ny, nz, row0, m, cols32.p, vals.p); \
                else stencil_kernel<K, false><<<g, 256, 0, c->stream>>>(nx, ny, nz, row0, m, cols.p, vals.p)
     switch (kind) { case 0: STK(0); break; case 1: STK(1); break; case 2: STK(2); break; default: STK(3); }
 #undef STK

@@ -348,6 +348,7 @@ struct AssemblyInput {
   const int64_t *rowptr = nullptr;   // device, m+1 (CSR)
   const int64_t *coo_rows = nullptr; // device, nnz (COO, global rows)
   const int64_t *cols = nullptr;     // device, nnz (global cols)
+  const int32_t *cols32 = nullptr;   // device, nnz: 32-bit global cols instead (CSR only, cols unset)
   const double *vals = nullptr;      // device, nnz
   int64_t nnz = 0;
   int insert_mode = MX_INSERT_VALUES;
@@ -355,7 +356,8 @@ struct AssemblyInput {
 Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
               const AssemblyInput &in);
 void stencil_coo(Comm *c, int kind, int64_t nx, int64_t ny, int64_t nz, int64_t row0,
-                 int64_t m, DBuf<int64_t> &rows, DBuf<int64_t> &cols, DBuf<double> &vals);
+                 int64_t m, DBuf<int64_t> &rows, DBuf<int64_t> &cols, DBuf<int32_t> &cols32,
+                 DBuf<double> &vals);
 void convert_index(const void *src, int bytes, int64_t n, int64_t *dst, hipStream_t s);
 
 // PCJacobi application z_i = r_i * d_i.  mode 0: no PC; 1: per-row d (HBM

@@ -223,6 +223,10 @@ class DMat:
         """createAIJ(size=(M,N), csr=(indptr, cols, vals)): local rows, global cols."""
         if isinstance(indptr, torch.Tensor):
             ip, cl, vl = indptr, cols, vals
+            for t in (ip, cl):   # read in place by the library: no hidden copies
+                if not t.is_cuda or t.dtype not in (torch.int32, torch.int64) or not t.is_contiguous():
+                    raise TypeError("device CSR index arrays must be contiguous int32/int64 CUDA tensors")
+            _ptr(vl)
             dev = 1
             ipb, clb = ip.element_size(), cl.element_size()
             nnz = cl.numel()

@@ -61,6 +61,50 @@ def test_assembly_unsorted_duplicates(selfcomm, oracle_mod, add, maxlen):
     assert_csr_equal(A.csr(), O.csr())
 
 
+@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("itype", [np.int32, np.int64])
+@pytest.mark.parametrize("maxlen", [12, 64, 300])
+def test_assembly_index_widths(selfcomm, oracle_mod, maxlen, itype, where, fused):
+    """createAIJ(csr=...) with 32-bit (scipy's default) or 64-bit index arrays,
+    from host arrays or device tensors: 32-bit columns are read as is by the
+    fused passes and widened for the separate ones (long rows, knob 72 = 0);
+    device arrays are read in place.  Same CSR as the oracle either way, and
+    the column range check still fires."""
+    from mxsolve import _lib
+    from mxsolve._lib import MxError
+    from mxsolve.core import DMat
+    L = _lib.load()
+    rng = np.random.default_rng(maxlen + (itype == np.int32))
+    M, N = 301, 400
+    lens = rng.integers(0, maxlen + 1, M)
+    lens[rng.integers(0, M)] = maxlen
+    ip = np.concatenate([[0], np.cumsum(lens)]).astype(itype)
+    nnz = int(ip[-1])
+    cols = rng.integers(-2, N, nnz).astype(itype)
+    cols[: nnz // 3] = rng.integers(-1, 20, nnz // 3)     # duplicates
+    vals = rng.standard_normal(nnz)
+    tdt = torch.int32 if itype == np.int32 else torch.int64
+
+    def args(c):
+        if where == "host":
+            return ip, c, vals
+        return (torch.from_numpy(ip).to(tdt).cuda(), torch.from_numpy(c).to(tdt).cuda(), to_dev(vals))
+    old = L.mx_debug_set(72, fused)
+    try:
+        for add in (False, True):
+            A = DMat.from_csr(selfcomm, M, N, *args(cols), add=add)
+            O = oracle_mod.OracleMat.from_csr(M, N, ip.astype(np.int64), cols.astype(np.int64), vals, P=1, add=add)
+            assert_csr_equal(A.csr(), O.csr())
+        bad = cols.copy()
+        bad[nnz // 2] = N
+        with pytest.raises(MxError) as e:
+            DMat.from_csr(selfcomm, M, N, *args(bad))
+        assert e.value.code == 2
+    finally:
+        L.mx_debug_set(72, old)
+
+
 @pytest.mark.parametrize("add", [False, True])
 def test_assembly_huge_rows(selfcomm, oracle_mod, add):
     """Rows beyond the LDS sort (> 2048 entries): chunk sorts + merge passes,
