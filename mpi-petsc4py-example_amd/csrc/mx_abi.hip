@@ -114,6 +114,7 @@ int mx_comm_destroy(mx_comm c) {
     if (!c) return;
     if (c->c) { (void)hipSetDevice(c->c->device); delete c->c; }
     delete c;
+    scratch_trim();   // cached assembly transients go back to the driver
   });
 }
 
@@ -157,10 +158,10 @@ int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
     // fused assembly passes: a device array directly, a host array after its
     // copy; 64-bit ones are copied / taken as is too
     const bool c32 = col_bytes == 4;
-    DBuf<int64_t> ip((size_t)m + 1), cl;
-    DBuf<int32_t> cl32;
+    DBuf<int64_t> ip((size_t)m + 1, kScratch), cl(kScratch);
+    DBuf<int32_t> cl32(kScratch);
     if (!src_is_device) { if (c32) cl32.alloc((size_t)(nnz > 0 ? nnz : 1)); else cl.alloc((size_t)(nnz > 0 ? nnz : 1)); }
-    DBuf<double> vl((size_t)(src_is_device && nnz > 0 ? 0 : (nnz > 0 ? nnz : 1)));
+    DBuf<double> vl((size_t)(src_is_device && nnz > 0 ? 0 : (nnz > 0 ? nnz : 1)), kScratch);
     // host-side copies of the two scalars petsc4py checks
     int64_t first = 0, last = 0;
     if (src_is_device) {
@@ -178,7 +179,7 @@ int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
     if (first != 0) fail(MX_ERR_ARG, "I[0] is " + std::to_string(first) + ", expected 0");
     if (last != nnz) fail(MX_ERR_ARG, "size(J) is " + std::to_string(nnz) + ", expected " + std::to_string(last));
     if (!src_is_device) {
-      DBuf<char> stage((size_t)(m + 1) * indptr_bytes + 8);
+      DBuf<char> stage((size_t)(m + 1) * indptr_bytes + 8, kScratch);
       HIPCHECK(hipMemcpyAsync(stage.p, indptr, (size_t)(m + 1) * indptr_bytes, hipMemcpyHostToDevice, st));
       convert_index(stage.p, indptr_bytes, m + 1, ip.p, st);
       HIPCHECK(hipStreamSynchronize(st));
@@ -215,8 +216,8 @@ int mx_mat_create_coo(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
     Comm *k = C(c);
     hipStream_t st = k->stream;
     const size_t cnt = (size_t)(n > 0 ? n : 1);
-    DBuf<int64_t> r(cnt), cl(cnt);
-    DBuf<double> v(cnt);
+    DBuf<int64_t> r(cnt, kScratch), cl(cnt, kScratch);
+    DBuf<double> v(cnt, kScratch);
     if (n) {
       const hipMemcpyKind kind = src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
       HIPCHECK(hipMemcpyAsync(r.p, rows, sizeof(int64_t) * n, kind, st));
@@ -238,9 +239,9 @@ int mx_mat_create_stencil(mx_comm c, int kind, int64_t nx, int64_t ny, int64_t n
     int64_t row0 = 0;
     for (int i = 0; i < k->rank; ++i) row0 += q + (i < r ? 1 : 0);
     const int64_t m = q + (k->rank < r ? 1 : 0);
-    DBuf<int64_t> rp, cl;
-    DBuf<int32_t> cl32;
-    DBuf<double> vl;
+    DBuf<int64_t> rp(kScratch), cl(kScratch);
+    DBuf<int32_t> cl32(kScratch);
+    DBuf<double> vl(kScratch);
     stencil_coo(k, kind, nx, ny, nz, row0, m, rp, cl, cl32, vl);
     AssemblyInput in;
     in.rowptr = rp.p; in.cols = cl.p; in.cols32 = cl32.p; in.vals = vl.p;
@@ -572,6 +573,7 @@ int mx_debug_set(int key, int value) {
     case 77: old = g_knobs.maxpy_grid; g_knobs.maxpy_grid = std::min(std::max(value, 0), 16384); break;
     case 78: old = g_knobs.zmc_units; g_knobs.zmc_units = value; break;
     case 80: old = g_knobs.cg_pbws; g_knobs.cg_pbws = value; break;
+    case 81: old = g_knobs.scratch_cache; g_knobs.scratch_cache = value; if (!value) scratch_trim(); break;
     case 79: old = g_knobs.zmc_bpc; g_knobs.zmc_bpc = std::min(std::max(value, 0), 8); break;
     case 69: old = g_knobs.cg_pbw; g_knobs.cg_pbw = value; break;
     case 68: old = g_knobs.ru_2line; g_knobs.ru_2line = value; break;

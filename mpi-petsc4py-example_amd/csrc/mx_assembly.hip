@@ -173,7 +173,7 @@ static int64_t coo_redistribute(Comm *c, const std::vector<int64_t> &rr, int64_t
   hipStream_t st = c->stream;
   DBuf<int64_t> ranges((size_t)P + 1);
   HIPCHECK(hipMemcpyAsync(ranges.p, rr.data(), sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, st));
-  DBuf<int> owner((size_t)std::max<int64_t>(n, 1)), err(1);
+  DBuf<int> owner((size_t)std::max<int64_t>(n, 1), kScratch), err(1);
   DBuf<unsigned long long> cnt((size_t)P);
   HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * P, st));
   HIPCHECK(hipMemsetAsync(err.p, 0, sizeof(int), st));
@@ -200,7 +200,7 @@ static int64_t coo_redistribute(Comm *c, const std::vector<int64_t> &rr, int64_t
   std::vector<int64_t> soff(P + 1, 0);
   for (int q = 0; q < P; ++q) soff[q + 1] = soff[q] + send[q];
   DBuf<CooEntry> sbuf((size_t)std::max<int64_t>(soff[P], 1));
-  DBuf<int64_t> pos((size_t)std::max<int64_t>(n, 1));
+  DBuf<int64_t> pos((size_t)std::max<int64_t>(n, 1), kScratch);
   for (int q = 0; q < P; ++q) {
     if (!send[q]) continue;
     coo_flag_kernel<<<grid_for(n, 256, 8192), 256, 0, st>>>(n, owner.p, q, pos.p);
@@ -2085,17 +2085,17 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   HIPCHECK(hipMemsetAsync(err.p, 0, sizeof(int), st));
 
   // ---- group entries by row
-  DBuf<int64_t> rowptr_own, gcol, gpos;
-  DBuf<double> gval;
+  DBuf<int64_t> rowptr_own(kScratch), gcol(kScratch), gpos(kScratch);
+  DBuf<double> gval(kScratch);
   const int64_t *rowptr = in.rowptr;
   const int64_t *col = in.cols;
   const int32_t *col32 = in.cols ? nullptr : in.cols32;   // read as is by the fused passes
-  DBuf<int64_t> col_wide;
+  DBuf<int64_t> col_wide(kScratch);
   if (col32 && in.coo_rows) fail(MX_ERR_INTERNAL, "32-bit columns with COO input");
   const double *val = in.vals;
   const int64_t *pos = nullptr;
-  DBuf<int64_t> rd_rows, rd_cols;
-  DBuf<double> rd_vals;
+  DBuf<int64_t> rd_rows(kScratch), rd_cols(kScratch);
+  DBuf<double> rd_vals(kScratch);
   AssemblyInput cin = in;
   if (in.coo_rows && c->size > 1) {   // off-process rows: stash exchange first
     cin.nnz = coo_redistribute(c, A->rranges, M, in.coo_rows, in.cols, in.vals, in.nnz, rd_rows, rd_cols, rd_vals);
@@ -2104,7 +2104,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   }
   if (cin.coo_rows) {
     const AssemblyInput &in = cin;
-    DBuf<unsigned long long> cnt((size_t)m + 1);
+    DBuf<unsigned long long> cnt((size_t)m + 1, kScratch);
     HIPCHECK(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * (m + 1), st));
     if (nnz) {
       coo_count_kernel<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(nnz, in.coo_rows, in.cols, A->rstart, m, cnt.p, err.p);
@@ -2144,8 +2144,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
 
   const bool multi = c->size > 1;
   const int64_t nw = multi ? cdiv(N, 32) : 0;
-  DBuf<unsigned> bitmap((size_t)std::max<int64_t>(nw, 1));
-  DBuf<int64_t> wbase((size_t)std::max<int64_t>(nw, 1));
+  DBuf<unsigned> bitmap((size_t)std::max<int64_t>(nw, 1), kScratch);
+  DBuf<int64_t> wbase((size_t)std::max<int64_t>(nw, 1), kScratch);
   if (nw) HIPCHECK(hipMemsetAsync(bitmap.p, 0, sizeof(unsigned) * nw, st));
   A->dptr.alloc((size_t)m + 1);
   A->optr.alloc((size_t)m + 1);
@@ -2171,8 +2171,8 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
     if (herr & 4) fail(MX_ERR_ARG, "row pointer array is not nondecreasing");
     if (herr & 1) fail(MX_ERR_OUTOFRANGE, "Column too large: max " + std::to_string(N - 1));
   };
-  DBuf<int64_t> ccol, cnt_out;
-  DBuf<double> cval;
+  DBuf<int64_t> ccol(kScratch), cnt_out(kScratch);
+  DBuf<double> cval(kScratch);
   double t_canon;
   if (fused) {
     // ---- canonicalise + split counts in one register pass (canon_count_kernel)
@@ -2198,7 +2198,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
     ccol.alloc((size_t)std::max<int64_t>(tot_in, 1));
     cval.alloc((size_t)std::max<int64_t>(tot_in, 1));
     cnt_out.alloc((size_t)m + 1);
-    DBuf<int64_t> long_rows((size_t)m + 1);
+    DBuf<int64_t> long_rows((size_t)m + 1, kScratch);
     if (m) {
 #define CANON(WW) canon_rows_wave_kernel<WW><<<sgrid, 256, 0, st>>>(m, rowptr, col, val, pos, N, add, ccol.p, cval.p, cnt_out.p, long_rows.p, &lmax.p[1], err.p)
       switch (SW) { case 8: CANON(8); break; case 16: CANON(16); break; case 32: CANON(32); break; default: CANON(64); }

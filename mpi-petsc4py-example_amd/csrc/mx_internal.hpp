@@ -29,28 +29,45 @@ void hip_check(hipError_t e, const char *what, const char *file, int line);
 // hipMalloc, or (knob 18) a physically contiguous allocation for large
 // buffers when the driver can provide one (falls back to hipMalloc)
 hipError_t dev_malloc(void **p, size_t bytes);
+// Transient (scratch) buffers: big ones come from / go back to a small
+// per-device cache instead of hipMalloc / hipFree (mx_vec.hip).
+hipError_t scratch_malloc(void **p, size_t bytes);
+void scratch_free(void *p);
+void scratch_trim();
+struct ScratchTag {};
+constexpr ScratchTag kScratch{};
 
 // Owning device allocation (hipMalloc).  The library allocates matrix storage
 // and solver work vectors itself; user vectors arrive as raw device pointers.
+// DBuf(kScratch): a transient buffer of one call (scratch_malloc / scratch_free).
 template <class T> struct DBuf {
   T *p = nullptr;
   size_t n = 0;
+  bool scratch = false;
   DBuf() = default;
+  explicit DBuf(ScratchTag) : scratch(true) {}
   explicit DBuf(size_t count) { alloc(count); }
+  DBuf(size_t count, ScratchTag) : scratch(true) { alloc(count); }
   DBuf(const DBuf &) = delete;
   DBuf &operator=(const DBuf &) = delete;
-  DBuf(DBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
-  DBuf &operator=(DBuf &&o) noexcept { reset(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; return *this; }
+  DBuf(DBuf &&o) noexcept : p(o.p), n(o.n), scratch(o.scratch) { o.p = nullptr; o.n = 0; }
+  DBuf &operator=(DBuf &&o) noexcept {
+    reset(); p = o.p; n = o.n; scratch = o.scratch; o.p = nullptr; o.n = 0; return *this;
+  }
   ~DBuf() { reset(); }
   void alloc(size_t count) {
     reset();
     n = count;
     if (count) {
-      hipError_t e = dev_malloc(reinterpret_cast<void **>(&p), count * sizeof(T));
+      void **q = reinterpret_cast<void **>(&p);
+      hipError_t e = scratch ? scratch_malloc(q, count * sizeof(T)) : dev_malloc(q, count * sizeof(T));
       if (e != hipSuccess) { p = nullptr; n = 0; fail(MX_ERR_MEM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed"); }
     }
   }
-  void reset() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+  void reset() {
+    if (p) { if (scratch) scratch_free(p); else (void)hipFree(p); }
+    p = nullptr; n = 0;
+  }
   T *get() const { return p; }
 };
 
@@ -266,7 +283,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; int cg_pbws = 1; };
+                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; int cg_pbws = 1; int scratch_cache = 1; };
 extern Knobs g_knobs;
 
 struct Halo {

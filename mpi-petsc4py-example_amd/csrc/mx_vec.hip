@@ -12,6 +12,8 @@
 // bitwise reproducible run to run (the order differs from PETSc's BLAS ddot,
 // which is itself unspecified).
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
@@ -24,6 +26,95 @@ hipError_t dev_malloc(void **p, size_t bytes) {
     (void)hipGetLastError();
   }
   return hipMalloc(p, bytes);
+}
+
+// Assembly's transients (the generated or copied input, widened columns,
+// canonical copies) are allocated and freed once per assembly.  hipFree of a
+// big buffer took 7-97 ms in streaks and a contiguous allocation once 5.5 s
+// (tools/asm_outliers.py + tools/slow_calls.py: 14 repeated 27-point share
+// assemblies, hipFree 604 ms in total), so big ones (>= 64 MiB) stay in a
+// per-device cache of at most min(1/8 of HBM, 48 GiB), oldest evicted first:
+// the next assembly of the same size takes them back without a driver call.
+// Plain hipMalloc (no contiguous placement: nothing streams them twice).
+namespace {
+struct ScratchBlock { void *p; size_t bytes; int device; };
+std::mutex g_scr_mu;
+std::vector<ScratchBlock> g_scr_free;                  // cached, oldest first
+std::unordered_map<void *, ScratchBlock> g_scr_live;   // big ones handed out
+size_t g_scr_bytes = 0;
+constexpr size_t SCRATCH_MIN = (size_t)64 << 20, SCRATCH_ROUND = (size_t)2 << 20;
+
+size_t scratch_cap() {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); return 0; }
+  return std::min(tot / 8, (size_t)48 << 30);
+}
+}  // namespace
+
+hipError_t scratch_malloc(void **p, size_t bytes) {
+  if (bytes < SCRATCH_MIN || !g_knobs.scratch_cache) return hipMalloc(p, bytes);
+  const size_t want = (bytes + SCRATCH_ROUND - 1) / SCRATCH_ROUND * SCRATCH_ROUND;
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> g(g_scr_mu);
+    int best = -1;   // the smallest cached block that fits within 25% slack
+    for (int i = 0; i < (int)g_scr_free.size(); ++i) {
+      const ScratchBlock &b = g_scr_free[i];
+      if (b.device == dev && b.bytes >= want && b.bytes <= want + want / 4 &&
+          (best < 0 || b.bytes < g_scr_free[best].bytes))
+        best = i;
+    }
+    if (best >= 0) {
+      const ScratchBlock b = g_scr_free[best];
+      g_scr_free.erase(g_scr_free.begin() + best);
+      g_scr_bytes -= b.bytes;
+      g_scr_live[b.p] = b;
+      *p = b.p;
+      return hipSuccess;
+    }
+  }
+  hipError_t e = hipMalloc(p, want);
+  if (e != hipSuccess) {   // out of memory: give the cache back, then retry once
+    (void)hipGetLastError();
+    scratch_trim();
+    e = hipMalloc(p, want);
+    if (e != hipSuccess) return e;
+  }
+  std::lock_guard<std::mutex> g(g_scr_mu);
+  g_scr_live[*p] = ScratchBlock{*p, want, dev};
+  return hipSuccess;
+}
+
+void scratch_free(void *p) {
+  if (!p) return;
+  ScratchBlock b{nullptr, 0, 0};
+  {
+    std::lock_guard<std::mutex> g(g_scr_mu);
+    auto it = g_scr_live.find(p);
+    if (it != g_scr_live.end()) { b = it->second; g_scr_live.erase(it); }
+  }
+  if (!b.p) { (void)hipFree(p); return; }
+  // hipFree's implicit device synchronisation, kept: whoever takes the block
+  // next must not overlap work still queued on it (any stream)
+  (void)hipDeviceSynchronize();
+  const size_t cap = scratch_cap();
+  std::lock_guard<std::mutex> g(g_scr_mu);
+  if (b.bytes > cap) { (void)hipFree(p); return; }
+  g_scr_free.push_back(b);
+  g_scr_bytes += b.bytes;
+  while (g_scr_bytes > cap && !g_scr_free.empty()) {
+    (void)hipFree(g_scr_free.front().p);
+    g_scr_bytes -= g_scr_free.front().bytes;
+    g_scr_free.erase(g_scr_free.begin());
+  }
+}
+
+void scratch_trim() {
+  std::lock_guard<std::mutex> g(g_scr_mu);
+  for (const ScratchBlock &b : g_scr_free) (void)hipFree(b.p);
+  g_scr_free.clear();
+  g_scr_bytes = 0;
 }
 
 // one block per value: out[v] = sum_b partials[v][b], fixed order (16 loads
