@@ -204,8 +204,8 @@ def assembly_from_host(comm, nx: int, ny: int, nz: int, kind: str = "7pt") -> di
     info = A.info()
     A.destroy()
     del ip, cj, vv
-    canon_b = 32 * nnz + 16 * M          # rowptr + int64 cols + vals read, sorted cols + vals + counts written
-    split_b = 36 * nnz + 32 * M          # count pass (cols) + fill pass (cols, vals -> int32 cols, vals, diag)
+    canon_b = 4 * nnz + 24 * M           # fused count pass: rowptr + int32 cols read, A_d / A_o counts written
+    split_b = 24 * nnz + 32 * M          # fused fill pass: rowptr, cols, vals, split row pointers -> int32 cols, vals, diag
     gbs = lambda b, ms: round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
     return {"workload": f"{kind} {nx}x{ny}x{nz}, int32 I/J + fp64 V host arrays", "rows": M, "nnz": nnz,
             "wall_s": round(wall, 4), "phases_ms": {k: round(v, 3) for k, v in ph.items() if k.endswith("_ms")},
@@ -463,14 +463,16 @@ def config_leg(comm, tag: str, kind: str, dims, ksp: str, expect) -> dict:
     m, nnz = info["m"], info["nnz_d"] + info["nnz_o"]
     S = {"poisson2d": 5, "poisson3d27": 27}.get(kind, 7)
     gbs = lambda b, ms: round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
-    # byte models of the phases (one rank): the generator writes S int64 + fp64
-    # slots per row and canonicalisation reads them with the row pointer and
-    # writes the kept entries and the counts; the split reads the canonical
-    # entries and writes int32 columns + values and the diagonal; the layouts
-    # read A_d and write the SELL values, read them back for the value codes
-    # and the row-pair codes
-    gen_canon_b = 32 * S * m + 16 * nnz + 16 * m
-    split_b = 40 * m + 36 * nnz
+    # byte models of the phases (one rank): the generator writes S column
+    # (cb = 4 bytes below 2^31 global rows, else 8) + fp64 slots per row and
+    # the row pointer; the fused count pass reads the row pointer and the
+    # columns and writes the A_d / A_o counts; the fused fill pass (split)
+    # reads the row pointer, the slots and the split row pointers and writes
+    # int32 columns + values and the diagonal; the layouts read A_d and write
+    # the SELL values, read them back for the value codes and the row-pair codes
+    cb = 4 if nx * ny * (1 if kind == "poisson2d" else nz) < 2 ** 31 else 8
+    gen_canon_b = (2 * cb + 8) * S * m + 32 * m
+    split_b = (cb + 8) * S * m + 12 * nnz + 32 * m
     layout_b = 12 * nnz + 8 * m + 3 * 8 * info["sell_slots_d"] + 2 * info["sell_slots_d"]
     asm = {"assembly_s": round(t_asm, 4),
            "phases": {"generate+canonicalise": {"ms": round(ph["canon_ms"], 3), "bytes": gen_canon_b,
