@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """test_fused_equals_separate_ranks' case (poisson3d 14^3, in-process ranks)
 under the current MXSOLVE_KNOBS, printing where the fused modes' x differs
-from the separate passes' (rank, count, first rows, values).
-    MXSOLVE_KNOBS=81=2 python tools/poison_probe.py [P] [n]"""
+from the separate passes' (rank, count, first rows, values).  Written for a
+poisoned-reuse allocator build (not in the library).
+    python tools/poison_probe.py [P] [n]"""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpi-petsc4py-example_amd"))
 import numpy as np  # noqa: E402
