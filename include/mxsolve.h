@@ -191,7 +191,10 @@ int mx_layout_split(int64_t N, int P, int64_t *ranges /* P+1 */);
  * follow insert_mode (INSERT: last wins; ADD: summed in input order).
  * Checks (petsc4py Mat_AllocAIJ_CSR): indptr[0] == 0, indptr[m] == nnz,
  * nondecreasing -> MX_ERR_ARG; column >= N -> MX_ERR_OUTOFRANGE.
- * src_is_device: the three arrays are device pointers.                          */
+ * src_is_device: the three arrays are device pointers, read in place (they
+ * must stay valid and unchanged until the call returns).  4-byte column ids
+ * are read as they are (no widened copy) whenever every row has at most 64
+ * entries.                                                                       */
 int mx_mat_create_csr(mx_comm c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
                       const void *indptr, int indptr_bytes, const void *cols, int col_bytes,
                       const double *vals, int64_t nnz, int insert_mode, int src_is_device,
