@@ -1401,6 +1401,10 @@ static void cg_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const doubl
   const size_t nx = xb >= 4 ? nv : 0, nx8 = xb == 8 ? nv : 0;
   Carve cv(workspace(A, carve_size({nv, nv, npart, nhist, nv, nv, nx, nx, nx8, nx8, nx8, nx8})));
   struct { double *p; } r{cv.take(nv)}, w{cv.take(nv)}, part{cv.take(npart)}, hist{cv.take(nhist)}, pv{cv.take(nv)};
+  // a history entry no kernel writes (a solve that stops on an exactly zero
+  // residual) reads as 0.0, as PETSc's, not as an earlier solve's value left
+  // in the reused work space
+  if (hist_host) HIPCHECK(hipMemsetAsync(hist.p, 0, sizeof(double) * nhist, st));
   double *pv2 = cv.take(nv);   // fused CG: p_i alternates between pv (i even) and pv2
   // x batches of B: p_j in buffer j % B, the B buffers carved consecutively
   // (equally spaced: the kernels address them from pv; unused slots repeat
@@ -1725,6 +1729,7 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
       part{cv.take(npart), npart}, hist{cv.take(nhist), nhist};
   vec_set(st, (int64_t)vsc.n, 1.0, vsc.p);
   HIPCHECK(hipMemsetAsync(hh.p, 0, sizeof(double) * hh.n, st));
+  if (hist_host) HIPCHECK(hipMemsetAsync(hist.p, 0, sizeof(double) * hist.n, st));   // as in CG
   struct { KspState *p; } sd{state_buf(A)};
   KspState hs;
   init_state(hs, p, MX_NORM_PRECONDITIONED);

@@ -364,6 +364,40 @@ def test_mode5_nonsymmetric_full_rows(selfcomm, oracle_mod):
     assert np.linalg.norm(x.cpu().numpy() - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
 
 
+def test_history_entries_not_written_read_zero(selfcomm, oracle_mod):
+    """A residual-history entry that no kernel writes (the solve above stops
+    at iteration 2 and PETSc's history holds 0.0 there) reads as 0.0 again
+    after a GMRES solve on the same operator has filled the shared KSP work
+    space -- not as that solve's leftovers (found by filling reused device
+    blocks with 0xA5 bytes, knob 81 = 2)."""
+    from mxsolve import _lib
+    from mxsolve.core import DMat
+    L = _lib.load()
+    n = 128
+    ip, c, v = oracle_mod.stencil("poisson3d", n)
+    M = ip.size - 1
+    rows = np.repeat(np.arange(M), np.diff(ip))
+    v = np.where(c - rows == n * n, -1.5, v)
+    b = torch.from_numpy(np.random.default_rng(47).random(M)).cuda()
+    old = L.mx_debug_set(9, 5)
+    old27 = L.mx_debug_set(27, 1)
+    try:
+        A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+        x = torch.zeros(M, dtype=torch.float64, device="cuda")
+        r1 = A.solve(b, x, ksp="cg", pc="jacobi", rtol=1e-8, max_it=300, history=True)
+        y = torch.zeros(M, dtype=torch.float64, device="cuda")
+        A.solve(b, y, ksp="gmres", pc="jacobi", rtol=0.0, max_it=60)
+        x.zero_()
+        r3 = A.solve(b, x, ksp="cg", pc="jacobi", rtol=1e-8, max_it=300, history=True)
+        A.destroy()
+    finally:
+        L.mx_debug_set(9, old)
+        L.mx_debug_set(27, old27)
+    h1, h3 = np.asarray(r1["history"]), np.asarray(r3["history"])
+    assert (r1["its"], r1["reason"]) == (r3["its"], r3["reason"])
+    assert np.array_equal(h1.view(np.uint64), h3.view(np.uint64)), (h1, h3)
+
+
 @pytest.mark.parametrize("dims,max_it", [((128, 128, 128), 10000), ((256, 128, 40), 10000), ((128, 128, 128), 37)])
 def test_two_line_residual_update(selfcomm, oracle_mod, dims, max_it):
     """Knob 68: CG mode 5's residual update with two lines per wave (line y's
