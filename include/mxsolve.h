@@ -430,10 +430,12 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         p.Ap pass on the iterations between x-step batches (the halo pack
  *         forms the ghost planes' p_i from r and p_{i-1}; the same bits as
  *         the separate passes): 1 on (default), 0 off
- * key 81: assembly's transient buffers >= 64 MiB go back to a per-device
- *         cache (at most 1/8 of HBM, 48 GiB) instead of hipFree, for the next
- *         assembly to take (1, default; 0 off and the cache emptied; emptied
- *         too by mx_comm_destroy)
+ * key 81: freed device buffers >= 64 MiB (assembly's transients, a
+ *         destroyed operator's arrays) go to a per-device cache (at most 1/8
+ *         of HBM, 48 GiB) instead of hipFree, for the next allocation of a
+ *         similar size and kind to take (1, default; 0 off and the cache
+ *         emptied; emptied too by mx_comm_destroy; 2: as 1, and every block
+ *         handed out is filled with 0xA5 bytes first -- tests)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

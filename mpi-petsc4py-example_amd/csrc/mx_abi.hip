@@ -513,7 +513,7 @@ int mx_dev_alloc(int device, size_t bytes, void **ptr) {
   });
 }
 
-int mx_dev_free(void *ptr) { return guard([&] { if (ptr) HIPCHECK(hipFree(ptr)); }); }
+int mx_dev_free(void *ptr) { return guard([&] { dev_free(ptr); }); }
 
 int mx_debug_set(int key, int value) {
   int old = -1;

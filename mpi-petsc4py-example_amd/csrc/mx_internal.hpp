@@ -29,10 +29,11 @@ void hip_check(hipError_t e, const char *what, const char *file, int line);
 // hipMalloc, or (knob 18) a physically contiguous allocation for large
 // buffers when the driver can provide one (falls back to hipMalloc)
 hipError_t dev_malloc(void **p, size_t bytes);
-// Transient (scratch) buffers: big ones come from / go back to a small
-// per-device cache instead of hipMalloc / hipFree (mx_vec.hip).
+// Transient (scratch) buffers of one call.  Big buffers of either kind come
+// from / go back to a small per-device cache instead of hipMalloc / hipFree
+// (dev_free; scratch_trim empties the cache; mx_vec.hip).
 hipError_t scratch_malloc(void **p, size_t bytes);
-void scratch_free(void *p);
+void dev_free(void *p);
 void scratch_trim();
 struct ScratchTag {};
 constexpr ScratchTag kScratch{};
@@ -65,7 +66,7 @@ template <class T> struct DBuf {
     }
   }
   void reset() {
-    if (p) { if (scratch) scratch_free(p); else (void)hipFree(p); }
+    if (p) dev_free(p);
     p = nullptr; n = 0;
   }
   T *get() const { return p; }

@@ -20,101 +20,124 @@
 
 namespace mx {
 
-hipError_t dev_malloc(void **p, size_t bytes) {
-  if (g_knobs.contig && bytes >= ((size_t)64 << 20)) {
-    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
-    (void)hipGetLastError();
-  }
-  return hipMalloc(p, bytes);
-}
-
-// Assembly's transients (the generated or copied input, widened columns,
-// canonical copies) are allocated and freed once per assembly.  hipFree of a
-// big buffer took 7-97 ms in streaks and a contiguous allocation once 5.5 s
-// (tools/asm_outliers.py + tools/slow_calls.py: 14 repeated 27-point share
-// assemblies, hipFree 604 ms in total), so big ones (>= 64 MiB) stay in a
-// per-device cache of at most min(1/8 of HBM, 48 GiB), oldest evicted first:
-// the next assembly of the same size takes them back without a driver call.
-// Plain hipMalloc (no contiguous placement: nothing streams them twice).
+// Big device buffers (>= 64 MiB) go through a small per-device cache.
+// Assembly allocates and frees its transients (the generated or copied input,
+// widened columns, canonical copies) once per call, and destroying an operator
+// frees its arrays: over 14 repeated 27-point share assemblies hipFree of a big
+// buffer took 7-97 ms in streaks (160 ms assemblies against a 17 ms median),
+// and contiguous allocations of a re-created operator 1.5-5.5 s now and then
+// (tools/asm_outliers.py, tools/asm_time.py, tools/slow_calls.py).  A freed big
+// buffer is therefore kept (after a device synchronisation, as hipFree would
+// do) in a cache of at most min(1/8 of HBM, 48 GiB), oldest evicted first, and
+// the next allocation of a similar size takes it back without a driver call.
+// Library buffers (dev_malloc) are physically contiguous when the driver can
+// provide it (knob 18) and only take cached blocks of the same kind;
+// transients (scratch_malloc) take any and are plain hipMalloc otherwise.
+// Knob 81 = 0: no caching; 2: every block handed out is first filled with
+// 0xA5 bytes (tests: a buffer read before it is written shows up).
 namespace {
-struct ScratchBlock { void *p; size_t bytes; int device; };
-std::mutex g_scr_mu;
-std::vector<ScratchBlock> g_scr_free;                  // cached, oldest first
-std::unordered_map<void *, ScratchBlock> g_scr_live;   // big ones handed out
-size_t g_scr_bytes = 0;
-constexpr size_t SCRATCH_MIN = (size_t)64 << 20, SCRATCH_ROUND = (size_t)2 << 20;
+struct BigBlock { void *p; size_t bytes; int device; bool contig; };
+std::mutex g_big_mu;
+std::vector<BigBlock> g_big_free;                  // cached, oldest first
+std::unordered_map<void *, BigBlock> g_big_live;   // big blocks handed out
+size_t g_big_bytes = 0;
+constexpr size_t BIG_MIN = (size_t)64 << 20, BIG_ROUND = (size_t)2 << 20;
 
-size_t scratch_cap() {
+size_t cache_cap() {
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); return 0; }
   return std::min(tot / 8, (size_t)48 << 30);
 }
-}  // namespace
 
-hipError_t scratch_malloc(void **p, size_t bytes) {
-  if (bytes < SCRATCH_MIN || !g_knobs.scratch_cache) return hipMalloc(p, bytes);
-  const size_t want = (bytes + SCRATCH_ROUND - 1) / SCRATCH_ROUND * SCRATCH_ROUND;
-  int dev = 0;
-  HIPCHECK(hipGetDevice(&dev));
-  {
-    std::lock_guard<std::mutex> g(g_scr_mu);
-    int best = -1;   // the smallest cached block that fits within 25% slack
-    for (int i = 0; i < (int)g_scr_free.size(); ++i) {
-      const ScratchBlock &b = g_scr_free[i];
-      if (b.device == dev && b.bytes >= want && b.bytes <= want + want / 4 &&
-          (best < 0 || b.bytes < g_scr_free[best].bytes))
-        best = i;
-    }
-    if (best >= 0) {
-      const ScratchBlock b = g_scr_free[best];
-      g_scr_free.erase(g_scr_free.begin() + best);
-      g_scr_bytes -= b.bytes;
-      g_scr_live[b.p] = b;
-      *p = b.p;
-      return hipSuccess;
-    }
+// the smallest cached block of this device (and kind: need_contig 1 / 0, or
+// -1 for any) that fits within 25% slack
+bool cache_take(size_t want, int dev, int need_contig, void **p) {
+  std::lock_guard<std::mutex> g(g_big_mu);
+  int best = -1;
+  for (int i = 0; i < (int)g_big_free.size(); ++i) {
+    const BigBlock &b = g_big_free[i];
+    if (b.device == dev && b.bytes >= want && b.bytes <= want + want / 4 &&
+        (need_contig < 0 || (int)b.contig == need_contig) && (best < 0 || b.bytes < g_big_free[best].bytes))
+      best = i;
   }
-  hipError_t e = hipMalloc(p, want);
-  if (e != hipSuccess) {   // out of memory: give the cache back, then retry once
-    (void)hipGetLastError();
-    scratch_trim();
-    e = hipMalloc(p, want);
-    if (e != hipSuccess) return e;
-  }
-  std::lock_guard<std::mutex> g(g_scr_mu);
-  g_scr_live[*p] = ScratchBlock{*p, want, dev};
-  return hipSuccess;
+  if (best < 0) return false;
+  const BigBlock b = g_big_free[best];
+  g_big_free.erase(g_big_free.begin() + best);
+  g_big_bytes -= b.bytes;
+  g_big_live[b.p] = b;
+  *p = b.p;
+  return true;
 }
 
-void scratch_free(void *p) {
-  if (!p) return;
-  ScratchBlock b{nullptr, 0, 0};
-  {
-    std::lock_guard<std::mutex> g(g_scr_mu);
-    auto it = g_scr_live.find(p);
-    if (it != g_scr_live.end()) { b = it->second; g_scr_live.erase(it); }
+hipError_t big_malloc(void **p, size_t bytes, bool library) {
+  const bool cache = bytes >= BIG_MIN && g_knobs.scratch_cache;
+  const bool want_contig = library && bytes >= BIG_MIN && g_knobs.contig;
+  const size_t want = cache ? (bytes + BIG_ROUND - 1) / BIG_ROUND * BIG_ROUND : bytes;
+  auto poison = [&] {
+    if (g_knobs.scratch_cache == 2) { HIPCHECK(hipMemset(*p, 0xA5, want)); HIPCHECK(hipDeviceSynchronize()); }
+  };
+  int dev = 0;
+  if (cache) {
+    HIPCHECK(hipGetDevice(&dev));
+    if (cache_take(want, dev, library ? (int)want_contig : -1, p)) { poison(); return hipSuccess; }
   }
-  if (!b.p) { (void)hipFree(p); return; }
+  bool contig = false;
+  if (want_contig) {
+    contig = hipExtMallocWithFlags(p, want, hipDeviceMallocContiguous) == hipSuccess;
+    if (!contig) (void)hipGetLastError();
+  }
+  if (!contig) {
+    hipError_t e = hipMalloc(p, want);
+    if (e != hipSuccess && cache) {   // out of memory: give the cache back, then retry once
+      (void)hipGetLastError();
+      scratch_trim();
+      e = hipMalloc(p, want);
+    }
+    if (e != hipSuccess) return e;
+  }
+  if (cache) {
+    {
+      std::lock_guard<std::mutex> g(g_big_mu);
+      g_big_live[*p] = BigBlock{*p, want, dev, contig};
+    }
+    poison();
+  }
+  return hipSuccess;
+}
+}  // namespace
+
+hipError_t dev_malloc(void **p, size_t bytes) { return big_malloc(p, bytes, true); }
+hipError_t scratch_malloc(void **p, size_t bytes) { return big_malloc(p, bytes, false); }
+
+void dev_free(void *p) {
+  if (!p) return;
+  BigBlock b{nullptr, 0, 0, false};
+  {
+    std::lock_guard<std::mutex> g(g_big_mu);
+    auto it = g_big_live.find(p);
+    if (it != g_big_live.end()) { b = it->second; g_big_live.erase(it); }
+  }
+  if (!b.p || !g_knobs.scratch_cache) { (void)hipFree(p); return; }
   // hipFree's implicit device synchronisation, kept: whoever takes the block
   // next must not overlap work still queued on it (any stream)
   (void)hipDeviceSynchronize();
-  const size_t cap = scratch_cap();
-  std::lock_guard<std::mutex> g(g_scr_mu);
+  const size_t cap = cache_cap();
+  std::lock_guard<std::mutex> g(g_big_mu);
   if (b.bytes > cap) { (void)hipFree(p); return; }
-  g_scr_free.push_back(b);
-  g_scr_bytes += b.bytes;
-  while (g_scr_bytes > cap && !g_scr_free.empty()) {
-    (void)hipFree(g_scr_free.front().p);
-    g_scr_bytes -= g_scr_free.front().bytes;
-    g_scr_free.erase(g_scr_free.begin());
+  g_big_free.push_back(b);
+  g_big_bytes += b.bytes;
+  while (g_big_bytes > cap && !g_big_free.empty()) {
+    (void)hipFree(g_big_free.front().p);
+    g_big_bytes -= g_big_free.front().bytes;
+    g_big_free.erase(g_big_free.begin());
   }
 }
 
 void scratch_trim() {
-  std::lock_guard<std::mutex> g(g_scr_mu);
-  for (const ScratchBlock &b : g_scr_free) (void)hipFree(b.p);
-  g_scr_free.clear();
-  g_scr_bytes = 0;
+  std::lock_guard<std::mutex> g(g_big_mu);
+  for (const BigBlock &b : g_big_free) (void)hipFree(b.p);
+  g_big_free.clear();
+  g_big_bytes = 0;
 }
 
 // one block per value: out[v] = sum_b partials[v][b], fixed order (16 loads
