@@ -463,7 +463,8 @@ int mx_debug_assembly_times(double *out, int n);
 int mx_debug_stream_read(mx_comm c, const double *x_dev, int64_t n, int width_bytes, double *out_dev);
 /* Device memory for vectors (what PETSc's VecCreate allocates): physically
  * contiguous for >= 64 MiB when the driver can provide it (key 18), else
- * hipMalloc; the shim wraps it as a torch tensor.                            */
+ * hipMalloc; the shim wraps it as a torch tensor.  Blocks >= 64 MiB come
+ * from / return to the library's device buffer cache (key 81).               */
 int mx_dev_alloc(int device, size_t bytes, void **ptr);
 int mx_dev_free(void *ptr);
 /* Communication latency on the communicator's stream, iters back to back
