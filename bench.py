@@ -568,6 +568,86 @@ def rnd(v, k):
     return None if v is None else round(v, k)
 
 
+# Wall-time budget of one timed leg (seconds; MXSOLVE_BENCH_LEG_BUDGET_S).  A
+# leg normally takes a few seconds (RCCL warm-up, W + K iterations, the
+# converged solve); a hung one (a multi-rank RCCL graph capture that never
+# completes, a peer that never arrives) must not eat the driver's run.
+LEG_BUDGET_S = 60.0
+
+
+class LegWatchdog:
+    """Backstop of one leg's budget: a timer that calls `abort` (mx_comm_abort:
+    ncclCommAbort / the shared-memory world's abort flag) when the leg is still
+    running `after_s` seconds in, for a rank blocked somewhere that does not
+    poll a deadline of its own (the library's waits already fail after knobs
+    33 / 47, which run_legs sets to the budget).  The blocked call then fails
+    with MX_ERR_COMM and the leg is recorded as failed."""
+
+    def __init__(self, after_s: float, abort):
+        import threading
+        self.fired = False
+        self._abort = abort
+        self._t = threading.Timer(after_s, self._fire)
+        self._t.daemon = True
+
+    def _fire(self):
+        self.fired = True
+        try:
+            self._abort()
+        except Exception:  # noqa: BLE001  (the blocked call reports the failure)
+            pass
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._t.cancel()
+        return False
+
+
+def run_legs(specs, run_leg, set_knobs, budget_s: float, abort, err_type):
+    """Run the timed legs in order under a wall-time budget each.  Per leg the
+    library's deadlines -- knob 33 (no progress in a solve) and knob 47 (plain
+    stream waits) -- are set to the budget unless the leg sets its own, and a
+    LegWatchdog aborts the communicator at twice the budget.  A leg that fails
+    (MX_ERR_COMM: an RCCL error, a deadline, the watchdog) ends the loop: the
+    communicator is aborted, so no later leg or collective can run; the line is
+    then printed from the legs already measured (the first leg failing raises:
+    there is nothing to report).  Returns (legs, failed, comm_dead)."""
+    legs, failed, dead = [], [], None
+    dl = int(budget_s * 1000)
+    for name, kn in specs:
+        old = set_knobs({33: dl, 47: dl, **kn})
+        t0 = time.perf_counter()
+        wd = LegWatchdog(2 * budget_s, abort)
+        try:
+            with wd:
+                leg = run_leg(name, kn)
+            leg["wall_s"] = round(time.perf_counter() - t0, 3)
+            legs.append(leg)
+        except err_type as e:
+            if not legs:
+                raise
+            failed.append({"leg": name, "knobs": kn, "error": str(e), "wall_s": round(time.perf_counter() - t0, 3),
+                           "budget_s": budget_s, "watchdog_fired": wd.fired})
+            dead = str(e)
+            break
+        finally:
+            set_knobs(old)
+    return legs, failed, dead
+
+
+def parse_stall(spec: str | None):
+    """MXSOLVE_BENCH_STALL_LEG=<leg name>:<seconds> -- rehearsal hook: in that
+    leg the last rank sleeps before the timed solve (a peer that stops
+    answering), so the budget can be exercised."""
+    if not spec or ":" not in spec:
+        return None
+    name, s = spec.rsplit(":", 1)
+    return name, float(s)
+
+
 def parity_record(its: int, reason: int, rel: float, o: dict) -> dict:
     return {"checker": f"oracle/petsc_oracle.c CG + Jacobi, P = {o['P']} row-block model, converged "
                        f"(rtol 1e-5), {o['solve_s']} s on the host",
@@ -701,62 +781,55 @@ def main():
     if world == 1:
         leg_specs = [("auto", {})]
     else:
-        # eager legs first: a multi-rank RCCL capture has only ever run on the
-        # driver's node, so if it fails there (an RCCL error, or no progress
-        # for 30 s: knob 33), the eager legs are already measured and the
-        # line is still printed from them
-        # mode 5 fuses the direction update into the split p.Ap pass between
-        # x-step batches (knob 80, default on); "mode5sep" keeps the separate
-        # direction update pass (the same bits), so the first 8-GPU run shows
-        # which pays on xGMI
-        leg_specs = [("mode2/eager", {9: 2, 7: 1}), ("mode5/eager", {9: 5, 7: 1}),
+        # the library's default first ("auto": CG mode 5 with the direction
+        # update fused into the split p.Ap pass where it applies, else mode 2;
+        # eager launches), then the alternatives: mode 2, mode 5 with the
+        # separate direction update pass (knob 80 = 0, the same bits), and
+        # last the RCCL graph-replay legs -- a multi-rank RCCL capture has
+        # only ever run on the driver's node, so if it fails or hangs there,
+        # the eager legs are already measured and the line is still printed
+        # from them (every leg runs under a wall-time budget: run_legs)
+        leg_specs = [("auto", {}), ("mode2/eager", {9: 2, 7: 1}),
                      ("mode5sep/eager", {9: 5, 80: 0, 7: 1}),
                      ("mode2/graph", {9: 2, 7: 2, 33: 30000}), ("mode5/graph", {9: 5, 7: 2, 33: 30000})]
 
     def set_knobs(kn):
         return {k: L.mx_debug_set(k, v) for k, v in kn.items()}
 
-    legs = []
-    comm_dead = None
-    for name, kn in leg_specs:
-        old = set_knobs(kn)
-        try:
-            # rehearsal hook: the failure path of a leg (MXSOLVE_BENCH_FAIL_LEG=<leg name>)
-            if os.environ.get("MXSOLVE_BENCH_FAIL_LEG") == name:
-                raise _lib.MxError(_lib.MX_ERR_COMM, f"injected failure of leg {name}")
-            if args.warmup > 0:
-                A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=args.warmup)
+    stall = parse_stall(os.environ.get("MXSOLVE_BENCH_STALL_LEG"))
+
+    def run_leg(name, kn):
+        # rehearsal hook: the failure path of a leg (MXSOLVE_BENCH_FAIL_LEG=<leg name>)
+        if os.environ.get("MXSOLVE_BENCH_FAIL_LEG") == name:
+            raise _lib.MxError(_lib.MX_ERR_COMM, f"injected failure of leg {name}")
+        if args.warmup > 0:
+            A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=args.warmup)
+        barrier()
+        if stall and stall[0] == name and rank == world - 1:
+            time.sleep(stall[1])             # rehearsal hook: a peer that stops answering
+        t0 = time.perf_counter()
+        r = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=args.steps)
+        barrier()
+        dt_local = time.perf_counter() - t0
+        dt = max_over_ranks(dt_local)
+        assert r["its"] == args.steps, r
+        leg = {"leg": name, "knobs": kn, "cg_mode": r["cg_mode"], "cg_xbatch": r["cg_xbatch"],
+               "value": round(args.steps / dt, 3),
+               "ms_per_step": round(dt / args.steps * 1e3, 4), "_dt": dt,
+               "per_rank_timed_s": [round(v, 5) for v in gather(dt_local)]}
+        if not args.no_solve:
+            x.zero_()
             barrier()
             t0 = time.perf_counter()
-            r = A.solve(b, x, ksp="cg", pc="jacobi", rtol=0.0, max_it=args.steps)
+            rs = A.solve(b, x, ksp="cg", pc="jacobi")
             barrier()
-            dt_local = time.perf_counter() - t0
-            dt = max_over_ranks(dt_local)
-            assert r["its"] == args.steps, r
-            leg = {"leg": name, "knobs": kn, "cg_mode": r["cg_mode"], "cg_xbatch": r["cg_xbatch"],
-                   "value": round(args.steps / dt, 3),
-                   "ms_per_step": round(dt / args.steps * 1e3, 4), "_dt": dt,
-                   "per_rank_timed_s": [round(v, 5) for v in gather(dt_local)]}
-            if not args.no_solve:
-                x.zero_()
-                barrier()
-                t0 = time.perf_counter()
-                rs = A.solve(b, x, ksp="cg", pc="jacobi")
-                barrier()
-                ts = max_over_ranks(time.perf_counter() - t0)
-                leg.update({"its": rs["its"], "reason": rs["reason"], "solve_s": ts, "_x": x.clone()})
-            legs.append(leg)
-        except _lib.MxError as e:
-            if not legs:
-                raise
-            # the communicator is aborted: no further GPU legs or collectives
-            legs.append({"leg": name, "knobs": kn, "error": str(e)})
-            comm_dead = str(e)
-            break
-        finally:
-            set_knobs(old)
-    failed = [lg for lg in legs if "error" in lg]
-    legs = [lg for lg in legs if "error" not in lg]
+            ts = max_over_ranks(time.perf_counter() - t0)
+            leg.update({"its": rs["its"], "reason": rs["reason"], "solve_s": ts, "_x": x.clone()})
+        return leg
+
+    budget = float(os.environ.get("MXSOLVE_BENCH_LEG_BUDGET_S", LEG_BUDGET_S))
+    legs, failed, comm_dead = run_legs(leg_specs, run_leg, set_knobs, budget,
+                                       lambda: L.mx_comm_abort(comm.h) if world > 1 else None, _lib.MxError)
 
     # parity: every leg's converged solve against the oracle (the checker, run
     # on rank 0 after the GPU work; at N = 1 it is the cpu_baseline leg's own
@@ -799,7 +872,7 @@ def main():
     bytes_csr = spmv_bytes(m, nnz_loc, ng)
     bytes_spmv = spmv_format_bytes(info, m, nnz_loc, ng)
     pw = dom = comm_lat = None
-    achieved = avg_ms = spmv_avg_ms = spmv_alone_ms = mult_ms = cold_ms = bytes_launch = None
+    achieved = avg_ms = spmv_avg_ms = spmv_alone_ms = mult_ms = cold_ms = cold_kernel_ms = bytes_launch = None
     if comm_dead is None:       # (an aborted communicator runs nothing more)
         # roofline pass: the same CG iterations with a HIP event pair on every
         # MatMult-family launch (on the library stream the kernel runs on; one
@@ -858,19 +931,12 @@ def main():
         # standalone SpMV timing (same kernel, back-to-back)
         y = comm.empty(m)
         spmv_alone_ms, mult_ms = A.bench_mult(b, y, 50)
-        # cold-cache MatMult: stream 512 MB through the caches first
-        flush = torch.empty(1 << 26, dtype=torch.float64, device=y.device)
-        cold = []
-        for _ in range(3):
-            flush.fill_(1.0)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            A.mult(b, y)
-            e1.record()
-            e1.synchronize()
-            cold.append(e0.elapsed_time(e1))
+        # cold-cache MatMult: 1 GB streamed through the caches first (SURVEY
+        # §8d), the MatMult queued behind it by the library (no host launch
+        # gap inside the span; round 5's torch events around A.mult() held one)
+        flush = torch.empty(1 << 27, dtype=torch.float64, device=y.device)
+        cold_kernel_ms, cold_ms = A.bench_mult_cold(b, y, flush, 5)
         del flush
-        cold_ms = sorted(cold)[1]
 
         # communication latency on the library stream (N > 1): the two CG
         # all-reduces and the halo exchange, back to back; diagnostics for scaling
@@ -963,7 +1029,10 @@ def main():
                                 "GBps": round(bytes_spmv / (spmv_alone_ms * 1e-3) / 1e9, 1),
                                 "matmult_ms": round(mult_ms, 5),
                                 "cold_matmult_ms": round(cold_ms, 5),
-                                "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1)} if spmv_alone_ms else None,
+                                "cold_kernel_ms": round(cold_kernel_ms, 5) if cold_kernel_ms > 0 else None,
+                                "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1),
+                                "cold_frac": round(bytes_spmv / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            if spmv_alone_ms else None,
             "spmv_general": general,
             "cg_iter_bytes_survey": cg_iter_bytes(m, nnz_loc, ng),
             "cg_fusion_mode": mode,

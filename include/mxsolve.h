@@ -137,8 +137,11 @@ typedef struct {
 
 /* ---- library ---------------------------------------------------------------- */
 int mx_version(void);
-/* PetscFinalize: waits for all device work the library queued.  Handles must
- * be destroyed before (or not used after) this call.                        */
+/* PetscFinalize: waits for all device work the library queued and returns
+ * the device buffer cache (key 81: freed buffers kept for reuse, at most 1/8
+ * of HBM) to the driver -- the library's counterpart of torch's empty_cache.
+ * Handles must be destroyed before (or not used after) this call; calling it
+ * again later (more work, then a trim) is allowed.                           */
 int mx_finalize(void);
 int mx_last_error(char *buf, size_t len);
 
@@ -159,7 +162,11 @@ int mx_comm_create_rccl(int rank, int size, int device, const void *uid, size_t 
  * [collective]                                                                  */
 int mx_comm_create_shm(int rank, int size, int device, const char *name, int64_t slot_kib,
                        mx_comm *out);
-/* Release peers blocked in a shared-memory collective (a failing rank calls it). */
+/* Release peers blocked in a shared-memory collective (a failing rank calls
+ * it), or abort an RCCL communicator (ncclCommAbort: its in-flight kernels
+ * stop; waits on this rank fail with MX_ERR_COMM).  May be called from another
+ * host thread than the one blocked in the collective (a wall-time watchdog);
+ * every later collective on the communicator fails with MX_ERR_COMM.          */
 int mx_comm_abort(mx_comm c);
 /* Single-rank communicator (PETSC_COMM_SELF / MPI.COMM_WORLD of size 1).       */
 int mx_comm_create_self(int device, mx_comm *out);
@@ -222,6 +229,15 @@ int mx_mat_get_diagonal(mx_mat A, double *d_dev);
  * per SpMV kernel launch and per full MatMult (halo included).  [collective]     */
 int mx_mat_bench_mult(mx_mat A, const double *x_dev, double *y_dev, int iters,
                       double *spmv_ms, double *mult_ms);
+/* Cold-cache timing for bench.py: `iters` times, stream the
+ * flush_n-double device buffer flush_dev in (plain loads: L2 and the
+ * memory-side cache then hold clean flush lines only), then one MatMult.  Medians over iters, device ms: the SpMV kernel
+ * alone (one rank: events attached to its dispatch; else < 0) and the whole
+ * MatMult from an event queued right behind the flush.  Every launch is
+ * enqueued while the flush still runs, so no host gap is inside the spans.
+ * [collective]                                                                 */
+int mx_mat_bench_mult_cold(mx_mat A, const double *x_dev, double *y_dev, double *flush_dev, int64_t flush_n,
+                           int iters, double *spmv_ms, double *mult_ms);
 int mx_mat_destroy(mx_mat A);
 
 /* ---- Vec (local length n, device pointers; reductions are collective) ----- */
@@ -295,8 +311,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         vector is aligned (0/1, default 0: one row per thread per step)
  * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
  * key 15: grid cap of the halo-boundary SpMV launch (0 = default 2048)
- * key 18: library buffers >= 64 MiB physically contiguous when the driver can
- *         provide them (hipDeviceMallocContiguous, else hipMalloc; 0/1, default 1)
  * key 19: one-byte row masks for aligned-offset slices when every slice has
  *         <= 8 offsets (read at assembly; 0/1, default 1)
  * key 21: CG vector passes issue four steps' loads together: 0 never, 1 always,
@@ -430,12 +444,16 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         p.Ap pass on the iterations between x-step batches (the halo pack
  *         forms the ghost planes' p_i from r and p_{i-1}; the same bits as
  *         the separate passes): 1 on (default), 0 off
- * key 81: freed device buffers >= 64 MiB (assembly's transients, a
- *         destroyed operator's arrays) go to a per-device cache (at most 1/8
- *         of HBM, 48 GiB) instead of hipFree, for the next allocation of a
- *         similar size and kind to take (1, default; 0 off and the cache
- *         emptied; emptied too by mx_comm_destroy; 2: as 1, and every block
- *         handed out is filled with 0xA5 bytes first -- tests)
+ * key 81: freed device buffers >= 1 MiB (assembly's transients, a
+ *         destroyed operator's arrays, KSP work space) go to a per-device
+ *         cache (at most 1/8 of HBM, 48 GiB) instead of hipFree, for the next
+ *         allocation of a similar size to take (1, default; 0 off and the
+ *         cache emptied; emptied too by mx_comm_destroy and mx_finalize; 2: as
+ *         1, and every block handed out is filled with 0xA5 bytes first --
+ *         tests: a buffer read before it is written shows up)
+ * (key 18, physically contiguous allocations, was retired in round 6: freed
+ *  contiguous blocks whose address range was reused were still reached through
+ *  stale translations -- DESIGN.md section 11)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches
@@ -461,10 +479,9 @@ int mx_debug_assembly_times(double *out, int n);
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,
  * and writes one partial sum per workgroup to out_dev.                      */
 int mx_debug_stream_read(mx_comm c, const double *x_dev, int64_t n, int width_bytes, double *out_dev);
-/* Device memory for vectors (what PETSc's VecCreate allocates): physically
- * contiguous for >= 64 MiB when the driver can provide it (key 18), else
- * hipMalloc; the shim wraps it as a torch tensor.  Blocks >= 64 MiB come
- * from / return to the library's device buffer cache (key 81).               */
+/* Device memory for vectors (what PETSc's VecCreate allocates): hipMalloc;
+ * the shim wraps it as a torch tensor.  Blocks >= 1 MiB come from / return to
+ * the library's device buffer cache (key 81).                                */
 int mx_dev_alloc(int device, size_t bytes, void **ptr);
 int mx_dev_free(void *ptr);
 /* Communication latency on the communicator's stream, iters back to back

@@ -1,10 +1,12 @@
 // mx_abi.hip -- extern "C" entry points of libmxsolve.so (declared in include/mxsolve.h).
 // Every call: set the handle's device, run, translate exceptions to an error
 // code + thread-local message.  No torch types cross this boundary.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "mx_internal.hpp"
 
@@ -88,7 +90,7 @@ int mx_comm_create_shm(int rank, int size, int device, const char *name, int64_t
   });
 }
 
-int mx_comm_abort(mx_comm c) { return guard([&] { if (c && c->c) abort_shm_comm(c->c); }); }
+int mx_comm_abort(mx_comm c) { return guard([&] { if (c && c->c) abort_comm_async(c->c); }); }
 
 int mx_comm_create_self(int device, mx_comm *out) {
   return guard([&] {
@@ -409,6 +411,41 @@ int mx_mat_bench_mult(mx_mat a, const double *x, double *y, int iters, double *s
   });
 }
 
+int mx_mat_bench_mult_cold(mx_mat a, const double *x, double *y, double *flush, int64_t flush_n, int iters,
+                           double *spmv_ms, double *mult_ms) {
+  return guard([&] {
+    Mat *A = M(a);
+    hipStream_t st = A->comm->stream;
+    if (iters < 1 || !flush || flush_n < 1) fail(MX_ERR_ARG, "cold MatMult: iters and a flush buffer are needed");
+    Comm *cm = A->comm;
+    if (cm->red_scratch.n < (size_t)RED_BLOCKS + 64) cm->red_scratch.alloc((size_t)RED_BLOCKS + 64);
+    hipEvent_t ev[4];
+    for (auto &e : ev) HIPCHECK(hipEventCreate(&e));
+    std::vector<double> ks, ms;
+    for (int k = 0; k < iters; ++k) {
+      flush_read(st, flush, flush_n, cm->red_scratch.p);   // the host enqueues the rest while this runs
+      HIPCHECK(hipEventRecord(ev[0], st));
+      const bool ext = A->comm->size == 1;
+      if (ext) g_ext_timing = ExtTiming{ev[2], ev[3], true, false};
+      matmult_overlap(A, x, y, SPMV_PLAIN, Jac{}, nullptr, nullptr);
+      const bool used = ext && g_ext_timing.used;
+      g_ext_timing = ExtTiming{};
+      HIPCHECK(hipEventRecord(ev[1], st));
+      HIPCHECK(hipEventSynchronize(ev[1]));
+      float t = 0.f, u = 0.f;
+      HIPCHECK(hipEventElapsedTime(&t, ev[0], ev[1]));
+      if (used) HIPCHECK(hipEventElapsedTime(&u, ev[2], ev[3]));
+      ms.push_back(t);
+      ks.push_back(used ? u : -1.0);
+    }
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    std::sort(ms.begin(), ms.end());
+    std::sort(ks.begin(), ks.end());
+    if (mult_ms) *mult_ms = ms[ms.size() / 2];
+    if (spmv_ms) *spmv_ms = ks[ks.size() / 2];
+  });
+}
+
 int mx_mat_destroy(mx_mat a) {
   return guard([&] {
     if (!a) return;
@@ -479,6 +516,7 @@ int mx_finalize(void) {
       if (hipSetDevice(d) == hipSuccess) HIPCHECK(hipDeviceSynchronize());
     }
     (void)hipGetLastError();
+    scratch_trim();   // the device buffer cache goes back to the driver
   });
 }
 int mx_vec_rhs_hash(mx_comm c, int64_t i0, int64_t n, double *b) {
@@ -532,7 +570,6 @@ int mx_debug_set(int key, int value) {
     case 13: old = g_knobs.cg_vec; g_knobs.cg_vec = value; break;
     case 14: old = g_knobs.cg_nts; g_knobs.cg_nts = value; break;
     case 15: old = g_knobs.bnd_grid; g_knobs.bnd_grid = value; break;
-    case 18: old = g_knobs.contig; g_knobs.contig = value; break;
     case 19: old = g_knobs.mask8; g_knobs.mask8 = value; break;
     case 21: old = g_knobs.cg_unroll; g_knobs.cg_unroll = value; break;
     case 22: old = g_knobs.cg_upd_grid; g_knobs.cg_upd_grid = std::min(value, 65536); break;

@@ -2176,14 +2176,10 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   double t_canon;
   if (fused) {
     // ---- canonicalise + split counts in one register pass (canon_count_kernel)
-    // Drain the device first.  With several ranks' threads sharing one GPU
-    // (in-process ranks), this pass launched straight after the split
-    // arrays' allocation and zeroing read a few rows of columns as zeros in
-    // ~3% of 8-rank assemblies that followed solves in the same process
-    // (tools/asm_race.py: 12 of ~360; the columns were correct when read
-    // back afterwards); with this synchronisation 0 of 300, and the separate
-    // passes 0 of 330.  One synchronisation per assembly.
-    HIPCHECK(hipDeviceSynchronize());
+    // (no device synchronisation before it: round 5's in-process 8-rank
+    // assemblies that read a few rows of columns as zeros were reading
+    // through stale translations of freed contiguous allocations, retired in
+    // round 6 -- mx_vec.hip; tools/asm_race.py 0 of 320)
     if (m) {
 #define CCNT(WW) if (col32) canon_count_kernel<WW, int32_t><<<cgrid, 256, 0, st>>>(m, rowptr, col32, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p); \
                  else canon_count_kernel<WW, int64_t><<<cgrid, 256, 0, st>>>(m, rowptr, col, pos, N, add, A->cstart, A->cend, A->dptr.p, A->optr.p, bitmap.p, err.p)

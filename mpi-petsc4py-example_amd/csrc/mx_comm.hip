@@ -100,7 +100,7 @@ struct RcclComm : Comm {
     i64buf.alloc(2 * (size_t)s);
   }
   ~RcclComm() override {
-    if (nc) ncclCommDestroy(nc);
+    if (nc && !aborted) ncclCommDestroy(nc);   // (an aborted communicator is freed by ncclCommAbort)
     if (stream) (void)hipStreamDestroy(stream);
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
   }
@@ -119,6 +119,7 @@ struct RcclComm : Comm {
     NCCLCHECK(ncclGroupEnd());
   }
   void alltoall_i64(const int64_t *send, int64_t *recv) override {
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     HIPCHECK(hipMemcpyAsync(i64buf.p, send, sizeof(int64_t) * size, hipMemcpyHostToDevice, stream));
     NCCLCHECK(ncclGroupStart());
     for (int q = 0; q < size; ++q) {
@@ -130,12 +131,14 @@ struct RcclComm : Comm {
     wait_stream(stream);
   }
   void allgather_i64(int64_t v, int64_t *all) override {
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     HIPCHECK(hipMemcpyAsync(i64buf.p, &v, sizeof(int64_t), hipMemcpyHostToDevice, stream));
     NCCLCHECK(ncclAllGather(i64buf.p, i64buf.p + size, 1, ncclInt64, nc, stream));
     HIPCHECK(hipMemcpyAsync(all, i64buf.p + size, sizeof(int64_t) * size, hipMemcpyDeviceToHost, stream));
     wait_stream(stream);
   }
   void barrier() override {
+    if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     HIPCHECK(hipMemsetAsync(i64buf.p, 0, sizeof(int64_t), stream));
     NCCLCHECK(ncclAllReduce(i64buf.p, i64buf.p, 1, ncclInt64, ncclSum, nc, stream));
     wait_stream(stream);
@@ -167,8 +170,11 @@ struct RcclComm : Comm {
       const hipError_t e = query();
       if (e == hipSuccess) return;
       if (e != hipErrorNotReady) HIPCHECK(e);
+      // aborted from another thread (mx_comm_abort: a caller's wall-time
+      // budget ran out): the RCCL kernels have been told to stop
+      if (aborted) fail(MX_ERR_COMM, std::string(what) + ": RCCL communicator aborted");
       ncclResult_t ar = ncclSuccess;
-      if (nc && ncclCommGetAsyncError(nc, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress) {
+      if (ncclCommGetAsyncError(nc, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress) {
         abort_comm();
         fail(MX_ERR_COMM, std::string(what) + ": RCCL asynchronous error: " + ncclGetErrorString(ar));
       }
@@ -191,12 +197,13 @@ struct RcclComm : Comm {
       if (spins > 200) usleep(50); else sched_yield();
     }
   }
+  // Callable from any thread (mx_comm_abort), once: ncclCommAbort stops the
+  // communicator's in-flight kernels and frees it; every later call on this
+  // rank fails with MX_ERR_COMM (nc is kept, and never used again)
   void abort_comm() {
-    if (nc) (void)ncclCommAbort(nc);
-    nc = nullptr;
-    aborted = true;
+    if (!aborted.exchange(true) && nc) (void)ncclCommAbort(nc);
   }
-  bool aborted = false;
+  std::atomic<bool> aborted{false};
   void wait_stream(hipStream_t s) override {
     if (aborted) fail(MX_ERR_COMM, "RCCL communicator was aborted");
     hipStream_t q = s ? s : stream;
@@ -520,8 +527,9 @@ struct ShmComm : Comm {
 Comm *make_shm_comm(int rank, int size, int device, const char *name, int64_t slot_kib) {
   return new ShmComm(rank, size, device, name, slot_kib);
 }
-void abort_shm_comm(Comm *c) {
+void abort_comm_async(Comm *c) {
   if (auto *s = dynamic_cast<ShmComm *>(c)) s->abort_world();
+  else if (auto *r = dynamic_cast<RcclComm *>(c)) r->abort_comm();
 }
 
 void *make_local_world(int size) {

@@ -26,12 +26,11 @@ void hip_check(hipError_t e, const char *what, const char *file, int line);
 #define HIPCHECK(x) ::mx::hip_check((x), #x, __FILE__, __LINE__)
 
 // ---------------------------------------------------------------- device buffers
-// hipMalloc, or (knob 18) a physically contiguous allocation for large
-// buffers when the driver can provide one (falls back to hipMalloc)
+// hipMalloc (library-owned arrays)
 hipError_t dev_malloc(void **p, size_t bytes);
-// Transient (scratch) buffers of one call.  Big buffers of either kind come
-// from / go back to a small per-device cache instead of hipMalloc / hipFree
-// (dev_free; scratch_trim empties the cache; mx_vec.hip).
+// Transient (scratch) buffers of one call.  Buffers of 1 MiB or more of either
+// kind come from / go back to a small per-device cache instead of hipMalloc /
+// hipFree (dev_free; scratch_trim empties the cache; mx_vec.hip).
 hipError_t scratch_malloc(void **p, size_t bytes);
 void dev_free(void *p);
 void scratch_trim();
@@ -113,7 +112,7 @@ struct Comm {
 Comm *make_self_comm(int device);
 Comm *make_rccl_comm(int rank, int size, int device, const void *uid, size_t len);
 Comm *make_shm_comm(int rank, int size, int device, const char *name, int64_t slot_kib);
-void abort_shm_comm(Comm *c);
+void abort_comm_async(Comm *c);   // mx_comm_abort: shared-memory world or RCCL communicator
 void *make_local_world(int size);
 Comm *make_local_comm(void *world, int rank, int device);
 void destroy_local_world(void *world);
@@ -277,7 +276,7 @@ struct VCodes { const uint8_t *code; const int64_t *cptr; const double *tab; int
 struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
                 int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
                 int bnd_grid = 0;
-                int contig = 1; int mask8 = 1; int cg_unroll = 2;
+                int mask8 = 1; int cg_unroll = 2;
                 int cg_upd_grid = 0; int vcodes = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
                 int cg_xbatch = 0; int pdict = 1; int cg_ntl = 3;
                 int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
@@ -515,6 +514,7 @@ void vec_scale(hipStream_t s, int64_t n, double a, double *x);
 void vec_set(hipStream_t s, int64_t n, double a, double *x);
 void vec_rhs_hash(hipStream_t s, int64_t i0, int64_t n, double *b);
 void debug_stall(hipStream_t s, int stall_us);
+void flush_read(hipStream_t s, const double *x, int64_t n, double *partials);   // RED_BLOCKS partials
 void debug_stream_read(hipStream_t s, const double *x, int64_t n, int width, double *out);
 void exclusive_scan_i64(const int64_t *in, int64_t *out, int64_t n, hipStream_t s,
                         int64_t *total_host);

@@ -20,28 +20,39 @@
 
 namespace mx {
 
-// Big device buffers (>= 64 MiB) go through a small per-device cache.
+// Device buffers of 1 MiB or more go through a small per-device cache.
 // Assembly allocates and frees its transients (the generated or copied input,
 // widened columns, canonical copies) once per call, and destroying an operator
 // frees its arrays: over 14 repeated 27-point share assemblies hipFree of a big
-// buffer took 7-97 ms in streaks (160 ms assemblies against a 17 ms median),
-// and contiguous allocations of a re-created operator 1.5-5.5 s now and then
-// (tools/asm_outliers.py, tools/asm_time.py, tools/slow_calls.py).  A freed big
+// buffer took 7-97 ms in streaks (160 ms assemblies against a 17 ms median;
+// tools/asm_outliers.py, tools/asm_time.py, tools/slow_calls.py).  A freed
 // buffer is therefore kept (after a device synchronisation, as hipFree would
 // do) in a cache of at most min(1/8 of HBM, 48 GiB), oldest evicted first, and
-// the next allocation of a similar size takes it back without a driver call.
-// Library buffers (dev_malloc) are physically contiguous when the driver can
-// provide it (knob 18) and only take cached blocks of the same kind;
-// transients (scratch_malloc) take any and are plain hipMalloc otherwise.
-// Knob 81 = 0: no caching; 2: every block handed out is first filled with
-// 0xA5 bytes (tests: a buffer read before it is written shows up).
+// the next allocation of a similar size takes it back without a driver call;
+// mx_finalize, mx_comm_destroy and knob 81 = 0 give it back to the driver.
+// Knob 81 = 2: every block handed out is first filled with 0xA5 bytes, so a
+// buffer read before it is written shows up (the GPU suite runs green that
+// way, profiles/r06a_gpu_suite_poisoned.log).
+//
+// Every buffer is plain hipMalloc memory.  Physically contiguous allocations
+// (hipExtMallocWithFlags(hipDeviceMallocContiguous), rounds 1-5) were retired
+// in round 6: once such a block had been freed and its address range taken by
+// another allocation, some kernels still reached the old pages through stale
+// translations (a whole workgroup's x writes lost, rows
+// of freshly generated columns read as zeros, an illegal address) -- with
+// them off, 0 failures where they failed every run.
 namespace {
-struct BigBlock { void *p; size_t bytes; int device; bool contig; };
+struct BigBlock { void *p; size_t bytes; int device; };
 std::mutex g_big_mu;
 std::vector<BigBlock> g_big_free;                  // cached, oldest first
-std::unordered_map<void *, BigBlock> g_big_live;   // big blocks handed out
+std::unordered_map<void *, BigBlock> g_big_live;   // cached-size blocks handed out
 size_t g_big_bytes = 0;
-constexpr size_t BIG_MIN = (size_t)64 << 20, BIG_ROUND = (size_t)2 << 20;
+constexpr size_t BIG_MIN = (size_t)1 << 20;
+// sizes are rounded so that near sizes share blocks: 64 KiB below 64 MiB, 2 MiB above
+size_t round_size(size_t b) {
+  const size_t r = b < ((size_t)64 << 20) ? ((size_t)64 << 10) : ((size_t)2 << 20);
+  return (b + r - 1) / r * r;
+}
 
 size_t cache_cap() {
   size_t fr = 0, tot = 0;
@@ -49,15 +60,14 @@ size_t cache_cap() {
   return std::min(tot / 8, (size_t)48 << 30);
 }
 
-// the smallest cached block of this device (and kind: need_contig 1 / 0, or
-// -1 for any) that fits within 25% slack
-bool cache_take(size_t want, int dev, int need_contig, void **p) {
+// the smallest cached block of this device that fits within 25% slack
+bool cache_take(size_t want, int dev, void **p) {
   std::lock_guard<std::mutex> g(g_big_mu);
   int best = -1;
   for (int i = 0; i < (int)g_big_free.size(); ++i) {
     const BigBlock &b = g_big_free[i];
     if (b.device == dev && b.bytes >= want && b.bytes <= want + want / 4 &&
-        (need_contig < 0 || (int)b.contig == need_contig) && (best < 0 || b.bytes < g_big_free[best].bytes))
+        (best < 0 || b.bytes < g_big_free[best].bytes))
       best = i;
   }
   if (best < 0) return false;
@@ -69,36 +79,28 @@ bool cache_take(size_t want, int dev, int need_contig, void **p) {
   return true;
 }
 
-hipError_t big_malloc(void **p, size_t bytes, bool library) {
+hipError_t big_malloc(void **p, size_t bytes) {
   const bool cache = bytes >= BIG_MIN && g_knobs.scratch_cache;
-  const bool want_contig = library && bytes >= BIG_MIN && g_knobs.contig;
-  const size_t want = cache ? (bytes + BIG_ROUND - 1) / BIG_ROUND * BIG_ROUND : bytes;
+  const size_t want = cache ? round_size(bytes) : bytes;
   auto poison = [&] {
     if (g_knobs.scratch_cache == 2) { HIPCHECK(hipMemset(*p, 0xA5, want)); HIPCHECK(hipDeviceSynchronize()); }
   };
   int dev = 0;
   if (cache) {
     HIPCHECK(hipGetDevice(&dev));
-    if (cache_take(want, dev, library ? (int)want_contig : -1, p)) { poison(); return hipSuccess; }
+    if (cache_take(want, dev, p)) { poison(); return hipSuccess; }
   }
-  bool contig = false;
-  if (want_contig) {
-    contig = hipExtMallocWithFlags(p, want, hipDeviceMallocContiguous) == hipSuccess;
-    if (!contig) (void)hipGetLastError();
+  hipError_t e = hipMalloc(p, want);
+  if (e != hipSuccess && cache) {   // out of memory: give the cache back, then retry once
+    (void)hipGetLastError();
+    scratch_trim();
+    e = hipMalloc(p, want);
   }
-  if (!contig) {
-    hipError_t e = hipMalloc(p, want);
-    if (e != hipSuccess && cache) {   // out of memory: give the cache back, then retry once
-      (void)hipGetLastError();
-      scratch_trim();
-      e = hipMalloc(p, want);
-    }
-    if (e != hipSuccess) return e;
-  }
+  if (e != hipSuccess) return e;
   if (cache) {
     {
       std::lock_guard<std::mutex> g(g_big_mu);
-      g_big_live[*p] = BigBlock{*p, want, dev, contig};
+      g_big_live[*p] = BigBlock{*p, want, dev};
     }
     poison();
   }
@@ -106,12 +108,12 @@ hipError_t big_malloc(void **p, size_t bytes, bool library) {
 }
 }  // namespace
 
-hipError_t dev_malloc(void **p, size_t bytes) { return big_malloc(p, bytes, true); }
-hipError_t scratch_malloc(void **p, size_t bytes) { return big_malloc(p, bytes, false); }
+hipError_t dev_malloc(void **p, size_t bytes) { return big_malloc(p, bytes); }
+hipError_t scratch_malloc(void **p, size_t bytes) { return big_malloc(p, bytes); }
 
 void dev_free(void *p) {
   if (!p) return;
-  BigBlock b{nullptr, 0, 0, false};
+  BigBlock b{nullptr, 0, 0};
   {
     std::lock_guard<std::mutex> g(g_big_mu);
     auto it = g_big_live.find(p);
@@ -119,9 +121,15 @@ void dev_free(void *p) {
   }
   if (!b.p || !g_knobs.scratch_cache) { (void)hipFree(p); return; }
   // hipFree's implicit device synchronisation, kept: whoever takes the block
-  // next must not overlap work still queued on it (any stream)
+  // next must not overlap work still queued on it (any stream) -- on the
+  // block's own device, whatever device the calling thread has current (a
+  // Python finaliser may run on any thread); the capacity is that device's too
+  int cur = b.device;
+  (void)hipGetDevice(&cur);
+  if (cur != b.device) (void)hipSetDevice(b.device);
   (void)hipDeviceSynchronize();
   const size_t cap = cache_cap();
+  if (cur != b.device) (void)hipSetDevice(cur);
   std::lock_guard<std::mutex> g(g_big_mu);
   if (b.bytes > cap) { (void)hipFree(p); return; }
   g_big_free.push_back(b);
@@ -177,6 +185,14 @@ double host_dot(Comm *c, int64_t n, const double *x, const double *y) {
   HIPCHECK(hipMemcpyAsync(&h, out, sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
   return h;
+}
+
+// cold-cache helper (mx_mat_bench_mult_cold): stream n doubles in with plain
+// loads (L2 and the memory-side cache then hold the flush buffer, clean, and
+// none of the operator's data); partials: RED_BLOCKS doubles
+void flush_read(hipStream_t s, const double *x, int64_t n, double *partials) {
+  dot_partials_kernel<<<RED_BLOCKS, 256, 0, s>>>(n, x, x, partials);
+  HIPCHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------------- VecMDot / VecMAXPY on arbitrary vectors

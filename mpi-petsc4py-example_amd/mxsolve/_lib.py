@@ -89,6 +89,7 @@ SIGNATURES = {
     "mx_mat_mult": (C.c_int, [P, P, P]),
     "mx_mat_get_diagonal": (C.c_int, [P, P]),
     "mx_mat_bench_mult": (C.c_int, [P, P, P, C.c_int, DP, DP]),
+    "mx_mat_bench_mult_cold": (C.c_int, [P, P, P, P, I64, C.c_int, DP, DP]),
     "mx_mat_destroy": (C.c_int, [P]),
     "mx_vec_dot": (C.c_int, [P, I64, P, P, DP]),
     "mx_vec_norm2": (C.c_int, [P, I64, P, DP]),

@@ -71,8 +71,8 @@ class _DeviceBuffer:
 
 
 def device_vector(n: int, device: int) -> torch.Tensor:
-    """A float64 vector in HBM: large ones in the library's (physically
-    contiguous when available) allocations, small ones from torch's cache."""
+    """A float64 vector in HBM: large ones from the library's allocator (its
+    device buffer cache, mx_dev_alloc), small ones from torch's cache."""
     if n * 8 < BIG_VECTOR_BYTES:
         return torch.empty(n, dtype=torch.float64, device=torch.device("cuda", device))
     buf = _DeviceBuffer(n, device)
@@ -313,6 +313,14 @@ class DMat:
     def bench_mult(self, x: torch.Tensor, y: torch.Tensor, iters: int):
         s, m = C.c_double(), C.c_double()
         call("mx_mat_bench_mult", self.h, _ptr(x), _ptr(y), iters, C.byref(s), C.byref(m))
+        return s.value, m.value
+
+    def bench_mult_cold(self, x: torch.Tensor, y: torch.Tensor, flush: torch.Tensor, iters: int = 5):
+        """Cold-cache MatMult (flush buffer filled before each): median device
+        ms of the SpMV kernel alone (one rank; else < 0) and of the MatMult."""
+        s, m = C.c_double(), C.c_double()
+        call("mx_mat_bench_mult_cold", self.h, _ptr(x), _ptr(y), _ptr(flush), flush.numel(), iters,
+             C.byref(s), C.byref(m))
         return s.value, m.value
 
     def solve(self, b: torch.Tensor, x: torch.Tensor, ksp: str = "cg", pc: str = "jacobi",

@@ -96,12 +96,16 @@ def _selfcomm_stream():
 
 
 def _knobs(L):
-    """Every mx_debug_set key's current value (set to 0 and back: a valid key
-    returns the 0 just set on the way back, an unknown one -1)."""
+    """Every mx_debug_set key's current value (set to a probe value and back:
+    a valid key returns the probe value on the way back, an unknown one -1).
+    Key 81 is probed with 1, not 0: setting it to 0 empties the device buffer
+    cache, and the cache's blocks must carry over from test to test (under
+    key 81 = 2 a block read before it is written shows up across tests too)."""
     vals = {}
     for k in range(1, 100):
-        old = L.mx_debug_set(k, 0)
-        if L.mx_debug_set(k, old) == 0:
+        probe = 1 if k == 81 else 0
+        old = L.mx_debug_set(k, probe)
+        if L.mx_debug_set(k, old) == probe:
             vals[k] = old
     return vals
 
