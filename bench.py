@@ -423,6 +423,103 @@ def spmv_general_leg(comm, n: int) -> dict:
     return out
 
 
+def random_csr(N: int, k: int = 6, seed: int = 11):
+    """test.py:14's matrix family at scale: each row holds its diagonal and k
+    off-diagonal columns drawn uniformly over all N (redrawn until no row
+    repeats a column, so the CSR is already canonical), columns ascending,
+    values -U[0, 1) off the diagonal and 1 + sum |a_ij| on it; host int64 row
+    pointer, int32 columns, fp64 values (createAIJ(csr=...), test.py:24)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    rows = np.arange(N, dtype=np.int64)
+    c = rng.integers(0, N, size=(N, k), dtype=np.int64)
+    while True:
+        cols = np.concatenate([rows[:, None], c], axis=1)
+        cols.sort(axis=1)
+        dup = np.nonzero(np.any(cols[:, 1:] == cols[:, :-1], axis=1))[0]
+        if dup.size == 0:
+            break
+        c[dup] = rng.integers(0, N, size=(dup.size, k), dtype=np.int64)
+    del cols
+    v = -rng.random((N, k))
+    allc = np.concatenate([rows[:, None], c], axis=1)
+    allv = np.concatenate([(1.0 + np.abs(v).sum(axis=1))[:, None], v], axis=1)
+    del c, v
+    order = np.argsort(allc, axis=1, kind="stable")
+    cols = np.take_along_axis(allc, order, axis=1).astype(np.int32).reshape(-1)
+    vals = np.take_along_axis(allv, order, axis=1).reshape(-1)
+    indptr = np.arange(0, N * (k + 1) + 1, k + 1, dtype=np.int64)
+    return indptr, cols, vals
+
+
+def spmv_random_leg(comm, lg: int = 24) -> dict:
+    """The unstructured AIJ MatMult: test.py:14's
+    random-pattern family at 2^lg rows x 7 through createAIJ(csr=...) from host
+    arrays.  MatMult checked bit for bit against the row-ordered product of the
+    same CSR (PETSc's MatMult_SeqAIJ order), then timed standalone (warm) and
+    cold (behind a 1 GB streamed flush), each against two byte models: the
+    streamed bytes (the layout's slots + x once + y once) and the sector model
+    (+ one 64-B sector per off-diagonal gather: x's uniformly random reads
+    share no line)."""
+    import numpy as np
+    import torch
+    from mxsolve.core import DMat, dispatch_counts
+    N = 1 << lg
+    t0 = time.perf_counter()
+    ip, cj, vv = random_csr(N)
+    t_gen = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    A = DMat.from_csr(comm, N, N, ip, cj, vv)
+    torch.cuda.synchronize()
+    t_asm = time.perf_counter() - t0
+    info = A.info()
+    m, nnz = info["m"], info["nnz_d"] + info["nnz_o"]
+    xh = np.random.default_rng(5).standard_normal(N)
+    xt = torch.from_numpy(xh).to(f"cuda:{torch.cuda.current_device()}")
+    y = comm.empty(m)
+    dispatch_counts(reset=True)
+    A.mult(xt, y)
+    kinds = [k for k, v in dispatch_counts().items() if v]
+    yref = csr_rowsum_reference(ip, cj, vv, xh)
+    bitexact = bool(np.array_equal(y.cpu().numpy().view(np.uint64), yref.view(np.uint64)))
+    del ip, cj, vv, yref, xh
+    warm_ms, _ = A.bench_mult(xt, y, 50)
+    flush = torch.empty(1 << 27, dtype=torch.float64, device=y.device)
+    cold_kernel_ms, cold_ms = A.bench_mult_cold(xt, y, flush, 5)
+    del flush
+    slots = info["sell_slots_d"]
+    streamed = 12 * slots + 16 * m + 16 * ((m + 63) // 64)
+    gathers = nnz - m                                  # the off-diagonal entries
+    sector = streamed - 8 * m + 64 * gathers           # x read by sectors instead of once
+    f = lambda b, ms: round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    g = lambda b, ms: round(b / (ms * 1e-3) / 1e9, 1)
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "spmv_traffic.json")) as fh:
+            traffic = json.load(fh).get(f"random2^{lg}/N1")
+    except (OSError, ValueError):
+        pass
+    out = {"workload": f"uniform random pattern, 2^{lg} rows x 7 (diagonal + 6 random columns), createAIJ(csr=...) "
+                       "from host int64/int32/fp64 arrays",
+           "rows": m, "nnz": nnz, "sell_slots": slots, "kernels": kinds,
+           "csr_gen_s": round(t_gen, 2), "assembly_s": round(t_asm, 4),
+           "matmult_bitexact_vs_rowsum": bitexact,
+           "streamed_bytes": streamed, "sector_bytes": sector, "peak": HBM_PEAK_GBS,
+           "warm_ms": round(warm_ms, 5), "warm_GBps_streamed": g(streamed, warm_ms),
+           "warm_frac_streamed": f(streamed, warm_ms), "warm_GBps_sector": g(sector, warm_ms),
+           "warm_frac_sector": f(sector, warm_ms),
+           "cold_ms": round(cold_ms, 5), "cold_kernel_ms": round(cold_kernel_ms, 5) if cold_kernel_ms > 0 else None,
+           "cold_frac_sector": f(sector, cold_ms),
+           "traffic": traffic.get("bytes_per_launch") if traffic else None,
+           "traffic_ratio_vs_sector": round(traffic["bytes_per_launch"] / sector, 3) if traffic else None,
+           "traffic_source": traffic.get("source") if traffic else None}
+    A.destroy()
+    del xt, y
+    torch.cuda.empty_cache()
+    return out
+
+
 # The other BASELINE.json configurations on one GPU (C2, C4, C5's per-GPU
 # share), reported beside the headline outside its timed region.  The
 # expected iteration counts and reasons are the ones the full-size oracle
@@ -668,6 +765,7 @@ def main():
     ap.add_argument("--no-asm", action="store_true", help="skip the createAIJ-from-host-arrays leg")
     ap.add_argument("--no-general", action="store_true", help="skip the streamed-values SpMV leg (spmv_general)")
     ap.add_argument("--no-configs", action="store_true", help="skip the C2 / C4 / C5-share configuration legs")
+    ap.add_argument("--no-random", action="store_true", help="skip the random-pattern (unstructured AIJ) SpMV leg")
     ap.add_argument("--cpu-config", choices=sorted(CPU_CONFIGS),
                     help="only the host (oracle) baseline of another BASELINE configuration: one JSON line")
     args = ap.parse_args()
@@ -965,6 +1063,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_general:
         general = spmv_general_leg(comm, n)
 
+    random_leg = None
+    if rank == 0 and world == 1 and not args.no_random:
+        random_leg = spmv_random_leg(comm)
+
     configs = None
     if rank == 0 and world == 1 and not args.no_configs:
         configs = [config_leg(comm, *c) for c in BENCH_CONFIGS]
@@ -1031,9 +1133,14 @@ def main():
                                 "cold_matmult_ms": round(cold_ms, 5),
                                 "cold_kernel_ms": round(cold_kernel_ms, 5) if cold_kernel_ms > 0 else None,
                                 "cold_GBps": round(bytes_spmv / (cold_ms * 1e-3) / 1e9, 1),
-                                "cold_frac": round(bytes_spmv / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                                "cold_frac": round(bytes_spmv / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                # the kernel alone (dispatch-attached events): the span above also
+                                # holds the queue gap between the flush kernel's end and its start
+                                "cold_kernel_frac": round(bytes_spmv / (cold_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                if cold_kernel_ms and cold_kernel_ms > 0 else None}
             if spmv_alone_ms else None,
             "spmv_general": general,
+            "spmv_random": random_leg,
             "cg_iter_bytes_survey": cg_iter_bytes(m, nnz_loc, ng),
             "cg_fusion_mode": mode,
             "cg_xbatch": xb,
