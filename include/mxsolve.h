@@ -29,7 +29,7 @@ extern "C" {
 #endif
 
 /* 2: mx_ksp_result grew the pbw / mdot / maxpy timing fields (its size changed) */
-#define MX_ABI_VERSION 2
+#define MX_ABI_VERSION 3
 
 enum {
   MX_OK = 0,
@@ -133,6 +133,9 @@ typedef struct {
   int64_t pair_code;                  /* 1: the coded z-march MatMult runs -- 5/7-point code
                                          dictionary not uniform per slot, every block
                                          select-free (values from the LDS table; key 52) */
+  int64_t cb_blocks;                  /* > 0: the column-block two-pass MatMult runs, with
+                                         this many blocks of x (unstructured blocks whose
+                                         entries mostly lie far from the diagonal; key 84) */
 } mx_mat_info;
 
 /* ---- library ---------------------------------------------------------------- */
@@ -451,6 +454,11 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         cache emptied; emptied too by mx_comm_destroy and mx_finalize; 2: as
  *         1, and every block handed out is filled with 0xA5 bytes first --
  *         tests: a buffer read before it is written shows up)
+ * key 84: the column-block two-pass MatMult for unstructured blocks (read at
+ *         assembly; mx_spmv_cb.hip): 1 (default) on one rank when A_d is a
+ *         general SELL block of >= 2^20 rows with half its entries or more
+ *         2^17 columns or further from the diagonal, 2 for every general
+ *         block (tests), 0 never; the same bits as the one-pass kernel
  * (key 18, physically contiguous allocations, was retired in round 6: freed
  *  contiguous blocks whose address range was reused were still reached through
  *  stale translations -- DESIGN.md section 11)
@@ -464,7 +472,8 @@ int mx_debug_set(int key, int value);
  * CG mode 5's p.Ap and residual-update z-march passes, 13 / 14 coded z-march
  * (split: ghost units), 15 CG mode 5's direction update fused into the p.Ap
  * pass (key 69), 16 the same fused into the split p.Ap pass on P > 1 ranks
- * (key 80).  Writes min(n, 17) counts; reset != 0
+ * (key 80), 17 the column-block two-pass MatMult (key 84).  Writes min(n, 18)
+ * counts; reset != 0
  * zeroes them.  Not a PETSc call: it lets the parity tests show which
  * kernel ran (replayed graph launches are not counted).                     */
 int mx_debug_dispatch_counts(int64_t *out, int n, int reset);

@@ -558,6 +558,7 @@ void load_code_objects() {
   load_code_assembly();
   load_code_spmv();
   load_code_spmv_pair();
+  load_code_spmv_cb();
   load_code_ksp();
   load_code_direct();
 }

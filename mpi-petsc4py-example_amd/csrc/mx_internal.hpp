@@ -252,6 +252,15 @@ struct Sell {
   // a non-uniform code dictionary (pair_blocks > 0, no puni) whose every block
   // is select-free: the flags are in pblk, and the coded z-march runs on it
   bool pair_code_clean = false;
+  // column-block two-pass MatMult (mx_spmv_cb.hip) for unstructured blocks:
+  // the entries in (column block of 2^cb_bs columns, row, column) order --
+  // cb_col / cb_val, block b at [cb_bstart[b], cb_bstart[b+1]) -- the
+  // products' buffer cb_prod in that order, and cb_perm: each SELL slot's
+  // position in it (-1 padding); cb_nblk = 0: not built
+  int cb_bs = 0, cb_nblk = 0;
+  DBuf<int64_t> cb_bstart;
+  DBuf<int32_t> cb_col, cb_perm;
+  DBuf<double> cb_val, cb_prod;
 };
 constexpr uint32_t PBLK_GHOST_LO = 1u << 30;
 constexpr uint32_t PBLK_GHOST_HI = 1u << 31;
@@ -283,7 +292,7 @@ struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 
                 int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
                 int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
                 int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; int cg_pbws = 1; int scratch_cache = 1; };
+                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; int cg_pbws = 1; int scratch_cache = 1; int cb = 1; };
 extern Knobs g_knobs;
 
 struct Halo {
@@ -455,7 +464,8 @@ enum Dispatch {
   DSP_PAIR_ZMC_SPLIT = 14,
   DSP_ZM_PBW = 15,       // CG mode 5: the direction update fused into the p.Ap pass (knob 69)
   DSP_ZM_PBWS = 16,      // CG mode 5 on P > 1 ranks: the same fused into the split p.Ap pass (knob 80)
-  DSP_COUNT = 17
+  DSP_CB = 17,           // the column-block two-pass MatMult (mx_spmv_cb.hip, knob 84)
+  DSP_COUNT = 18
 };
 void note_dispatch(int kind);
 extern std::atomic<long long> g_dispatch[DSP_COUNT];
@@ -497,6 +507,12 @@ int cg5_pbws_matmult(Mat *A, KspState *s, const double *r, double *const pb[8], 
 // a boundary launch (P > 1 with ghost entries and overlap on)
 bool matmult_splits(const Mat *A);
 void mat_mult(Mat *A, const double *x, double *y);
+// column-block two-pass MatMult (mx_spmv_cb.hip): built at assembly for
+// unstructured one-rank blocks; cb_launch returns the pass-2 grid (partials)
+void build_cb(Mat *A, hipStream_t st);
+bool cb_applies(const Mat *A, int mode, bool split);
+int cb_launch(Mat *A, int mode, const double *x, double *y, const Jac &jac, double *partials, const int *done,
+              const Fold &fold, const double *xscale, hipStream_t st);
 
 // vector kernels (mx_vec.hip)
 constexpr int RED_BLOCKS = 1024;   // fixed grid of the reduction kernels
@@ -546,6 +562,7 @@ void load_code_vec();
 void load_code_assembly();
 void load_code_spmv();
 void load_code_spmv_pair();
+void load_code_spmv_cb();
 void load_code_ksp();
 void load_code_direct();
 void load_code_objects();

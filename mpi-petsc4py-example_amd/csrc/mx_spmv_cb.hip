@@ -1,0 +1,294 @@
+// mx_spmv_cb.hip -- the column-block two-pass MatMult for unstructured AIJ
+// blocks (test.py:14's scipy.sparse.random family; MatMult_SeqAIJ order).
+//
+// The one-pass SELL kernel gathers x[c] once per entry.  On a matrix whose
+// columns are spread over the whole vector (uniformly random patterns) every
+// gather is an L2 miss that fetches a 64-B sector from the memory side, and
+// the kernel runs at the rate of those misses: 2^24 rows x 7 take 1.99 ms,
+// the gathers alone 1.87 ms (tools/gather_probe.hip).  Gathers that hit L2 run
+// about 2.8x faster (x of 2 MB: 150 G gathers/s against 54 G).  So:
+//
+//   pass 1 (cb_prod_kernel): the entries in (column block, row, column)
+//     order -- column blocks of 2^bs doubles of x (2 MB at 2^24 rows) --
+//     each XCD walking every 8th block with all its workgroups, so the
+//     block's piece of x is in that XCD's L2 while the values and column ids
+//     stream in and the products p_k = a_k * x[c_k] stream out in that order;
+//   pass 2 (cb_sum_kernel): the SELL-64 walk of the rows, summing each row's
+//     products in ascending column order through perm (the slot's pass-1
+//     position); a slice's products of one column block are contiguous in
+//     pass-1 order, so a wave's reads touch a line or two per block instead
+//     of one random sector per entry.
+//
+// Every product is rounded once and every row is summed from 0.0 in
+// ascending column order, one rounding per add: the bits of MatMult_SeqAIJ
+// and of the one-pass kernel (tests/test_gpu_cb.py).  Built at assembly for
+// one-rank general SELL blocks whose entries mostly lie far from the
+// diagonal (mx_assembly.hip build_cb); key 84 selects it.
+#include <hipcub/hipcub.hpp>
+
+#include "mx_device.hpp"
+#include "mx_internal.hpp"
+
+namespace mx {
+
+namespace {
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+constexpr int CB_E = 4;   // pass 1: entries per thread per step (two 16-B value loads in flight)
+
+template <class T> __device__ __forceinline__ T ldnt(const T *p) { return __builtin_nontemporal_load(p); }
+
+// -------------------------------------------------------------- build kernels
+// far-entry count: |col - row| >= 2^17 (outside what one slice's L2 reuse
+// can serve), summed per block
+__global__ void __launch_bounds__(256) cb_far_kernel(int64_t m, const int64_t *__restrict__ ptr,
+                                                     const int32_t *__restrict__ col, unsigned long long *far) {
+  unsigned long long c = 0;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < m; r += (int64_t)gridDim.x * 256)
+    for (int64_t e = ptr[r]; e < ptr[r + 1]; ++e) {
+      const int64_t d = (int64_t)col[e] - r;
+      c += (d >= (1 << 17) || d <= -(1 << 17)) ? 1 : 0;
+    }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(far, c);
+}
+
+__global__ void cb_keys_kernel(int64_t nnz, const int32_t *__restrict__ col, int bs, uint32_t *__restrict__ key,
+                               int32_t *__restrict__ idx) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x) {
+    key[e] = (uint32_t)col[e] >> bs;
+    idx[e] = (int32_t)e;
+  }
+}
+
+// pass-1 arrays in sorted order, the inverse permutation, and the block starts
+__global__ void cb_scatter_kernel(int64_t nnz, const uint32_t *__restrict__ skey, const int32_t *__restrict__ src,
+                                  const int32_t *__restrict__ col, const double *__restrict__ val,
+                                  int32_t *__restrict__ c1, double *__restrict__ v1, int32_t *__restrict__ pinv,
+                                  int64_t *__restrict__ bstart, int nblk) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t e = src[k];
+    c1[k] = col[e];
+    v1[k] = val[e];
+    pinv[e] = (int32_t)k;
+    const uint32_t kk = skey[k], kp = k ? skey[k - 1] : 0u;
+    if (k == 0) for (uint32_t b = 0; b <= kk; ++b) bstart[b] = 0;
+    else for (uint32_t b = kp + 1; b <= kk; ++b) bstart[b] = k;
+    if (k == nnz - 1) for (int b = (int)kk + 1; b <= nblk; ++b) bstart[b] = nnz;
+  }
+}
+
+// perm in the SELL-64 slot layout of A_d (Sell: pair p of lane l at sptr +
+// 128 p + 2 l (+0/+1), the odd tail at sptr + 128 (w/2) + l); padding -1
+__global__ void cb_perm_kernel(int64_t m, const int64_t *__restrict__ ptr, const int64_t *__restrict__ sptr,
+                               const int32_t *__restrict__ wid, const int32_t *__restrict__ pinv,
+                               int32_t *__restrict__ perm) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < m; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = r / SLICE;
+    const int lane = (int)(r % SLICE);
+    const int w = wid[s], np = w >> 1;
+    const int64_t base = sptr[s];
+    const int64_t e0 = ptr[r], len = ptr[r + 1] - e0;
+    for (int j = 0; j < w; ++j) {
+      const int64_t pos = j < 2 * np ? base + 128 * (j >> 1) + 2 * lane + (j & 1) : base + 128 * np + lane;
+      perm[pos] = j < len ? pinv[e0 + j] : -1;
+    }
+  }
+}
+
+// -------------------------------------------------------------- pass 1
+// block b of the grid runs on XCD b % 8 (round-robin dispatch: blocks b and
+// b + 8 share an XCD; speed only, never results); that XCD's workgroups
+// split each of its column blocks' entry ranges between them
+template <bool SC>
+__global__ void __launch_bounds__(256) cb_prod_kernel(int nblk, const int64_t *__restrict__ bstart,
+                                                      const int32_t *__restrict__ c1, const double *__restrict__ v1,
+                                                      const double *__restrict__ x, const double *__restrict__ xscale,
+                                                      double *__restrict__ prod, const int *__restrict__ done) {
+  if (done && *done) return;
+  const double s = SC ? *xscale : 1.0;
+  // the operand as the one-pass kernel forms it: x, or fl(s * x) (GMRES's
+  // unnormalised basis vector), then one rounding for the product
+  auto opnd = [&](int32_t c) { const double v = x[c]; return SC ? s * v : v; };
+  const int xg = blockIdx.x & 7, wi = blockIdx.x >> 3, nper = gridDim.x >> 3;
+  for (int C = xg; C < nblk; C += 8) {
+    const int64_t b0 = bstart[C], b1 = bstart[C + 1], len = b1 - b0;
+    const int64_t chunk = ((len + nper - 1) / nper + 1) & ~(int64_t)1;
+    const int64_t lo = b0 + chunk * wi, hi = min(b1, lo + chunk);
+    int64_t k = lo + 2 * threadIdx.x;
+    for (; k + 512 * (CB_E / 2 - 1) + 1 < hi; k += 512 * (CB_E / 2)) {
+      d2v v[CB_E / 2];
+      i2v c[CB_E / 2];
+#pragma unroll
+      for (int e = 0; e < CB_E / 2; ++e) {
+        v[e] = ldnt(reinterpret_cast<const d2v *>(v1 + k + 512 * e));
+        c[e] = ldnt(reinterpret_cast<const i2v *>(c1 + k + 512 * e));
+      }
+      double xa[CB_E / 2], xb[CB_E / 2];
+#pragma unroll
+      for (int e = 0; e < CB_E / 2; ++e) { xa[e] = opnd(c[e].x); xb[e] = opnd(c[e].y); }
+#pragma unroll
+      for (int e = 0; e < CB_E / 2; ++e) {
+        d2v p;
+        p.x = v[e].x * xa[e];
+        p.y = v[e].y * xb[e];
+        __builtin_nontemporal_store(p, reinterpret_cast<d2v *>(prod + k + 512 * e));
+      }
+    }
+    for (; k < hi; k += 512) {
+      prod[k] = ldnt(v1 + k) * opnd(ldnt(c1 + k));
+      if (k + 1 < hi) prod[k + 1] = ldnt(v1 + k + 1) * opnd(ldnt(c1 + k + 1));
+    }
+  }
+}
+
+// -------------------------------------------------------------- pass 2
+// one wave per slice; the row's products in ascending column order (batches
+// of 8 entries: every perm and product load of a batch in flight together),
+// then the mode's epilogue as the one-pass kernel has it (mx_spmv.hip finish)
+template <int MODE>
+__global__ void __launch_bounds__(256) cb_sum_kernel(int64_t m, int64_t nslices, const int64_t *__restrict__ sptr,
+                                                     const int32_t *__restrict__ wid, const int32_t *__restrict__ perm,
+                                                     const double *__restrict__ prod, const double *__restrict__ x,
+                                                     double *__restrict__ y, const Jac jac, double *__restrict__ partials,
+                                                     const int *__restrict__ done, const Fold fold) {
+  if (done && *done) return;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  double dot = 0.0;
+  for (int64_t s = (int64_t)blockIdx.x * 4 + wv; s < nslices; s += (int64_t)gridDim.x * 4) {
+    const int w = wid[s];
+    const int np = w >> 1;
+    const bool odd = (w & 1) != 0;
+    const int nb = np + (odd ? 1 : 0);
+    const int32_t *__restrict__ pb = perm + sptr[s];
+    const i2v *__restrict__ pp = reinterpret_cast<const i2v *>(pb) + lane;
+    double sum = 0.0;
+    for (int p0 = 0; p0 < nb; p0 += 4) {
+      int c[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int p = p0 + q;
+        i2v cc = i2v{-1, -1};
+        if (p < np) cc = ldnt(pp + (int64_t)p * SLICE);
+        else if (odd && p == np) cc.x = ldnt(pb + (int64_t)np * 2 * SLICE + lane);
+        c[2 * q] = cc.x;
+        c[2 * q + 1] = cc.y;
+      }
+      double t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[q] = prod[c[q] >= 0 ? c[q] : 0];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const double u = sum + t[q];
+        sum = c[q] >= 0 ? u : sum;
+      }
+    }
+    const int64_t row = s * SLICE + lane;
+    if (row < m) {
+      const double out = spmv_jac(MODE) ? papply(jac, sum, row) : sum;   // PCApply_Jacobi fused: w_i * d_i
+      y[row] = out;
+      if (MODE == SPMV_DOT) dot += x[row] * sum;                          // VecDot(p, w) partial, p = x
+    }
+  }
+  if constexpr (MODE == SPMV_DOT) {
+    double v[1] = {dot};
+    block_partials<1>(v, partials, gridDim.x, fold);
+  }
+}
+}  // namespace
+
+bool cb_applies(const Mat *A, int mode, bool split) {
+  return A->sd.cb_nblk > 0 && g_knobs.cb != 0 && !split && A->nghost == 0 &&
+         (mode == SPMV_PLAIN || mode == SPMV_PLAIN_S || mode == SPMV_JACOBI || mode == SPMV_JACOBI_S ||
+          mode == SPMV_DOT);
+}
+
+int cb_launch(Mat *A, int mode, const double *x, double *y, const Jac &jac, double *partials, const int *done,
+              const Fold &fold_in, const double *xscale, hipStream_t st) {
+  Sell &S = A->sd;
+  const unsigned g1 = (unsigned)(2 * device_cu_count()) & ~7u;   // two workgroups per CU, a multiple of 8
+  const bool sc = spmv_scaled(mode);
+  // (plain launches: a dispatch-attached timer, g_ext_timing, would time one
+  // of the two passes; callers' events around the MatMult time both)
+  if (sc) cb_prod_kernel<true><<<g1, 256, 0, st>>>(S.cb_nblk, S.cb_bstart.p, S.cb_col.p, S.cb_val.p, x, xscale,
+                                                   S.cb_prod.p, done);
+  else cb_prod_kernel<false><<<g1, 256, 0, st>>>(S.cb_nblk, S.cb_bstart.p, S.cb_col.p, S.cb_val.p, x, xscale,
+                                                   S.cb_prod.p, done);
+  HIPCHECK(hipGetLastError());
+  const int g2 = (int)std::min<int64_t>(8192, std::max<int64_t>(1, cdiv(S.nslices, 4)));
+  Fold fold = fold_in;
+  if (fold.cnt) { fold.ntotal = fold.ncount = g2; fold.base = 0; }
+  note_dispatch(DSP_CB);
+#define CBS(MD) cb_sum_kernel<MD><<<g2, 256, 0, st>>>(A->m, S.nslices, S.sptr.p, S.width.p, S.cb_perm.p, S.cb_prod.p, \
+                                                     x, y, jac, partials, done, fold)
+  switch (mode) {
+    case SPMV_PLAIN: case SPMV_PLAIN_S: CBS(SPMV_PLAIN); break;
+    case SPMV_JACOBI: case SPMV_JACOBI_S: CBS(SPMV_JACOBI); break;
+    case SPMV_DOT: CBS(SPMV_DOT); break;
+    default: fail(MX_ERR_INTERNAL, "column-block MatMult: unsupported mode");
+  }
+#undef CBS
+  HIPCHECK(hipGetLastError());
+  return g2;
+}
+
+// Build the pass-1 arrays and perm for A_d when it is a general SELL block
+// whose entries mostly lie far from the diagonal (key 84: 1 = that test and
+// at least 2^20 rows, 2 = any general block -- tests; 0 = never).
+void build_cb(Mat *A, hipStream_t st) {
+  Sell &S = A->sd;
+  S.cb_nblk = 0;
+  const int64_t m = A->m, nnz = A->nnz_d;
+  if (!g_knobs.cb || m < 64 || nnz < 1 || A->nghost != 0 || S.dia_slices != 0 || S.ntab != 0 || S.pair_shape != 0 ||
+      nnz >= ((int64_t)1 << 31))
+    return;
+  if (g_knobs.cb == 1) {
+    if (m < ((int64_t)1 << 20)) return;
+    DBuf<unsigned long long> far(1);
+    HIPCHECK(hipMemsetAsync(far.p, 0, sizeof(unsigned long long), st));
+    cb_far_kernel<<<grid_for(m, 256, 4096), 256, 0, st>>>(m, A->dptr.p, A->dcol.p, far.p);
+    HIPCHECK(hipGetLastError());
+    unsigned long long h = 0;
+    HIPCHECK(hipMemcpyAsync(&h, far.p, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    if (h * 2 < (unsigned long long)nnz) return;   // half the entries or more far from the diagonal
+  }
+  // column blocks: 2 MB of x (2^18 doubles) from 2^22 columns, fewer columns
+  // per block below so that every XCD gets at least two
+  int bs = 18;
+  while (bs > 6 && (A->n >> bs) < 16) --bs;
+  const int nblk = (int)((A->n + ((int64_t)1 << bs) - 1) >> bs);
+  int kbits = 1;
+  while ((1 << kbits) < nblk) ++kbits;
+  DBuf<uint32_t> key((size_t)nnz, kScratch), skey((size_t)nnz, kScratch);
+  DBuf<int32_t> idx((size_t)nnz, kScratch), src((size_t)nnz, kScratch), pinv((size_t)nnz, kScratch);
+  cb_keys_kernel<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(nnz, A->dcol.p, bs, key.p, idx.p);
+  HIPCHECK(hipGetLastError());
+  size_t tb = 0;
+  HIPCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, skey.p, idx.p, src.p, (int)nnz, 0, kbits, st));
+  DBuf<char> tmp(std::max<size_t>(tb, 1), kScratch);
+  HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key.p, skey.p, idx.p, src.p, (int)nnz, 0, kbits, st));
+  S.cb_col.alloc((size_t)nnz);
+  S.cb_val.alloc((size_t)nnz);
+  S.cb_prod.alloc((size_t)nnz);
+  S.cb_bstart.alloc((size_t)nblk + 1);
+  S.cb_perm.alloc((size_t)std::max<int64_t>(S.slots, 1));
+  cb_scatter_kernel<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(nnz, skey.p, src.p, A->dcol.p, A->dval.p, S.cb_col.p,
+                                                              S.cb_val.p, pinv.p, S.cb_bstart.p, nblk);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemsetAsync(S.cb_perm.p, 0xFF, sizeof(int32_t) * (size_t)std::max<int64_t>(S.slots, 1), st));
+  cb_perm_kernel<<<grid_for(m, 256, 8192), 256, 0, st>>>(m, A->dptr.p, S.sptr.p, S.width.p, pinv.p, S.cb_perm.p);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipStreamSynchronize(st));   // the scratch arrays are freed on return
+  S.cb_bs = bs;
+  S.cb_nblk = nblk;
+}
+
+void load_code_spmv_cb() {
+  hipFuncAttributes a;
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&cb_sum_kernel<SPMV_PLAIN>));
+  (void)hipGetLastError();
+}
+
+}  // namespace mx

@@ -54,7 +54,7 @@ class MatInfo(C.Structure):
                 ("pair_units", C.c_int64), ("pair_blocks", C.c_int64), ("pair_block_bytes", C.c_int64),
                 ("pair_uniform", C.c_int64), ("pair_lean", C.c_int64),
                 ("pair_zmarch", C.c_int64), ("pair_f64", C.c_int64), ("pair_form27", C.c_int64),
-                ("pair_code", C.c_int64)]
+                ("pair_code", C.c_int64), ("cb_blocks", C.c_int64)]
 
 
 P = C.c_void_p
@@ -132,7 +132,7 @@ def load():
         fn = getattr(lib, name)   # AttributeError if the ABI lost a symbol
         fn.restype = res
         fn.argtypes = args
-    if lib.mx_version() != 2:
+    if lib.mx_version() != 3:
         raise ImportError("libmxsolve ABI version mismatch")
     # diagnostics / A/B runs: MXSOLVE_KNOBS="27=0+3=8192" (mx_debug_set keys, include/mxsolve.h)
     for kv in filter(None, os.environ.get("MXSOLVE_KNOBS", "").split("+")):

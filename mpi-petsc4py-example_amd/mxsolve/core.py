@@ -412,7 +412,7 @@ def vmaxpy(comm: DeviceComm, y, alphas, xs):
 
 DISPATCH_KINDS = ("sell", "sell_cg", "pair_lean", "pair_zm", "pair_zm_split", "pair_zm27", "pair_zm27_split",
                   "pair_zmf64", "pair_zmf64_split", "pair_zmcg", "boundary", "zm_pw", "zm_rupd", "pair_zmc",
-                  "pair_zmc_split", "zm_pbw", "zm_pbws")
+                  "pair_zmc_split", "zm_pbw", "zm_pbws", "cb")
 
 
 def dispatch_counts(reset: bool = False) -> dict:

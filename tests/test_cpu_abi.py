@@ -31,7 +31,7 @@ def test_cpu_only_calls():
     import ctypes as C
     from mxsolve import _lib
     L = _lib.load()
-    assert L.mx_version() == 2
+    assert L.mx_version() == 3
     r = (C.c_int64 * 5)()
     assert L.mx_layout_split(10, 4, r) == 0 and list(r) == [0, 3, 6, 8, 10]
     p = _lib.KSPParams()

@@ -17,7 +17,7 @@
 //     column block instead of 384 random sectors.
 // Every product is rounded once and the sum runs in PETSc's order, so y is
 // bitwise the one-pass kernel's (checked here).
-//   hipcc --offload-arch=gfx950 -O3 tools/colblock_probe.hip -o tools/colblock_probe
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/colblock_probe.hip -o tools/colblock_probe
 //   tools/colblock_probe [lg] [BS] [reps]
 #include <hip/hip_runtime.h>
 
@@ -56,26 +56,41 @@ __global__ void __launch_bounds__(256) spmv_onepass(int64_t nslices, const int *
 }
 
 // pass 1: block b of the grid runs on XCD b % 8 (round-robin dispatch);
-// the XCD's nper workgroups split each of its column blocks' entry ranges
+// the XCD's nper workgroups split each of its column blocks' entry ranges.
+// E entries per thread per step (E / 2 16-B value loads in flight)
+template <int E>
 __global__ void __launch_bounds__(256) pass1(int ncb, const int64_t *__restrict__ bstart, const int *__restrict__ c1,
                                              const double *__restrict__ v1, const double *__restrict__ x,
                                              double *__restrict__ prod) {
   const int xcd = blockIdx.x & 7, wi = blockIdx.x >> 3, nper = gridDim.x >> 3;
   for (int C = xcd; C < ncb; C += 8) {
     const int64_t b0 = bstart[C], b1 = bstart[C + 1], len = b1 - b0;
-    const int64_t chunk = (len + nper - 1) / nper;
+    const int64_t chunk = ((len + nper - 1) / nper + 1) & ~(int64_t)1;
     const int64_t lo = b0 + chunk * wi, hi = min(b1, lo + chunk);
-    // two elements per thread per step (16-B value and 8-B column loads)
     int64_t k = lo + 2 * threadIdx.x;
-    for (; k + 1 < hi; k += 512) {
-      const d2v v = ldnt(reinterpret_cast<const d2v *>(v1 + k));
-      const i2v c = ldnt(reinterpret_cast<const i2v *>(c1 + k));
-      d2v p;
-      p.x = v.x * x[c.x];
-      p.y = v.y * x[c.y];
-      __builtin_nontemporal_store(p, reinterpret_cast<d2v *>(prod + k));
+    for (; k + 2 * 256 * (E / 2 - 1) + 1 < hi; k += 512 * (E / 2)) {
+      d2v v[E / 2];
+      i2v c[E / 2];
+#pragma unroll
+      for (int e = 0; e < E / 2; ++e) {
+        v[e] = ldnt(reinterpret_cast<const d2v *>(v1 + k + 512 * e));
+        c[e] = ldnt(reinterpret_cast<const i2v *>(c1 + k + 512 * e));
+      }
+      double xa[E / 2], xb[E / 2];
+#pragma unroll
+      for (int e = 0; e < E / 2; ++e) { xa[e] = x[c[e].x]; xb[e] = x[c[e].y]; }
+#pragma unroll
+      for (int e = 0; e < E / 2; ++e) {
+        d2v p;
+        p.x = v[e].x * xa[e];
+        p.y = v[e].y * xb[e];
+        __builtin_nontemporal_store(p, reinterpret_cast<d2v *>(prod + k + 512 * e));
+      }
     }
-    if (k < hi) prod[k] = ldnt(v1 + k) * x[ldnt(c1 + k)];
+    for (; k < hi; k += 512) {
+      prod[k] = ldnt(v1 + k) * x[ldnt(c1 + k)];
+      if (k + 1 < hi) prod[k + 1] = ldnt(v1 + k + 1) * x[ldnt(c1 + k + 1)];
+    }
   }
 }
 
@@ -174,12 +189,15 @@ int main(int argc, char **argv) {
   std::printf("N = 2^%d x %d, column blocks of 2^%d doubles (%d blocks), sector model %.2f GB\n", lg, K, BS, ncb, sector / 1e9);
   const double t1 = timeit([&] { spmv_onepass<<<8192, 256>>>(ns, d_sc, d_sv, d_x, d_y); }, reps);
   std::printf("one pass                 %8.1f us  sector frac %.3f\n", t1 * 1e3, sector / t1 / 1e6 / 8000);
-  for (int g : {1024, 2048, 4096, 8192}) {
-    const double a = timeit([&] { pass1<<<g, 256>>>(ncb, d_b, d_c1, d_v1, d_x, d_prod); }, reps);
-    const double b = timeit([&] { pass2<<<8192, 256>>>(ns, d_perm, d_prod, d_y2); }, reps);
-    const double ab = timeit([&] { pass1<<<g, 256>>>(ncb, d_b, d_c1, d_v1, d_x, d_prod); pass2<<<8192, 256>>>(ns, d_perm, d_prod, d_y2); }, reps);
-    std::printf("two pass, grid %5d:    pass1 %7.1f us (%.0f GB/s on 20 B/nnz)  pass2 %7.1f us  both %7.1f us  sector frac %.3f\n",
-                g, a * 1e3, 20.0 * nnz / a / 1e6, b * 1e3, ab * 1e3, sector / ab / 1e6 / 8000);
+  const double t2 = timeit([&] { pass2<<<8192, 256>>>(ns, d_perm, d_prod, d_y2); }, reps);
+  std::printf("pass2 alone              %8.1f us  (%.0f GB/s on perm + y)\n", t2 * 1e3, (4.0 * nnz + 8.0 * N) / t2 / 1e6);
+  for (int g : {512, 768, 1024, 1536}) {
+    const double a2 = timeit([&] { pass1<2><<<g, 256>>>(ncb, d_b, d_c1, d_v1, d_x, d_prod); }, reps);
+    const double a4 = timeit([&] { pass1<4><<<g, 256>>>(ncb, d_b, d_c1, d_v1, d_x, d_prod); }, reps);
+    const double a8 = timeit([&] { pass1<8><<<g, 256>>>(ncb, d_b, d_c1, d_v1, d_x, d_prod); }, reps);
+    const double ab = timeit([&] { pass1<4><<<g, 256>>>(ncb, d_b, d_c1, d_v1, d_x, d_prod); pass2<<<8192, 256>>>(ns, d_perm, d_prod, d_y2); }, reps);
+    std::printf("grid %5d: pass1 E=2 %7.1f  E=4 %7.1f  E=8 %7.1f us (E=4: %.0f GB/s on 20 B/nnz)  E=4 + pass2 %7.1f us  sector frac %.3f\n",
+                g, a2 * 1e3, a4 * 1e3, a8 * 1e3, 20.0 * nnz / a4 / 1e6, ab * 1e3, sector / ab / 1e6 / 8000);
   }
   std::vector<double> y1(N), y2(N);
   CK(hipMemcpy(y1.data(), d_y, 8 * N, hipMemcpyDeviceToHost));
