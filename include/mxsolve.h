@@ -482,7 +482,8 @@ int mx_debug_dispatch_counts(int64_t *out, int n, int reset);
  * arrays (+ index widening), 1 row canonicalisation (longest row, sort,
  * duplicate fold), 2 MPIAIJ split (A_d / A_o / garray), 3 SpMV layouts (SELL,
  * value codes, row pairs, dictionary), 4 halo plan, 5 total, 6 bytes read
- * from host memory.  Writes min(n, 7) values.                              */
+ * from host memory, 7 allocation of the copied input's device buffers (before
+ * phase 0, within 5).  Writes min(n, 8) values.                             */
 int mx_debug_assembly_times(double *out, int n);
 /* Calibration stream for PMC byte counters: reads n doubles once with
  * width_bytes (8 or 16) per lane, non-temporal like the SpMV matrix stream,

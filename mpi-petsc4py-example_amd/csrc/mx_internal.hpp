@@ -362,6 +362,7 @@ struct Mat {
 // wall clock between stream synchronisations, milliseconds.
 struct AsmTimes {
   double h2d_ms = 0, canon_ms = 0, split_ms = 0, layout_ms = 0, halo_ms = 0, total_ms = 0;
+  double alloc_ms = 0;     // device buffers of the copied input (within total, not within h2d)
   double host_bytes = 0;   // bytes read from host memory (createAIJ from host arrays)
 };
 extern thread_local AsmTimes g_asm_times;

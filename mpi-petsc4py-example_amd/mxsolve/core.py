@@ -423,13 +423,13 @@ def dispatch_counts(reset: bool = False) -> dict:
     return {k: int(out[i]) for i, k in enumerate(DISPATCH_KINDS)}
 
 
-ASM_PHASES = ("h2d_ms", "canon_ms", "split_ms", "layout_ms", "halo_ms", "total_ms", "host_bytes")
+ASM_PHASES = ("h2d_ms", "canon_ms", "split_ms", "layout_ms", "halo_ms", "total_ms", "host_bytes", "alloc_ms")
 
 
 def assembly_times() -> dict:
     """Phase times of this thread's last createAIJ(csr=...) (mx_debug_assembly_times)."""
-    out = (C.c_double * 7)()
-    call("mx_debug_assembly_times", out, 7)
+    out = (C.c_double * len(ASM_PHASES))()
+    call("mx_debug_assembly_times", out, len(ASM_PHASES))
     return {k: float(out[i]) for i, k in enumerate(ASM_PHASES)}
 
 

@@ -17,6 +17,8 @@
 #   benchfast        bench.py --steps 100 --no-cpu --no-asm --no-general
 #   shm2             N = 2 rehearsal on one GPU (MXSOLVE_TRANSPORT=shm, torchrun)
 #   shm2fail         the same with the mode2/graph leg failing (the line must still print)
+#   shm2stall        the same with rank 1 stalling 40 s in the mode2/eager leg under an 8-s leg
+#                    budget (BUDGET): the watchdog aborts the leg, the line still prints
 #   prof             tools/profile.sh (trace + FETCH/WRITE PMC passes + calibration)
 #   configs          tools/bench_configs.py (C2/C3/C4/C5-share converged solves)
 #   general:LEGS     tools/bench_general.py LEGS (comma separated)
@@ -64,6 +66,9 @@ for step in "$@"; do
             --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 50 --warmup 5 ;;
     shm2fail) MXSOLVE_TRANSPORT=shm MXSOLVE_BENCH_FAIL_LEG=mode2/graph run shm2fail 400 python3 -u -m torch.distributed.run \
                 --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 50 --warmup 5 ;;
+    shm2stall) MXSOLVE_TRANSPORT=shm MXSOLVE_BENCH_LEG_BUDGET_S=${BUDGET:-8} MXSOLVE_BENCH_STALL_LEG=mode2/eager:40 \
+                 run shm2stall 400 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 50 --warmup 5 ;;
     prof) run prof 1000 bash tools/profile.sh ;;
     configs) run configs 700 python3 -u tools/bench_configs.py ;;
     c4prof) run c4prof 600 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_c4trace -o run -- \
