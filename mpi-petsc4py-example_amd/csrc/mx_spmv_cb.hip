@@ -23,9 +23,7 @@
 // ascending column order, one rounding per add: the bits of MatMult_SeqAIJ
 // and of the one-pass kernel (tests/test_gpu_cb.py).  Built at assembly for
 // one-rank general SELL blocks whose entries mostly lie far from the
-// diagonal (mx_assembly.hip build_cb); key 84 selects it.
-#include <hipcub/hipcub.hpp>
-
+// diagonal (build_cb, a counting placement: no sort); key 84 selects it.
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
 
@@ -53,28 +51,72 @@ __global__ void __launch_bounds__(256) cb_far_kernel(int64_t m, const int64_t *_
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(far, c);
 }
 
-__global__ void cb_keys_kernel(int64_t nnz, const int32_t *__restrict__ col, int bs, uint32_t *__restrict__ key,
-                               int32_t *__restrict__ idx) {
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * blockDim.x) {
-    key[e] = (uint32_t)col[e] >> bs;
-    idx[e] = (int32_t)e;
+// Pass-1 order without a sort: entry e (CSR order) goes to
+//   base[bin][R] + (entries of its bin in earlier rows of its 256-row group R)
+//                + (its rank among the row's entries of that bin),
+// base = the exclusive scan of the per-(bin, group) counts in bin-major
+// order.  Columns ascend along a row, so a row's entries of one bin are
+// consecutive, and the order within a bin is (row, column).  At most
+// CB_MAXBLK bins (the block size grows past 2^18 columns to keep it).
+constexpr int CB_MAXBLK = 64;
+__global__ void __launch_bounds__(256) cb_count_kernel(int64_t m, const int64_t *__restrict__ ptr,
+                                                       const int32_t *__restrict__ col, int bs, int nblk, int64_t ngrp,
+                                                       int64_t *__restrict__ cnt) {
+  __shared__ unsigned c[CB_MAXBLK];
+  for (int64_t R = blockIdx.x; R < ngrp; R += gridDim.x) {
+    if (threadIdx.x < CB_MAXBLK) c[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t r = R * 256 + threadIdx.x;
+    if (r < m)
+      for (int64_t e = ptr[r]; e < ptr[r + 1]; ++e) atomicAdd(&c[(uint32_t)col[e] >> bs], 1u);
+    __syncthreads();
+    if (threadIdx.x < nblk) cnt[(int64_t)threadIdx.x * ngrp + R] = c[threadIdx.x];
+    __syncthreads();
   }
 }
 
-// pass-1 arrays in sorted order, the inverse permutation, and the block starts
-__global__ void cb_scatter_kernel(int64_t nnz, const uint32_t *__restrict__ skey, const int32_t *__restrict__ src,
-                                  const int32_t *__restrict__ col, const double *__restrict__ val,
-                                  int32_t *__restrict__ c1, double *__restrict__ v1, int32_t *__restrict__ pinv,
-                                  int64_t *__restrict__ bstart, int nblk) {
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t e = src[k];
-    c1[k] = col[e];
-    v1[k] = val[e];
-    pinv[e] = (int32_t)k;
-    const uint32_t kk = skey[k], kp = k ? skey[k - 1] : 0u;
-    if (k == 0) for (uint32_t b = 0; b <= kk; ++b) bstart[b] = 0;
-    else for (uint32_t b = kp + 1; b <= kk; ++b) bstart[b] = k;
-    if (k == nnz - 1) for (int b = (int)kk + 1; b <= nblk; ++b) bstart[b] = nnz;
+__global__ void __launch_bounds__(256) cb_place_kernel(int64_t m, int64_t nnz, const int64_t *__restrict__ ptr,
+                                                       const int32_t *__restrict__ col, const double *__restrict__ val,
+                                                       int bs, int nblk, int64_t ngrp, const int64_t *__restrict__ base,
+                                                       int32_t *__restrict__ c1, double *__restrict__ v1,
+                                                       int32_t *__restrict__ pinv, int64_t *__restrict__ bstart) {
+  __shared__ int pre[CB_MAXBLK][256];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int64_t R = blockIdx.x; R < ngrp; R += gridDim.x) {
+    for (int b = 0; b < nblk; ++b) pre[b][t] = 0;
+    const int64_t r = R * 256 + t;
+    const int64_t e0 = r < m ? ptr[r] : 0, e1 = r < m ? ptr[r + 1] : 0;
+    for (int64_t e = e0; e < e1; ++e) pre[(uint32_t)col[e] >> bs][t] += 1;
+    __syncthreads();
+    // per bin, the exclusive prefix over the group's rows: wave wv takes bins
+    // wv, wv + 4, ...; lane l the rows 4 l .. 4 l + 3
+    for (int b = wv; b < nblk; b += 4) {
+      const int a0 = pre[b][4 * lane], a1 = pre[b][4 * lane + 1], a2 = pre[b][4 * lane + 2], a3 = pre[b][4 * lane + 3];
+      int incl = a0 + a1 + a2 + a3;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+      }
+      const int ex = incl - (a0 + a1 + a2 + a3);
+      pre[b][4 * lane] = ex;
+      pre[b][4 * lane + 1] = ex + a0;
+      pre[b][4 * lane + 2] = ex + a0 + a1;
+      pre[b][4 * lane + 3] = ex + a0 + a1 + a2;
+    }
+    __syncthreads();
+    int pb = -1, k = 0;
+    for (int64_t e = e0; e < e1; ++e) {
+      const int b = (int)((uint32_t)col[e] >> bs);
+      k = b == pb ? k + 1 : 0;
+      pb = b;
+      const int64_t pos = base[(int64_t)b * ngrp + R] + pre[b][t] + k;
+      c1[pos] = col[e];
+      v1[pos] = val[e];
+      pinv[e] = (int32_t)pos;
+    }
+    if (R == 0 && t <= nblk) bstart[t] = t < nblk ? base[(int64_t)t * ngrp] : nnz;
+    __syncthreads();
   }
 }
 
@@ -254,28 +296,28 @@ void build_cb(Mat *A, hipStream_t st) {
     HIPCHECK(hipStreamSynchronize(st));
     if (h * 2 < (unsigned long long)nnz) return;   // half the entries or more far from the diagonal
   }
-  // column blocks: 2 MB of x (2^18 doubles) from 2^22 columns, fewer columns
-  // per block below so that every XCD gets at least two
+  // column blocks: 2 MB of x (2^18 doubles) from 2^22 columns; fewer columns
+  // per block below, so that every XCD gets at least two, and more above
+  // 2^24 columns (at most CB_MAXBLK blocks)
   int bs = 18;
   while (bs > 6 && (A->n >> bs) < 16) --bs;
+  while (((A->n + ((int64_t)1 << bs) - 1) >> bs) > CB_MAXBLK) ++bs;
   const int nblk = (int)((A->n + ((int64_t)1 << bs) - 1) >> bs);
-  int kbits = 1;
-  while ((1 << kbits) < nblk) ++kbits;
-  DBuf<uint32_t> key((size_t)nnz, kScratch), skey((size_t)nnz, kScratch);
-  DBuf<int32_t> idx((size_t)nnz, kScratch), src((size_t)nnz, kScratch), pinv((size_t)nnz, kScratch);
-  cb_keys_kernel<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(nnz, A->dcol.p, bs, key.p, idx.p);
+  const int64_t ngrp = cdiv(m, 256);
+  DBuf<int64_t> cnt((size_t)nblk * (size_t)ngrp, kScratch);
+  DBuf<int32_t> pinv((size_t)nnz, kScratch);
+  cb_count_kernel<<<(unsigned)std::min<int64_t>(ngrp, 16384), 256, 0, st>>>(m, A->dptr.p, A->dcol.p, bs, nblk, ngrp,
+                                                                          cnt.p);
   HIPCHECK(hipGetLastError());
-  size_t tb = 0;
-  HIPCHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.p, skey.p, idx.p, src.p, (int)nnz, 0, kbits, st));
-  DBuf<char> tmp(std::max<size_t>(tb, 1), kScratch);
-  HIPCHECK(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, key.p, skey.p, idx.p, src.p, (int)nnz, 0, kbits, st));
+  exclusive_scan_i64(cnt.p, cnt.p, (int64_t)nblk * ngrp, st, nullptr);
   S.cb_col.alloc((size_t)nnz);
   S.cb_val.alloc((size_t)nnz);
   S.cb_prod.alloc((size_t)nnz);
   S.cb_bstart.alloc((size_t)nblk + 1);
   S.cb_perm.alloc((size_t)std::max<int64_t>(S.slots, 1));
-  cb_scatter_kernel<<<grid_for(nnz, 256, 8192), 256, 0, st>>>(nnz, skey.p, src.p, A->dcol.p, A->dval.p, S.cb_col.p,
-                                                              S.cb_val.p, pinv.p, S.cb_bstart.p, nblk);
+  cb_place_kernel<<<(unsigned)std::min<int64_t>(ngrp, 16384), 256, 0, st>>>(m, nnz, A->dptr.p, A->dcol.p, A->dval.p, bs,
+                                                                          nblk, ngrp, cnt.p, S.cb_col.p, S.cb_val.p,
+                                                                          pinv.p, S.cb_bstart.p);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipMemsetAsync(S.cb_perm.p, 0xFF, sizeof(int32_t) * (size_t)std::max<int64_t>(S.slots, 1), st));
   cb_perm_kernel<<<grid_for(m, 256, 8192), 256, 0, st>>>(m, A->dptr.p, S.sptr.p, S.width.p, pinv.p, S.cb_perm.p);
