@@ -283,11 +283,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
                     const double *vals, const double *b, double *x);
 
 /* ---- measurement knobs (A/B runs only; defaults are the product path) -------
- * key 1: SpMV non-temporal matrix loads (0/1, default 1)
- * key 3: SpMV grid size in workgroups (0 = default: one resident generation,
- *        see keys 26 / 28, one workgroup fewer per XCD)
- * key 4: aligned-offset (DIA-in-SELL) slices at assembly (0/1, default 1)
- * key 5: uniform-diagonal Jacobi applied as one scalar (0/1, default 1)
  * key 6: halo exchange overlapping the interior slices when P > 1 (0/1, default 1)
  * key 7: CG iterations replayed from a captured hipGraph batch after one eager
  *        batch: 0 never, 1 single-rank communicators (default; equal at 256^3,
@@ -302,54 +297,25 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *        MatMult stores no product: a p.Ap pass, and the update pass
  *        recomputes A p where it forms r - alpha A p (one rank, lean 5/7-point
  *        z-march layout, no or uniform Jacobi; else 2)
- * key 10: where CG folds its per-workgroup partials: 0 one-block fold kernels;
- *        1 the update pass folds its own inside the launch, and the MatMult's
- *        halo-boundary launch when the product is split (default); 2 the
- *        MatMult always; 3 as 1, and on one rank the update pass folds the
- *        MatMult's partials in its prologue (no fold launch; measured equal)
- * key 11: skew (doubles) added between consecutive KSP work vectors
- * key 12: grid of the CG vector passes (0 = default: row walk 8192 / 1024
- *         workgroups for the direction / update pass, paired walk 4096)
  * key 13: CG vector passes walk row pairs with 16-B accesses when every
  *         vector is aligned (0/1, default 0: one row per thread per step)
- * key 14: non-temporal stores in the CG vector passes' row walk (0/1, default 0)
- * key 15: grid cap of the halo-boundary SpMV launch (0 = default 2048)
- * key 19: one-byte row masks for aligned-offset slices when every slice has
- *         <= 8 offsets (read at assembly; 0/1, default 1)
  * key 21: CG vector passes issue four steps' loads together: 0 never, 1 always,
  *         2 auto (default: up to 6M local rows)
- * key 22: grid cap of the CG update pass (0 = default 1024 workgroups)
  * key 23: value codes -- one byte per slot into a table of <= 255 distinct
  *         values -- for the diagonal block (read at assembly and at launch;
  *         0/1, default 1)
- * key 25: non-temporal y stores in the SpMV (0/1, default 0)
- * key 26: resident workgroups per CU for the single-row SpMV grid (default 6)
  * key 27: row-pair SpMV layout for 5/7/27-point patterns (read at assembly and
  *         at launch; 0/1, default 1)
- * key 28: resident workgroups per CU for the row-pair SpMV grid (default 4)
  * key 29: CG modes 2/5 apply the deferred x steps every B iterations from B
  *         rotating direction buffers (1, 2, 4 or 8; default 0 = auto: 4 in
  *         mode 5, else 2; 8 -- the same bits -- measured within +-1% of 4 per
  *         256^3 iteration: the batch launch's eleven streams give back what
  *         the rarer x pass saves)
- * key 30: the row-pair block dictionary (read at assembly: 1, default, when
- *         repeats pay for the indirection; 2 always; 0 one block per unit)
- * key 32: non-temporal loads in the CG vector passes: bit 0 the direction
- *         update's r / p_{i-1} reads, bit 1 the update pass's w / r reads
- *         (default 3)
  * key 33: no-progress deadline in ms of the KSP poller's wait on an RCCL
  *         communicator (re-armed whenever the device's count of iterations
  *         begun moves); past it the communicator is aborted and the call fails
  *         with MX_ERR_COMM (default 120000).  An RCCL asynchronous error aborts
  *         at once in every wait
- * key 34: grid of the CG initial-norms pass (0 = default: the direction update's grid,
- *         whose fused iteration-0 norms it must match bit for bit)
- * key 35: row-pair SpMV reads uniform-slot dictionary blocks as slot values +
- *         lane masks when the matrix has them (0/1, default 1)
- * key 36: grid of the GMRES MDot pass (0 = default: 3 workgroups per CU)
- * key 37: the Jacobi-fused row-pair MatMult (GMRES) takes dinv from a table
- *         indexed by the rows' diagonal code instead of reading the dinv
- *         vector (0/1, default 1; the same bits)
  * key 38: the lean row-pair MatMult (mx_spmv_pair.hip) for uniform-slot 5/7-point
  *         layouts (0/1, default 1; the same bits)
  * key 39: its z-march form (a wave marches a column of units one plane apart,
@@ -357,14 +323,8 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 40: z-march resident workgroups per CU (1..8, default 4)
  * key 41: z-march segment length in planes (default 32, shortened when a slab
  *         has too few columns for every wave)
- * key 42: z-march planes per step (1 or 2, default 2)
  * key 43: grid of the SpMV for fp64-valued (uncoded) layouts (default 8192
- *         workgroups; 0 = the resident grid of key 26)
- * key 44: fp64 row-pair layout + z-march MatMult for uncoded 5/7-point blocks
- *         (read at assembly; 0/1, default 1; the same bits)
- * key 45: 27-point z-march resident workgroups per CU (default 6; 0 = key 40)
- * key 46: CG mode 5: the residual-update pass folds the p.Ap pass's partials
- *         itself (1, default) or a one-block fold kernel runs between (0)
+ *         workgroups; 0 = one resident generation)
  * key 47: deadline in ms of the RCCL waits that observe no progress (stream /
  *         event waits, setup collectives, barrier); 0 = none (default 600000:
  *         a slow peer is not an error, a dead one fails the call after 10 min).
@@ -372,18 +332,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  * key 48: 27-point column words (read at assembly; 0/1, default 1): the
  *         27-point z-march zeroes empty runs and x-line edges where it loads
  *         them (no per-run branches, no selects; the same bits)
- * key 49: 27-point z-march planes per step (1, default, or 2)
- * key 54: GMRES basis stride padding in rows (multiple of 32; default 256:
- *         2 KB between the vectors' rows, -1.8% per GMRES(30) step at 256^3)
- * key 55: CG mode 5 (p.Ap pass + residual update recomputing A p) also for
- *         the 27-point column-word z-march on one rank (1, default; 0: mode 2)
- * key 56: workgroups per CU of that 27-point residual update (default 5, the
- *         resident count at its 96 VGPRs; 0: key 45's)
- * key 57: workgroups per CU of CG mode 5's 5/7-point p.Ap pass (0, default:
- *         key 40's)
- * key 58: workgroups per CU of CG mode 5's 5/7-point residual update
- *         (default 3: -1 to -2% per C2 / C3 iteration against key 40's 4; 0:
- *         key 40's)
  * key 59: CG mode 5's p.Ap pass on a symmetric operator sums each row's
  *         forward half, p^T A p = sum_i p_i (a_ii p_i + 2 fwd_i) -- 27-point:
  *         symmetry from the column-word layout; 5/7-point: A_d checked once
@@ -399,10 +347,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         read-back (default 0), so the no-progress deadline can be driven
  * (keys 16, 24, 31, 50, 51, 62-64, 66, 67 -- variants measured and not kept --
  *  were retired in round 5; setting them has no effect)
- * key 65: z-march grids that fill whole task rounds (1, default: the
- *         workgroups per CU, at most the configured, whose tasks per XCD are
- *         a whole number of rounds of its waves -- C5's share: 4 instead of 5
- *         for the residual update; 0: the configured counts)
  * key 68: CG mode 5's 7-point residual update with two lines per wave (line
  *         y's +n operand is line y + 1's centre pair: 8 vector loads per two
  *         units instead of 10; the same row sums, the norm partials grouped
@@ -430,19 +374,6 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         at most 64 entries (1, default; 0: the canonical copy in HBM, then
  *         the split passes -- the path rows longer than 64 always take; the
  *         same arrays bit for bit)
- * key 74: the 27-point two-line residual update and p.Ap pass split the
- *         line groups of every plane across the XCDs, in segments of L
- *         planes, instead of one slab of NZ / 8 planes per XCD, when the
- *         segments come out longer than the slab (1, default; 0 off):
- *         C5's share residual update 75.0 -> 72.3 us, p.Ap pass 26.0 -> 24.3
- * key 75: workgroups per CU of the key-74 residual update (default 2; 0: the
- *         slab form's count -- 4 at C5's share: 72.5 against 69.2 us)
- * key 76: workgroups per CU of the key-74 p.Ap pass (default 3; 0: key 45's
- *         -- 6: 24.4 against 23.5 us at C5's share)
- * key 77: grid of the GMRES MAXPY + norm pass (0, default: 1024 workgroups;
- *         at most 16384)
- * key 78: planes per step of the coded z-march (1, default; 2; 0: key 42's)
- * key 79: workgroups per CU of the coded z-march (0, default: key 40's)
  * key 80: CG mode 5 on P > 1 ranks fuses the direction update into the split
  *         p.Ap pass on the iterations between x-step batches (the halo pack
  *         forms the ghost planes' p_i from r and p_{i-1}; the same bits as
@@ -461,7 +392,11 @@ int mx_lu_solve_csr(mx_comm c, int64_t n, const int64_t *indptr, const int64_t *
  *         block (tests), 0 never; the same bits as the one-pass kernel
  * (key 18, physically contiguous allocations, was retired in round 6: freed
  *  contiguous blocks whose address range was reused were still reached through
- *  stale translations -- DESIGN.md section 11)
+ *  stale translations -- DESIGN.md section 12.1)
+ * (keys 1, 3, 4, 5, 10, 11, 12, 14, 15, 19, 22, 25, 26, 28, 30, 32, 34-37,
+ *  42, 44-46, 49, 54-58, 65, 74-79 -- settings measured in rounds 1-5 and
+ *  fixed at their chosen values -- are compile-time constants since round 6
+ *  (mx_internal.hpp Knobs); setting them has no effect and returns -1)
  * Returns the previous value.                                                   */
 int mx_debug_set(int key, int value);
 /* Test hook: host-side counts of the MatMult-family kernel launches

@@ -632,72 +632,35 @@ int mx_dev_free(void *ptr) { return guard([&] { dev_free(ptr); }); }
 int mx_debug_set(int key, int value) {
   int old = -1;
   switch (key) {
-    case 1: old = g_knobs.spmv_nt; g_knobs.spmv_nt = value; break;
-    case 3: old = g_knobs.spmv_grid; if (value >= 0) g_knobs.spmv_grid = value; break;   // 0: resident grid
-    case 4: old = g_knobs.dia; g_knobs.dia = value; break;
-    case 5: old = g_knobs.jac_const; g_knobs.jac_const = value; break;
     case 6: old = g_knobs.overlap; g_knobs.overlap = value; break;
     case 7: old = g_knobs.graph; g_knobs.graph = value; break;
     case 8: old = g_knobs.force_coll; g_knobs.force_coll = value; break;
     case 9: old = g_knobs.cg_fuse; g_knobs.cg_fuse = value; break;
-    case 10: old = g_knobs.cg_fold; g_knobs.cg_fold = value; break;
-    case 11: old = g_knobs.ws_skew; g_knobs.ws_skew = value; break;
-    case 12: old = g_knobs.cg_vec_grid; g_knobs.cg_vec_grid = value; break;
     case 13: old = g_knobs.cg_vec; g_knobs.cg_vec = value; break;
-    case 14: old = g_knobs.cg_nts; g_knobs.cg_nts = value; break;
-    case 15: old = g_knobs.bnd_grid; g_knobs.bnd_grid = value; break;
-    case 19: old = g_knobs.mask8; g_knobs.mask8 = value; break;
     case 21: old = g_knobs.cg_unroll; g_knobs.cg_unroll = value; break;
-    case 22: old = g_knobs.cg_upd_grid; g_knobs.cg_upd_grid = std::min(value, 65536); break;
     case 23: old = g_knobs.vcodes; g_knobs.vcodes = value; break;
-    case 25: old = g_knobs.spmv_ynt; g_knobs.spmv_ynt = value; break;
-    case 26: old = g_knobs.spmv_bpc; g_knobs.spmv_bpc = value; break;
     case 27: old = g_knobs.spmv_pairs; g_knobs.spmv_pairs = value; break;
-    case 28: old = g_knobs.spmv_pair_bpc; g_knobs.spmv_pair_bpc = value; break;
     case 29: old = g_knobs.cg_xbatch; g_knobs.cg_xbatch = value; break;
-    case 30: old = g_knobs.pdict; g_knobs.pdict = value; break;
-    case 32: old = g_knobs.cg_ntl; g_knobs.cg_ntl = value; break;
     case 33: old = g_knobs.comm_timeout_ms; if (value > 0) g_knobs.comm_timeout_ms = value; break;
-    case 34: old = g_knobs.norm_grid; g_knobs.norm_grid = std::min(std::max(value, 0), 16384); break;
-    case 35: old = g_knobs.pair_uni; g_knobs.pair_uni = value; break;
-    case 36: old = g_knobs.mdot_grid; g_knobs.mdot_grid = std::min(std::max(value, 0), RED_BLOCKS); break;
-    case 37: old = g_knobs.pair_dtab; g_knobs.pair_dtab = value; break;
     case 38: old = g_knobs.pair_lean; g_knobs.pair_lean = value; break;
     case 39: old = g_knobs.pair_zm; g_knobs.pair_zm = value; break;
     case 40: old = g_knobs.pair_zm_bpc; g_knobs.pair_zm_bpc = std::min(std::max(value, 1), 8); break;
     case 41: old = g_knobs.pair_zm_len; g_knobs.pair_zm_len = std::min(std::max(value, 1), 1024); break;
-    case 42: old = g_knobs.pair_zm_units; g_knobs.pair_zm_units = value == 2 ? 2 : 1; break;
     case 43: old = g_knobs.spmv_fp64_grid; g_knobs.spmv_fp64_grid = std::min(std::max(value, 0), 65536); break;
-    case 44: old = g_knobs.pair_f64; g_knobs.pair_f64 = value; break;
-    case 45: old = g_knobs.pair_zm27_bpc; g_knobs.pair_zm27_bpc = std::min(std::max(value, 0), 8); break;
-    case 46: old = g_knobs.cg5_fold; g_knobs.cg5_fold = value; break;
     case 47: old = g_knobs.comm_wait_ms; g_knobs.comm_wait_ms = std::max(value, 0); break;
     case 48: old = g_knobs.pair_col27; g_knobs.pair_col27 = value; break;
-    case 49: old = g_knobs.pair_zm27_units; g_knobs.pair_zm27_units = value == 2 ? 2 : 1; break;
     case 52: old = g_knobs.pair_zmc; g_knobs.pair_zmc = value; break;
     case 53: old = g_knobs.pair_unitv; g_knobs.pair_unitv = value; break;
-    case 55: old = g_knobs.cg5_27; g_knobs.cg5_27 = value; break;
     case 60: old = g_knobs.pair_zm27p; g_knobs.pair_zm27p = value; break;
     case 70: old = g_knobs.zm27_2line; g_knobs.zm27_2line = value; break;
     case 72: old = g_knobs.asm_fused; g_knobs.asm_fused = value; break;
-    case 74: old = g_knobs.zm27_xcol; g_knobs.zm27_xcol = value; break;
-    case 75: old = g_knobs.zm27_xcol_ru; g_knobs.zm27_xcol_ru = value; break;
-    case 76: old = g_knobs.zm27_xcol_pw; g_knobs.zm27_xcol_pw = value; break;
-    case 77: old = g_knobs.maxpy_grid; g_knobs.maxpy_grid = std::min(std::max(value, 0), 16384); break;
-    case 78: old = g_knobs.zmc_units; g_knobs.zmc_units = value; break;
     case 80: old = g_knobs.cg_pbws; g_knobs.cg_pbws = value; break;
     case 81: old = g_knobs.scratch_cache; g_knobs.scratch_cache = value; if (!value) scratch_trim(); break;
     case 84: old = g_knobs.cb; g_knobs.cb = value; break;
-    case 79: old = g_knobs.zmc_bpc; g_knobs.zmc_bpc = std::min(std::max(value, 0), 8); break;
     case 69: old = g_knobs.cg_pbw; g_knobs.cg_pbw = value; break;
     case 68: old = g_knobs.ru_2line; g_knobs.ru_2line = value; break;
-    case 65: old = g_knobs.zm_balance; g_knobs.zm_balance = value; break;
     case 61: old = g_knobs.gm_stall_us; g_knobs.gm_stall_us = std::min(std::max(value, 0), 2000000); break;
     case 59: old = g_knobs.pw_sym27; g_knobs.pw_sym27 = value; break;
-    case 57: old = g_knobs.pw_bpc; g_knobs.pw_bpc = std::min(std::max(value, 0), 8); break;
-    case 58: old = g_knobs.ru_bpc; g_knobs.ru_bpc = std::min(std::max(value, 0), 8); break;
-    case 56: old = g_knobs.pair_zm27_ru_bpc; g_knobs.pair_zm27_ru_bpc = std::min(std::max(value, 0), 8); break;
-    case 54: old = g_knobs.gm_pad; g_knobs.gm_pad = std::min(std::max(value, 0), 1 << 20); break;
     default: break;
   }
   return old;

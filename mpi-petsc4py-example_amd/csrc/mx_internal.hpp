@@ -281,18 +281,26 @@ constexpr int VCODE_ABSENT = VCODE_MAX - 1;
 constexpr int CODE_BATCH = 8 * SLICE;   // bytes per 8-slot batch of a slice
 struct VCodes { const uint8_t *code; const int64_t *cptr; const double *tab; int ntab; };
 
-// runtime knobs for A/B measurements (mx_debug_set); defaults are the product path
-struct Knobs { int spmv_nt = 1; int spmv_grid = 0; int dia = 1; int jac_const = 1; int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_fold = 1; int ws_skew = 0;
-                int cg_vec_grid = 0; int cg_vec = 0; int cg_nts = 0;
-                int bnd_grid = 0;
-                int mask8 = 1; int cg_unroll = 2;
-                int cg_upd_grid = 0; int vcodes = 1; int spmv_ynt = 0; int spmv_bpc = 6; int spmv_pairs = 1; int spmv_pair_bpc = 4;
-                int cg_xbatch = 0; int pdict = 1; int cg_ntl = 3;
-                int comm_timeout_ms = 120000; int norm_grid = 0; int pair_uni = 1; int mdot_grid = 0; int pair_dtab = 1;
-                int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int pair_zm_units = 2;
-                int spmv_fp64_grid = 8192; int pair_f64 = 1; int pair_zm27_bpc = 6; int cg5_fold = 1;
-                int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zm27_units = 1;
-                int pair_zmc = 1; int pair_unitv = 1; int gm_pad = 256; int cg5_27 = 1; int pair_zm27_ru_bpc = 5; int pw_bpc = 0; int ru_bpc = 3; int pw_sym27 = 1; int pair_zm27p = 1; int gm_stall_us = 0; int zm_balance = 1; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1; int asm_fused = 1; int zm27_xcol = 1; int zm27_xcol_ru = 2; int zm27_xcol_pw = 3; int maxpy_grid = 0; int zmc_units = 1; int zmc_bpc = 0; int cg_pbws = 1; int scratch_cache = 1; int cb = 1; };
+// Runtime switches (mx_debug_set, include/mxsolve.h): the product path's
+// defaults, and the alternatives the tests compare it with bit for bit.
+// The settings measured and fixed in rounds 1-5 are compile-time constants
+// (round 6: 37 keys retired; static members, so every `g_knobs.x` reads on).
+struct Knobs {
+  int overlap = 1; int graph = 1; int force_coll = 0; int cg_fuse = 3; int cg_vec = 0; int cg_unroll = 2;
+  int vcodes = 1; int spmv_pairs = 1; int cg_xbatch = 0; int comm_timeout_ms = 120000;
+  int pair_lean = 1; int pair_zm = 1; int pair_zm_bpc = 4; int pair_zm_len = 32; int spmv_fp64_grid = 8192;
+  int comm_wait_ms = 600000; int pair_col27 = 1; int pair_zmc = 1; int pair_unitv = 1; int pw_sym27 = 1;
+  int pair_zm27p = 1; int gm_stall_us = 0; int ru_2line = 3; int cg_pbw = 5; int zm27_2line = 1;
+  int asm_fused = 1; int cg_pbws = 1; int scratch_cache = 1; int cb = 1;
+  // fixed (the value each former key's A/B chose; DESIGN.md sections 4-11)
+  static constexpr int spmv_nt = 1, spmv_grid = 0, dia = 1, jac_const = 1, cg_fold = 1, ws_skew = 0;
+  static constexpr int cg_vec_grid = 0, cg_nts = 0, bnd_grid = 0, mask8 = 1, cg_upd_grid = 0, spmv_ynt = 0;
+  static constexpr int spmv_bpc = 6, spmv_pair_bpc = 4, pdict = 1, cg_ntl = 3, norm_grid = 0, pair_uni = 1;
+  static constexpr int mdot_grid = 0, pair_dtab = 1, pair_zm_units = 2, pair_f64 = 1, pair_zm27_bpc = 6;
+  static constexpr int cg5_fold = 1, pair_zm27_units = 1, gm_pad = 256, cg5_27 = 1, pair_zm27_ru_bpc = 5;
+  static constexpr int pw_bpc = 0, ru_bpc = 3, zm_balance = 1, zm27_xcol = 1, zm27_xcol_ru = 2, zm27_xcol_pw = 3;
+  static constexpr int maxpy_grid = 0, zmc_units = 1, zmc_bpc = 0;
+};
 extern Knobs g_knobs;
 
 struct Halo {

@@ -194,66 +194,30 @@ def _with_knob(L, key, value, fn):
 @pytest.mark.parametrize("kind,n,shape", [("poisson2d", 256, 5), ("poisson3d", 64, 7), ("poisson3d27", 48, 27),
                                           ("convdiff3d", 64, 7)])
 def test_pair_code_dictionary(selfcomm, oracle_mod, kind, n, shape):
-    """Row-pair code blocks deduplicated into a dictionary (knob 30 = 1, the
-    default): a few distinct blocks, MatMult bit-exact against the oracle and
-    against the one-block-per-unit layout (knob 30 = 0); knob 30 = 2 makes
-    every unit hash alike, so the byte-for-byte check must refuse the
-    dictionary and keep the per-unit blocks (unless there is only one)."""
+    """Row-pair code blocks deduplicated into a dictionary: a few distinct
+    blocks, MatMult bit-exact against the oracle.  (The per-unit layout and
+    the forced-collision check of rounds 3-5, knob 30, are retired.)"""
     ip, c, v = oracle_mod.stencil(kind, n)
     M = ip.size - 1
-    L = lib()
     info1, got1, exp = mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=13)
-    info0, got0, _ = _with_knob(L, 30, 0, lambda: mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=13))
-    info2, got2, _ = _with_knob(L, 30, 2, lambda: mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=13))
-    assert info1["pair_shape"] == shape and info0["pair_shape"] == shape
+    assert info1["pair_shape"] == shape
     assert 0 < info1["pair_blocks"] <= info1["pair_units"] // 4
-    assert info0["pair_blocks"] == 0
-    # one distinct block (3D 64^3: every pair unit is two interior x-lines;
-    # the y-boundary slices carry another offset pattern) is the one case the
-    # forced collision cannot break
-    assert info2["pair_blocks"] == (1 if info1["pair_blocks"] == 1 else 0)
-    for got in (got0, got1, got2):
-        assert np.array_equal(got, exp)
-
-
-def test_pair_code_dictionary_cg(selfcomm):
-    """CG on 3D 7-point 64^3 with and without the code dictionary: same
-    iteration count, same solution bits."""
-    from mxsolve.core import DMat, rhs_hash
-    L = lib()
-
-    def run():
-        A = DMat.stencil(selfcomm, "poisson3d", 64)
-        m = A.info()["m"]
-        b = selfcomm.empty(m)
-        rhs_hash(selfcomm, 0, b)
-        x = selfcomm.zeros(m)
-        r = A.solve(b, x, ksp="cg", pc="jacobi")
-        return r["its"], r["reason"], x.cpu().numpy().copy(), A.info()["pair_blocks"]
-
-    on = _with_knob(L, 39, 0, run)          # the sweep form: the general kernel's p.w grouping
-    off = _with_knob(L, 30, 0, run)
-    assert on[3] > 0 and off[3] == 0
-    assert on[:2] == off[:2]
-    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
+    assert np.array_equal(got1, exp)
 
 
 @pytest.mark.parametrize("kind,n,shape,uni", [("poisson2d", 256, 5, 1), ("poisson3d", 64, 7, 1),
                                               ("poisson3d", 32, 7, 1), ("convdiff3d", 64, 7, 0)])
 def test_pair_uniform_blocks(selfcomm, oracle_mod, kind, n, shape, uni):
-    """Uniform-slot dictionary blocks (knob 35 = 1, the default: each block's
-    slot values and lane masks read by scalar loads, no code bytes): MatMult
-    bit-exact against the oracle and against the LDS-table path (knob 35 = 0).
-    The convection-diffusion operator's face coefficients vary along x, so
-    its blocks are not uniform; nor is a dictionary whose slot-row holds two
-    values."""
+    """Uniform-slot dictionary blocks (each block's slot values and lane masks
+    read by scalar loads, no code bytes): MatMult bit-exact against the
+    oracle.  The convection-diffusion operator's face coefficients vary along
+    x, so its blocks are not uniform (the LDS-table path); nor is a dictionary
+    whose slot-row holds two values."""
     ip, c, v = oracle_mod.stencil(kind, n)
     M = ip.size - 1
-    L = lib()
     info1, got1, exp = mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=17)
-    info0, got0, _ = _with_knob(L, 35, 0, lambda: mult_bits(selfcomm, oracle_mod, M, ip, c, v, seed=17))
     assert info1["pair_shape"] == shape and info1["pair_blocks"] > 0 and info1["pair_uniform"] == uni
-    assert np.array_equal(got1, exp) and np.array_equal(got0, exp)
+    assert np.array_equal(got1, exp)
     # two values in the diagonal slot-row of the interior units: not uniform
     v2 = v.copy()
     rows = np.repeat(np.arange(M), np.diff(ip))
@@ -263,34 +227,11 @@ def test_pair_uniform_blocks(selfcomm, oracle_mod, kind, n, shape, uni):
     assert info2["pair_uniform"] == 0 and np.array_equal(got2, exp2)
 
 
-def test_pair_uniform_cg(selfcomm):
-    """CG (MatMult + p.w in one pass) on 3D 7-point 64^3 with the uniform-slot
-    blocks and with the LDS table: same iterations, same solution bits."""
-    from mxsolve.core import DMat, rhs_hash
-    L = lib()
-
-    def run():
-        A = DMat.stencil(selfcomm, "poisson3d", 64)
-        m = A.info()["m"]
-        b = selfcomm.empty(m)
-        rhs_hash(selfcomm, 0, b)
-        x = selfcomm.zeros(m)
-        r = A.solve(b, x, ksp="cg", pc="jacobi")
-        return r["its"], r["reason"], x.cpu().numpy().copy()
-
-    # the lean kernel's sweep form keeps the general kernel's p.w grouping
-    on = _with_knob(L, 39, 0, run)
-    off = _with_knob(L, 35, 0, run)
-    assert on[:2] == off[:2]
-    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
-
-
 @pytest.mark.parametrize("kind,n,ksp", [("convdiff3d", 24, "gmres"), ("poisson3d27", 16, "gmres")])
 def test_pair_jacobi_by_code(selfcomm, oracle_mod, kind, n, ksp):
-    """GMRES(30) + vector Jacobi on the row-pair path: dinv from the table
-    indexed by the rows' diagonal code (knob 37 = 1, default) and from the
-    dinv vector (knob 37 = 0) give the same iterations, history and solution
-    bits; both against the oracle."""
+    """GMRES(30) + vector Jacobi on the row-pair path, dinv from the table
+    indexed by the rows' diagonal code: iterations, reason and solution
+    against the oracle."""
     from mxsolve.core import DMat
     ip, c, v = oracle_mod.stencil(kind, n)
     M = ip.size - 1
@@ -307,10 +248,6 @@ def test_pair_jacobi_by_code(selfcomm, oracle_mod, kind, n, ksp):
         return r["its"], r["reason"], r["history"].copy(), x.cpu().numpy().copy()
 
     on = run()
-    off = _with_knob(L, 37, 0, run)
-    assert on[:2] == off[:2]
-    assert np.array_equal(on[2].view(np.uint64), off[2].view(np.uint64))
-    assert np.array_equal(on[3].view(np.uint64), off[3].view(np.uint64))
     O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v)
     o = O.solve(b, ksp=ksp, rtol=1e-8)
     assert on[1] == o["reason"] and abs(on[0] - o["its"]) <= 1
@@ -328,14 +265,15 @@ def _with_knobs(L, kv, fn):
 
 
 # lean-kernel forms: default (z-march, two planes per step, 4 workgroups per
-# CU, segments of up to 32 planes), the sweep form (39 = 0), one plane per
-# step (42 = 1), short / odd segments with tails (41), other grids (40)
-# -- and for the 27-point z-march: its per-run-branch body instead of the
-# column-zeroed one (48 = 0), two planes per step (49 = 2), other grids (45),
+# CU, segments of up to 32 planes), the sweep form (39 = 0), short / odd
+# segments with tails (41), other grids (40) -- and for the 27-point z-march:
+# its per-run-branch body instead of the column-zeroed one (48 = 0),
 # multiply-and-add for the -1 slots instead of their exact-product fma (53 = 0),
-# the carried-operand body instead of the plane-pipelined one (60 = 0)
-LEAN_FORMS = [{}, {39: 0}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}, {40: 2},
-              {48: 0}, {49: 2, 45: 3}, {48: 0, 49: 2, 41: 5}, {53: 0}, {60: 0}, {60: 0, 53: 0}]
+# the carried-operand body instead of the plane-pipelined one (60 = 0).
+# (The plane-step and 27-point grid variants, keys 42 / 49 / 45, are fixed
+# since round 6.)
+LEAN_FORMS = [{}, {39: 0}, {41: 3}, {41: 1, 40: 1}, {41: 5, 40: 3}, {40: 2},
+              {48: 0}, {48: 0, 41: 5}, {53: 0}, {60: 0}, {60: 0, 53: 0}]
 
 
 @pytest.mark.parametrize("form", range(len(LEAN_FORMS)))
@@ -446,19 +384,14 @@ def test_pair_f64_zmarch(selfcomm, oracle_mod, kind, n, f64):
             x[rng.integers(0, M, 40)] = -np.inf
             x[rng.integers(0, M, 40)] = np.nan
         exp = O.mult(x).view(np.uint64)
-        outs = []
-        for knob in (1, 0):
-            def run():
-                A = DMat.from_csr(selfcomm, M, M, ip, c, v)
-                y = torch.zeros(M, dtype=torch.float64, device="cuda")
-                A.mult(torch.from_numpy(x).cuda(), y)
-                info = A.info()
-                A.destroy()
-                return info, y.cpu().numpy().view(np.uint64)
-            outs.append(_with_knob(L, 44, knob, run))
-        (i1, g1), (i0, g0) = outs
-        assert i1["value_codes"] == 0 and i1["pair_f64"] == f64 and i0["pair_f64"] == 0
-        assert np.array_equal(g1, exp) and np.array_equal(g0, exp)
+        A = DMat.from_csr(selfcomm, M, M, ip, c, v)
+        y = torch.zeros(M, dtype=torch.float64, device="cuda")
+        A.mult(torch.from_numpy(x).cuda(), y)
+        i1 = A.info()
+        A.destroy()
+        g1 = y.cpu().numpy().view(np.uint64)
+        assert i1["value_codes"] == 0 and i1["pair_f64"] == f64
+        assert np.array_equal(g1, exp)
     A = DMat.from_csr(selfcomm, M, M, ip, c, v)
     b = rng.random(M)
     xs = torch.zeros(M, dtype=torch.float64, device="cuda")
@@ -480,7 +413,7 @@ def _periodic_2d(oracle_mod, n):
     return ip, c, v * f[rows]
 
 
-ZMC_FORMS = [{}, {42: 1}, {41: 3}, {41: 1, 40: 1}, {41: 5, 42: 1, 40: 3}]
+ZMC_FORMS = [{}, {41: 3}, {41: 1, 40: 1}, {41: 5, 40: 3}]
 
 
 @pytest.mark.parametrize("form", range(len(ZMC_FORMS)))
