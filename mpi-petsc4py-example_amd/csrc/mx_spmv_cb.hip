@@ -17,7 +17,8 @@
 //     products in ascending column order through perm (the slot's pass-1
 //     position); a slice's products of one column block are contiguous in
 //     pass-1 order, so a wave's reads touch a line or two per block instead
-//     of one random sector per entry.
+//     of one random sector per entry.  The diagonal entries stay out of pass
+//     1: pass 2 forms a_ii * x_i from the diagonal and x, both coalesced.
 //
 // Every product is rounded once and every row is summed from 0.0 in
 // ascending column order, one rounding per add: the bits of MatMult_SeqAIJ
@@ -33,6 +34,7 @@ namespace {
 typedef double d2v __attribute__((ext_vector_type(2)));
 typedef int i2v __attribute__((ext_vector_type(2)));
 constexpr int CB_E = 4;   // pass 1: entries per thread per step (two 16-B value loads in flight)
+constexpr int32_t CB_DIAG = -2;   // perm: the row's diagonal entry (its product formed in pass 2)
 
 template <class T> __device__ __forceinline__ T ldnt(const T *p) { return __builtin_nontemporal_load(p); }
 
@@ -60,15 +62,16 @@ __global__ void __launch_bounds__(256) cb_far_kernel(int64_t m, const int64_t *_
 // CB_MAXBLK bins (the block size grows past 2^18 columns to keep it).
 constexpr int CB_MAXBLK = 64;
 __global__ void __launch_bounds__(256) cb_count_kernel(int64_t m, const int64_t *__restrict__ ptr,
-                                                       const int32_t *__restrict__ col, int bs, int nblk, int64_t ngrp,
-                                                       int64_t *__restrict__ cnt) {
+                                                       const int32_t *__restrict__ col, int64_t doff, int bs, int nblk,
+                                                       int64_t ngrp, int64_t *__restrict__ cnt) {
   __shared__ unsigned c[CB_MAXBLK];
   for (int64_t R = blockIdx.x; R < ngrp; R += gridDim.x) {
     if (threadIdx.x < CB_MAXBLK) c[threadIdx.x] = 0;
     __syncthreads();
     const int64_t r = R * 256 + threadIdx.x;
     if (r < m)
-      for (int64_t e = ptr[r]; e < ptr[r + 1]; ++e) atomicAdd(&c[(uint32_t)col[e] >> bs], 1u);
+      for (int64_t e = ptr[r]; e < ptr[r + 1]; ++e)
+        if (col[e] != r + doff) atomicAdd(&c[(uint32_t)col[e] >> bs], 1u);
     __syncthreads();
     if (threadIdx.x < nblk) cnt[(int64_t)threadIdx.x * ngrp + R] = c[threadIdx.x];
     __syncthreads();
@@ -77,7 +80,8 @@ __global__ void __launch_bounds__(256) cb_count_kernel(int64_t m, const int64_t 
 
 __global__ void __launch_bounds__(256) cb_place_kernel(int64_t m, int64_t nnz, const int64_t *__restrict__ ptr,
                                                        const int32_t *__restrict__ col, const double *__restrict__ val,
-                                                       int bs, int nblk, int64_t ngrp, const int64_t *__restrict__ base,
+                                                       int64_t doff, int bs, int nblk, int64_t ngrp,
+                                                       const int64_t *__restrict__ base,
                                                        int32_t *__restrict__ c1, double *__restrict__ v1,
                                                        int32_t *__restrict__ pinv, int64_t *__restrict__ bstart) {
   __shared__ int pre[CB_MAXBLK][256];
@@ -86,7 +90,8 @@ __global__ void __launch_bounds__(256) cb_place_kernel(int64_t m, int64_t nnz, c
     for (int b = 0; b < nblk; ++b) pre[b][t] = 0;
     const int64_t r = R * 256 + t;
     const int64_t e0 = r < m ? ptr[r] : 0, e1 = r < m ? ptr[r + 1] : 0;
-    for (int64_t e = e0; e < e1; ++e) pre[(uint32_t)col[e] >> bs][t] += 1;
+    for (int64_t e = e0; e < e1; ++e)
+      if (col[e] != r + doff) pre[(uint32_t)col[e] >> bs][t] += 1;
     __syncthreads();
     // per bin, the exclusive prefix over the group's rows: wave wv takes bins
     // wv, wv + 4, ...; lane l the rows 4 l .. 4 l + 3
@@ -107,6 +112,7 @@ __global__ void __launch_bounds__(256) cb_place_kernel(int64_t m, int64_t nnz, c
     __syncthreads();
     int pb = -1, k = 0;
     for (int64_t e = e0; e < e1; ++e) {
+      if (col[e] == r + doff) { pinv[e] = CB_DIAG; continue; }   // the diagonal: pass 2 forms it
       const int b = (int)((uint32_t)col[e] >> bs);
       k = b == pb ? k + 1 : 0;
       pb = b;
@@ -115,7 +121,7 @@ __global__ void __launch_bounds__(256) cb_place_kernel(int64_t m, int64_t nnz, c
       v1[pos] = val[e];
       pinv[e] = (int32_t)pos;
     }
-    if (R == 0 && t <= nblk) bstart[t] = t < nblk ? base[(int64_t)t * ngrp] : nnz;
+    if (R == 0 && t <= nblk) bstart[t] = t < nblk ? base[(int64_t)t * ngrp] : nnz;   // nnz: the pass-1 entries
     __syncthreads();
   }
 }
@@ -188,17 +194,26 @@ __global__ void __launch_bounds__(256) cb_prod_kernel(int nblk, const int64_t *_
 // one wave per slice; the row's products in ascending column order (batches
 // of 8 entries: every perm and product load of a batch in flight together),
 // then the mode's epilogue as the one-pass kernel has it (mx_spmv.hip finish)
-template <int MODE>
+template <int MODE, bool SC>
 __global__ void __launch_bounds__(256) cb_sum_kernel(int64_t m, int64_t nslices, const int64_t *__restrict__ sptr,
                                                      const int32_t *__restrict__ wid, const int32_t *__restrict__ perm,
                                                      const double *__restrict__ prod, const double *__restrict__ x,
-                                                     double *__restrict__ y, const Jac jac, double *__restrict__ partials,
+                                                     const double *__restrict__ diag, int64_t doff,
+                                                     const double *__restrict__ xscale, double *__restrict__ y,
+                                                     const Jac jac, double *__restrict__ partials,
                                                      const int *__restrict__ done, const Fold fold) {
   if (done && *done) return;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const double xs = SC ? *xscale : 1.0;
   double dot = 0.0;
   for (int64_t s = (int64_t)blockIdx.x * 4 + wv; s < nslices; s += (int64_t)gridDim.x * 4) {
+    // the diagonal entry's product (CB_DIAG in perm): a_ii * x_i from the
+    // diagonal and x itself, coalesced, instead of through pass 1 -- the
+    // same single rounding (of the scaled operand first, as pass 1 has it)
+    const int64_t rd = min(s * SLICE + lane, m - 1);
+    const double xd = x[rd + doff];
+    const double dprod = diag[rd] * (SC ? xs * xd : xd);
     const int w = wid[s];
     const int np = w >> 1;
     const bool odd = (w & 1) != 0;
@@ -222,15 +237,15 @@ __global__ void __launch_bounds__(256) cb_sum_kernel(int64_t m, int64_t nslices,
       for (int q = 0; q < 8; ++q) t[q] = prod[c[q] >= 0 ? c[q] : 0];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const double u = sum + t[q];
-        sum = c[q] >= 0 ? u : sum;
+        const double u = sum + (c[q] == CB_DIAG ? dprod : t[q]);
+        sum = (c[q] >= 0 || c[q] == CB_DIAG) ? u : sum;
       }
     }
     const int64_t row = s * SLICE + lane;
     if (row < m) {
       const double out = spmv_jac(MODE) ? papply(jac, sum, row) : sum;   // PCApply_Jacobi fused: w_i * d_i
       y[row] = out;
-      if (MODE == SPMV_DOT) dot += x[row] * sum;                          // VecDot(p, w) partial, p = x
+      if (MODE == SPMV_DOT) dot += x[row] * sum;                          // VecDot(p, w) partial, p = x (SC: never)
     }
   }
   if constexpr (MODE == SPMV_DOT) {
@@ -262,12 +277,16 @@ int cb_launch(Mat *A, int mode, const double *x, double *y, const Jac &jac, doub
   Fold fold = fold_in;
   if (fold.cnt) { fold.ntotal = fold.ncount = g2; fold.base = 0; }
   note_dispatch(DSP_CB);
-#define CBS(MD) cb_sum_kernel<MD><<<g2, 256, 0, st>>>(A->m, S.nslices, S.sptr.p, S.width.p, S.cb_perm.p, S.cb_prod.p, \
-                                                     x, y, jac, partials, done, fold)
+  const int64_t doff = A->rstart - A->cstart;   // A_d's column of row r's diagonal: r + doff
+#define CBS(MD, SCL) cb_sum_kernel<MD, SCL><<<g2, 256, 0, st>>>(A->m, S.nslices, S.sptr.p, S.width.p, S.cb_perm.p, \
+                                                               S.cb_prod.p, x, A->diag.p, doff, xscale, y, jac, partials, \
+                                                               done, fold)
   switch (mode) {
-    case SPMV_PLAIN: case SPMV_PLAIN_S: CBS(SPMV_PLAIN); break;
-    case SPMV_JACOBI: case SPMV_JACOBI_S: CBS(SPMV_JACOBI); break;
-    case SPMV_DOT: CBS(SPMV_DOT); break;
+    case SPMV_PLAIN: CBS(SPMV_PLAIN, false); break;
+    case SPMV_PLAIN_S: CBS(SPMV_PLAIN, true); break;
+    case SPMV_JACOBI: CBS(SPMV_JACOBI, false); break;
+    case SPMV_JACOBI_S: CBS(SPMV_JACOBI, true); break;
+    case SPMV_DOT: CBS(SPMV_DOT, false); break;
     default: fail(MX_ERR_INTERNAL, "column-block MatMult: unsupported mode");
   }
 #undef CBS
@@ -306,18 +325,20 @@ void build_cb(Mat *A, hipStream_t st) {
   const int64_t ngrp = cdiv(m, 256);
   DBuf<int64_t> cnt((size_t)nblk * (size_t)ngrp, kScratch);
   DBuf<int32_t> pinv((size_t)nnz, kScratch);
-  cb_count_kernel<<<(unsigned)std::min<int64_t>(ngrp, 16384), 256, 0, st>>>(m, A->dptr.p, A->dcol.p, bs, nblk, ngrp,
-                                                                          cnt.p);
+  const int64_t doff = A->rstart - A->cstart;
+  cb_count_kernel<<<(unsigned)std::min<int64_t>(ngrp, 16384), 256, 0, st>>>(m, A->dptr.p, A->dcol.p, doff, bs, nblk,
+                                                                          ngrp, cnt.p);
   HIPCHECK(hipGetLastError());
-  exclusive_scan_i64(cnt.p, cnt.p, (int64_t)nblk * ngrp, st, nullptr);
+  int64_t nnz1 = 0;   // the off-diagonal entries (pass 1)
+  exclusive_scan_i64(cnt.p, cnt.p, (int64_t)nblk * ngrp, st, &nnz1);
   S.cb_col.alloc((size_t)nnz);
   S.cb_val.alloc((size_t)nnz);
   S.cb_prod.alloc((size_t)nnz);
   S.cb_bstart.alloc((size_t)nblk + 1);
   S.cb_perm.alloc((size_t)std::max<int64_t>(S.slots, 1));
-  cb_place_kernel<<<(unsigned)std::min<int64_t>(ngrp, 16384), 256, 0, st>>>(m, nnz, A->dptr.p, A->dcol.p, A->dval.p, bs,
-                                                                          nblk, ngrp, cnt.p, S.cb_col.p, S.cb_val.p,
-                                                                          pinv.p, S.cb_bstart.p);
+  cb_place_kernel<<<(unsigned)std::min<int64_t>(ngrp, 16384), 256, 0, st>>>(m, nnz1, A->dptr.p, A->dcol.p, A->dval.p,
+                                                                          doff, bs, nblk, ngrp, cnt.p, S.cb_col.p,
+                                                                          S.cb_val.p, pinv.p, S.cb_bstart.p);
   HIPCHECK(hipGetLastError());
   HIPCHECK(hipMemsetAsync(S.cb_perm.p, 0xFF, sizeof(int32_t) * (size_t)std::max<int64_t>(S.slots, 1), st));
   cb_perm_kernel<<<grid_for(m, 256, 8192), 256, 0, st>>>(m, A->dptr.p, S.sptr.p, S.width.p, pinv.p, S.cb_perm.p);
@@ -329,7 +350,7 @@ void build_cb(Mat *A, hipStream_t st) {
 
 void load_code_spmv_cb() {
   hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&cb_sum_kernel<SPMV_PLAIN>));
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&cb_sum_kernel<SPMV_PLAIN, false>));
   (void)hipGetLastError();
 }
 
