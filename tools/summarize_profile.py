@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short(name):
     """'void mx::spmv_sell_kernel<3, true, 7, false>(long, ...)' -> 'spmv_sell_kernel<3,true,7,false>'."""
-    n = re.sub(r"^void\s+", "", name)
+    n = re.sub(r"^void\s+", "", name).replace("(anonymous namespace)::", "")
     n = n.split("(")[0].replace("mx::", "").replace(" ", "")
     return n
 
