@@ -355,7 +355,7 @@ int mx_mat_get_info(mx_mat a, mx_mat_info *info) {
     info->pair_form27 = A->sd.pair_shape == 27 && pair_lean_kind(A)
                             ? (pair_lean_kind(A) == 2 ? (A->sd.pcol27.p ? 2 : 1) : 0) : -1;
     info->pair_code = pair_code_applies(A) && (A->nghost == 0 || matmult_splits(A)) ? 1 : 0;
-    info->cb_blocks = A->sd.cb_nblk;
+    info->cb_blocks = (A->nghost == 0 || matmult_splits(A)) ? A->sd.cb_nblk : 0;   // where it runs (cb_applies)
   });
 }
 

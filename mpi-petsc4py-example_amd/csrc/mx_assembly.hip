@@ -2278,7 +2278,7 @@ Mat *assemble(Comm *c, int64_t M, int64_t N, int64_t m_local, int64_t n_local,
   build_sell(A->so, m, A->nghost, A->optr.p, A->ocol.p, A->oval.p, st, false);
   build_value_codes(A->sd, A->so.nslices ? A->so.width.p : nullptr, m, A->n, st, vd);
   build_pair_f64(A->sd, m, A->n, A->so.nslices ? A->so.width.p : nullptr, st);
-  if (!multi) build_cb(A.get(), st);   // unstructured blocks: the column-block MatMult
+  build_cb(A.get(), st);   // unstructured blocks: the column-block MatMult
   A->partials.alloc((size_t)std::max(spmv_blocks(A.get()) + 64, RED_BLOCKS) * 4 + 64);
   HIPCHECK(hipStreamSynchronize(st));
   const double t_layout = wall_ms();

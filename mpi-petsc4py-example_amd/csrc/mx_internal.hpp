@@ -520,8 +520,8 @@ void mat_mult(Mat *A, const double *x, double *y);
 // unstructured one-rank blocks; cb_launch returns the pass-2 grid (partials)
 void build_cb(Mat *A, hipStream_t st);
 bool cb_applies(const Mat *A, int mode, bool split);
-int cb_launch(Mat *A, int mode, const double *x, double *y, const Jac &jac, double *partials, const int *done,
-              const Fold &fold, const double *xscale, hipStream_t st);
+int cb_launch(Mat *A, int mode, bool split, const double *x, double *y, const Jac &jac, double *partials,
+              const int *done, const Fold &fold, const double *xscale, hipStream_t st);
 
 // vector kernels (mx_vec.hip)
 constexpr int RED_BLOCKS = 1024;   // fixed grid of the reduction kernels

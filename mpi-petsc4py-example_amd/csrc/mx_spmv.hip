@@ -858,7 +858,7 @@ static int launch_main(Mat *A, const double *x, double *y, int mode, Jac jac, do
   // coded z-march for non-uniform code dictionaries (every non-CG mode,
   // GMRES's scaled operand included)
   if (!cgp) {
-    if (cb_applies(A, mode, split)) return cb_launch(A, mode, x, y, jac, partials, done_flag, fold_in, xscale, st);
+    if (cb_applies(A, mode, split)) return cb_launch(A, mode, split, x, y, jac, partials, done_flag, fold_in, xscale, st);
     const int lg = pair_lean_launch(A, mode, split, x, y, partials, done_flag, fold_in, st, jac, xscale);
     if (lg) return lg;
   }

@@ -23,7 +23,7 @@
 // Every product is rounded once and every row is summed from 0.0 in
 // ascending column order, one rounding per add: the bits of MatMult_SeqAIJ
 // and of the one-pass kernel (tests/test_gpu_cb.py).  Built at assembly for
-// one-rank general SELL blocks whose entries mostly lie far from the
+// general SELL diagonal blocks whose entries mostly lie far from the
 // diagonal (build_cb, a counting placement: no sort); key 84 selects it.
 #include "mx_device.hpp"
 #include "mx_internal.hpp"
@@ -194,9 +194,13 @@ __global__ void __launch_bounds__(256) cb_prod_kernel(int nblk, const int64_t *_
 // one wave per slice; the row's products in ascending column order (batches
 // of 8 entries: every perm and product load of a batch in flight together),
 // then the mode's epilogue as the one-pass kernel has it (mx_spmv.hip finish)
-template <int MODE, bool SC>
+// SPLIT (P > 1 with ghost entries): a slice with A_o entries (wid_o) stores
+// its rows' diagonal-block sums; the halo-boundary kernel continues them over
+// A_o once the halo has arrived and applies the epilogue (mx_spmv.hip)
+template <int MODE, bool SC, bool SPLIT>
 __global__ void __launch_bounds__(256) cb_sum_kernel(int64_t m, int64_t nslices, const int64_t *__restrict__ sptr,
-                                                     const int32_t *__restrict__ wid, const int32_t *__restrict__ perm,
+                                                     const int32_t *__restrict__ wid, const int32_t *__restrict__ wid_o,
+                                                     const int32_t *__restrict__ perm,
                                                      const double *__restrict__ prod, const double *__restrict__ x,
                                                      const double *__restrict__ diag, int64_t doff,
                                                      const double *__restrict__ xscale, double *__restrict__ y,
@@ -242,6 +246,10 @@ __global__ void __launch_bounds__(256) cb_sum_kernel(int64_t m, int64_t nslices,
       }
     }
     const int64_t row = s * SLICE + lane;
+    if (SPLIT && wid_o[s]) {
+      if (row < m) y[row] = sum;
+      continue;
+    }
     if (row < m) {
       const double out = spmv_jac(MODE) ? papply(jac, sum, row) : sum;   // PCApply_Jacobi fused: w_i * d_i
       y[row] = out;
@@ -255,14 +263,17 @@ __global__ void __launch_bounds__(256) cb_sum_kernel(int64_t m, int64_t nslices,
 }
 }  // namespace
 
+// one rank, or P > 1 when the product splits (the boundary kernel finishes
+// the rows with ghost entries); the inline A_o continuation stays with the
+// one-pass kernel
 bool cb_applies(const Mat *A, int mode, bool split) {
-  return A->sd.cb_nblk > 0 && g_knobs.cb != 0 && !split && A->nghost == 0 &&
+  return A->sd.cb_nblk > 0 && g_knobs.cb != 0 && (split || A->nghost == 0) &&
          (mode == SPMV_PLAIN || mode == SPMV_PLAIN_S || mode == SPMV_JACOBI || mode == SPMV_JACOBI_S ||
           mode == SPMV_DOT);
 }
 
-int cb_launch(Mat *A, int mode, const double *x, double *y, const Jac &jac, double *partials, const int *done,
-              const Fold &fold_in, const double *xscale, hipStream_t st) {
+int cb_launch(Mat *A, int mode, bool split, const double *x, double *y, const Jac &jac, double *partials,
+              const int *done, const Fold &fold_in, const double *xscale, hipStream_t st) {
   Sell &S = A->sd;
   const unsigned g1 = (unsigned)(2 * device_cu_count()) & ~7u;   // two workgroups per CU, a multiple of 8
   const bool sc = spmv_scaled(mode);
@@ -278,9 +289,9 @@ int cb_launch(Mat *A, int mode, const double *x, double *y, const Jac &jac, doub
   if (fold.cnt) { fold.ntotal = fold.ncount = g2; fold.base = 0; }
   note_dispatch(DSP_CB);
   const int64_t doff = A->rstart - A->cstart;   // A_d's column of row r's diagonal: r + doff
-#define CBS(MD, SCL) cb_sum_kernel<MD, SCL><<<g2, 256, 0, st>>>(A->m, S.nslices, S.sptr.p, S.width.p, S.cb_perm.p, \
-                                                               S.cb_prod.p, x, A->diag.p, doff, xscale, y, jac, partials, \
-                                                               done, fold)
+#define CBS2(MD, SCL, SPL) cb_sum_kernel<MD, SCL, SPL><<<g2, 256, 0, st>>>(A->m, S.nslices, S.sptr.p, S.width.p, \
+      A->so.width.p, S.cb_perm.p, S.cb_prod.p, x, A->diag.p, doff, xscale, y, jac, partials, done, fold)
+#define CBS(MD, SCL) do { if (split) CBS2(MD, SCL, true); else CBS2(MD, SCL, false); } while (0)
   switch (mode) {
     case SPMV_PLAIN: CBS(SPMV_PLAIN, false); break;
     case SPMV_PLAIN_S: CBS(SPMV_PLAIN, true); break;
@@ -290,6 +301,7 @@ int cb_launch(Mat *A, int mode, const double *x, double *y, const Jac &jac, doub
     default: fail(MX_ERR_INTERNAL, "column-block MatMult: unsupported mode");
   }
 #undef CBS
+#undef CBS2
   HIPCHECK(hipGetLastError());
   return g2;
 }
@@ -301,7 +313,7 @@ void build_cb(Mat *A, hipStream_t st) {
   Sell &S = A->sd;
   S.cb_nblk = 0;
   const int64_t m = A->m, nnz = A->nnz_d;
-  if (!g_knobs.cb || m < 64 || nnz < 1 || A->nghost != 0 || S.dia_slices != 0 || S.ntab != 0 || S.pair_shape != 0 ||
+  if (!g_knobs.cb || m < 64 || nnz < 1 || S.dia_slices != 0 || S.ntab != 0 || S.pair_shape != 0 ||
       nnz >= ((int64_t)1 << 31))
     return;
   if (g_knobs.cb == 1) {
@@ -350,7 +362,7 @@ void build_cb(Mat *A, hipStream_t st) {
 
 void load_code_spmv_cb() {
   hipFuncAttributes a;
-  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&cb_sum_kernel<SPMV_PLAIN, false>));
+  (void)hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&cb_sum_kernel<SPMV_PLAIN, false, false>));
   (void)hipGetLastError();
 }
 

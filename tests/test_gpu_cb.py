@@ -137,3 +137,76 @@ def test_cb_auto_choice(selfcomm):
     S = DMat.stencil(selfcomm, "poisson3d", 128, 128, 64)
     assert S.info()["cb_blocks"] == 0
     S.destroy()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_cb_ranks_split(oracle_mod, P):
+    """P in-process ranks: each rank's diagonal block takes the column-block
+    MatMult, the rows with ghost entries are finished by the halo-boundary
+    kernel.  MatMult bit-exact against the oracle; GMRES(30) + Jacobi bit for
+    bit the one-pass run (key 84 = 0), its and reason the oracle's."""
+    from mxsolve.core import LocalWorld, DMat
+    N = 1 << 12
+    ip, c, v = _random_csr(N, 7, 23)
+    ranges = oracle_mod.split_ownership(N, P)
+    xh = np.random.default_rng(8).standard_normal(N)
+    b = np.random.default_rng(4).random(N)
+    # MatMult_MPIAIJ order: the diagonal block's sum, then the ghost block's
+    O = oracle_mod.OracleMat.from_csr(N, N, ip, c, v, P=P)
+    yo = O.mult(xh)
+
+    def body(comm):
+        r0, r1 = ranges[comm.rank], ranges[comm.rank + 1]
+        lip = ip[r0:r1 + 1] - ip[r0]
+        A = DMat.from_csr(comm, N, N, lip, c[ip[r0]:ip[r1]], v[ip[r0]:ip[r1]])
+        cbk = A.info()["cb_blocks"]
+        y = comm.empty(r1 - r0)
+        A.mult(torch.from_numpy(xh[r0:r1].copy()).cuda(), y)
+        x = comm.zeros(r1 - r0)
+        res = A.solve(torch.from_numpy(b[r0:r1].copy()).cuda(), x, ksp="gmres", pc="jacobi", history=True)
+        A.destroy()
+        return cbk, y.cpu().numpy(), res["its"], res["reason"], res["history"], x.cpu().numpy()
+
+    outs = {}
+    for cb in (2, 0):
+        old = _knob(84, cb)           # set once, outside the rank threads
+        w = LocalWorld(P)
+        try:
+            outs[cb] = w.run(body)
+        finally:
+            _knob(84, old)
+            w.destroy()
+    assert all(o[0] > 0 for o in outs[2]) and all(o[0] == 0 for o in outs[0])
+    y = np.concatenate([o[1] for o in outs[2]])
+    assert np.array_equal(y.view(np.uint64), yo.view(np.uint64))
+    for a, z in zip(outs[2], outs[0]):
+        assert (a[2], a[3]) == (z[2], z[3])
+        assert np.array_equal(a[4].view(np.uint64), z[4].view(np.uint64))
+        assert np.array_equal(a[5].view(np.uint64), z[5].view(np.uint64))
+    o = O.solve(b, ksp="gmres", pc="jacobi")
+    x = np.concatenate([a[5] for a in outs[2]])
+    assert (outs[2][0][2], outs[2][0][3]) == (o["its"], o["reason"])
+    assert np.linalg.norm(x - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
+
+
+def test_cb_rows_without_diagonal(selfcomm, oracle_mod):
+    """Rows that hold entries but no diagonal, and explicit zeros on the
+    diagonal: the pass-2 diagonal products only where a diagonal entry is."""
+    N = 1 << 12
+    ip, c, v = _random_csr(N, 6, 31)
+    keep = np.ones(c.size, bool)
+    rows = np.repeat(np.arange(N), np.diff(ip))
+    keep[(c == rows) & (rows % 5 == 0)] = False        # every fifth row loses its diagonal
+    v = v.copy()
+    v[(c == rows) & (rows % 7 == 0)] = 0.0             # an explicit zero diagonal
+    c2, v2 = c[keep], v[keep]
+    ip2 = np.zeros(N + 1, np.int64)
+    np.cumsum(np.bincount(rows[keep], minlength=N), out=ip2[1:])
+    A = _mat(selfcomm, N, ip2, c2, v2, 2)
+    assert A.info()["cb_blocks"] > 0
+    xh = np.random.default_rng(12).standard_normal(N)
+    y = selfcomm.empty(N)
+    A.mult(torch.from_numpy(xh).cuda(), y)
+    yo = oracle_mod.OracleMat.from_csr(N, N, ip2, c2, v2).mult(xh)
+    assert np.array_equal(y.cpu().numpy().view(np.uint64), yo.view(np.uint64))
+    A.destroy()
