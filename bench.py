@@ -483,7 +483,7 @@ def spmv_random_leg(comm, lg: int = 24) -> dict:
     kinds = [k for k, v in dispatch_counts().items() if v]
     yref = csr_rowsum_reference(ip, cj, vv, xh)
     bitexact = bool(np.array_equal(y.cpu().numpy().view(np.uint64), yref.view(np.uint64)))
-    del ip, cj, vv, yref, xh
+    del yref, xh
     warm_ms, _ = A.bench_mult(xt, y, 50)
     flush = torch.empty(1 << 27, dtype=torch.float64, device=y.device)
     cold_kernel_ms, cold_ms = A.bench_mult_cold(xt, y, flush, 5)
@@ -514,8 +514,36 @@ def spmv_random_leg(comm, lg: int = 24) -> dict:
            "traffic": traffic.get("bytes_per_launch") if traffic else None,
            "traffic_ratio_vs_sector": round(traffic["bytes_per_launch"] / sector, 3) if traffic else None,
            "traffic_source": traffic.get("source") if traffic else None}
+    # test.py:12-17's solve on this family: GMRES(30) + Jacobi, a fixed 60
+    # iterations (two restart cycles, rtol 0), through the column-block MatMult
+    # and through the one-pass SELL kernel (key 84 = 0, reassembled)
+    from mxsolve import _lib
+    from mxsolve.core import rhs_hash
+    b = comm.empty(m)
+    rhs_hash(comm, 0, b)
+
+    def gmres_rate(M):
+        x = comm.zeros(m)
+        M.solve(b, x, ksp="gmres", pc="jacobi", rtol=0.0, max_it=30)   # KSPSetUp, graph capture
+        x.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = M.solve(b, x, ksp="gmres", pc="jacobi", rtol=0.0, max_it=60)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        return {"its": r["its"], "its_per_s": round(r["its"] / dt, 1), "ms_per_it": round(dt * 1e3 / r["its"], 4)}
+
+    out["gmres30_jacobi"] = {"column_block": gmres_rate(A)}
     A.destroy()
-    del xt, y
+    L = _lib.load()
+    old = L.mx_debug_set(84, 0)
+    try:
+        B = DMat.from_csr(comm, N, N, ip, cj, vv)
+    finally:
+        L.mx_debug_set(84, old)
+    out["gmres30_jacobi"]["one_pass"] = gmres_rate(B)
+    B.destroy()
+    del ip, cj, vv, xt, y, b
     torch.cuda.empty_cache()
     return out
 

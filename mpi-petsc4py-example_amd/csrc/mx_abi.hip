@@ -144,34 +144,45 @@ int mx_layout_split(int64_t N, int P, int64_t *ranges) {
   });
 }
 
-// Host-to-device copy of a caller's (pageable) array for createAIJ(csr=...):
-// chunks of 64 MiB are page-locked in place (hipHostRegister) and copied, each
-// unregistered once its copy is done.  Registration runs ahead on H2D_REG_THREADS
-// host threads (a chunk of fresh numpy pages takes longer to lock than its
-// DMA) while the calling thread issues the copies in order, so the copy engine
-// streams at the pinned rate: 55.7 GB/s on the 1.47 GB 256^3 payload, against
-// 38-49 GB/s for the runtime's staged pageable copy and 25 GB/s registering
-// the whole payload first (tools/h2d_pin_probe.hip, tools/h2d_lib_probe.py).
+// Host-to-device copy of a caller's (pageable) arrays for createAIJ(csr=...):
+// indptr, cols and vals go through ONE pipeline of chunks.  Each chunk is
+// page-locked in place (hipHostRegister), copied, and unregistered once its
+// copy is done.  Registration runs ahead on H2D_REG_THREADS host threads (a
+// chunk of fresh numpy pages takes longer to lock than its DMA) while the
+// calling thread issues the copies in order.  Chunk sizes ramp from 4 MiB to
+// 64 MiB, so the first copy starts after a 4 MiB registration (0.25 ms)
+// rather than a 64 MiB one (4 ms); one pipeline over the three arrays avoids
+// a drain and a ramp per array (tools/h2d_pin_probe.hip, tools/h2d_lib_probe.py).
 // A chunk whose registration fails (memory already pinned, a page shared with
-// another registration) is copied as it is.  Small arrays: one plain copy.
+// another registration) is copied as it is; arrays under 1 MiB: plain copies.
+struct H2dSeg { void *dst; const void *src; size_t bytes; };
 constexpr int H2D_REG_THREADS = 4;
-static void h2d_pinned(void *dst, const void *src, size_t bytes, hipStream_t st) {
-  constexpr size_t CH = (size_t)64 << 20, PAGE = 4096;
-  if (bytes < 2 * CH) {
-    HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
-    return;
+static void h2d_pinned(const std::vector<H2dSeg> &segs, hipStream_t st) {
+  constexpr size_t CH0 = (size_t)4 << 20, CH = (size_t)64 << 20, SMALL = (size_t)1 << 20, PAGE = 4096;
+  struct Cut { char *dst; uintptr_t a, b; bool pin; };
+  std::vector<Cut> cuts;
+  size_t k = 0;    // pinned chunks cut so far (the ramp)
+  for (const H2dSeg &g : segs) {
+    if (!g.bytes) continue;
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(g.src), s1 = s0 + g.bytes;
+    if (g.bytes < SMALL) { cuts.push_back({static_cast<char *>(g.dst), s0, s1, false}); continue; }
+    // chunk boundaries on page boundaries, so no page is registered twice
+    for (uintptr_t a = s0; a < s1; ++k) {
+      const size_t len = std::min(CH, CH0 << std::min<size_t>(k, 4));
+      const uintptr_t b = std::min(s1, (a & ~(uintptr_t)(PAGE - 1)) + len);
+      cuts.push_back({static_cast<char *>(g.dst) + (a - s0), a, b, true});
+      a = b;
+    }
   }
-  // chunk boundaries on page boundaries, so no page is registered twice
-  const uintptr_t s0 = reinterpret_cast<uintptr_t>(src), s1 = s0 + bytes;
-  struct Chunk { uintptr_t a, b, reg; size_t reg_len; std::atomic<int> state{0}; hipEvent_t ev = nullptr; };  // 0 pending, 1 pinned, 2 not pinned
-  std::vector<uintptr_t> cuts{s0};
-  while (cuts.back() < s1) cuts.push_back(std::min(s1, (cuts.back() & ~(uintptr_t)(PAGE - 1)) + CH));
-  const size_t n = cuts.size() - 1;
+  struct Chunk { char *dst; uintptr_t a, b, reg; size_t reg_len; bool pin; std::atomic<int> state{0}; hipEvent_t ev = nullptr; };  // 0 pending, 1 pinned, 2 not pinned
+  const size_t n = cuts.size();
   std::vector<Chunk> ch(n);
   for (size_t i = 0; i < n; ++i) {
-    ch[i].a = cuts[i]; ch[i].b = cuts[i + 1];
-    ch[i].reg = cuts[i] & ~(uintptr_t)(PAGE - 1);
-    ch[i].reg_len = ((cuts[i + 1] + PAGE - 1) & ~(uintptr_t)(PAGE - 1)) - ch[i].reg;
+    Chunk &c = ch[i];
+    c.dst = cuts[i].dst; c.a = cuts[i].a; c.b = cuts[i].b; c.pin = cuts[i].pin;
+    c.reg = c.a & ~(uintptr_t)(PAGE - 1);
+    c.reg_len = ((c.b + PAGE - 1) & ~(uintptr_t)(PAGE - 1)) - c.reg;
+    if (!c.pin) c.state.store(2);
   }
   std::atomic<bool> stop{false};
   std::vector<std::thread> reg;
@@ -179,6 +190,7 @@ static void h2d_pinned(void *dst, const void *src, size_t bytes, hipStream_t st)
   for (int t = 0; t < nt; ++t)
     reg.emplace_back([&, t] {
       for (size_t i = (size_t)t; i < n && !stop.load(); i += (size_t)nt) {
+        if (!ch[i].pin) continue;   // small: a plain copy
         const bool ok = hipHostRegister(reinterpret_cast<void *>(ch[i].reg), ch[i].reg_len, hipHostRegisterDefault) == hipSuccess;
         ch[i].state.store(ok ? 1 : 2, std::memory_order_release);
       }
@@ -195,11 +207,11 @@ static void h2d_pinned(void *dst, const void *src, size_t bytes, hipStream_t st)
     (void)hipGetLastError();   // failed registrations
   };
   try {
-    size_t done = 0;   // chunks unregistered
+    size_t done = 0;   // chunks released
     for (size_t i = 0; i < n; ++i) {
       while (ch[i].state.load(std::memory_order_acquire) == 0) std::this_thread::yield();
-      HIPCHECK(hipMemcpyAsync(static_cast<char *>(dst) + (ch[i].a - s0), reinterpret_cast<const void *>(ch[i].a),
-                              ch[i].b - ch[i].a, hipMemcpyHostToDevice, st));
+      HIPCHECK(hipMemcpyAsync(ch[i].dst, reinterpret_cast<const void *>(ch[i].a), ch[i].b - ch[i].a,
+                              hipMemcpyHostToDevice, st));
       HIPCHECK(hipEventCreateWithFlags(&ch[i].ev, hipEventDisableTiming));
       HIPCHECK(hipEventRecord(ch[i].ev, st));
       for (; done + 2 < i + 1; ++done) {   // two chunks in flight: release the older ones
@@ -258,13 +270,13 @@ int mx_mat_create_csr(mx_comm c, int64_t Mg, int64_t Ng, int64_t m_local, int64_
       DBuf<char> stage((size_t)(m + 1) * indptr_bytes + 8, kScratch);
       t_copy = wall_ms();   // the copy phase starts once its buffers exist
       g_asm_times.alloc_ms = t_copy - t0;
-      h2d_pinned(stage.p, indptr, (size_t)(m + 1) * indptr_bytes, st);
-      convert_index(stage.p, indptr_bytes, m + 1, ip.p, st);
+      std::vector<H2dSeg> segs{{stage.p, indptr, (size_t)(m + 1) * indptr_bytes}};
       if (nnz) {
-        void *cdst = c32 ? (void *)cl32.p : (void *)cl.p;
-        h2d_pinned(cdst, cols, (size_t)nnz * col_bytes, st);
-        h2d_pinned(vl.p, vals, sizeof(double) * nnz, st);
+        segs.push_back({c32 ? (void *)cl32.p : (void *)cl.p, cols, (size_t)nnz * col_bytes});
+        segs.push_back({vl.p, vals, sizeof(double) * nnz});
       }
+      h2d_pinned(segs, st);
+      convert_index(stage.p, indptr_bytes, m + 1, ip.p, st);
       HIPCHECK(hipStreamSynchronize(st));
     }
     HIPCHECK(hipStreamSynchronize(st));
@@ -698,3 +710,28 @@ int mx_ksp_solve(mx_mat a, const mx_ksp_params *p, const double *b, double *x, m
 }
 
 }  // extern "C"
+
+namespace mx {
+// The process's first pipelined copy (threads registering chunks while copies
+// run) is ~1 ms slower on 1.47 GB than later ones; the first pinned transfer
+// alone costs ~8 ms more.  Paid once at initialisation (load_code_objects) on
+// a 32 MiB buffer: four chunks (4, 8, 16, 4 MiB) on the four registration
+// threads (tools/h2d_sweep.py, profiles/r06w_h2d_*.txt).
+void h2d_warm() {
+  constexpr size_t W = (size_t)32 << 20;
+  char *h = static_cast<char *>(std::aligned_alloc(4096, W));
+  void *d = nullptr;
+  hipStream_t st = nullptr;
+  if (h && hipMalloc(&d, W) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
+    std::memset(h, 0, W);
+    try {
+      h2d_pinned({{d, h, W}}, st);
+    } catch (const Error &) {
+    }
+  }
+  if (st) (void)hipStreamDestroy(st);
+  if (d) (void)hipFree(d);
+  std::free(h);
+  (void)hipGetLastError();
+}
+}  // namespace mx

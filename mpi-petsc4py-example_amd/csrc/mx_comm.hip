@@ -553,27 +553,11 @@ void load_code_comm() {
 }
 
 void load_code_objects() {
-  // the runtime's first pinned host-to-device copy carries a one-time cost
-  // (~8 ms; createAIJ from host arrays page-locks them, mx_abi.hip
-  // h2d_pinned): paid here, at initialisation, once per process
+  // the one-time costs of the first pinned, pipelined host-to-device copy
+  // (createAIJ from host arrays: mx_abi.hip h2d_pinned), paid at
+  // initialisation once per process
   static std::once_flag once;
-  std::call_once(once, [] {
-    // one registered 16 MiB copy: the first pinned host-to-device transfer of
-    // a process is the slow one, not the first registration alone
-    constexpr size_t W = (size_t)16 << 20;
-    char *h = static_cast<char *>(std::aligned_alloc(4096, W));
-    void *d = nullptr;
-    if (h && hipMalloc(&d, W) == hipSuccess) {
-      std::memset(h, 0, W);
-      if (hipHostRegister(h, W, hipHostRegisterDefault) == hipSuccess) {
-        if (hipMemcpy(d, h, W, hipMemcpyHostToDevice) != hipSuccess) (void)hipGetLastError();
-        (void)hipHostUnregister(h);
-      }
-      (void)hipFree(d);
-    }
-    std::free(h);
-    (void)hipGetLastError();
-  });
+  std::call_once(once, [] { h2d_warm(); });
   load_code_comm();
   load_code_vec();
   load_code_assembly();

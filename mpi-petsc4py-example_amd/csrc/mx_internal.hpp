@@ -575,5 +575,7 @@ void load_code_spmv_cb();
 void load_code_ksp();
 void load_code_direct();
 void load_code_objects();
+// the first pinned, pipelined host-to-device copy's one-time costs (mx_abi.hip)
+void h2d_warm();
 
 }  // namespace mx

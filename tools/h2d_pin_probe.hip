@@ -6,7 +6,7 @@
 //              runs (register + copy overlapped), each unregistered after.
 // Times are host wall clock around the whole operation, median of reps.
 //   hipcc --offload-arch=gfx950 -O2 tools/h2d_pin_probe.hip -o tools/h2d_pin_probe
-//   tools/h2d_pin_probe [MB] [chunk_MB] [reps] [fresh 0/1]
+//   tools/h2d_pin_probe [MB] [chunk_MB] [reps] [fresh 0/1] [copy streams]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,8 +28,10 @@ int main(int argc, char **argv) {
   std::memset(h, 1, bytes);   // the caller's arrays exist (touched) before createAIJ
   void *d;
   CK(hipMalloc(&d, bytes));
-  hipStream_t s;
+  hipStream_t s, s2[4];
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const int ns = argc > 5 ? std::max(1, std::min(4, std::atoi(argv[5]))) : 1;   // pipelined copies round-robin over ns streams
+  for (auto &q : s2) CK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
   auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
   std::vector<double> tp, tr, treg, tcp, tun, tpipe;
   const bool fresh = argc > 4 && std::atoi(argv[4]) != 0;   // a new (touched) host buffer every rep
@@ -62,14 +64,16 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < nch; ++i) {
       const size_t off = i * chunk, len = std::min(chunk, bytes - off);
       CK(hipHostRegister(h + off, len, hipHostRegisterDefault));
-      CK(hipMemcpyAsync(static_cast<char *>(d) + off, h + off, len, hipMemcpyHostToDevice, s));
-      CK(hipEventRecord(ev[i], s));
+      hipStream_t q = ns == 1 ? s : s2[i % ns];
+      CK(hipMemcpyAsync(static_cast<char *>(d) + off, h + off, len, hipMemcpyHostToDevice, q));
+      CK(hipEventRecord(ev[i], q));
       if (i >= 2) {   // keep two chunks in flight; release the one before
         CK(hipEventSynchronize(ev[i - 2]));
         CK(hipHostUnregister(h + (i - 2) * chunk));
       }
     }
     CK(hipStreamSynchronize(s));
+    for (auto &q : s2) CK(hipStreamSynchronize(q));
     for (size_t i = nch >= 2 ? nch - 2 : 0; i < nch; ++i) CK(hipHostUnregister(h + i * chunk));
     tpipe.push_back(now() - t0);
     std::printf("rep %d: pageable %.1f ms, register+copy %.1f ms, pipelined %.1f ms\n", r, tp.back() * 1e3,
@@ -77,7 +81,7 @@ int main(int argc, char **argv) {
     for (auto &e : ev) CK(hipEventDestroy(e));
   }
   const double gb = bytes / 1e9;
-  std::printf("payload %.2f GB, chunk %zu MB\n", gb, chunk >> 20);
+  std::printf("payload %.2f GB, chunk %zu MB, %d copy stream(s)\n", gb, chunk >> 20, ns);
   std::printf("pageable copy           %7.1f ms  %5.1f GB/s\n", med(tp) * 1e3, gb / med(tp));
   std::printf("register + copy + unreg %7.1f ms  %5.1f GB/s  (register %.1f, copy %.1f = %.1f GB/s, unregister %.1f ms)\n",
               med(tr) * 1e3, gb / med(tr), med(treg) * 1e3, med(tcp) * 1e3, gb / med(tcp), med(tun) * 1e3);
