@@ -909,13 +909,26 @@ __global__ void __launch_bounds__(256) mdot_chunk_kernel(int64_t n, const double
 // column (hh[k][j] = 0 - (-h_j)) and the non-finite check, evaluated by every
 // workgroup (workgroup 0 commits), then VecMAXPY_Seq's grouping (first nv%4
 // vectors, then groups of four) and ||w||^2, folded in-launch (fold.cnt) or
-// as plain partials
+// as plain partials.
+// Chunk form, as mdot_chunk_kernel: a workgroup holds 512 MAXPY_WP rows of w
+// in registers and walks the basis vectors one at a time, a contiguous piece
+// of each, the next vector's loads issued before the current one's products.
+// A group's terms gather in a per-row accumulator g (g = a_j v_j, g = g +
+// a_j v_j, then u = u + g): each row's expression is VecMAXPY_Seq's,
+// u + (((a0 v0 + a1 v1) + a2 v2) + a3 v3), bit for bit.  The one-row-per-lane
+// form read all k + 2 vectors at once across the chip and fell from 0.85 of
+// peak at k = 2 to 0.73 at k = 29 (C4 256^3, profiles/r06o); MDot's walk
+// holds 0.80 there.
+#ifndef MAXPY_WP
+#define MAXPY_WP 8
+#endif
 __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__restrict__ w,
                                                          const double *__restrict__ V, int64_t ldv, int nv,
                                                          KspState *__restrict__ s, const double *__restrict__ red_k,
                                                          const double *__restrict__ vscale,
                                                          double *__restrict__ hh, int ld,
                                                          double *__restrict__ partials, const Fold fold) {
+  constexpr int WP = MAXPY_WP;
   if (s->inner_stop) return;
   __shared__ double a[MAX_RESTART + 1], sc[MAX_RESTART + 1];
   __shared__ int bad;
@@ -936,20 +949,71 @@ __global__ void __launch_bounds__(256) maxpy_norm_kernel(int64_t n, double *__re
     for (int j = threadIdx.x; j < nv; j += 256) hh[(size_t)(nv - 1) * ld + j] = 0.0 - a[j];
   const int rem = nv & 3;
   double v[1] = {0.0};
-  {
-    const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-      double u = w[i];
-      int j = 0;
-      auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
-      if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
-      else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
-      else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
-      for (; j < nv; j += 4)
-        u = u + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
-      w[i] = u;
-      v[0] += u * u;
+  dbl2 *__restrict__ w2 = reinterpret_cast<dbl2 *>(w);
+  const int64_t n2 = n >> 1, csz = 256 * WP, nfull = n2 / csz, ldv2 = ldv >> 1;   // ldv: a multiple of 32
+  auto chunk = [&](int64_t c0, auto fullc) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(fullc)::value;
+    dbl2 u[WP], g[WP];
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+      const int64_t i = c0 + k * 256 + threadIdx.x;
+      u[k] = (FULL || i < n2) ? w2[i] : dbl2{0.0, 0.0};
     }
+    auto vload = [&](int j, dbl2 (&t)[WP]) __attribute__((always_inline)) {
+      const dbl2 *__restrict__ vq = reinterpret_cast<const dbl2 *>(V) + (int64_t)j * ldv2;
+#pragma unroll
+      for (int k = 0; k < WP; ++k) {
+        const int64_t i = c0 + k * 256 + threadIdx.x;
+        t[k] = (FULL || i < n2) ? __builtin_nontemporal_load(vq + i) : dbl2{0.0, 0.0};
+      }
+    };
+    dbl2 ta[WP], tb[WP];
+    vload(0, ta);
+    // j's place in its group: the first nv % 4 vectors form the first group
+    for (int j = 0; j < nv; j += 2) {            // wave-uniform
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int jj = j + q;
+        if (jj >= nv) break;
+        dbl2 (&cur)[WP] = q ? tb : ta;
+        dbl2 (&nxt)[WP] = q ? ta : tb;
+        if (jj + 1 < nv) vload(jj + 1, nxt);
+        const bool first = jj < rem ? jj == 0 : ((jj - rem) & 3) == 0;
+        const bool last = jj < rem ? jj == rem - 1 : ((jj - rem) & 3) == 3;
+        const double aj = a[jj], sj = sc[jj];
+#pragma unroll
+        for (int k = 0; k < WP; ++k) {
+          const double px = aj * (sj * cur[k].x), py = aj * (sj * cur[k].y);
+          g[k].x = first ? px : g[k].x + px;
+          g[k].y = first ? py : g[k].y + py;
+          if (last) { u[k].x = u[k].x + g[k].x; u[k].y = u[k].y + g[k].y; }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+      const int64_t i = c0 + k * 256 + threadIdx.x;
+      if (FULL || i < n2) {
+        w2[i] = u[k];
+        v[0] += u[k].x * u[k].x;
+        v[0] += u[k].y * u[k].y;
+      }
+    }
+  };
+  for (int64_t c = blockIdx.x; c < nfull; c += gridDim.x) chunk(c * csz, std::true_type{});
+  if (nfull * csz < n2 && (int64_t)blockIdx.x == nfull % gridDim.x) chunk(nfull * csz, std::false_type{});
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // odd length: the last row
+    const int64_t i = n - 1;
+    double u = w[i];
+    int j = 0;
+    auto vj = [&](int j) { return sc[j] * gm_ld(V + (int64_t)j * ldv + i); };
+    if (rem == 1) { u = a[0] * vj(0) + u; j = 1; }
+    else if (rem == 2) { u = u + (a[0] * vj(0) + a[1] * vj(1)); j = 2; }
+    else if (rem == 3) { u = u + ((a[0] * vj(0) + a[1] * vj(1)) + a[2] * vj(2)); j = 3; }
+    for (; j < nv; j += 4)
+      u = u + (((a[j] * vj(j) + a[j + 1] * vj(j + 1)) + a[j + 2] * vj(j + 2)) + a[j + 3] * vj(j + 3));
+    w[i] = u;
+    v[0] += u * u;
   }
   block_partials<1>(v, partials, gridDim.x, fold);
 }
@@ -1767,7 +1831,8 @@ static void gmres_solve(Mat *A, const mx_ksp_params &p, const Jac dinv, const do
   Poller poller(A, st);            // its pinned words: the step count (HW_PROGRESS)
   Fold fnorm;                      // ||w||^2 of the MAXPY pass, folded in-launch into s->red[0]
   // MAXPY + norm grid (knob 77; one partial per workgroup, within part's rows)
-  const int xgrid = g_knobs.maxpy_grid > 0 ? std::min<int>(g_knobs.maxpy_grid, (int)std::min<size_t>(npart, 16384)) : RED_BLOCKS;
+  // the MAXPY + norm pass walks the basis in chunks on MDot's grid (maxpy_norm_kernel)
+  const int xgrid = g_knobs.maxpy_grid > 0 ? std::min<int>(g_knobs.maxpy_grid, (int)std::min<size_t>(npart, 16384)) : mdot_grid();
   fnorm.cnt = s->fold_upd; fnorm.out = sred; fnorm.ntotal = fnorm.ncount = xgrid;
   while (true) {
     // KSPInitialResidual: vv0 = B (b - A x)
