@@ -427,8 +427,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
     const int cbA = colA * 128 + 2 * lane, cbB = colB * 128 + 2 * lane;
     dbl2 zmA = bload2(xr, z0 * D + cbA - D), cA = bload2(xr, z0 * D + cbA);
     dbl2 zmB = bload2(xr, z0 * D + cbB - D), cB = bload2(xr, z0 * D + cbB);
+    // block words one plane ahead (their scalar loads off the step's path)
+    uint32_t bwAn = (uint32_t)pblk[z0 * a.P + colA], bwBn = (uint32_t)pblk[z0 * a.P + colB];
     for (int z = z0; z < z1; ++z) {
-      const uint32_t bwA = (uint32_t)pblk[z * a.P + colA], bwB = (uint32_t)pblk[z * a.P + colB];
+      const uint32_t bwA = bwAn, bwB = bwBn;
+      if (z + 1 < z1) { bwAn = (uint32_t)pblk[(z + 1) * a.P + colA]; bwBn = (uint32_t)pblk[(z + 1) * a.P + colB]; }
       const int rA = z * D + cbA, rB = z * D + cbB;
       const dbl2 zpA = bload2(xr, rA + D), zpB = bload2(xr, rB + D);
       const dbl2 nA = bload2(xr, rA + a.anchor[1] + ((bwA & (PBLK_RUN0 << 1)) ? PAIR_OOR : 0));
