@@ -875,3 +875,39 @@ def test_distributed_mode5_fused_direction(oracle_mod, P, kind, n):
     xb = fused[0][5]
     assert dcs[0]["zm_pbws"] >= P * (its - its // xb - 1) and dcs[1]["zm_pbws"] == 0, dcs
     assert dcs[0]["zm_pw"] < dcs[1]["zm_pw"], dcs
+
+
+def test_host_csr_concurrent_shared_pages(oracle_mod):
+    """Four in-process ranks assemble createAIJ(csr=...) at once from slices of
+    one host CSR (local_csr: views into the same column and value arrays, so
+    neighbouring ranks' slices share a page at each boundary), every slice
+    large enough for the page-locked pipeline.  Only whole pages inside a
+    slice are registered (mx_abi.hip h2d_pinned); overlapping registrations
+    from concurrent rank threads faulted the GPU.  MatMult
+    bit-exact against the P-rank oracle."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from mxsolve.core import DMat
+    P, M = 4, 1 << 19
+    ip, c, v = bench.random_csr(M)
+    ranges = oracle_mod.split_ownership(M, P)
+    assert all((ip[ranges[r + 1]] - ip[ranges[r]]) * 4 > (1 << 20) for r in range(P))
+    O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
+    x = np.random.default_rng(3).standard_normal(M)
+    y_ref = O.mult(x)
+
+    def body(comm):
+        r = comm.rank
+        lip, lc, lv = local_csr(ip, c, v, ranges[r], ranges[r + 1])
+        A = DMat.from_csr(comm, M, M, lip, lc, lv)
+        xl = torch.from_numpy(x[ranges[r]:ranges[r + 1]].copy()).cuda()
+        yl = torch.zeros(ranges[r + 1] - ranges[r], dtype=torch.float64, device="cuda")
+        A.mult(xl, yl)
+        out = yl.cpu().numpy()
+        A.destroy()
+        return out
+
+    y = np.concatenate(run_ranks(P, body))
+    assert np.array_equal(y.view(np.uint64), y_ref.view(np.uint64))
