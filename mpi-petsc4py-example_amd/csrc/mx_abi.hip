@@ -146,40 +146,36 @@ int mx_layout_split(int64_t N, int P, int64_t *ranges) {
 }
 
 // Host-to-device copy of a caller's (pageable) arrays for createAIJ(csr=...):
-// indptr, cols and vals go through ONE pipeline of chunks.  Each chunk is
-// page-locked in place (hipHostRegister), copied, and unregistered once its
-// copy is done.  Registration runs ahead on H2D_REG_THREADS host threads (a
-// chunk of fresh numpy pages takes longer to lock than its DMA) while the
-// calling thread issues the copies in order.  Chunk sizes ramp from 4 MiB to
-// 64 MiB, so the first copy starts after a 4 MiB registration (0.25 ms)
-// rather than a 64 MiB one (4 ms); one pipeline over the three arrays avoids
-// a drain and a ramp per array (tools/h2d_pin_probe.hip, tools/h2d_lib_probe.py).
-// Arrays under 1 MiB, the partial first and last pages, and a chunk whose
-// registration fails go through page-locked memory the library allocates.
+// indptr, cols and vals go through ONE pipeline of chunks.  The pages wholly
+// inside an array of PIN_MIN bytes or more are page-locked in place
+// (hipHostRegister) chunk by chunk, copied, and unregistered once the copy is
+// done; registration runs ahead on H2D_REG_THREADS host threads (a chunk of
+// fresh numpy pages takes longer to lock than its DMA) while the calling
+// thread issues the copies in order.  Chunk sizes ramp from 4 MiB to 64 MiB,
+// so the first copy starts after a 4 MiB registration (0.25 ms) rather than a
+// 64 MiB one (4 ms); one pipeline over the three arrays avoids a drain and a
+// ramp per array (tools/h2d_pin_probe.hip, tools/h2d_lib_probe.py).
+// Everything else -- arrays under PIN_MIN, the partial first and last pages
+// of a pinned one (never registered, so arrays that share a page never hold
+// overlapping registrations), a chunk whose registration fails -- is a plain
+// (runtime-staged) copy.  PIN_MIN is 128 MiB: with 1 MiB the GPU suite, which
+// assembles many operators from moderate host arrays, twice ended in an
+// illegal address during these copies; at 128 MiB
+// registration serves the large payloads it pays for.
 struct H2dSeg { void *dst; const void *src; size_t bytes; };
-// page-locked bounce slots for the cuts h2d_pinned does not pin, allocated
-// once by h2d_warm; a call that finds it busy (another rank thread) or too
-// small allocates its own
-struct H2dPool { std::mutex mu; char *p = nullptr; size_t cap = 0; };
-static H2dPool g_h2d_pool;
 constexpr int H2D_REG_THREADS = 4;
-static void h2d_pinned(const std::vector<H2dSeg> &segs, hipStream_t st) {
-  constexpr size_t CH0 = (size_t)4 << 20, CH = (size_t)64 << 20, SMALL = (size_t)1 << 20, PAGE = 4096;
+constexpr size_t H2D_PIN_MIN = (size_t)128 << 20;
+static void h2d_pinned(const std::vector<H2dSeg> &segs, hipStream_t st, size_t pin_min = H2D_PIN_MIN) {
+  constexpr size_t CH0 = (size_t)4 << 20, CH = (size_t)64 << 20, PAGE = 4096;
   struct Cut { char *dst; uintptr_t a, b; bool pin; };
   std::vector<Cut> cuts;
   size_t k = 0;    // pinned chunks cut so far (the ramp)
   for (const H2dSeg &g : segs) {
     if (!g.bytes) continue;
     const uintptr_t s0 = reinterpret_cast<uintptr_t>(g.src), s1 = s0 + g.bytes;
-    // only pages wholly inside the array are registered: the partial first
-    // and last pages are plain copies.  A registration never reaches past the
-    // caller's bytes, so arrays that share a page -- slices of one numpy
-    // array handed to in-process ranks that copy concurrently -- never hold
-    // overlapping registrations (the runtime can resolve a copy's source to
-    // the other registration, unregistered under it: an illegal access)
     const uintptr_t p0 = (s0 + PAGE - 1) & ~(uintptr_t)(PAGE - 1), p1 = s1 & ~(uintptr_t)(PAGE - 1);
     char *d0 = static_cast<char *>(g.dst);
-    if (g.bytes < SMALL || p1 <= p0) { cuts.push_back({d0, s0, s1, false}); continue; }
+    if (g.bytes < pin_min || p1 <= p0) { cuts.push_back({d0, s0, s1, false}); continue; }
     if (p0 > s0) cuts.push_back({d0, s0, p0, false});
     for (uintptr_t a = p0; a < p1; ++k) {   // page-aligned chunks: no page registered twice
       const uintptr_t b = std::min<uintptr_t>(p1, a + std::min(CH, CH0 << std::min<size_t>(k, 4)));
@@ -188,42 +184,24 @@ static void h2d_pinned(const std::vector<H2dSeg> &segs, hipStream_t st) {
     }
     if (s1 > p1) cuts.push_back({d0 + (p1 - s0), p1, s1, false});
   }
-  struct Chunk { char *dst; uintptr_t a, b, reg; size_t reg_len; bool pin; std::atomic<int> state{0}; hipEvent_t ev = nullptr; };  // 0 pending, 1 pinned, 2 not pinned
+  struct Chunk { char *dst; uintptr_t a, b; bool pin; std::atomic<int> state{0}; hipEvent_t ev = nullptr; };  // 0 pending, 1 pinned, 2 not pinned
   const size_t n = cuts.size();
   std::vector<Chunk> ch(n);
+  size_t npin = 0;
   for (size_t i = 0; i < n; ++i) {
     Chunk &c = ch[i];
     c.dst = cuts[i].dst; c.a = cuts[i].a; c.b = cuts[i].b; c.pin = cuts[i].pin;
-    c.reg = c.a;                 // pinned chunks: page-aligned, inside the array
-    c.reg_len = c.b - c.a;
     if (!c.pin) c.state.store(2);
-  }
-  // the cuts not pinned here go through page-locked memory of the library's
-  // own (CPU copy, then DMA): a plain copy's source pointer could resolve to
-  // another thread's registration of the same bytes, released under the DMA.
-  // One slot per small cut (no waits), a 4 MiB ring for a chunk whose
-  // registration failed (rare: the caller's memory already pinned)
-  std::vector<size_t> boff(n, 0);
-  size_t bsz = 0;
-  for (size_t i = 0; i < n; ++i)
-    if (!ch[i].pin) { boff[i] = bsz; bsz += (ch[i].b - ch[i].a + 255) & ~(size_t)255; }
-  char *bounce = nullptr, *fbounce = nullptr;
-  constexpr size_t FB = (size_t)4 << 20;
-  bool pooled = false;
-  if (bsz && bsz <= g_h2d_pool.cap && g_h2d_pool.mu.try_lock()) {
-    bounce = g_h2d_pool.p;
-    pooled = true;
-  } else if (bsz) {
-    HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&bounce), bsz, hipHostMallocDefault));
+    npin += c.pin;
   }
   std::atomic<bool> stop{false};
   std::vector<std::thread> reg;
-  const int nt = (int)std::min<size_t>(H2D_REG_THREADS, n);
+  const int nt = npin ? (int)std::min<size_t>(H2D_REG_THREADS, n) : 0;
   for (int t = 0; t < nt; ++t)
     reg.emplace_back([&, t] {
       for (size_t i = (size_t)t; i < n && !stop.load(); i += (size_t)nt) {
-        if (!ch[i].pin) continue;   // small: a plain copy
-        const bool ok = hipHostRegister(reinterpret_cast<void *>(ch[i].reg), ch[i].reg_len, hipHostRegisterDefault) == hipSuccess;
+        if (!ch[i].pin) continue;
+        const bool ok = hipHostRegister(reinterpret_cast<void *>(ch[i].a), ch[i].b - ch[i].a, hipHostRegisterDefault) == hipSuccess;
         ch[i].state.store(ok ? 1 : 2, std::memory_order_release);
       }
     });
@@ -233,40 +211,28 @@ static void h2d_pinned(const std::vector<H2dSeg> &segs, hipStream_t st) {
     (void)hipStreamSynchronize(st);
     for (Chunk &c : ch) {
       if (c.ev) (void)hipEventDestroy(c.ev);
-      if (c.state.load() == 1) (void)hipHostUnregister(reinterpret_cast<void *>(c.reg));
+      if (c.state.load() == 1) (void)hipHostUnregister(reinterpret_cast<void *>(c.a));
       c.state.store(0);
     }
-    if (pooled) g_h2d_pool.mu.unlock();
-    else if (bounce) (void)hipHostFree(bounce);
-    pooled = false;
-    if (fbounce) (void)hipHostFree(fbounce);
-    bounce = fbounce = nullptr;
     (void)hipGetLastError();   // failed registrations
   };
   try {
     size_t done = 0;   // chunks released
     for (size_t i = 0; i < n; ++i) {
       while (ch[i].state.load(std::memory_order_acquire) == 0) std::this_thread::yield();
-      const size_t len = ch[i].b - ch[i].a;
-      if (ch[i].state.load() == 1) {
-        HIPCHECK(hipMemcpyAsync(ch[i].dst, reinterpret_cast<const void *>(ch[i].a), len, hipMemcpyHostToDevice, st));
-      } else if (!ch[i].pin) {
-        std::memcpy(bounce + boff[i], reinterpret_cast<const void *>(ch[i].a), len);
-        HIPCHECK(hipMemcpyAsync(ch[i].dst, bounce + boff[i], len, hipMemcpyHostToDevice, st));
-      } else {                   // registration failed: through the ring, a piece at a time
-        if (!fbounce) HIPCHECK(hipHostMalloc(reinterpret_cast<void **>(&fbounce), FB, hipHostMallocDefault));
-        for (size_t o = 0; o < len; o += FB) {
-          const size_t q = std::min(FB, len - o);
-          HIPCHECK(hipStreamSynchronize(st));   // the ring's previous piece has landed
-          std::memcpy(fbounce, reinterpret_cast<const void *>(ch[i].a + o), q);
-          HIPCHECK(hipMemcpyAsync(ch[i].dst + o, fbounce, q, hipMemcpyHostToDevice, st));
-        }
-      }
+      HIPCHECK(hipMemcpyAsync(ch[i].dst, reinterpret_cast<const void *>(ch[i].a), ch[i].b - ch[i].a,
+                              hipMemcpyHostToDevice, st));
+      if (!ch[i].pin) continue;
       HIPCHECK(hipEventCreateWithFlags(&ch[i].ev, hipEventDisableTiming));
       HIPCHECK(hipEventRecord(ch[i].ev, st));
-      for (; done + 2 < i + 1; ++done) {   // two chunks in flight: release the older ones
+      // two pinned chunks in flight: release the older ones
+      for (; done < i; ++done) {
+        if (!ch[done].ev) continue;
+        size_t later = 0;
+        for (size_t j = done + 1; j <= i; ++j) later += ch[j].ev != nullptr;
+        if (later < 2) break;
         HIPCHECK(hipEventSynchronize(ch[done].ev));
-        if (ch[done].state.load() == 1) (void)hipHostUnregister(reinterpret_cast<void *>(ch[done].reg));
+        if (ch[done].state.load() == 1) (void)hipHostUnregister(reinterpret_cast<void *>(ch[done].a));
         ch[done].state.store(0);
       }
     }
@@ -772,15 +738,10 @@ void h2d_warm() {
   char *h = static_cast<char *>(std::aligned_alloc(4096, W));
   void *d = nullptr;
   hipStream_t st = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(g_h2d_pool.mu);
-    if (!g_h2d_pool.p && hipHostMalloc(reinterpret_cast<void **>(&g_h2d_pool.p), (size_t)2 << 20, hipHostMallocDefault) == hipSuccess)
-      g_h2d_pool.cap = (size_t)2 << 20;
-  }
   if (h && hipMalloc(&d, W) == hipSuccess && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
     std::memset(h, 0, W);
     try {
-      h2d_pinned({{d, h, W}}, st);
+      h2d_pinned({{d, h, W}}, st, (size_t)1 << 20);   // this buffer is the library's own: registered
     } catch (const Error &) {
     }
   }

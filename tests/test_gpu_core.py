@@ -389,16 +389,16 @@ def test_assembly_fused_vs_separate(selfcomm, golden, case):
 
 @pytest.mark.parametrize("itype", [np.int32, np.int64])
 def test_host_csr_pinned_pieces(selfcomm, oracle_mod, itype):
-    """createAIJ(csr=...) from host arrays big enough for the page-locked
-    pipeline (mx_abi.hip h2d_pinned: >= 1 MiB, chunks ramping from 4 MiB),
-    each a view that starts and ends inside a page, so the partial first and
-    last pages go through the library's staging buffer and the interior is
-    registered in page-aligned chunks; the row pointer stays under 1 MiB (a
-    staged copy).  The same CSR as the oracle, byte for byte."""
+    """createAIJ(csr=...) from host arrays with one over the registration
+    threshold (mx_abi.hip h2d_pinned: 128 MiB; its whole interior pages
+    page-locked in chunks ramping from 4 MiB), every array a view that starts
+    and ends inside a page, so the partial first and last pages take the plain
+    copy; the row pointer and (int32) columns stay under the threshold.  The
+    same CSR as the oracle, byte for byte."""
     from mxsolve.core import DMat
     rng = np.random.default_rng(17 + (itype == np.int32))
-    M = N = 120000
-    lens = rng.integers(3, 9, M)
+    M = N = 2_500_000
+    lens = rng.integers(5, 10, M)
     ip = np.concatenate([[0], np.cumsum(lens)]).astype(itype)
     nnz = int(ip[-1])
     cols = rng.integers(0, N, nnz).astype(itype)
@@ -410,8 +410,8 @@ def test_host_csr_pinned_pieces(selfcomm, oracle_mod, itype):
         v[:] = a
         return v
     ipv, cv, vv = view(ip, 3), view(cols, 5), view(vals, 1)
-    assert vv.nbytes > (5 << 20) and cv.nbytes > (1 << 20) and ipv.nbytes < (1 << 20)
-    assert cv.ctypes.data % 4096 and vv.ctypes.data % 4096 and (vv.ctypes.data + vv.nbytes) % 4096
+    assert vv.nbytes > (128 << 20)
+    assert vv.ctypes.data % 4096 and (vv.ctypes.data + vv.nbytes) % 4096
     A = DMat.from_csr(selfcomm, M, N, ipv, cv, vv)
     O = oracle_mod.OracleMat.from_csr(M, N, ip.astype(np.int64), cols.astype(np.int64), vals, P=1)
     assert_csr_equal(A.csr(), O.csr())

@@ -880,11 +880,11 @@ def test_distributed_mode5_fused_direction(oracle_mod, P, kind, n):
 def test_host_csr_concurrent_shared_pages(oracle_mod):
     """Four in-process ranks assemble createAIJ(csr=...) at once from slices of
     one host CSR (local_csr: views into the same column and value arrays, so
-    neighbouring ranks' slices share a page at each boundary), every slice
-    large enough for the page-locked pipeline.  Only whole pages inside a
-    slice are registered (mx_abi.hip h2d_pinned); overlapping registrations
-    from concurrent rank threads faulted the GPU.  MatMult
-    bit-exact against the P-rank oracle."""
+    neighbouring ranks' slices share a page at each boundary), each slice
+    1-4 MB.  Round 6 first page-locked arrays from 1 MiB, and this pattern's
+    overlapping registrations from concurrent rank threads faulted the GPU
+    (DESIGN.md §12.4); slices under the 128 MiB threshold take the plain
+    copy.  MatMult bit-exact against the P-rank oracle."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -893,7 +893,6 @@ def test_host_csr_concurrent_shared_pages(oracle_mod):
     P, M = 4, 1 << 19
     ip, c, v = bench.random_csr(M)
     ranges = oracle_mod.split_ownership(M, P)
-    assert all((ip[ranges[r + 1]] - ip[ranges[r]]) * 4 > (1 << 20) for r in range(P))
     O = oracle_mod.OracleMat.from_csr(M, M, ip, c, v, P=P)
     x = np.random.default_rng(3).standard_normal(M)
     y_ref = O.mult(x)
