@@ -92,7 +92,9 @@ def test_cb_gmres_equals_one_pass_and_oracle(selfcomm, oracle_mod):
 
 def test_cb_cg_symmetric_random(selfcomm, oracle_mod):
     """CG + Jacobi on a symmetric random pattern (A + A^T + diagonal
-    dominance): the MatMult's p.Ap partials come from the two-pass kernel."""
+    dominance), CG mode 2 (auto's choice from 3M rows; mode 1 fuses the
+    direction update into a MatMult form the two-pass kernel does not take):
+    the MatMult's p.Ap partials come from the two-pass kernel."""
     import scipy.sparse as sp
     N = 1 << 13
     ip, c, v = _random_csr(N, 5, 17)
@@ -104,10 +106,18 @@ def test_cb_cg_symmetric_random(selfcomm, oracle_mod):
     S = S.tocsr()
     S.sort_indices()
     b = np.random.default_rng(6).random(N)
+    from mxsolve.core import dispatch_counts
     A = _mat(selfcomm, N, S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data, 2)
     assert A.info()["cb_blocks"] > 0
     x = selfcomm.zeros(N)
-    r = A.solve(torch.from_numpy(b).cuda(), x, ksp="cg", pc="jacobi")
+    old = _knob(9, 2)          # CG mode 2 (auto's choice from 3M rows): a plain MatMult + p.w
+    try:
+        dispatch_counts(reset=True)
+        r = A.solve(torch.from_numpy(b).cuda(), x, ksp="cg", pc="jacobi")
+        dc = dispatch_counts(reset=True)
+    finally:
+        _knob(9, old)
+    assert dc["cb"] >= r["its"], dc
     o = oracle_mod.OracleMat.from_csr(N, N, S.indptr, S.indices, S.data).solve(b, ksp="cg", pc="jacobi")
     assert (r["its"], r["reason"]) == (o["its"], o["reason"])
     xv = x.cpu().numpy()
@@ -210,3 +220,56 @@ def test_cb_rows_without_diagonal(selfcomm, oracle_mod):
     yo = oracle_mod.OracleMat.from_csr(N, N, ip2, c2, v2).mult(xh)
     assert np.array_equal(y.cpu().numpy().view(np.uint64), yo.view(np.uint64))
     A.destroy()
+
+
+def test_cb_ranks_cg_split(oracle_mod):
+    """CG + Jacobi (mode 2) on a symmetric random pattern over two in-process
+    ranks: the MatMult's DOT form through the column-block path in split mode (the
+    rows with ghost entries leave their p.y terms to the halo-boundary
+    kernel).  Bit for bit the one-pass run (key 84 = 0); its and reason the
+    P-rank oracle's, x within relative L2 1e-10."""
+    import scipy.sparse as sp
+    from mxsolve.core import LocalWorld, DMat, dispatch_counts
+    P, N = 2, 1 << 13
+    ip, c, v = _random_csr(N, 5, 29)
+    R = sp.csr_matrix((v, c, ip), shape=(N, N))
+    S = (R + R.T).tocsr()
+    S.setdiag(0.0)
+    S.eliminate_zeros()
+    S = (S + sp.diags(1.0 + np.asarray(abs(S).sum(axis=1)).ravel())).tocsr()
+    S.sort_indices()
+    ip, c, v = S.indptr.astype(np.int64), S.indices.astype(np.int32), S.data
+    ranges = oracle_mod.split_ownership(N, P)
+    b = np.random.default_rng(7).random(N)
+
+    def body(comm):
+        r0, r1 = ranges[comm.rank], ranges[comm.rank + 1]
+        A = DMat.from_csr(comm, N, N, ip[r0:r1 + 1] - ip[r0], c[ip[r0]:ip[r1]], v[ip[r0]:ip[r1]])
+        cbk = A.info()["cb_blocks"]
+        x = comm.zeros(r1 - r0)
+        res = A.solve(torch.from_numpy(b[r0:r1].copy()).cuda(), x, ksp="cg", pc="jacobi", history=True)
+        A.destroy()
+        return cbk, res["its"], res["reason"], res["history"], x.cpu().numpy()
+
+    outs, dcs = {}, {}
+    for cb in (2, 0):
+        old, oldm = _knob(84, cb), _knob(9, 2)   # CG mode 2: the plain DOT MatMult
+        w = LocalWorld(P)
+        try:
+            dispatch_counts(reset=True)
+            outs[cb] = w.run(body)
+            dcs[cb] = dispatch_counts(reset=True)
+        finally:
+            _knob(84, old)
+            _knob(9, oldm)
+            w.destroy()
+    assert all(o[0] > 0 for o in outs[2]) and all(o[0] == 0 for o in outs[0])
+    assert dcs[2]["cb"] >= P * outs[2][0][1] and dcs[0]["cb"] == 0, (dcs[2], dcs[0])
+    for a, z in zip(outs[2], outs[0]):
+        assert (a[1], a[2]) == (z[1], z[2])
+        assert np.array_equal(a[3].view(np.uint64), z[3].view(np.uint64))
+        assert np.array_equal(a[4].view(np.uint64), z[4].view(np.uint64))
+    o = oracle_mod.OracleMat.from_csr(N, N, ip, c, v, P=P).solve(b, ksp="cg", pc="jacobi")
+    x = np.concatenate([a[4] for a in outs[2]])
+    assert (outs[2][0][1], outs[2][0][2]) == (o["its"], o["reason"])
+    assert np.linalg.norm(x - o["x"]) <= 1e-10 * np.linalg.norm(o["x"])
